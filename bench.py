@@ -1,0 +1,277 @@
+#!/usr/bin/env python3
+"""Bench: device-resident CRC32C over 64 KiB packets x 512 B chunks (BASELINE.json).
+
+One step = one pass of the hot path (hadoop_rpc_send_packet's per-chunk
+checksum loop, src/hadooprpc.c:733-742, for a whole batch) over one batch
+already resident in HBM: config 2 = 4096 packets x 65536 B = 256 MiB,
+bytesPerChecksum 512, 524288 checksums, on every rank (weak scaling: each
+GPU checksums its own 256 MiB batch, no data-path collective).  The batch
+rotates over NBUF distinct 256 MiB buffers so consecutive steps cannot be
+served from the 256 MiB Infinity Cache.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+N > 1 is launched by torch.distributed.run (one rank per GPU).  After the
+timed region the ranks' checksum arrays are gathered to rank 0 over RCCL
+(the only collective; timed separately as "gather_ms").
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib.util
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+KERNEL_NAME = "hdfs_crc32c_plan_kernel"
+
+
+def load_package():
+    if "hdfs_crc32c_amd" in sys.modules:
+        return sys.modules["hdfs_crc32c_amd"]
+    spec = importlib.util.spec_from_file_location(
+        "hdfs_crc32c_amd", os.path.join(ROOT, "native-hdfs-fuse_amd", "__init__.py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["hdfs_crc32c_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def config_packets(name: str, oracle_mod):
+    """Packet descriptors of one rank's batch, per BASELINE.json configs."""
+    if name == "c2":  # 4096 x 64 KiB, bpc 512
+        return oracle_mod.uniform_packets(4096), "4096 x 64KiB packets, 512B chunks (BASELINE config 2)"
+    if name == "c3":  # one 4 MiB block
+        return oracle_mod.uniform_packets(64), "one 4MiB block as 64 x 64KiB packets, 512B chunks (config 3)"
+    if name == "c4":  # 128 MiB file = 32 blocks round-robin over the ranks
+        return None, "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
+    if name == "c5":
+        return oracle_mod.mixed_packets(4096), "4096 x 64KiB packets, bpc cycling 512/1024/4096 (config 5)"
+    raise SystemExit("unknown config " + name)
+
+
+def c4_rank_packets(oracle_mod, rank: int, world: int):
+    blocks = [b for b in range(32) if b % world == rank]
+    pk = oracle_mod.uniform_packets(64 * len(blocks))
+    return pk, blocks
+
+
+def baseline_metric() -> str:
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            return json.load(f)["metric"]
+    except Exception:
+        return "GiB/s CRC32C, device-resident 64 KiB packets \u00d7 512 B chunks, 1/2/4/8 GPU"
+
+
+def latest_pmc(profile_dir: str):
+    """HBM bytes per launch of the kernel from the committed rocprofv3 PMC
+    summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
+    files = sorted(glob.glob(os.path.join(profile_dir, "*pmc*.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            d = json.load(f)
+        return d
+    except Exception:
+        return None
+
+
+def cpu_baseline(oracle_mod, pk, payload_np: np.ndarray, seconds: float):
+    """The reference's own crc32c.c (oracle/_ref, kind "reference") or the
+    clean-room oracle (kind "port"), per chunk as hadooprpc.c:739-742, on
+    the host cores of this box: bounded sample = the same batch, repeated
+    until `seconds` of wall time per thread count."""
+    try:
+        impl = oracle_mod.Reference()
+        kind = "reference"
+    except Exception:
+        impl = oracle_mod.Oracle()
+        kind = "port"
+    nout = oracle_mod.total_checksums(pk)
+    out = np.zeros(nout, np.uint32)
+    nbytes = int(pk["len"].astype(np.int64).sum())
+    threads = max(1, min(16, os.cpu_count() or 1))
+    res = {}
+    for t in sorted({1, threads}):
+        dt = impl.batch_mt_seconds(payload_np, pk, out, t, 1)
+        reps = max(1, int(seconds / max(dt, 1e-6)))
+        dt = impl.batch_mt_seconds(payload_np, pk, out, t, reps)
+        res[t] = nbytes * reps / dt / GIB
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
+    except Exception:
+        pass
+    return {
+        "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "sample": "%s: the config batch (%d packets, %.0f MiB) per pass, %.0fs per thread count; reference "
+                  "crc32c.c built -O2 (its Makefile builds -O0)" % (kind, pk.size, nbytes / 2**20, seconds),
+        "one_core_gib_s": round(res[1], 3), "host_cpus": os.cpu_count(), "cpu_model": cpu_model,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--nbuf", type=int, default=4, help="rotating payload buffers (defeat the 256 MiB L3)")
+    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import oracle
+
+    hdfs = load_package()
+    hdfs.lib()
+
+    if args.config == "c4":
+        pk, _blocks = c4_rank_packets(oracle, rank, world)
+        workload = "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
+        nbuf = 1
+    else:
+        pk, workload = config_packets(args.config, oracle)
+        nbuf = args.nbuf if args.config != "c3" else 1
+    nbytes = int(pk["len"].astype(np.int64).sum())
+    extent = int((pk["payload_off"] + pk["len"]).max())
+    nout = hdfs.total_checksums(pk)
+
+    ctx = hdfs.Context(local_rank)
+    plan = ctx.plan(pk)
+    dev = torch.device("cuda", local_rank)
+    # buffer 0: the documented xorshift64 stream (checked against the CPU
+    # path below); the rest: device-generated random bytes.
+    payload0 = oracle.xorshift64_bytes(extent, oracle.SEED + rank)
+    bufs = [torch.from_numpy(payload0).to(dev)]
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    for _ in range(1, nbuf):
+        bufs.append(torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g))
+    outs = [torch.zeros(max(nout, 1), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def step(i):
+        b = i % nbuf
+        plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sptr)
+
+    # correctness gate (outside the timed region): every buffer-0 checksum
+    step(0)
+    torch.cuda.synchronize()
+    want = (oracle.Reference() if oracle.Reference.available() else oracle.Oracle()).batch(payload0, pk, nout)
+    got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
+    bit_exact = bool(np.array_equal(got0, want))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(i)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)  # avg per launch, on the launch stream
+
+    if world > 1:
+        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(tt[0]), float(tt[1])
+        ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        bit_exact = bool(ok.item())
+        # RCCL gather of every rank's checksum array to rank 0 (the path's only exchange)
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        gathered = [torch.empty_like(outs[0]) for _ in range(world)] if rank == 0 else None
+        dist.gather(outs[0], gathered, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) * 1e3
+    else:
+        gather_ms = None
+
+    total_bytes = nbytes * world * args.steps
+    value = total_bytes / elapsed / GIB
+    achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
+
+    host = None
+    if rank == 0 and not args.no_host and args.config != "c4":
+        pinned = torch.from_numpy(payload0).pin_memory()
+        hp = pinned.numpy()
+        ctx.batch_host(hp, pk)  # warm (allocates staging)
+        h0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            ctx.batch_host(hp, pk)
+        host = round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2)
+
+    if rank == 0:
+        pmc = latest_pmc(os.path.join(ROOT, "profiles"))
+        traffic = None
+        if pmc and pmc.get("kernel") == KERNEL_NAME and pmc.get("config") == args.config:
+            traffic = pmc.get("hbm_bytes_per_launch")
+        cpu = None if args.no_cpu else cpu_baseline(oracle, pk, payload0, args.cpu_seconds)
+        line = {
+            "metric": baseline_metric(),
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (xorshift64 stream + device random bytes, %d rotating %d MiB buffers per rank)"
+                    % (nbuf, extent >> 20),
+            "config": {"workload": workload, "config": args.config, "packets_per_rank": int(pk.size),
+                       "packet_bytes": int(pk["len"][0]), "bytes_per_checksum": sorted(set(int(x) for x in pk["bpc"])),
+                       "payload_bytes_per_rank": nbytes, "checksums_per_rank": nout,
+                       "parallelism": "dp%d (independent shards, RCCL gather of checksums after timing)" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "kernel": KERNEL_NAME, "kernel_avg_us": round(kernel_ms * 1e3, 2),
+                         "algorithmic_bytes_per_launch": nbytes},
+            "cpu_baseline": cpu,
+            "bit_exact_vs_reference": bit_exact,
+            "host_resident_gib_s": host,
+            "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        }
+        print(json.dumps(line), flush=True)
+    plan.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

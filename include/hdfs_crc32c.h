@@ -1,0 +1,143 @@
+/*
+ * hdfs_crc32c.h -- C ABI of the MI355X-native CRC32C chunk-checksum path of
+ * native-hdfs-fuse (libhdfs_crc32c.so).
+ *
+ * Every entry point is plain C: pointers, sizes and integers, no HIP or torch
+ * types in the signatures (a HIP stream is passed as `void *`).  Batch entry
+ * points return 0 on success or a negative errno, the reference's convention
+ * (src/hadooprpc.c:440-486, 630-636).  They never fall back to a CPU
+ * implementation: without a usable GPU they return -ENODEV.
+ *
+ * Reference interfaces replaced (file:line under the reference tree):
+ *   crc32c()             src/crc32c.c:333-343 (declared by hand at src/hadooprpc.c:31)
+ *   crc32c_chunks*()     the per-chunk loop of hadoop_rpc_send_packet,
+ *                        src/hadooprpc.c:639 + 727-748 (roundup, crc32c(0, ...), htonl)
+ *   crc32c_packetize()   the packet cutting of hadoop_rpc_send_packets,
+ *                        src/hadooprpc.c:827-857
+ *   crc32c_multi_*()     no reference counterpart: blocks written in parallel
+ *                        (src/fuse.c:580-647 writes them one at a time) sharded
+ *                        over several GPUs of one node.
+ */
+#ifndef HDFS_CRC32C_H
+#define HDFS_CRC32C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDFS_CRC32C_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------
+ * 1. Drop-in scalar checksum (host CPU).
+ *
+ * Same signature and semantics as the reference export (src/crc32c.c:333):
+ * `crc` is the finished CRC32C of the preceding bytes (0 to start), the result
+ * is the CRC32C of the concatenation, in host byte order; any alignment;
+ * len == 0 returns crc.  Cannot fail, reentrant, thread-safe.  This is the
+ * per-call host path (a GPU round trip per 512-byte chunk would be absurd);
+ * batches go through the GPU entry points below.
+ * ------------------------------------------------------------------------- */
+uint32_t crc32c(uint32_t crc, const void *buf, size_t len);
+
+/* Checksum flags. */
+#define CRC32C_BIG_ENDIAN 0x1u /* store htonl(crc), the wire order of hadooprpc.c:71-75 */
+
+/* One packet of a batch: `len` payload bytes starting `payload_off` bytes into
+ * the batch payload buffer, cut into chunks of `bpc` bytes
+ * (bytesPerChecksum); its ceil(len / bpc) checksums go to out[out_idx ...].
+ * Exactly hadooprpc.c:733-742 per packet: chunk i covers
+ * [i*bpc, i*bpc + min(bpc, len - i*bpc)), checksummed from crc = 0. */
+typedef struct crc32c_packet {
+    uint64_t payload_off;
+    uint64_t out_idx;
+    uint32_t len;
+    uint32_t bpc;
+} crc32c_packet;
+
+/* Number of checksums of one packet: roundup(len, bpc) (hadooprpc.c:639). */
+uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc);
+
+/* Packet lengths hadoop_rpc_send_packets produces for one block write of
+ * `len` bytes starting at `blockoffset` (hadooprpc.c:827-857), including the
+ * final empty packet.  Writes up to `max` lengths; returns the count. */
+uint64_t crc32c_packetize(uint64_t len, uint64_t blockoffset, uint32_t packetsize, uint32_t bpc, uint64_t *lens,
+                          uint64_t max);
+
+/* ---------------------------------------------------------------------------
+ * 2. GPU context (one HIP device).  Thread-safe: calls on one context are
+ * serialised internally; use one context per thread for concurrency.
+ * ------------------------------------------------------------------------- */
+typedef struct crc32c_ctx crc32c_ctx;
+
+int crc32c_ctx_create(int device, crc32c_ctx **out);
+int crc32c_ctx_destroy(crc32c_ctx *ctx);
+/* Number of visible HIP devices (0 when there is no GPU). */
+int crc32c_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * 3. Device-resident batches.
+ *
+ * A plan is built once per batch SHAPE from host packet descriptors (work
+ * decomposition into 8 KiB tiles, uploaded to the device) and executed on
+ * any payload with that shape.  Payload and checksum buffers are device
+ * pointers; execution is asynchronous on `stream` (a hipStream_t, NULL =
+ * the default stream).
+ * Alignment contract: payload_off values that are multiples of 16 with
+ * bpc in {512, 1024, 2048, 4096, 8192} take the fast path; anything else is
+ * still exact (general path).  The payload buffer must be readable up to the
+ * next 16-byte boundary after each packet's last byte (device allocations
+ * always are).
+ * ------------------------------------------------------------------------- */
+typedef struct crc32c_plan crc32c_plan;
+
+int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, uint32_t flags,
+                       crc32c_plan **out);
+int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out, void *stream);
+int crc32c_plan_destroy(crc32c_plan *plan);
+/* Total checksums the plan writes (max over packets of out_idx + nchunks). */
+uint64_t crc32c_plan_nchecksums(const crc32c_plan *plan);
+/* Payload bytes the plan checksums (sum of packet lengths). */
+uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
+
+/* One-shot device batch: builds a plan, runs it on `stream` and waits for it. */
+int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,
+                      uint32_t *dev_out, uint32_t flags, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * 4. Host-resident batches (file pages on their way to the DataNode socket).
+ * The payload is copied to the GPU through pinned staging buffers
+ * (hipMemcpyAsync, double-buffered over two streams), checksummed, and the
+ * checksums copied back into `out` (host memory).  Blocking.
+ * ------------------------------------------------------------------------- */
+int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                      uint32_t *out, uint32_t flags);
+
+/* The reference's per-packet loop (hadooprpc.c:733-742) on one host packet:
+ * out receives ceil(len / bpc) checksums.  Uses the process-wide default
+ * context (device 0, or $HDFS_CRC32C_DEVICE), created on first use. */
+int crc32c_chunks(const void *packet, size_t len, uint32_t bpc, uint32_t *out, uint32_t flags);
+
+/* ---------------------------------------------------------------------------
+ * 5. Several GPUs of one node, one process.  Packets are sharded in groups of
+ * `group_packets` consecutive packets (64 = one 4 MiB HDFS block of 64 KiB
+ * packets) dealt round-robin over the devices; each device checksums its
+ * shard and copies its checksums straight into the host `out` array.
+ * ------------------------------------------------------------------------- */
+typedef struct crc32c_multi crc32c_multi;
+
+int crc32c_multi_create(const int *devices, int ndevices, crc32c_multi **out);
+int crc32c_multi_destroy(crc32c_multi *m);
+int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                            uint32_t group_packets, uint32_t *out, uint32_t flags);
+
+/* Last error text of the calling thread (static storage, never NULL). */
+const char *crc32c_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HDFS_CRC32C_H */

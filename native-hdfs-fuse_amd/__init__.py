@@ -1,0 +1,275 @@
+"""Python view of libhdfs_crc32c.so -- the MI355X CRC32C chunk path of
+native-hdfs-fuse, behind the C ABI in ``include/hdfs_crc32c.h``.
+
+The reference is a C program; its interface for this path is the C function
+``crc32c(crc, buf, len)`` (``src/crc32c.c:333``) called once per chunk by
+``hadoop_rpc_send_packet`` (``src/hadooprpc.c:733-742``).  This module is a
+thin ctypes mirror of the C ABI used by the tests and the bench; the product
+is the shared library.  No CPU fallback exists for the GPU entry points: if
+the library cannot reach a gfx950 device they raise ``Crc32cError``.
+
+Device buffers are passed as raw pointers (``tensor.data_ptr()`` when the
+caller uses torch for allocation) and streams as raw ``hipStream_t`` handles
+(``torch.cuda.current_stream().cuda_stream``).
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhdfs_crc32c.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
+
+CRC32C_BIG_ENDIAN = 0x1
+
+PACKET_DTYPE = np.dtype(
+    [("payload_off", "<u8"), ("out_idx", "<u8"), ("len", "<u4"), ("bpc", "<u4")], align=True
+)
+TILE_DTYPE = np.dtype([("src", "<u8"), ("out", "<u4"), ("meta", "<u4")])
+GEN_DTYPE = np.dtype([("src", "<u8"), ("out", "<u4"), ("len", "<u4")])
+
+
+class Crc32cError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__("%s (rc=%d %s)" % (msg, rc, errno.errorcode.get(-rc, "?")))
+        self.rc = rc
+
+
+def build(quiet: bool = True) -> str:
+    """Compile the library in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+    out = subprocess.DEVNULL if quiet else None
+    jobs = str(min(8, os.cpu_count() or 1))
+    subprocess.run(["make", "-C", HERE, "-j" + jobs], check=True, stdout=out)
+    return LIB_PATH
+
+
+_LIB = None
+
+
+def lib():
+    """Load (not build) the shared library; raises if it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(LIB_PATH + " is not built (run build())")
+        _LIB = _bind(ctypes.CDLL(LIB_PATH))
+    return _LIB
+
+
+def _bind(L):
+    u32, u64, i32, vp, sz = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    pp = ctypes.POINTER(vp)
+    sig = {
+        "crc32c": (u32, [u32, vp, sz]),
+        "crc32c_nchunks": (u64, [u64, u32]),
+        "crc32c_packetize": (u64, [u64, u64, u32, u32, vp, u64]),
+        "crc32c_device_count": (i32, []),
+        "crc32c_ctx_create": (i32, [i32, pp]),
+        "crc32c_ctx_destroy": (i32, [vp]),
+        "crc32c_plan_create": (i32, [vp, vp, sz, u32, pp]),
+        "crc32c_plan_exec": (i32, [vp, vp, vp, vp]),
+        "crc32c_plan_destroy": (i32, [vp]),
+        "crc32c_plan_nchecksums": (u64, [vp]),
+        "crc32c_plan_payload_bytes": (u64, [vp]),
+        "crc32c_chunks_dev": (i32, [vp, vp, sz, vp, vp, u32, vp]),
+        "crc32c_batch_host": (i32, [vp, vp, vp, sz, vp, u32]),
+        "crc32c_chunks": (i32, [vp, sz, u32, vp, u32]),
+        "crc32c_multi_create": (i32, [vp, i32, pp]),
+        "crc32c_multi_destroy": (i32, [vp]),
+        "crc32c_multi_batch_host": (i32, [vp, vp, vp, sz, u32, vp, u32]),
+        "crc32c_last_error": (ctypes.c_char_p, []),
+        "crc32c_debug_plan": (i32, [vp, sz, vp, sz, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "crc32c_debug_lds_image": (sz, [vp, sz, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise Crc32cError(rc, "%s: %s" % (what, lib().crc32c_last_error().decode(errors="replace")))
+
+
+def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def as_packets(pkts) -> np.ndarray:
+    return np.ascontiguousarray(pkts, dtype=PACKET_DTYPE)
+
+
+# --- 1. drop-in scalar (host CPU, identical to src/crc32c.c:333) ----------
+def crc32c(data, crc: int = 0) -> int:
+    a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
+    return int(lib().crc32c(crc & 0xFFFFFFFF, _np_ptr(a), a.nbytes))
+
+
+def nchunks(length: int, bpc: int) -> int:
+    return int(lib().crc32c_nchunks(length, bpc))
+
+
+def packetize(length: int, blockoffset: int, packetsize: int, bpc: int) -> list:
+    n = int(lib().crc32c_packetize(length, blockoffset, packetsize, bpc, None, 0))
+    lens = np.zeros(max(n, 1), np.uint64)
+    lib().crc32c_packetize(length, blockoffset, packetsize, bpc, _np_ptr(lens), n)
+    return [int(x) for x in lens[:n]]
+
+
+def device_count() -> int:
+    return int(lib().crc32c_device_count())
+
+
+# --- 2-4. GPU context, plans, host batches --------------------------------
+class Context:
+    """One HIP device (crc32c_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib().crc32c_ctx_create(device, ctypes.byref(h)), "crc32c_ctx_create")
+        self.handle = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.handle:
+            lib().crc32c_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def plan(self, pkts, flags: int = 0) -> "Plan":
+        return Plan(self, pkts, flags)
+
+    def batch_host(self, payload: np.ndarray, pkts, flags: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+        """Host-resident batch: pinned H2D -> kernel -> D2H (crc32c_batch_host)."""
+        pkts = as_packets(pkts)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        n = total_checksums(pkts)
+        if out is None:
+            out = np.zeros(max(n, 1), np.uint32)
+        _check(lib().crc32c_batch_host(self.handle, _np_ptr(payload), _np_ptr(pkts), pkts.size, _np_ptr(out), flags),
+               "crc32c_batch_host")
+        return out[:n]
+
+    def chunks_dev(self, pkts, dev_payload: int, dev_out: int, flags: int = 0, stream: int = 0) -> None:
+        pkts = as_packets(pkts)
+        _check(lib().crc32c_chunks_dev(self.handle, _np_ptr(pkts), pkts.size, ctypes.c_void_p(dev_payload),
+                                       ctypes.c_void_p(dev_out), flags, ctypes.c_void_p(stream)), "crc32c_chunks_dev")
+
+
+class Plan:
+    """Device-resident batch plan (crc32c_plan): build once, execute many."""
+
+    def __init__(self, ctx: Context, pkts, flags: int = 0):
+        pkts = as_packets(pkts)
+        h = ctypes.c_void_p()
+        _check(lib().crc32c_plan_create(ctx.handle, _np_ptr(pkts), pkts.size, flags, ctypes.byref(h)),
+               "crc32c_plan_create")
+        self.ctx = ctx  # keeps the context alive
+        self.handle = h
+        self.nchecksums = int(lib().crc32c_plan_nchecksums(h))
+        self.payload_bytes = int(lib().crc32c_plan_payload_bytes(h))
+
+    def exec(self, dev_payload: int, dev_out: int, stream: int = 0) -> None:
+        _check(lib().crc32c_plan_exec(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
+                                      ctypes.c_void_p(stream)), "crc32c_plan_exec")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().crc32c_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Multi:
+    """Several GPUs of one node in one process (crc32c_multi)."""
+
+    def __init__(self, devices):
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = ctypes.c_void_p()
+        _check(lib().crc32c_multi_create(devs, len(devices), ctypes.byref(h)), "crc32c_multi_create")
+        self.handle = h
+
+    def batch_host(self, payload: np.ndarray, pkts, group_packets: int = 64, flags: int = 0) -> np.ndarray:
+        pkts = as_packets(pkts)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        n = total_checksums(pkts)
+        out = np.zeros(max(n, 1), np.uint32)
+        _check(lib().crc32c_multi_batch_host(self.handle, _np_ptr(payload), _np_ptr(pkts), pkts.size, group_packets,
+                                             _np_ptr(out), flags), "crc32c_multi_batch_host")
+        return out[:n]
+
+    def close(self) -> None:
+        if self.handle:
+            lib().crc32c_multi_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def chunks(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:
+    """The reference's per-packet loop on one host packet, on the default GPU context."""
+    packet = np.ascontiguousarray(packet, dtype=np.uint8)
+    n = nchunks(packet.size, bpc)
+    out = np.zeros(max(n, 1), np.uint32)
+    _check(lib().crc32c_chunks(_np_ptr(packet), packet.size, bpc, _np_ptr(out), flags), "crc32c_chunks")
+    return out[:n]
+
+
+# --- helpers ----------------------------------------------------------------
+def total_checksums(pkts) -> int:
+    pkts = as_packets(pkts)
+    live = pkts[pkts["len"] > 0]
+    if live.size == 0:
+        return 0
+    per = (live["len"].astype(np.uint64) + live["bpc"].astype(np.uint64) - 1) // live["bpc"].astype(np.uint64)
+    return int((live["out_idx"] + per).max())
+
+
+def debug_plan(pkts):
+    """Work items a plan would upload (FastTile / GenItem arrays)."""
+    pkts = as_packets(pkts)
+    nt, ng = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().crc32c_debug_plan(_np_ptr(pkts), pkts.size, None, 0, None, 0, ctypes.byref(nt), ctypes.byref(ng)),
+           "crc32c_debug_plan")
+    tiles = np.zeros(max(nt.value, 1), TILE_DTYPE)
+    gen = np.zeros(max(ng.value, 1), GEN_DTYPE)
+    _check(lib().crc32c_debug_plan(_np_ptr(pkts), pkts.size, _np_ptr(tiles), nt.value, _np_ptr(gen), ng.value,
+                                   ctypes.byref(nt), ctypes.byref(ng)), "crc32c_debug_plan")
+    return tiles[: nt.value], gen[: ng.value]
+
+
+def debug_lds_image():
+    """The kernel's LDS image and affine constants (c_lg[5], c_small[4])."""
+    n = int(lib().crc32c_debug_lds_image(None, 0, None, None))
+    img = np.zeros(n, np.uint8)
+    c_lg = np.zeros(5, np.uint32)
+    c_small = np.zeros(4, np.uint32)
+    lib().crc32c_debug_lds_image(_np_ptr(img), n, _np_ptr(c_lg), _np_ptr(c_small))
+    return img, c_lg, c_small

@@ -1,0 +1,135 @@
+// cpu_crc32c.cpp -- the drop-in scalar export `crc32c(crc, buf, len)`.
+//
+// Replaces src/crc32c.c:333-343 with identical semantics: `crc` is a finished
+// CRC32C (pre-inverted on entry, post-inverted on exit, crc32c.c:237/312),
+// any alignment, len == 0 returns crc, thread-safe, cannot fail.  It is the
+// host path for single calls; batches go to the GPU (crc32c_gpu.hip).
+//
+// Two host implementations, chosen once by CPUID:
+//  * SSE4.2 `crc32` instruction; buffers >= 3 * kStripe bytes run three
+//    independent register chains over three consecutive stripes and merge
+//    them with a precomputed "append kStripe zero bytes" operator
+//    (crc32c.c:249-289 uses the same idea with two fixed stripe sizes).
+//  * portable slicing-by-8 tables (crc32c.c:78-107's fallback role).
+#include <cstring>
+#include <mutex>
+
+#include "crc_math.h"
+#include "hdfs_crc32c.h"
+
+namespace {
+
+using hdfs_crc::Gf2Op;
+
+constexpr size_t kStripe = 1024;
+
+uint32_t g_slice[8][256];
+uint32_t g_stripe_shift[4][256];  // Z^kStripe applied to byte k of a register
+bool g_have_sse42 = false;
+std::once_flag g_once;
+
+void init_once() {
+    const uint32_t *t0 = hdfs_crc::byte_table();
+    for (int b = 0; b < 256; ++b) {
+        g_slice[0][b] = t0[b];
+        for (int k = 1; k < 8; ++k) g_slice[k][b] = (g_slice[k - 1][b] >> 8) ^ t0[g_slice[k - 1][b] & 0xffu];
+    }
+    const Gf2Op z = hdfs_crc::op_zeros(kStripe);
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b) g_stripe_shift[k][b] = z.apply(b << (8 * k));
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_cpu_init();
+    g_have_sse42 = __builtin_cpu_supports("sse4.2");
+#endif
+}
+
+inline uint32_t stripe_shift(uint32_t r) {
+    return g_stripe_shift[0][r & 0xff] ^ g_stripe_shift[1][(r >> 8) & 0xff] ^ g_stripe_shift[2][(r >> 16) & 0xff] ^
+           g_stripe_shift[3][r >> 24];
+}
+
+// Register update over raw bytes (no conditioning), portable.
+uint32_t reg_update_sw(uint32_t r, const uint8_t *p, size_t n) {
+    for (; n && (reinterpret_cast<uintptr_t>(p) & 7u); --n) r = (r >> 8) ^ g_slice[0][(r ^ *p++) & 0xffu];
+    for (; n >= 8; n -= 8, p += 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        w ^= r;
+        r = g_slice[7][w & 0xff] ^ g_slice[6][(w >> 8) & 0xff] ^ g_slice[5][(w >> 16) & 0xff] ^
+            g_slice[4][(w >> 24) & 0xff] ^ g_slice[3][(w >> 32) & 0xff] ^ g_slice[2][(w >> 40) & 0xff] ^
+            g_slice[1][(w >> 48) & 0xff] ^ g_slice[0][w >> 56];
+    }
+    for (; n; --n) r = (r >> 8) ^ g_slice[0][(r ^ *p++) & 0xffu];
+    return r;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("sse4.2"))) uint32_t reg_update_hw(uint32_t r32, const uint8_t *p, size_t n) {
+    uint64_t r = r32;
+    for (; n && (reinterpret_cast<uintptr_t>(p) & 7u); --n) r = __builtin_ia32_crc32qi(uint32_t(r), *p++);
+    while (n >= 3 * kStripe) {
+        uint64_t a = r, b = 0, c = 0;
+        const uint8_t *pa = p, *pb = p + kStripe, *pc = p + 2 * kStripe;
+        for (size_t i = 0; i < kStripe; i += 8) {
+            uint64_t wa, wb, wc;
+            std::memcpy(&wa, pa + i, 8);
+            std::memcpy(&wb, pb + i, 8);
+            std::memcpy(&wc, pc + i, 8);
+            a = __builtin_ia32_crc32di(a, wa);
+            b = __builtin_ia32_crc32di(b, wb);
+            c = __builtin_ia32_crc32di(c, wc);
+        }
+        r = stripe_shift(stripe_shift(uint32_t(a)) ^ uint32_t(b)) ^ uint32_t(c);
+        p += 3 * kStripe;
+        n -= 3 * kStripe;
+    }
+    for (; n >= 8; n -= 8, p += 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        r = __builtin_ia32_crc32di(r, w);
+    }
+    for (; n; --n) r = __builtin_ia32_crc32qi(uint32_t(r), *p++);
+    return uint32_t(r);
+}
+#endif
+
+}  // namespace
+
+extern "C" uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
+    std::call_once(g_once, init_once);
+    const uint8_t *p = static_cast<const uint8_t *>(buf);
+    uint32_t r = ~crc;
+#if defined(__x86_64__)
+    if (g_have_sse42) return ~reg_update_hw(r, p, len);
+#endif
+    return ~reg_update_sw(r, p, len);
+}
+
+extern "C" uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc) {
+    // roundup(len, bpc) (hadooprpc.c:639, roundup.h:7-11).
+    return bpc ? (len + bpc - 1) / bpc : 0;
+}
+
+extern "C" uint64_t crc32c_packetize(uint64_t len, uint64_t blockoffset, uint32_t packetsize, uint32_t bpc,
+                                     uint64_t *lens, uint64_t max) {
+    // hadooprpc.c:827-857.  A packet that would start off a chunk boundary
+    // only finishes that chunk (832-840); a zero-length packet ends the
+    // block (644, 853-856).
+    if (bpc == 0 || packetsize == 0) return 0;
+    uint64_t sent = 0, n = 0;
+    for (;;) {
+        uint64_t plen = len - sent < packetsize ? len - sent : packetsize;
+        const uint64_t past = (blockoffset + sent) % bpc;
+        if (plen > 0 && past != 0) {
+            plen = bpc - past;
+            // The reference only asserts that the trimmed packet fits the
+            // remaining bytes (hadooprpc.c:622); clamp instead of overrunning.
+            if (plen > len - sent) plen = len - sent;
+        }
+        if (lens && n < max) lens[n] = plen;
+        ++n;
+        if (plen == 0) break;
+        sent += plen;
+    }
+    return n;
+}

@@ -1,0 +1,486 @@
+// crc32c_runtime.hip -- host side of the C ABI (include/hdfs_crc32c.h):
+// device contexts, batch plans, the host-resident staging pipeline and the
+// one-process multi-GPU driver.  Every GPU entry point returns 0 or -errno
+// and never substitutes a CPU computation: no GPU => -ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "crc_math.h"
+#include "hdfs_crc32c.h"
+#include "kernel_abi.h"
+#include "plan.h"
+
+using namespace hdfs_crc;
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                                   \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) return fail(-EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                                          __LINE__);                                                    \
+    } while (0)
+
+// Restores the caller's current device (torch and other libraries keep their own).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr size_t kSliceBytes = 32ull << 20;  // host pipeline slice (whole packets)
+
+struct Stage {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint8_t *h_payload = nullptr, *d_payload = nullptr;
+    size_t payload_cap = 0;
+    uint8_t *h_desc = nullptr, *d_desc = nullptr;
+    size_t desc_cap = 0;
+    uint32_t *h_out = nullptr, *d_out = nullptr;
+    size_t out_cap = 0;
+    bool pending = false;
+    // packets of the slice in flight: (global out_idx, local out index, count)
+    std::vector<uint64_t> scatter;
+};
+
+}  // namespace
+
+struct crc32c_ctx {
+    int device = 0;
+    int num_cu = 0;
+    uint8_t *d_table = nullptr;
+    uint32_t c_lg[5];
+    uint32_t c_small[4];
+    std::mutex mu;
+    Stage stage[2];
+};
+
+struct crc32c_plan {
+    crc32c_ctx *ctx = nullptr;
+    FastTile *d_tiles = nullptr;
+    GenItem *d_gen = nullptr;
+    uint32_t ntiles = 0, ngen = 0;
+    uint64_t nchecksums = 0, payload_bytes = 0;
+    uint32_t flags = 0;
+};
+
+struct crc32c_multi {
+    std::vector<crc32c_ctx *> ctxs;
+};
+
+namespace {
+
+uint32_t grid_for(const crc32c_ctx *ctx, uint64_t items) {
+    const uint64_t waves_per_wg = kKernelThreads / 64;
+    uint64_t g = (items + waves_per_wg - 1) / waves_per_wg;
+    const uint64_t cap = uint64_t(ctx->num_cu) * kKernelWgPerCu;
+    if (g > cap) g = cap;
+    return uint32_t(g ? g : 1);
+}
+
+KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
+                   const void *payload, uint32_t *out, uint32_t flags) {
+    KParams p;
+    p.tiles = static_cast<const FastTile *>(tiles);
+    p.gen = static_cast<const GenItem *>(gen);
+    p.payload = static_cast<const uint8_t *>(payload);
+    p.out = out;
+    p.table = ctx->d_table;
+    p.ntiles = ntiles;
+    p.ngen = ngen;
+    p.flags = flags;
+    std::memcpy(p.c_lg, ctx->c_lg, sizeof p.c_lg);
+    std::memcpy(p.c_small, ctx->c_small, sizeof p.c_small);
+    return p;
+}
+
+int launch(const crc32c_ctx *ctx, const KParams &p, hipStream_t stream) {
+    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
+    if (!items) return 0;
+    HIP_TRY(launch_plan_kernel(p, grid_for(ctx, items), stream));
+    return 0;
+}
+
+int check_packets(const crc32c_packet *pkts, size_t npkts) {
+    if (npkts && !pkts) return fail(-EINVAL, "packets == NULL");
+    for (size_t i = 0; i < npkts; ++i)
+        if (pkts[i].bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
+    return 0;
+}
+
+template <class T>
+int grow_pinned_pair(T **h, T **d, size_t *cap, size_t need) {
+    if (*cap >= need) return 0;
+    if (*h) (void)hipHostFree(*h);
+    if (*d) (void)hipFree(*d);
+    *h = nullptr;
+    *d = nullptr;
+    *cap = 0;
+    size_t c = std::max(need, size_t(4096));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(h), c * sizeof(T), hipHostMallocDefault));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(d), c * sizeof(T)));
+    *cap = c;
+    return 0;
+}
+
+void free_stage(Stage &s) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.h_payload) (void)hipHostFree(s.h_payload);
+    if (s.d_payload) (void)hipFree(s.d_payload);
+    if (s.h_desc) (void)hipHostFree(s.h_desc);
+    if (s.d_desc) (void)hipFree(s.d_desc);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Stage();
+}
+
+// Completes the slice in flight on `s`: wait, then scatter its checksums.
+int drain_stage(Stage &s, uint32_t *out) {
+    if (!s.pending) return 0;
+    s.pending = false;
+    HIP_TRY(hipEventSynchronize(s.done));
+    for (size_t i = 0; i + 2 < s.scatter.size(); i += 3)
+        std::memcpy(out + s.scatter[i], s.h_out + s.scatter[i + 1], s.scatter[i + 2] * sizeof(uint32_t));
+    s.scatter.clear();
+    return 0;
+}
+
+bool is_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// Host-resident batch on one context (caller holds ctx->mu).
+int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_packet *pkts, size_t npkts,
+                      uint32_t *out, uint32_t flags) {
+    DeviceGuard guard(ctx->device);
+    for (Stage &s : ctx->stage) {
+        if (!s.stream) {
+            HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        }
+    }
+    const bool pinned = npkts && is_pinned(payload);
+    size_t i = 0;
+    int which = 0;
+    std::vector<crc32c_packet> local;
+    HostPlan plan;
+    while (i < npkts) {
+        // Slice = consecutive packets totalling about kSliceBytes.
+        size_t j = i;
+        uint64_t bytes = 0, lo = UINT64_MAX, hi = 0;
+        while (j < npkts && (j == i || bytes + pkts[j].len <= kSliceBytes)) {
+            bytes += pkts[j].len;
+            if (pkts[j].len) {
+                lo = std::min<uint64_t>(lo, pkts[j].payload_off);
+                hi = std::max<uint64_t>(hi, pkts[j].payload_off + pkts[j].len);
+            }
+            ++j;
+        }
+        Stage &s = ctx->stage[which];
+        int rc = drain_stage(s, out);
+        if (rc) return rc;
+        if (lo == UINT64_MAX) lo = hi = 0;
+        lo &= ~uint64_t(15);  // keep every packet's 16-byte phase (fast-path alignment)
+        // Contiguous-enough slices move as one range (direct from pinned
+        // memory, else through the pinned staging buffer); scattered
+        // packets are gathered packet by packet into the staging buffer.
+        const bool ranged = (hi - lo) <= bytes + bytes / 4 + 4096;
+        const size_t stage_bytes = ranged ? size_t(hi - lo) : size_t(bytes + 16 * (j - i));
+        rc = grow_pinned_pair(&s.h_payload, &s.d_payload, &s.payload_cap, stage_bytes + 16);
+        if (rc) return rc;
+        local.assign(pkts + i, pkts + j);
+        uint64_t nout = 0, gather_off = 0;
+        s.scatter.clear();
+        for (size_t k = 0; k < local.size(); ++k) {
+            const uint64_t n = crc32c_nchunks(local[k].len, local[k].bpc);
+            if (ranged) {
+                local[k].payload_off -= lo;
+            } else {
+                std::memcpy(s.h_payload + gather_off, payload + pkts[i + k].payload_off, local[k].len);
+                local[k].payload_off = gather_off;
+                gather_off = (gather_off + local[k].len + 15) & ~uint64_t(15);
+            }
+            s.scatter.push_back(pkts[i + k].out_idx);
+            s.scatter.push_back(nout);
+            s.scatter.push_back(n);
+            local[k].out_idx = nout;
+            nout += n;
+        }
+        rc = build_plan(local.data(), local.size(), &plan);
+        if (rc) return fail(rc, "invalid packet in batch");
+        const size_t desc_bytes = (plan.tiles.size() + plan.gen.size()) * 16;
+        rc = grow_pinned_pair(&s.h_desc, &s.d_desc, &s.desc_cap, desc_bytes + 16);
+        if (rc) return rc;
+        rc = grow_pinned_pair(&s.h_out, &s.d_out, &s.out_cap, size_t(nout) + 1);
+        if (rc) return rc;
+        std::memcpy(s.h_desc, plan.tiles.data(), plan.tiles.size() * 16);
+        std::memcpy(s.h_desc + plan.tiles.size() * 16, plan.gen.data(), plan.gen.size() * 16);
+        const uint8_t *src = s.h_payload;
+        if (ranged) {
+            if (pinned)
+                src = payload + lo;
+            else
+                std::memcpy(s.h_payload, payload + lo, size_t(hi - lo));
+        }
+        HIP_TRY(hipMemcpyAsync(s.d_payload, src, stage_bytes, hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, desc_bytes, hipMemcpyHostToDevice, s.stream));
+        const KParams p = params_for(ctx, s.d_desc, uint32_t(plan.tiles.size()), s.d_desc + plan.tiles.size() * 16,
+                                     uint32_t(plan.gen.size()), s.d_payload, s.d_out, flags);
+        rc = launch(ctx, p, s.stream);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nout * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
+        HIP_TRY(hipEventRecord(s.done, s.stream));
+        s.pending = true;
+        which ^= 1;
+        i = j;
+    }
+    for (Stage &s : ctx->stage) {
+        int rc = drain_stage(s, out);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+std::once_flag g_default_once;
+crc32c_ctx *g_default_ctx = nullptr;
+int g_default_rc = 0;
+
+}  // namespace
+
+extern "C" {
+
+const char *crc32c_last_error(void) { return g_err; }
+
+int crc32c_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int crc32c_ctx_create(int device, crc32c_ctx **out) {
+    if (!out) return fail(-EINVAL, "out == NULL");
+    *out = nullptr;
+    const int ndev = crc32c_device_count();
+    if (ndev <= 0) return fail(-ENODEV, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(-ENODEV, "device %d out of range (%d visible)", device, ndev);
+    std::unique_ptr<crc32c_ctx> c(new crc32c_ctx);
+    c->device = device;
+    DeviceGuard guard(device);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
+    c->num_cu = prop.multiProcessorCount;
+    std::vector<uint8_t> img(kLdsBytes);
+    build_lds_image(img.data());
+    affine_constants(c->c_lg, c->c_small);
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table), kLdsBytes));
+    HIP_TRY(hipMemcpy(c->d_table, img.data(), kLdsBytes, hipMemcpyHostToDevice));
+    *out = c.release();
+    return 0;
+}
+
+int crc32c_ctx_destroy(crc32c_ctx *ctx) {
+    if (!ctx) return 0;
+    {
+        DeviceGuard guard(ctx->device);
+        for (Stage &s : ctx->stage) free_stage(s);
+        if (ctx->d_table) (void)hipFree(ctx->d_table);
+    }
+    delete ctx;
+    return 0;
+}
+
+int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, uint32_t flags,
+                       crc32c_plan **out) {
+    if (!ctx || !out) return fail(-EINVAL, "ctx/out == NULL");
+    *out = nullptr;
+    int rc = check_packets(pkts, npkts);
+    if (rc) return rc;
+    HostPlan hp;
+    rc = build_plan(pkts, npkts, &hp);
+    if (rc) return fail(rc, "invalid packet batch");
+    if (hp.tiles.size() > UINT32_MAX || hp.gen.size() > UINT32_MAX) return fail(-E2BIG, "batch too large");
+    std::unique_ptr<crc32c_plan> p(new crc32c_plan);
+    p->ctx = ctx;
+    p->ntiles = uint32_t(hp.tiles.size());
+    p->ngen = uint32_t(hp.gen.size());
+    p->nchecksums = hp.nchecksums;
+    p->payload_bytes = hp.payload_bytes;
+    p->flags = flags;
+    DeviceGuard guard(ctx->device);
+    if (p->ntiles) {
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p->d_tiles), hp.tiles.size() * sizeof(FastTile)));
+        HIP_TRY(hipMemcpy(p->d_tiles, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile), hipMemcpyHostToDevice));
+    }
+    if (p->ngen) {
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p->d_gen), hp.gen.size() * sizeof(GenItem)));
+        HIP_TRY(hipMemcpy(p->d_gen, hp.gen.data(), hp.gen.size() * sizeof(GenItem), hipMemcpyHostToDevice));
+    }
+    *out = p.release();
+    return 0;
+}
+
+int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out, void *stream) {
+    if (!plan) return fail(-EINVAL, "plan == NULL");
+    if (plan->nchecksums == 0) return 0;
+    if (!dev_payload || !dev_out) return fail(-EINVAL, "payload/out == NULL");
+    if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
+        return fail(-EINVAL, "device payload must be 16-byte aligned");
+    DeviceGuard guard(plan->ctx->device);
+    const KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload,
+                                 dev_out, plan->flags);
+    return launch(plan->ctx, p, static_cast<hipStream_t>(stream));
+}
+
+int crc32c_plan_destroy(crc32c_plan *plan) {
+    if (!plan) return 0;
+    {
+        DeviceGuard guard(plan->ctx->device);
+        if (plan->d_tiles) (void)hipFree(plan->d_tiles);
+        if (plan->d_gen) (void)hipFree(plan->d_gen);
+    }
+    delete plan;
+    return 0;
+}
+
+uint64_t crc32c_plan_nchecksums(const crc32c_plan *plan) { return plan ? plan->nchecksums : 0; }
+uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan) { return plan ? plan->payload_bytes : 0; }
+
+int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,
+                      uint32_t *dev_out, uint32_t flags, void *stream) {
+    crc32c_plan *plan = nullptr;
+    int rc = crc32c_plan_create(ctx, pkts, npkts, flags, &plan);
+    if (rc) return rc;
+    rc = crc32c_plan_exec(plan, dev_payload, dev_out, stream);
+    if (!rc) {
+        DeviceGuard guard(ctx->device);
+        hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+        if (e != hipSuccess) rc = fail(-EIO, "hipStreamSynchronize: %s", hipGetErrorString(e));
+    }
+    crc32c_plan_destroy(plan);
+    return rc;
+}
+
+int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                      uint32_t *out, uint32_t flags) {
+    if (!ctx) return fail(-EINVAL, "ctx == NULL");
+    int rc = check_packets(pkts, npkts);
+    if (rc) return rc;
+    if (npkts && (!payload || !out)) return fail(-EINVAL, "payload/out == NULL");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    rc = batch_host_locked(ctx, static_cast<const uint8_t *>(payload), pkts, npkts, out, flags);
+    if (rc) {
+        for (Stage &s : ctx->stage) {
+            s.pending = false;
+            s.scatter.clear();
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+        }
+    }
+    return rc;
+}
+
+int crc32c_chunks(const void *packet, size_t len, uint32_t bpc, uint32_t *out, uint32_t flags) {
+    if (bpc == 0) return fail(-EINVAL, "bytesPerChecksum == 0");
+    if (len == 0) return 0;
+    if (len > UINT32_MAX) return fail(-EINVAL, "packet too large");
+    std::call_once(g_default_once, [] {
+        const char *env = std::getenv("HDFS_CRC32C_DEVICE");
+        g_default_rc = crc32c_ctx_create(env ? std::atoi(env) : 0, &g_default_ctx);
+    });
+    if (g_default_rc) return fail(g_default_rc, "default GPU context unavailable");
+    crc32c_packet p;
+    p.payload_off = 0;
+    p.out_idx = 0;
+    p.len = uint32_t(len);
+    p.bpc = bpc;
+    return crc32c_batch_host(g_default_ctx, packet, &p, 1, out, flags);
+}
+
+int crc32c_multi_create(const int *devices, int ndevices, crc32c_multi **out) {
+    if (!out || ndevices <= 0) return fail(-EINVAL, "bad arguments");
+    *out = nullptr;
+    std::unique_ptr<crc32c_multi> m(new crc32c_multi);
+    for (int i = 0; i < ndevices; ++i) {
+        crc32c_ctx *c = nullptr;
+        const int rc = crc32c_ctx_create(devices ? devices[i] : i, &c);
+        if (rc) {
+            for (crc32c_ctx *x : m->ctxs) crc32c_ctx_destroy(x);
+            return rc;
+        }
+        m->ctxs.push_back(c);
+    }
+    *out = m.release();
+    return 0;
+}
+
+int crc32c_multi_destroy(crc32c_multi *m) {
+    if (!m) return 0;
+    for (crc32c_ctx *c : m->ctxs) crc32c_ctx_destroy(c);
+    delete m;
+    return 0;
+}
+
+int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                            uint32_t group_packets, uint32_t *out, uint32_t flags) {
+    if (!m || m->ctxs.empty()) return fail(-EINVAL, "multi == NULL");
+    int rc = check_packets(pkts, npkts);
+    if (rc) return rc;
+    if (group_packets == 0) group_packets = 64;
+    const size_t g = m->ctxs.size();
+    // Groups of consecutive packets (an HDFS block's worth) dealt round-robin.
+    std::vector<std::vector<crc32c_packet>> shard(g);
+    for (size_t i = 0; i < npkts; ++i) shard[(i / group_packets) % g].push_back(pkts[i]);
+    std::vector<int> rcs(g, 0);
+    std::vector<std::string> errs(g);
+    std::vector<std::thread> th;
+    for (size_t d = 0; d < g; ++d)
+        th.emplace_back([&, d] {
+            rcs[d] = crc32c_batch_host(m->ctxs[d], payload, shard[d].data(), shard[d].size(), out, flags);
+            if (rcs[d]) errs[d] = crc32c_last_error();
+        });
+    for (auto &t : th) t.join();
+    for (size_t d = 0; d < g; ++d)
+        if (rcs[d]) return fail(rcs[d], "device %d: %s", m->ctxs[d]->device, errs[d].c_str());
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// crc_math.cpp -- see crc_math.h.
+#include "crc_math.h"
+
+#include <cstring>
+#include <mutex>
+
+namespace hdfs_crc {
+
+namespace {
+uint32_t g_t0[256];
+std::once_flag g_t0_once;
+
+void init_t0() {
+    // Eight reflected shift/xor steps per byte value (crc32c.c:54-65).
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t r = b;
+        for (int i = 0; i < 8; ++i) r = (r >> 1) ^ (kPoly & (0u - (r & 1u)));
+        g_t0[b] = r;
+    }
+}
+}  // namespace
+
+const uint32_t *byte_table() {
+    std::call_once(g_t0_once, init_t0);
+    return g_t0;
+}
+
+uint32_t append_zero_byte(uint32_t reg) {
+    const uint32_t *t = byte_table();
+    return (reg >> 8) ^ t[reg & 0xffu];
+}
+
+Gf2Op op_identity() {
+    Gf2Op o;
+    for (int j = 0; j < 32; ++j) o.col[j] = 1u << j;
+    return o;
+}
+
+Gf2Op op_compose(const Gf2Op &a, const Gf2Op &b) {
+    Gf2Op o;
+    for (int j = 0; j < 32; ++j) o.col[j] = a.apply(b.col[j]);
+    return o;
+}
+
+Gf2Op op_zeros(uint64_t nbytes) {
+    // Square-and-multiply on the one-zero-byte operator.
+    Gf2Op step, acc = op_identity();
+    for (int j = 0; j < 32; ++j) step.col[j] = append_zero_byte(1u << j);
+    while (nbytes) {
+        if (nbytes & 1u) acc = op_compose(step, acc);
+        step = op_compose(step, step);
+        nbytes >>= 1;
+    }
+    return acc;
+}
+
+uint32_t lin_bytes(const uint8_t *p, size_t n, uint32_t reg) {
+    const uint32_t *t = byte_table();
+    for (size_t i = 0; i < n; ++i) reg = (reg >> 8) ^ t[(reg ^ p[i]) & 0xffu];
+    return reg;
+}
+
+void build_lds_image(uint8_t *dst) {
+    std::memset(dst, 0, kLdsBytes);
+    const uint32_t *t0 = byte_table();
+    // vals[x] = lin(x followed by d zero bytes) for the 32 nibble-basis bytes
+    // (x = n for low nibbles, x = n << 4 for high nibbles), walked from d = 0
+    // up to d = 511.  The byte at block offset o is followed by d = 511 - o.
+    uint32_t lo[16], hi[16];
+    for (int n = 0; n < 16; ++n) {
+        lo[n] = t0[n];
+        hi[n] = t0[n << 4];
+    }
+    auto put = [&](size_t off, uint32_t v) { std::memcpy(dst + off, &v, 4); };
+    for (int d = 0; d < 512; ++d) {
+        const int o = 511 - d;       // block offset of the byte
+        const int q = o >> 4;        // lane column
+        const int k = o & 15;        // byte within the lane's 16-byte piece
+        for (int n = 0; n < 16; ++n) {
+            put(size_t(k) * 4096 + size_t(n) * 256 + size_t(q) * 4, lo[n]);
+            put(128 + size_t(k) * 256 + size_t(n) * 4096 + size_t(q) * 4, hi[n]);
+        }
+        for (int n = 0; n < 16; ++n) {
+            lo[n] = append_zero_byte(lo[n]);
+            hi[n] = append_zero_byte(hi[n]);
+        }
+    }
+    const Gf2Op z512 = op_zeros(512);
+    Gf2Op zs = z512;
+    for (int s = 1; s <= kMaxShift; ++s) {
+        for (int tn = 0; tn < 8; ++tn)
+            for (uint32_t n = 0; n < 16; ++n)
+                put(kLdsShiftOff + size_t(s - 1) * 512 + size_t(tn) * 64 + n * 4, zs.apply(n << (4 * tn)));
+        zs = op_compose(z512, zs);
+    }
+}
+
+void affine_constants(uint32_t c_lg[5], uint32_t c_small[4]) {
+    // crc32c(0, zeros(n)) = Z^n(0xffffffff) ^ 0xffffffff (crc32c.c:237, 312).
+    for (int lg = 0; lg < 5; ++lg) c_lg[lg] = op_zeros(512ull << lg).apply(0xffffffffu) ^ 0xffffffffu;
+    for (int r = 0; r < 4; ++r) c_small[r] = op_zeros(r).apply(0xffffffffu) ^ 0xffffffffu;
+}
+
+}  // namespace hdfs_crc

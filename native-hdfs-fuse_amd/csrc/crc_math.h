@@ -1,0 +1,58 @@
+// crc_math.h -- host-side GF(2) machinery for CRC32C (Castagnoli, reflected).
+//
+// Everything the GPU needs that is data rather than code is derived here once
+// per process: the byte table, "append n zero bytes" operators, the LDS image
+// of positional nibble tables and zero-shift operators, and the affine
+// constants.  Reference semantics followed: src/crc32c.c:43 (polynomial),
+// 50-73 (byte table), 84/106 (pre/post inversion), 137-200 (zero operators
+// used to combine CRCs of concatenated pieces).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace hdfs_crc {
+
+constexpr uint32_t kPoly = 0x82f63b78u;  // crc32c.c:43
+
+// 32x32 GF(2) matrix stored as the images of the 32 unit vectors.
+struct Gf2Op {
+    uint32_t col[32];
+    uint32_t apply(uint32_t v) const {
+        uint32_t r = 0;
+        for (int j = 0; v; ++j, v >>= 1)
+            if (v & 1u) r ^= col[j];
+        return r;
+    }
+};
+
+const uint32_t *byte_table();               // T0[b]: register after one byte b from register 0
+uint32_t append_zero_byte(uint32_t reg);     // linear register, one zero byte appended
+Gf2Op op_identity();
+Gf2Op op_compose(const Gf2Op &a, const Gf2Op &b);  // a after b
+Gf2Op op_zeros(uint64_t nbytes);                   // append nbytes zero bytes
+
+// Linear part of CRC32C over bytes with register starting at 0 (no
+// conditioning): crc32c(0, M) == lin(M) ^ crc32c(0, zeros(len)).
+uint32_t lin_bytes(const uint8_t *p, size_t n, uint32_t reg = 0);
+
+// ---- the GPU's LDS image (see DESIGN.md "LDS layout") ----
+// [0, 65536): positional nibble tables of one 512-byte block.  Lane column q
+//   (0..31) owns the 16 bytes at block offset 16q .. 16q+15; byte k of that
+//   piece, nibble value n:
+//     low nibble  at  k*4096 + n*256  + q*4          (address bit 7 = 0)
+//     high nibble at  128 + k*256 + n*4096 + q*4     (address bit 7 = 1)
+//   entry = lin(byte followed by 511 - (16q + k) zero bytes).
+// [65536, 65536 + 15*512): Z^(512*s), s = 1..15, as 8 nibble tables of 16
+//   entries: (s-1)*512 + t*64 + n*4 holds Z^(512 s)(n << 4t).
+constexpr size_t kLdsPosBytes = 65536;
+constexpr size_t kLdsShiftOff = 65536;
+constexpr int kMaxShift = 15;
+constexpr size_t kLdsBytes = kLdsPosBytes + kMaxShift * 512;
+
+// Fills `dst` (kLdsBytes) with the LDS image.
+void build_lds_image(uint8_t *dst);
+
+// crc32c(0, zeros(512 << lg)) for lg = 0..4 and crc32c(0, zeros(r)) for r = 0..3.
+void affine_constants(uint32_t c_lg[5], uint32_t c_small[4]);
+
+}  // namespace hdfs_crc

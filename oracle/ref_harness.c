@@ -1,0 +1,97 @@
+/*
+ * ref_harness.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Drives the UNMODIFIED reference implementation (/root/reference/src/crc32c.c,
+ * compiled where it lies by oracle/Makefile into oracle/_ref/) the way the
+ * reference's packet writer does: one crc32c(0, chunk, min(bpc, len - i*bpc))
+ * call per chunk (src/hadooprpc.c:733-742). Used to generate golden fixtures
+ * (tests/golden/make_golden.py) and as bench.py's cpu_baseline
+ * ("kind": "reference"). No reference source is copied into this repository.
+ */
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <time.h>
+
+/* The reference exports exactly this symbol (src/crc32c.c:333) and its only
+ * caller declares it by hand (src/hadooprpc.c:31). */
+uint32_t crc32c(uint32_t crc, const void *buf, size_t len);
+
+uint32_t ref_crc32c(uint32_t crc, const void *buf, size_t len)
+{
+    return crc32c(crc, buf, len);
+}
+
+typedef struct {
+    uint64_t payload_off;
+    uint64_t out_idx;
+    uint32_t len;
+    uint32_t bpc;
+} ref_packet;
+
+/* hadooprpc.c:639 + 733-742 for one packet. */
+static void ref_packet_chunks(const uint8_t *packet, uint64_t len, uint32_t bpc, uint32_t *out)
+{
+    uint64_t n = (len + bpc - 1) / bpc;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t idx = i * (uint64_t)bpc;
+        uint64_t m = len - idx < bpc ? len - idx : bpc;
+        out[i] = crc32c(0, packet + idx, (size_t)m);
+    }
+}
+
+void ref_batch(const void *payload, const ref_packet *pkts, uint64_t npkts, uint32_t *out)
+{
+    for (uint64_t i = 0; i < npkts; i++)
+        ref_packet_chunks((const uint8_t *)payload + pkts[i].payload_off, pkts[i].len, pkts[i].bpc,
+                          out + pkts[i].out_idx);
+}
+
+typedef struct {
+    const uint8_t *payload;
+    const ref_packet *pkts;
+    uint64_t lo, hi;
+    uint32_t *out;
+} ref_job;
+
+static void *ref_worker(void *arg)
+{
+    ref_job *j = (ref_job *)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++)
+        ref_packet_chunks(j->payload + j->pkts[i].payload_off, j->pkts[i].len, j->pkts[i].bpc,
+                          j->out + j->pkts[i].out_idx);
+    return NULL;
+}
+
+/* The batch on nthreads threads (contiguous packet slices), `reps` times.
+ * Returns elapsed wall seconds. */
+double ref_batch_mt(const void *payload, const ref_packet *pkts, uint64_t npkts, uint32_t *out, int nthreads,
+                    int reps)
+{
+    enum { MAXT = 256 };
+    pthread_t th[MAXT];
+    ref_job jobs[MAXT];
+    struct timespec t0, t1;
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > MAXT)
+        nthreads = MAXT;
+    /* First call resolves the reference's lazy SSE4.2 dispatch (crc32c.c:335-341)
+     * outside the timed region so threads do not race on it. */
+    (void)crc32c(0, "", 0);
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+        for (int t = 0; t < nthreads; t++) {
+            jobs[t].payload = (const uint8_t *)payload;
+            jobs[t].pkts = pkts;
+            jobs[t].lo = npkts * (uint64_t)t / (uint64_t)nthreads;
+            jobs[t].hi = npkts * (uint64_t)(t + 1) / (uint64_t)nthreads;
+            jobs[t].out = out;
+            pthread_create(&th[t], NULL, ref_worker, &jobs[t]);
+        }
+        for (int t = 0; t < nthreads; t++)
+            pthread_join(th[t], NULL);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

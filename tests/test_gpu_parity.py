@@ -1,0 +1,196 @@
+"""Parity of the HIP path with the oracle and the reference's golden vectors.
+
+Every test calls the GPU through the C ABI (libhdfs_crc32c.so via ctypes);
+torch only allocates device memory and provides the stream.  The bar is
+bit-exact equality (integer work)."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_batch_packets, golden_fill
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+def run_dev(hdfs, ctx, payload: np.ndarray, pk: np.ndarray, flags: int = 0, offset: int = 0) -> np.ndarray:
+    """Device-resident plan execution; `offset` shifts the payload inside the
+    device buffer (the plan itself sees payload_off values)."""
+    torch = _torch()
+    dev = torch.zeros(payload.size + offset + 64, dtype=torch.uint8, device="cuda")
+    dev[offset:offset + payload.size].copy_(torch.from_numpy(payload))
+    n = hdfs.total_checksums(pk)
+    out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    plan = hdfs.Plan(ctx, pk, flags)
+    assert plan.nchecksums == n
+    stream = torch.cuda.current_stream()
+    plan.exec(dev.data_ptr() + offset, out.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    plan.close()
+    return out.cpu().numpy().view(np.uint32)[:n]
+
+
+@pytest.mark.parametrize("name", ["c1_one_packet", "c3_one_block_4MiB", "c5_mixed_bpc_96", "ragged_tail_257",
+                                  "c2_4096_packets", "c5_mixed_bpc_4096"])
+def test_golden_batches_device_resident(hdfs, gpu_ctx, golden, name):
+    spec = [b for b in golden["batches"] if b["name"] == name][0]
+    pk = golden_batch_packets(spec)
+    payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+    got = run_dev(hdfs, gpu_ctx, payload, pk)
+    assert got.size == spec["nchecksums"]
+    assert ["%08x" % v for v in got[:8]] == spec["head"]
+    assert ["%08x" % v for v in got[-8:]] == spec["tail"]
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
+
+
+def test_golden_packets_host_path(hdfs, gpu_ctx, golden):
+    for c in golden["packets"]["cases"]:
+        buf = golden_fill(c["kind"], c["len"] + c["skip"], c["seed"])[c["skip"]:]
+        pk = np.zeros(1, hdfs.PACKET_DTYPE)
+        pk["len"] = c["len"]
+        pk["bpc"] = c["bpc"]
+        got = gpu_ctx.batch_host(np.ascontiguousarray(buf), pk)
+        assert ["%08x" % v for v in got] == c["crcs"], (c["bpc"], c["kind"], c["len"])
+
+
+def test_golden_packets_device_unaligned(hdfs, gpu_ctx, golden):
+    # Every fixture packet placed at a 16-byte-misaligned device offset (the
+    # general path) and at an aligned one (fast path where bpc allows).
+    cases = golden["packets"]["cases"]
+    bufs, pk = [], np.zeros(len(cases) * 2, hdfs.PACKET_DTYPE)
+    off, out = 0, 0
+    for i, c in enumerate(cases * 2):
+        mis = 3 if i < len(cases) else 0
+        buf = golden_fill(c["kind"], c["len"] + c["skip"], c["seed"])[c["skip"]:]
+        off += mis
+        pk[i] = (off, out, c["len"], c["bpc"])
+        bufs.append((off, buf))
+        off = (off + c["len"] + 15) & ~15
+        out += (c["len"] + c["bpc"] - 1) // c["bpc"]
+    payload = np.zeros(off + 16, np.uint8)
+    for o, b in bufs:
+        payload[o:o + b.size] = b
+    got = run_dev(hdfs, gpu_ctx, payload, pk)
+    want = [v for c in cases * 2 for v in c["crcs"]]
+    assert ["%08x" % v for v in got] == want
+
+
+def test_big_endian_flag(hdfs, gpu_ctx, orc):
+    pk = oracle.mixed_packets(6, pkt_len=10000)
+    payload = oracle.xorshift64_bytes(60000, 8)
+    le = run_dev(hdfs, gpu_ctx, payload, pk)
+    be = run_dev(hdfs, gpu_ctx, payload, pk, flags=hdfs.CRC32C_BIG_ENDIAN)
+    assert np.array_equal(le, orc.batch(payload, pk, le.size))
+    assert np.array_equal(be, le.byteswap())
+
+
+def test_edge_cases(hdfs, gpu_ctx, orc):
+    rows = [  # (len, bpc)
+        (0, 512), (1, 512), (3, 512), (4, 512), (15, 512), (16, 512), (511, 512), (512, 512), (513, 512),
+        (8191, 8192), (8192, 8192), (16384, 8192), (100, 100), (250, 100), (5000, 1536), (65535, 65536),
+        (70000, 16384), (20000, 7), (1, 1), (1000, 1),
+    ]
+    pk = np.zeros(len(rows), hdfs.PACKET_DTYPE)
+    off = out = 0
+    for i, (n, b) in enumerate(rows):
+        pk[i] = (off, out, n, b)
+        off = (off + n + 31) & ~15  # keep a little gap, 16-aligned
+        out += (n + b - 1) // b
+    payload = oracle.xorshift64_bytes(off + 32, 1234)
+    got = run_dev(hdfs, gpu_ctx, payload, pk)
+    assert np.array_equal(got, orc.batch(payload, pk, got.size))
+
+
+def test_payload_at_end_of_allocation(hdfs, gpu_ctx, orc):
+    # Chunks that end exactly at the last byte of the device buffer.
+    torch = _torch()
+    for n, bpc in [(1000, 512), (4096, 4096), (777, 100), (65536, 512)]:
+        payload = oracle.xorshift64_bytes(n, n)
+        dev = torch.from_numpy(payload).cuda()
+        pk = np.array([(0, 0, n, bpc)], hdfs.PACKET_DTYPE)
+        m = (n + bpc - 1) // bpc
+        out = torch.zeros(m, dtype=torch.int32, device="cuda")
+        gpu_ctx.chunks_dev(pk, dev.data_ptr(), out.data_ptr())
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.chunks(payload, bpc))
+
+
+def test_random_batches(hdfs, gpu_ctx, orc):
+    rng = np.random.default_rng(2024)
+    for trial in range(6):
+        npk = int(rng.integers(1, 200))
+        bpcs = rng.choice([512, 1024, 2048, 4096, 8192, 100, 1536, 4000], size=npk)
+        lens = rng.integers(0, 70000, size=npk)
+        pk = np.zeros(npk, hdfs.PACKET_DTYPE)
+        off = out = 0
+        for i in range(npk):
+            align = 16 if rng.random() < 0.8 else 1
+            off = (off + align - 1) // align * align
+            pk[i] = (off, out, lens[i], bpcs[i])
+            off += int(lens[i]) + int(rng.integers(0, 40))
+            out += (int(lens[i]) + int(bpcs[i]) - 1) // int(bpcs[i])
+        # output ranges assigned in a random packet order (independent of payload order)
+        counts = (pk["len"].astype(np.int64) + pk["bpc"] - 1) // pk["bpc"]
+        perm = rng.permutation(npk)
+        starts = np.zeros(npk, np.int64)
+        starts[perm] = np.concatenate([[0], np.cumsum(counts[perm])[:-1]])
+        pk["out_idx"] = starts
+        payload = oracle.xorshift64_bytes(off + 16, 500 + trial)
+        got = run_dev(hdfs, gpu_ctx, payload, pk)
+        assert np.array_equal(got, orc.batch(payload, pk, got.size)), trial
+
+
+def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
+    torch = _torch()
+    pk = oracle.uniform_packets(700)  # ~44 MiB: crosses the 32 MiB slice size
+    payload = oracle.xorshift64_bytes(700 * 65536, 42)
+    want = orc.batch(payload, pk, 700 * 128)
+    assert np.array_equal(gpu_ctx.batch_host(payload, pk), want)
+    pinned = torch.from_numpy(payload).pin_memory()
+    got = gpu_ctx.batch_host(pinned.numpy(), pk)
+    assert np.array_equal(got, want)
+    # scattered packets (gather path) with out_idx in reverse order
+    pk2 = oracle.uniform_packets(50, pkt_len=30000, stride=65536)
+    pk2["out_idx"] = pk2["out_idx"][::-1].copy()
+    want2 = orc.batch(payload, pk2, oracle.total_checksums(pk2))
+    assert np.array_equal(gpu_ctx.batch_host(payload, pk2), want2)
+
+
+def test_chunks_default_context(hdfs, orc):
+    pkt = oracle.xorshift64_bytes(65536, 99)
+    assert np.array_equal(hdfs.chunks(pkt, 512), orc.chunks(pkt, 512))
+    assert np.array_equal(hdfs.chunks(pkt[:1000], 512, hdfs.CRC32C_BIG_ENDIAN), orc.chunks(pkt[:1000], 512, True))
+
+
+def test_multi_single_device(hdfs, orc):
+    m = hdfs.Multi([0])
+    pk = oracle.uniform_packets(256)
+    payload = oracle.xorshift64_bytes(256 * 65536, 7)
+    assert np.array_equal(m.batch_host(payload, pk, group_packets=64), orc.batch(payload, pk, 256 * 128))
+    m.close()
+
+
+def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
+    """Config 2 at full size: bit-exact against the oracle, plus the
+    size-independent properties (CRC of zero and 0xFF chunks, chunk-shift
+    invariance)."""
+    pk = oracle.uniform_packets(4096)
+    payload = oracle.xorshift64_bytes(4096 * 65536, 0xC2)
+    payload[:65536] = 0
+    payload[65536:131072] = 0xFF
+    got = run_dev(hdfs, gpu_ctx, payload, pk)
+    assert np.array_equal(got, orc.batch(payload, pk, got.size))
+    assert np.all(got[:128] == 0x30FCEDC0)  # crc32c of 512 zero bytes (known answer)
+    assert np.all(got[128:256] == orc.crc32c(np.full(512, 0xFF, np.uint8)))
+    # shifting the payload by one chunk shifts the checksum vector by one
+    got2 = run_dev(hdfs, gpu_ctx, np.ascontiguousarray(payload[512:]), oracle.uniform_packets(4095))
+    assert np.array_equal(got2[:127], got[1:128])

@@ -1,0 +1,153 @@
+"""CPU checks of libhdfs_crc32c.so: it loads, exports every symbol the headers
+declare, its drop-in scalar crc32c() and packet helpers match the oracle, its
+work decomposition covers every chunk exactly once, and a bit-level model of
+the kernel evaluated on the library's own LDS image reproduces the oracle."""
+from __future__ import annotations
+
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import ROOT, golden_fill
+from kernel_model import KernelModel
+
+
+def _declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(crc32c\w*)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_exports_every_declared_symbol(hdfs):
+    names = _declared_functions()
+    assert "crc32c" in names and "crc32c_plan_exec" in names and len(names) >= 20
+    lib = hdfs.lib()
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+
+
+def test_scalar_dropin_known_answers(hdfs, golden):
+    for e in golden["known_answers"]["published"]:
+        assert "%08x" % hdfs.crc32c(bytes.fromhex(e["hex"])) == e["crc"]
+    for e in golden["known_answers"]["derived"]:
+        assert "%08x" % hdfs.crc32c(golden_fill(e["kind"], e["len"], 0)) == e["crc"], e["name"]
+    for e in golden["known_answers"]["chained"]:
+        buf = golden_fill("xorshift", e["len"], e["seed"])
+        c1 = hdfs.crc32c(buf[: e["split"]])
+        assert "%08x" % hdfs.crc32c(buf[e["split"]:], c1) == e["crc"]
+
+
+def test_scalar_dropin_random_vs_oracle(hdfs, orc):
+    # sizes around the 3 x 1024-byte stripe path and unaligned starts
+    rng = np.random.default_rng(1)
+    buf = oracle.xorshift64_bytes(1 << 16, 33)
+    for n in list(range(0, 40)) + [3071, 3072, 3073, 6144, 9999, 65000]:
+        off = int(rng.integers(0, 16))
+        crc = int(rng.integers(0, 2**32))
+        seg = buf[off:off + n]
+        assert hdfs.crc32c(seg, crc) == orc.crc32c(seg, crc), n
+
+
+def test_nchunks_and_packetize(hdfs, orc):
+    assert hdfs.nchunks(65536, 512) == 128
+    assert hdfs.nchunks(65537, 512) == 129
+    assert hdfs.nchunks(0, 512) == 0
+    for args in [(131072, 0, 65536, 512), (70000, 100, 65536, 512), (4194304, 0, 65536, 512),
+                 (1000, 513, 65536, 1024), (50, 10, 65536, 512), (0, 0, 65536, 512), (10**6, 12345, 65536, 4096)]:
+        assert hdfs.packetize(*args) == orc.packetize(*args), args
+
+
+def _cases():
+    yield "c2_shape", oracle.uniform_packets(64)
+    yield "mixed", oracle.mixed_packets(24)
+    yield "ragged", oracle.uniform_packets(9, pkt_len=65436, stride=65536)
+    odd = np.zeros(6, oracle.PACKET_DTYPE)
+    odd["payload_off"] = [0, 5, 20000, 30001, 40000, 50000]
+    odd["len"] = [4999, 3000, 7000, 3, 1, 9000]
+    odd["bpc"] = [512, 512, 100, 512, 1024, 1536]
+    odd["out_idx"] = np.cumsum([0] + [(l + b - 1) // b for l, b in zip(odd["len"][:-1], odd["bpc"][:-1])])
+    yield "odd", odd
+
+
+@pytest.mark.parametrize("name,pk", list(_cases()))
+def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
+    """Re-derive every checksum from the work items alone (CPU) and compare."""
+    tiles, gen = hdfs.debug_plan(pk)
+    extent = int((pk["payload_off"] + pk["len"]).max())
+    payload = oracle.xorshift64_bytes(extent + 64, 77)
+    n = oracle.total_checksums(pk)
+    want = orc.batch(payload, pk, n)
+    got = np.full(n, 0xDEADBEEF, np.uint32)
+    seen = np.zeros(n, np.int32)
+    for t in tiles:
+        nb, lg = int(t["meta"]) & 0xFF, (int(t["meta"]) >> 8) & 0xFF
+        assert 1 <= nb <= 16 and nb % (1 << lg) == 0 and int(t["src"]) % 16 == 0
+        bpc = 512 << lg
+        for c in range(nb >> lg):
+            s = int(t["src"]) + c * bpc
+            got[int(t["out"]) + c] = orc.crc32c(payload[s:s + bpc])
+            seen[int(t["out"]) + c] += 1
+    for g in gen:
+        s = int(g["src"])
+        got[int(g["out"])] = orc.crc32c(payload[s:s + int(g["len"])])
+        seen[int(g["out"])] += 1
+    assert np.all(seen == 1)
+    assert np.array_equal(got, want)
+
+
+def test_plan_fast_path_shapes(hdfs):
+    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(4096))
+    assert tiles.size == 4096 * 8 and gen.size == 0 and np.all(tiles["meta"] == 16)
+    tiles, gen = hdfs.debug_plan(oracle.mixed_packets(3))
+    assert list(tiles["meta"][:1]) == [16] and set(int(m) >> 8 for m in tiles["meta"]) == {0, 1, 3}
+    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65436))
+    assert gen.size == 1 and int(gen["len"][0]) == 65436 % 512
+
+
+@pytest.fixture(scope="module")
+def model(hdfs):
+    img, c_lg, c_small = hdfs.debug_lds_image()
+    return KernelModel(img, c_lg, c_small)
+
+
+def test_affine_constants(hdfs, orc, model):
+    for lg in range(5):
+        assert model.c_lg[lg] == orc.crc32c(np.zeros(512 << lg, np.uint8))
+    for r in range(4):
+        assert model.c_small[r] == orc.crc32c(np.zeros(r, np.uint8))
+
+
+@pytest.mark.parametrize("lg", [0, 1, 2, 3, 4])
+def test_kernel_model_fast_tiles(orc, model, lg):
+    bpc = 512 << lg
+    data = oracle.xorshift64_bytes(bpc * 6, 100 + lg)
+    data[:bpc] = 0
+    data[bpc:2 * bpc] = 0xFF
+    got = model.fast_chunks(data, lg)
+    want = orc.chunks(data, bpc)
+    assert np.array_equal(got, want)
+
+
+def test_kernel_model_general_chunks(orc, model):
+    buf = oracle.xorshift64_bytes(20000, 55)
+    for n in [1, 2, 3, 4, 5, 15, 16, 17, 100, 411, 511, 512, 513, 1000, 1536, 4095, 8192, 9001]:
+        assert model.general_chunk(buf[:n]) == orc.crc32c(buf[:n]), n
+    for n in [1, 3, 4, 700]:
+        assert model.general_chunk(np.zeros(n, np.uint8)) == orc.crc32c(np.zeros(n, np.uint8))
+
+
+def test_gpu_entry_points_fail_loudly_without_gpu(hdfs):
+    if hdfs.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(hdfs.Crc32cError) as ei:
+        hdfs.Context(0)
+    assert ei.value.rc == -19  # -ENODEV: no CPU substitute behind the GPU API
+    with pytest.raises(hdfs.Crc32cError):
+        hdfs.chunks(np.zeros(1024, np.uint8), 512)
