@@ -57,6 +57,16 @@ def lib():
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise FileNotFoundError(LIB_PATH + " is not built (run build())")
+        # One HIP runtime per process: torch ships its own libamdhip64 and
+        # links it by the unversioned name, so it must be loaded first; our
+        # NEEDED libamdhip64.so.7 then binds to the same copy by SONAME.
+        # (Loaded the other way round the process would hold two runtimes and
+        # torch would see no device.)  torch is plumbing only (device memory,
+        # streams, torch.distributed); nothing here computes with it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         _LIB = _bind(ctypes.CDLL(LIB_PATH))
     return _LIB
 

@@ -39,6 +39,21 @@ using hdfs_crc::KParams;
 constexpr uint32_t kLdsBytes = hdfs_crc::kKernelLdsBytes;
 constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
 
+// Work descriptors are read-only for the whole launch: reading them through
+// the constant address space lets every (wave-uniform) descriptor fetch be a
+// scalar s_load instead of a vector load that would join the payload loads
+// on the vector-memory counter.
+typedef const __attribute__((address_space(4))) FastTile *ConstTiles;
+
+__device__ __forceinline__ FastTile tile_at(const KParams &p, uint32_t i) {
+    const ConstTiles t = (ConstTiles)(p.tiles) + i;
+    FastTile r;
+    r.src = t->src;
+    r.out = t->out;
+    r.meta = t->meta;
+    return r;
+}
+
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t *lds, uint32_t off) {
     return *reinterpret_cast<const uint32_t *>(lds + off);
 }
@@ -102,26 +117,38 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 }
 
 // ---- fast path: one wave, 16 blocks of full chunks -----------------------
-__device__ __forceinline__ void fast_tile(const KParams &p, const uint8_t *lds, FastTile t, int lane) {
+// Loads of one tile: instruction i reads 1 KiB contiguous (blocks 2i, 2i+1).
+// Lanes of blocks a partial tile does not have re-read block 0 (always
+// valid memory) and are masked out in finish_tile, so the instruction
+// stream has no divergent branch and the wait counts stay exact.
+__device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8]) {
+    const uint32_t nb = t.meta & 0xffu;
+    const uint32_t h = uint32_t(lane) >> 5;
+    const uint8_t *base = p.payload + t.src;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t off = (2u * i + h < nb) ? 1024u * i + 16u * uint32_t(lane) : 16u * uint32_t(lane & 31);
+        v[i] = *reinterpret_cast<const uint4 *>(base + off);
+    }
+    // Keep the loads ahead of whatever compute follows (the scheduler would
+    // otherwise hoist the next tile's first lookups above them and wait).
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, FastTile t, const uint4 v[8],
+                                            int lane) {
     const uint32_t nb = t.meta & 0xffu;
     const uint32_t lg = (t.meta >> 8) & 0xffu;
     const uint32_t col4 = uint32_t(lane & 31) << 2;
     const uint32_t h = uint32_t(lane) >> 5;
-    const uint4 *src = reinterpret_cast<const uint4 *>(p.payload + t.src) + lane;
-
     uint32_t pc[8];
-    if (nb == 16) {
-        uint4 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = src[64 * i];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pc[i] = piece_lin(lds, v[i], col4);
-    } else {
-        uint4 v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = (2u * i + h < nb) ? src[64 * i] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pc[i] = piece_lin(lds, v[i], col4);
+    for (int i = 0; i < 8; ++i) {
+        pc[i] = piece_lin(lds, v[i], col4);
+        pc[i] = (2u * i + h < nb) ? pc[i] : 0u;
+        // One piece at a time: keeps the scheduler from hoisting every
+        // piece's 32 LDS reads together (register pressure -> spills).
+        __builtin_amdgcn_sched_barrier(0);
     }
 
     // Reduce-scatter over lane bits 0, 1, 3 (8 values -> 1), then all-reduce
@@ -166,6 +193,58 @@ __device__ __forceinline__ void fast_tile(const KParams &p, const uint8_t *lds, 
     if (rep) p.out[t.out + (blk >> lg)] = out_order(crc, p.flags);
 }
 
+// Grid-stride over fast tiles.  PIPE: the next tile's 8 KiB is in flight
+// (and the descriptor after it requested) while the current one is
+// computed, so each wave keeps HBM busy across its own compute.
+template <bool PIPE>
+__device__ __forceinline__ void fast_loop(const KParams &p, const uint8_t *lds, uint32_t wave, uint32_t nwaves,
+                                          int lane) {
+    // Tiles of this wave: wave, wave + nwaves, ... (n of them).  All loop
+    // control is scalar; tile indices go through readfirstlane so the
+    // compiler keeps them (and the descriptor loads) in SGPRs.
+    const uint32_t n = wave < p.ntiles ? (p.ntiles - 1u - wave) / nwaves + 1u : 0u;
+    auto tile_k = [&](uint32_t k) { return tile_at(p, __builtin_amdgcn_readfirstlane(wave + k * nwaves)); };
+    if (!PIPE) {
+        FastTile t = tile_k(0);
+        for (uint32_t k = 0; k < n; ++k) {
+            uint4 v[8];
+            load_tile(p, t, lane, v);
+            const FastTile tn = tile_k(k + 1 < n ? k + 1 : k);  // prefetch the next descriptor
+            finish_tile(p, lds, t, v, lane);
+            t = tn;
+        }
+        return;
+    }
+    // Two register buffers, unrolled by two so each buffer stays in its own
+    // registers: the other buffer's loads are issued before a buffer is
+    // computed, so its waits are vmcnt(15..8) and 8 KiB stays in flight.
+    // The last one or two tiles are drained outside the loop.
+    if (n == 0) return;
+    uint4 va[8], vb[8];
+    FastTile ta = tile_k(0);
+    load_tile(p, ta, lane, va);
+    uint32_t k = 0;
+    FastTile tb = tile_k(n > 1 ? 1 : 0);
+    while (k + 2 < n) {  // tiles k, k+1, k+2 exist
+        load_tile(p, tb, lane, vb);
+        const FastTile tc = tile_k(k + 2);
+        finish_tile(p, lds, ta, va, lane);
+        load_tile(p, tc, lane, va);
+        const FastTile td = tile_k(k + 3 < n ? k + 3 : k + 2);
+        finish_tile(p, lds, tb, vb, lane);
+        ta = tc;
+        tb = td;
+        k += 2;
+    }
+    if (k + 1 < n) {
+        load_tile(p, tb, lane, vb);
+        finish_tile(p, lds, ta, va, lane);
+        finish_tile(p, lds, tb, vb, lane);
+    } else {
+        finish_tile(p, lds, ta, va, lane);
+    }
+}
+
 // ---- general path: half a wave per chunk of any length / alignment -------
 __device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
     return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
@@ -189,6 +268,9 @@ __device__ __forceinline__ void load_piece(uintptr_t a0, uintptr_t cbeg, uintptr
     }
 }
 
+// Bytes sh .. sh+15 of the 32 bytes w[0..7]: a two-stage dword select (by 2,
+// then by 1) and v_alignbyte.  Written out as values so the compiler cannot
+// turn it into an indexed scratch access.
 // Bytes sh .. sh+15 of the 32 bytes w[0..7]: a two-stage dword select (by 2,
 // then by 1) and v_alignbyte.  Written out as values so the compiler cannot
 // turn it into an indexed scratch access.
@@ -239,30 +321,61 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
 
 }  // namespace
 
-__global__ __launch_bounds__(hdfs_crc::kKernelThreads, 4) void hdfs_crc32c_plan_kernel(KParams p) {
+template <int THREADS, bool PIPE>
+__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void hdfs_crc32c_plan_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     {
+        // Stage the tables: every load in flight before the first LDS write
+        // (the device copy is zero-padded to kTableAlloc bytes, so no load
+        // needs a guard).
+        constexpr uint32_t kVec = kLdsBytes / 16;
+        constexpr uint32_t kPer = (kVec + THREADS - 1) / THREADS;
         const uint4 *g = reinterpret_cast<const uint4 *>(p.table);
-        uint4 *s = reinterpret_cast<uint4 *>(lds);
-        for (uint32_t i = threadIdx.x; i < kLdsBytes / 16; i += hdfs_crc::kKernelThreads) s[i] = g[i];
+        uint4 *sm = reinterpret_cast<uint4 *>(lds);
+        uint4 r[kPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) r[k] = g[threadIdx.x + k * THREADS];
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k)
+            if (threadIdx.x + k * THREADS < kVec) sm[threadIdx.x + k * THREADS] = r[k];
     }
     __syncthreads();
     const int lane = int(threadIdx.x & 63u);
-    constexpr uint32_t kWaves = hdfs_crc::kKernelThreads / 64;
+    constexpr uint32_t kWaves = THREADS / 64;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
     const uint32_t nwaves = gridDim.x * kWaves;
-    const uint32_t total = p.ntiles + ((p.ngen + 1u) >> 1);
-    for (uint32_t it = wave; it < total; it += nwaves) {
-        if (it < p.ntiles)
-            fast_tile(p, lds, p.tiles[it], lane);
-        else
-            gen_pair(p, lds, it - p.ntiles, lane);
-    }
+    fast_loop<PIPE>(p, lds, wave, nwaves, lane);
+    const uint32_t npairs = (p.ngen + 1u) >> 1;
+    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair(p, lds, g, lane);
 }
 
 namespace hdfs_crc {
-hipError_t launch_plan_kernel(const KParams &p, uint32_t grid, hipStream_t stream) {
-    hipLaunchKernelGGL(hdfs_crc32c_plan_kernel, dim3(grid), dim3(kKernelThreads), 0, stream, p);
+const KernelVariant kVariants[kNumVariants] = {
+    {"wg512_pipe", 512, true},
+    {"wg512_plain", 512, false},
+    {"wg1024_plain", 1024, false},
+};
+
+hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream) {
+    if (variant < 0 || variant >= kNumVariants) variant = 0;
+    const KernelVariant &kv = kVariants[variant];
+    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
+    const uint64_t waves = uint64_t(kv.threads / 64);
+    uint64_t grid = (items + waves - 1) / waves;
+    const uint64_t cap = uint64_t(num_cu) * kKernelWgPerCu;
+    if (grid > cap) grid = cap;
+    if (grid == 0) grid = 1;
+    switch (variant) {
+    case 1:
+        hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<512, false>), dim3(uint32_t(grid)), dim3(512), 0, stream, p);
+        break;
+    case 2:
+        hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<1024, false>), dim3(uint32_t(grid)), dim3(1024), 0, stream, p);
+        break;
+    default:
+        hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<512, true>), dim3(uint32_t(grid)), dim3(512), 0, stream, p);
+        break;
+    }
     return hipGetLastError();
 }
 }  // namespace hdfs_crc

@@ -76,6 +76,7 @@ struct Stage {
 struct crc32c_ctx {
     int device = 0;
     int num_cu = 0;
+    int variant = 0;  // kernel variant, $HDFS_CRC32C_KVARIANT (A/B measurement only)
     uint8_t *d_table = nullptr;
     uint32_t c_lg[5];
     uint32_t c_small[4];
@@ -98,14 +99,6 @@ struct crc32c_multi {
 
 namespace {
 
-uint32_t grid_for(const crc32c_ctx *ctx, uint64_t items) {
-    const uint64_t waves_per_wg = kKernelThreads / 64;
-    uint64_t g = (items + waves_per_wg - 1) / waves_per_wg;
-    const uint64_t cap = uint64_t(ctx->num_cu) * kKernelWgPerCu;
-    if (g > cap) g = cap;
-    return uint32_t(g ? g : 1);
-}
-
 KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
                    const void *payload, uint32_t *out, uint32_t flags) {
     KParams p;
@@ -125,7 +118,7 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
 int launch(const crc32c_ctx *ctx, const KParams &p, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
     if (!items) return 0;
-    HIP_TRY(launch_plan_kernel(p, grid_for(ctx, items), stream));
+    HIP_TRY(launch_plan_kernel(p, ctx->variant, uint32_t(ctx->num_cu), stream));
     return 0;
 }
 
@@ -309,11 +302,12 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
-    std::vector<uint8_t> img(kLdsBytes);
+    if (const char *kv = std::getenv("HDFS_CRC32C_KVARIANT")) c->variant = std::atoi(kv);
+    std::vector<uint8_t> img(kTableAlloc, 0);
     build_lds_image(img.data());
     affine_constants(c->c_lg, c->c_small);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table), kLdsBytes));
-    HIP_TRY(hipMemcpy(c->d_table, img.data(), kLdsBytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table), kTableAlloc));
+    HIP_TRY(hipMemcpy(c->d_table, img.data(), kTableAlloc, hipMemcpyHostToDevice));
     *out = c.release();
     return 0;
 }

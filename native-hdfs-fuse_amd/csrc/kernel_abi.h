@@ -8,10 +8,12 @@
 
 namespace hdfs_crc {
 
-constexpr uint32_t kKernelThreads = 512;  // 8 waves per workgroup
 constexpr uint32_t kKernelLdsBytes = uint32_t(kLdsBytes);
 constexpr uint32_t kKernelShiftOff = uint32_t(kLdsShiftOff);
 constexpr uint32_t kKernelWgPerCu = 2;  // 2 x 73 KiB of LDS per CU
+// Device copy of the LDS image, zero-padded so every staging load of a
+// 1024-thread workgroup (16 B per thread per round) is in bounds.
+constexpr uint32_t kTableAlloc = ((kKernelLdsBytes + 16384 - 1) / 16384) * 16384;
 
 struct KParams {
     const FastTile *tiles;
@@ -26,6 +28,17 @@ struct KParams {
     uint32_t c_small[4];
 };
 
-hipError_t launch_plan_kernel(const KParams &p, uint32_t grid, hipStream_t stream);
+// Kernel variants (workgroup size x software pipelining); 0 is the default,
+// the others stay built for A/B measurement (tools/kbench.py).
+struct KernelVariant {
+    const char *name;
+    uint32_t threads;
+    bool pipelined;
+};
+constexpr int kNumVariants = 3;
+extern const KernelVariant kVariants[kNumVariants];
+
+// Persistent grid: min(work items / waves per workgroup, kKernelWgPerCu * CUs).
+hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream);
 
 }  // namespace hdfs_crc

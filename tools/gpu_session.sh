@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# One GPU-box session: smoke -> parity tests -> bench -> rocprofv3 kernel trace.
+# Each GPU step has its own time limit; a crash/timeout/signal stops the
+# session (no further GPU work), a plain test failure (rc 1) does not.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+STEPS="${STEPS:-smoke tests bench prof}"
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/session.log
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/session.log
+  tail -5 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+    bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    bench5) run bench5 600 python bench.py --config c5 --no-cpu ;;
+    kbench) run kbench 600 python tools/kbench.py --config c2 ;;
+    kbench5) run kbench5 600 python tools/kbench.py --config c5 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
+            python3 bench.py --steps 50 --warmup 10 --no-cpu --no-host ;;
+  esac
+done
+echo "session done"

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""A/B timing of the kernel variants in ONE process, interleaved rounds
+(cdna_hip_programming.md 5.4 rule 24).  Device-resident config-2 batches
+rotating over NBUF buffers; reports per-variant median/min kernel time and
+GB/s, and checks every variant's checksums against variant 0.
+
+    python tools/kbench.py [--rounds 7] [--iters 20] [--config c2|c5|c3]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--nbuf", type=int, default=4)
+    ap.add_argument("--variants", default="0,1,2")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import oracle
+    from bench import config_packets, load_package
+
+    hdfs = load_package()
+    pk, workload = config_packets(args.config, oracle)
+    nbytes = int(pk["len"].astype(np.int64).sum())
+    extent = int((pk["payload_off"] + pk["len"]).max())
+    nout = hdfs.total_checksums(pk)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g) for _ in range(args.nbuf)]
+    outs = [torch.zeros(nout, dtype=torch.int32, device=dev) for _ in range(args.nbuf)]
+    variants = [int(v) for v in args.variants.split(",")]
+    plans = {}
+    for v in variants:
+        os.environ["HDFS_CRC32C_KVARIANT"] = str(v)
+        ctx = hdfs.Context(0)
+        plans[v] = (ctx, ctx.plan(pk))
+    stream = torch.cuda.current_stream()
+    ref = None
+    for v in variants:
+        plans[v][1].exec(bufs[0].data_ptr(), outs[0].data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        got = outs[0].cpu().numpy().copy()
+        if ref is None:
+            ref = got
+        assert np.array_equal(got, ref), "variant %d differs" % v
+    times = {v: [] for v in variants}
+    for r in range(args.rounds):
+        for v in variants:
+            plan = plans[v][1]
+            for i in range(3):
+                plan.exec(bufs[i % args.nbuf].data_ptr(), outs[i % args.nbuf].data_ptr(), stream.cuda_stream)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(args.iters):
+                b = i % args.nbuf
+                plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / args.iters * 1e3)  # us per launch
+    res = {}
+    for v in variants:
+        t = sorted(times[v])
+        res[v] = {"median_us": round(t[len(t) // 2], 2), "min_us": round(t[0], 2),
+                  "GBps_median": round(nbytes / (t[len(t) // 2] * 1e-6) / 1e9, 1),
+                  "GBps_best": round(nbytes / (t[0] * 1e-6) / 1e9, 1)}
+    print(json.dumps({"config": args.config, "workload": workload, "bytes": nbytes, "variants": res}))
+
+
+if __name__ == "__main__":
+    main()
