@@ -3,7 +3,8 @@
 // Computes hadoop_rpc_send_packet's checksum vector (hadooprpc.c:733-742:
 // crc32c(0, chunk) per bytesPerChecksum chunk, crc32c.c semantics) for a
 // whole batch of device-resident packets in one launch.  Integer/bitwise
-// work, HBM-bound; no MFMA.  Design (DESIGN.md has the derivation):
+// work, HBM-bound; no MFMA.  Design (DESIGN.md has the derivation and the
+// measurements behind each choice):
 //
 //  * CRC32C is affine over GF(2): for a chunk M of n bytes,
 //      crc32c(0, M) = lin(M) ^ crc32c(0, zeros(n)),
@@ -11,7 +12,8 @@
 //    byte value).  So there is no serial dependency inside a chunk.
 //  * Coalesced HBM loads: one wave instruction reads 1 KiB contiguous
 //    (16 B per lane) = two 512-byte blocks; lane q of each half owns bytes
-//    16q .. 16q+15 of its block in EVERY instruction.
+//    16q .. 16q+15 of its block in EVERY instruction.  Loads are
+//    non-temporal buffer loads bounded by the tile (partial tiles read zeros).
 //  * The Castagnoli tables live in LDS as positional NIBBLE tables, one
 //    128-byte row per nibble value with one 4-byte column per lane: the 32
 //    lanes of a ds_read_b32 group always hit 32 different banks (bank =
@@ -22,6 +24,9 @@
 //    the 16 block results of a tile into 16 lanes for one coalesced store.
 //  * bpc = 1024..8192 (config 5): per-block results are shifted by
 //    Z^(512*s) (nibble tables in LDS) and XORed across the blocks of a chunk.
+//  * Work distribution: each workgroup owns an equal range of 8 KiB tiles;
+//    its waves pull tiles from an LDS counter (the SIMD arbiter's age
+//    priority makes static per-wave assignment finish 2x apart).
 //  * Tails / odd bpc / unaligned chunks: half a wave per chunk, the chunk is
 //    right-aligned into zero-prefixed virtual 512-byte blocks (leading zeros
 //    do not change lin), Horner-combined with Z^512.
@@ -38,6 +43,16 @@ using hdfs_crc::KParams;
 
 constexpr uint32_t kLdsBytes = hdfs_crc::kKernelLdsBytes;
 constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
+// Table bytes copied into LDS, rounded up to whole 1 KiB LDS-DMA pieces (the
+// device copy is zero-padded to kTableAlloc >= this).
+constexpr uint32_t kStageBytes = (kLdsBytes + 1023u) / 1024u * 1024u;
+static_assert(kStageBytes <= hdfs_crc::kTableAlloc, "staging reads past the device table");
+
+// Kernel modes (template bits).  Production = kModeNt | kModeEarly.
+constexpr int kModeNt = 1;        // payload loads non-temporal (streamed once)
+constexpr int kModeEarly = 2;     // first tile requested before the table staging
+constexpr int kModeStamps = 4;    // DIAGNOSTIC: per-wave timestamps
+constexpr int kModeMemDiag = 8;   // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -54,6 +69,17 @@ __device__ __forceinline__ FastTile tile_at(const KParams &p, uint32_t i) {
     return r;
 }
 
+// gfx950 has no v_xor3_b32 but has v_bitop3_b32 (any 3-input bitwise
+// function by truth table); 0x96 is a ^ b ^ c.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Opaque to the optimiser: stops InstCombine from re-associating the XOR
+// trees of different pieces into one tree over every LDS read of the tile
+// (which keeps all 256 reads live and spills).
+__device__ __forceinline__ void opaque(uint32_t &x) { asm volatile("" : "+v"(x)); }
+
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t *lds, uint32_t off) {
     return *reinterpret_cast<const uint32_t *>(lds + off);
 }
@@ -62,20 +88,27 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t *lds, uint32_t off) {
 // Byte k of the piece: low nibble row at k*4096 + n*256, high nibble row at
 // 128 + k*256 + n*4096; the lane's column is col*4.  Shifting the dword so
 // the byte sits in bits 8..15 makes both row offsets a single v_and_or.
+// MEMDIAG (diagnostic only): the lookups are skipped.
+template <bool MEMDIAG>
 __device__ __forceinline__ uint32_t piece_lin(const uint8_t *lds, uint4 d, uint32_t col4) {
     uint32_t acc = 0;
     const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
         const uint32_t x = dw[w];
+        if (MEMDIAG) {
+            acc ^= x;
+            continue;
+        }
         const uint32_t xs[4] = {x << 8, x, x >> 8, x >> 16};
+        uint32_t r[8];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const uint32_t k = 4 * w + t;
-            const uint32_t lo = ((xs[t] & 0x0F00u) | col4) + k * 4096u;
-            const uint32_t hi = ((xs[t] & 0xF000u) | col4) + 128u + k * 256u;
-            acc ^= lds_u32(lds, lo) ^ lds_u32(lds, hi);
+            r[2 * t] = lds_u32(lds, ((xs[t] & 0x0F00u) | col4) + k * 4096u);
+            r[2 * t + 1] = lds_u32(lds, ((xs[t] & 0xF000u) | col4) + 128u + k * 256u);
         }
+        acc = xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], acc));
     }
     return acc;
 }
@@ -117,24 +150,30 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 }
 
 // ---- fast path: one wave, 16 blocks of full chunks -----------------------
-// Loads of one tile: instruction i reads 1 KiB contiguous (blocks 2i, 2i+1).
-// Lanes of blocks a partial tile does not have re-read block 0 (always
-// valid memory) and are masked out in finish_tile, so the instruction
-// stream has no divergent branch and the wait counts stay exact.
+// Loads of one tile: instruction i reads 1 KiB contiguous (blocks 2i, 2i+1)
+// through a buffer descriptor whose range is the tile's nb * 512 valid
+// bytes.  Lanes of blocks a partial tile does not have fall outside the range
+// and read zeros without touching memory (lin() of zeros is 0, so they need
+// no mask), every lane uses the same one-VGPR offset plus an immediate, and
+// the instruction stream has no divergent branch.  AUX 2 = non-temporal.
+template <int AUX>
 __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8]) {
     const uint32_t nb = t.meta & 0xffu;
-    const uint32_t h = uint32_t(lane) >> 5;
-    const uint8_t *base = p.payload + t.src;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src), 0, int(nb * 512u), 0x00020000);
+    const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint32_t off = (2u * i + h < nb) ? 1024u * i + 16u * uint32_t(lane) : 16u * uint32_t(lane & 31);
-        v[i] = *reinterpret_cast<const uint4 *>(base + off);
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
+        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
-    // Keep the loads ahead of whatever compute follows (the scheduler would
-    // otherwise hoist the next tile's first lookups above them and wait).
+    // Keep the loads ahead of whatever compute follows.
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// lin() per piece, then reduce to one lin() per block, combine the blocks of
+// each chunk, store the chunk checksums.
+template <bool MEMDIAG>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, FastTile t, const uint4 v[8],
                                             int lane) {
     const uint32_t nb = t.meta & 0xffu;
@@ -144,8 +183,8 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     uint32_t pc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        pc[i] = piece_lin(lds, v[i], col4);
-        pc[i] = (2u * i + h < nb) ? pc[i] : 0u;
+        pc[i] = piece_lin<MEMDIAG>(lds, v[i], col4);
+        opaque(pc[i]);
         // One piece at a time: keeps the scheduler from hoisting every
         // piece's 32 LDS reads together (register pressure -> spills).
         __builtin_amdgcn_sched_barrier(0);
@@ -193,56 +232,11 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     if (rep) p.out[t.out + (blk >> lg)] = out_order(crc, p.flags);
 }
 
-// Grid-stride over fast tiles.  PIPE: the next tile's 8 KiB is in flight
-// (and the descriptor after it requested) while the current one is
-// computed, so each wave keeps HBM busy across its own compute.
-template <bool PIPE>
-__device__ __forceinline__ void fast_loop(const KParams &p, const uint8_t *lds, uint32_t wave, uint32_t nwaves,
-                                          int lane) {
-    // Tiles of this wave: wave, wave + nwaves, ... (n of them).  All loop
-    // control is scalar; tile indices go through readfirstlane so the
-    // compiler keeps them (and the descriptor loads) in SGPRs.
-    const uint32_t n = wave < p.ntiles ? (p.ntiles - 1u - wave) / nwaves + 1u : 0u;
-    auto tile_k = [&](uint32_t k) { return tile_at(p, __builtin_amdgcn_readfirstlane(wave + k * nwaves)); };
-    if (!PIPE) {
-        FastTile t = tile_k(0);
-        for (uint32_t k = 0; k < n; ++k) {
-            uint4 v[8];
-            load_tile(p, t, lane, v);
-            const FastTile tn = tile_k(k + 1 < n ? k + 1 : k);  // prefetch the next descriptor
-            finish_tile(p, lds, t, v, lane);
-            t = tn;
-        }
-        return;
-    }
-    // Two register buffers, unrolled by two so each buffer stays in its own
-    // registers: the other buffer's loads are issued before a buffer is
-    // computed, so its waits are vmcnt(15..8) and 8 KiB stays in flight.
-    // The last one or two tiles are drained outside the loop.
-    if (n == 0) return;
-    uint4 va[8], vb[8];
-    FastTile ta = tile_k(0);
-    load_tile(p, ta, lane, va);
-    uint32_t k = 0;
-    FastTile tb = tile_k(n > 1 ? 1 : 0);
-    while (k + 2 < n) {  // tiles k, k+1, k+2 exist
-        load_tile(p, tb, lane, vb);
-        const FastTile tc = tile_k(k + 2);
-        finish_tile(p, lds, ta, va, lane);
-        load_tile(p, tc, lane, va);
-        const FastTile td = tile_k(k + 3 < n ? k + 3 : k + 2);
-        finish_tile(p, lds, tb, vb, lane);
-        ta = tc;
-        tb = td;
-        k += 2;
-    }
-    if (k + 1 < n) {
-        load_tile(p, tb, lane, vb);
-        finish_tile(p, lds, ta, va, lane);
-        finish_tile(p, lds, tb, vb, lane);
-    } else {
-        finish_tile(p, lds, ta, va, lane);
-    }
+// One tile index from the workgroup's LDS counter (one ds_add_rtn per wave).
+__device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(pool_ctr, 1u);
+    return __builtin_amdgcn_readfirstlane(t);
 }
 
 // ---- general path: half a wave per chunk of any length / alignment -------
@@ -268,9 +262,6 @@ __device__ __forceinline__ void load_piece(uintptr_t a0, uintptr_t cbeg, uintptr
     }
 }
 
-// Bytes sh .. sh+15 of the 32 bytes w[0..7]: a two-stage dword select (by 2,
-// then by 1) and v_alignbyte.  Written out as values so the compiler cannot
-// turn it into an indexed scratch access.
 // Bytes sh .. sh+15 of the 32 bytes w[0..7]: a two-stage dword select (by 2,
 // then by 1) and v_alignbyte.  Written out as values so the compiler cannot
 // turn it into an indexed scratch access.
@@ -308,7 +299,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
             uint32_t w[8];
             load_piece(a0, cbeg, cend, ffend, w);
             load_piece(a0 + 16, cbeg, cend, ffend, w + 4);
-            lin = piece_lin(lds, funnel(w, uint32_t(a & 15u)), q << 2);
+            lin = piece_lin<false>(lds, funnel(w, uint32_t(a & 15u)), q << 2);
         }
         lin = allreduce32(lin);
         if (m < nbv) acc = zshift(lds, 1, acc) ^ lin;
@@ -321,40 +312,88 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
 
 }  // namespace
 
-template <int THREADS, bool PIPE>
-__global__ __launch_bounds__(THREADS, 2 * THREADS / 256) void hdfs_crc32c_plan_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    {
-        // Stage the tables: every load in flight before the first LDS write
-        // (the device copy is zero-padded to kTableAlloc bytes, so no load
-        // needs a guard).
-        constexpr uint32_t kVec = kLdsBytes / 16;
-        constexpr uint32_t kPer = (kVec + THREADS - 1) / THREADS;
-        const uint4 *g = reinterpret_cast<const uint4 *>(p.table);
-        uint4 *sm = reinterpret_cast<uint4 *>(lds);
-        uint4 r[kPer];
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) r[k] = g[threadIdx.x + k * THREADS];
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k)
-            if (threadIdx.x + k * THREADS < kVec) sm[threadIdx.x + k * THREADS] = r[k];
-    }
-    __syncthreads();
-    const int lane = int(threadIdx.x & 63u);
+// THREADS per workgroup, WPS = waves per SIMD the launch bound asks for
+// (= workgroups per CU x THREADS / 256; it caps VGPRs at 512 / WPS).
+template <int THREADS, int WPS, int MODE>
+__global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams p) {
+    constexpr bool NT = (MODE & kModeNt) != 0;
+    constexpr bool EARLY = (MODE & kModeEarly) != 0;
+    constexpr bool STAMPS = (MODE & kModeStamps) != 0;
+    constexpr bool MEMDIAG = (MODE & kModeMemDiag) != 0;
+    constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    // One LDS array: the tables, then the workgroup's tile counter.
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + 16];
+    uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStageBytes);
+    const int lane = int(threadIdx.x & 63u);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
+
+    // Diagnostic build only (STAMPS): per-wave s_memrealtime stamps at start,
+    // after table staging and at exit, plus HW_ID / XCC_ID, written to a
+    // buffer nothing else reads.  Production variants contain no stamp.
+    uint64_t t_start = 0, t_staged = 0;
+    if (STAMPS) t_start = __builtin_amdgcn_s_memrealtime();
+
+    // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
+    // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
+    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
+    uint32_t t = tbeg + wv;
+    FastTile ft{0, 0, 0};
+    uint4 v[8];
+    // EARLY: request the first tile before the table staging, so its HBM
+    // latency overlaps the 73 KiB L2 -> LDS copy.
+    if (EARLY && t < tend) {
+        ft = tile_at(p, t);
+        load_tile<AUX>(p, ft, lane, v);
+    }
+    // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
+    for (uint32_t c = wv; c < kStageBytes / 1024u; c += kWaves)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)(p.table + c * 1024u + 16u * uint32_t(lane)),
+            (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+    __syncthreads();
+    if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
+
+    if (!EARLY && t < tend) {
+        ft = tile_at(p, t);
+        load_tile<AUX>(p, ft, lane, v);
+    }
+    while (t < tend) {
+        finish_tile<MEMDIAG>(p, lds, ft, v, lane);
+        t = pool_grab(pool_ctr, lane);
+        if (t >= tend) break;
+        ft = tile_at(p, t);
+        load_tile<AUX>(p, ft, lane, v);
+    }
+
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
     const uint32_t nwaves = gridDim.x * kWaves;
-    fast_loop<PIPE>(p, lds, wave, nwaves, lane);
     const uint32_t npairs = (p.ngen + 1u) >> 1;
     for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair(p, lds, g, lane);
+    if (STAMPS && lane == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+        p.stamps[4 * wave + 0] = t_start;
+        p.stamps[4 * wave + 1] = t_staged;
+        p.stamps[4 * wave + 2] = t_end;
+        p.stamps[4 * wave + 3] = (uint64_t(xcc_id) << 32) | hw_id;
+    }
 }
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"wg512_pipe", 512, true},
-    {"wg512_plain", 512, false},
-    {"wg1024_plain", 1024, false},
+    {"wg1024_pool_nt_early", 1024, 2},          // production
+    {"wg1024_pool_nt", 1024, 2},                // A/B: no early first tile
+    {"wg1024_pool", 1024, 2},                   // A/B: default-policy loads
+    {"wg1024_pool_nt_early_stamps", 1024, 2},   // DIAGNOSTIC: timestamps
+    {"wg1024_pool_nt_early_memonly", 1024, 2},  // DIAGNOSTIC: wrong results, memory ceiling
+    {"wg512_pool_nt_early", 512, 2},            // A/B: 16 waves per CU
 };
+
+#define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
 
 hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream) {
     if (variant < 0 || variant >= kNumVariants) variant = 0;
@@ -362,20 +401,19 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
     const uint64_t waves = uint64_t(kv.threads / 64);
     uint64_t grid = (items + waves - 1) / waves;
-    const uint64_t cap = uint64_t(num_cu) * kKernelWgPerCu;
+    const uint64_t cap = uint64_t(num_cu) * kv.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
+    const dim3 g{uint32_t(grid), 1, 1}, b{kv.threads, 1, 1};
     switch (variant) {
-    case 1:
-        hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<512, false>), dim3(uint32_t(grid)), dim3(512), 0, stream, p);
-        break;
-    case 2:
-        hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<1024, false>), dim3(uint32_t(grid)), dim3(1024), 0, stream, p);
-        break;
-    default:
-        hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<512, true>), dim3(uint32_t(grid)), dim3(512), 0, stream, p);
-        break;
+    case 1: HDFS_LAUNCH(1024, 8, kModeNt); break;
+    case 2: HDFS_LAUNCH(1024, 8, 0); break;
+    case 3: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly | kModeStamps); break;
+    case 4: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly | kModeMemDiag); break;
+    case 5: HDFS_LAUNCH(512, 4, kModeNt | kModeEarly); break;
+    default: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly); break;
     }
     return hipGetLastError();
 }
+#undef HDFS_LAUNCH
 }  // namespace hdfs_crc

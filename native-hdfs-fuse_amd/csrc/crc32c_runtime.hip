@@ -112,6 +112,7 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
     p.flags = flags;
     std::memcpy(p.c_lg, ctx->c_lg, sizeof p.c_lg);
     std::memcpy(p.c_small, ctx->c_small, sizeof p.c_small);
+    p.stamps = nullptr;
     return p;
 }
 
@@ -363,6 +364,18 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
     const KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload,
                                  dev_out, plan->flags);
     return launch(plan->ctx, p, static_cast<hipStream_t>(stream));
+}
+
+int crc32c_debug_plan_exec_stamped(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
+                                   uint64_t *dev_stamps, void *stream) {
+    if (!plan || !dev_stamps) return fail(-EINVAL, "plan/stamps == NULL");
+    if (plan->nchecksums == 0) return 0;
+    DeviceGuard guard(plan->ctx->device);
+    KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, dev_out,
+                           plan->flags);
+    p.stamps = dev_stamps;
+    HIP_TRY(launch_plan_kernel(p, 3, uint32_t(plan->ctx->num_cu), static_cast<hipStream_t>(stream)));  // stamps variant
+    return 0;
 }
 
 int crc32c_plan_destroy(crc32c_plan *plan) {

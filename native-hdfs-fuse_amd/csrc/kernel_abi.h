@@ -26,16 +26,17 @@ struct KParams {
     uint32_t flags;
     uint32_t c_lg[5];
     uint32_t c_small[4];
+    uint64_t *stamps;  // diagnostic variant only: 4 x u64 per wave
 };
 
-// Kernel variants (workgroup size x software pipelining); 0 is the default,
-// the others stay built for A/B measurement (tools/kbench.py).
+// Kernel variants; 0 is the production kernel, the others stay built for
+// A/B measurement and diagnostics (tools/kbench.py, tools/stamps.py).
 struct KernelVariant {
     const char *name;
     uint32_t threads;
-    bool pipelined;
+    uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 3;
+constexpr int kNumVariants = 6;
 extern const KernelVariant kVariants[kNumVariants];
 
 // Persistent grid: min(work items / waves per workgroup, kKernelWgPerCu * CUs).

@@ -24,6 +24,8 @@ for s in $STEPS; do
     tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench5) run bench5 600 python bench.py --config c5 --no-cpu ;;
+    pmc) run pmc 1100 bash tools/pmc_session.sh ;;
+    stamps) run stamps 300 python tools/stamps.py c2 ;;
     kbench) run kbench 600 python tools/kbench.py --config c2 ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-wave timeline of the CRC32C kernel from the stamped
+variant (s_memrealtime, 100 MHz).  Prints start/staging/end distributions
+(us, relative to the first wave start) overall and per XCD.  Stamps are only
+in the diagnostic build's buffer; read the SHARES, not the length."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    import torch
+
+    import oracle
+    from bench import config_packets, load_package
+
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    hdfs = load_package()
+    pk, _ = config_packets(cfg, oracle)
+    extent = int((pk["payload_off"] + pk["len"]).max())
+    nout = hdfs.total_checksums(pk)
+    dev = torch.device("cuda", 0)
+    bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev) for _ in range(4)]
+    out = torch.zeros(nout, dtype=torch.int32, device=dev)
+    os.environ["HDFS_CRC32C_KVARIANT"] = "2"
+    ctx = hdfs.Context(0)
+    plan = ctx.plan(pk)
+    stamps = torch.zeros(4 * 256 * 2 * 16, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    res = []
+    for rep in range(4):
+        for b in range(3):
+            plan.exec(bufs[b].data_ptr(), out.data_ptr(), s)
+        stamps.zero_()
+        plan.exec_stamped(bufs[3].data_ptr(), out.data_ptr(), stamps.data_ptr(), s)
+        torch.cuda.synchronize()
+        st = stamps.cpu().numpy().reshape(-1, 4)
+        st = st[st[:, 0] != 0]
+        t0 = st[:, 0].min()
+        start = (st[:, 0] - t0) / 100.0
+        staged = (st[:, 1] - t0) / 100.0
+        end = (st[:, 2] - t0) / 100.0
+        xcc = (st[:, 3] >> 32) & 0xF
+        q = lambda a: [round(float(np.percentile(a, x)), 2) for x in (0, 10, 50, 90, 100)]
+        wg = np.arange(st.shape[0]) // 16
+        cu = (xcc << 16) | ((st[:, 3] & 0xFFFFFFFF) >> 8)
+        wg_end = {}
+        wg_cu = {}
+        for w in np.unique(wg):
+            m = wg == w
+            wg_end[int(w)] = (float(end[m].min()), float(end[m].max()))
+            wg_cu[int(w)] = int(cu[m][0])
+        spread_in_wg = [b - a for a, b in wg_end.values()]
+        by_cu = {}
+        for w, c in wg_cu.items():
+            by_cu.setdefault(c, []).append(wg_end[w][1])
+        pair_gap = [max(v) - min(v) for v in by_cu.values() if len(v) == 2]
+        res.append({
+            "wg_end_spread_us_pct": q(np.array(spread_in_wg)),
+            "cu_pair_end_gap_us_pct": q(np.array(pair_gap)) if pair_gap else None,
+            "wgs_per_cu": sorted(set(len(v) for v in by_cu.values())),
+            "cu_last_end_us_pct": q(np.array([max(v) for v in by_cu.values()])),
+            "waves": int(st.shape[0]), "span_us": round(float(end.max()), 2),
+            "start_us_pct": q(start), "staging_us_pct": q(staged - start), "work_us_pct": q(end - staged),
+            "end_us_pct": q(end),
+            "per_xcd_end_max": [round(float(end[xcc == x].max()), 2) if np.any(xcc == x) else None for x in range(8)],
+            "per_xcd_waves": [int(np.sum(xcc == x)) for x in range(8)],
+        })
+    print(json.dumps({"config": cfg, "runs": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
