@@ -27,11 +27,14 @@ int crc32c_debug_plan(const crc32c_packet *pkts, size_t npkts, void *tiles, size
  * lg = 0..4, and crc32c(0, zeros(r)), r = 0..3. */
 size_t crc32c_debug_lds_image(void *dst, size_t cap, uint32_t *c_lg5, uint32_t *c_small4);
 
-/* Diagnostic launch of a plan with per-wave timestamps (4 x u64 per wave:
- * s_memrealtime at start, after table staging, at exit; XCC_ID << 32 |
- * HW_ID).  dev_stamps must hold 4 * (waves launched) entries. */
-int crc32c_debug_plan_exec_stamped(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
-                                   uint64_t *dev_stamps, void *stream);
+/* Diagnostic launch of a plan with an explicit kernel variant (see
+ * kernel_abi.h kVariants; variants 3 and 6 write per-wave timestamps,
+ * 4 x u64 per wave: s_memrealtime at start, after table staging, at exit;
+ * XCC_ID << 32 | HW_ID, into dev_stamps, which must then hold 4 * (waves
+ * launched) entries; variants 4 and 6 compute WRONG checksums on purpose
+ * (memory-only ceiling)). */
+int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
+                                   uint64_t *dev_stamps, int variant, void *stream);
 
 /* DIAGNOSTIC: plain streaming read of `bytes` device bytes (grid x 256
  * threads, grid-stride, 16 B per lane; shape 0/1/3 = 4/8/16 loads in flight

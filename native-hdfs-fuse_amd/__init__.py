@@ -95,7 +95,7 @@ def _bind(L):
         "crc32c_last_error": (ctypes.c_char_p, []),
         "crc32c_debug_plan": (i32, [vp, sz, vp, sz, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_debug_lds_image": (sz, [vp, sz, vp, vp]),
-        "crc32c_debug_plan_exec_stamped": (i32, [vp, vp, vp, vp, vp]),
+        "crc32c_debug_plan_exec_variant": (i32, [vp, vp, vp, vp, i32, vp]),
         "crc32c_debug_stream_probe": (i32, [vp, u64, vp, u32, i32, vp]),
     }
     for name, (res, args) in sig.items():
@@ -203,11 +203,11 @@ class Plan:
         _check(lib().crc32c_plan_exec(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
                                       ctypes.c_void_p(stream)), "crc32c_plan_exec")
 
-    def exec_stamped(self, dev_payload: int, dev_out: int, dev_stamps: int, stream: int = 0) -> None:
-        """Diagnostic: run the stamped kernel variant (per-wave timestamps)."""
-        _check(lib().crc32c_debug_plan_exec_stamped(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
-                                                    ctypes.c_void_p(dev_stamps), ctypes.c_void_p(stream)),
-               "crc32c_debug_plan_exec_stamped")
+    def exec_variant(self, dev_payload: int, dev_out: int, variant: int, dev_stamps: int = 0, stream: int = 0) -> None:
+        """Diagnostic: run an explicit kernel variant (3/6 write per-wave timestamps)."""
+        _check(lib().crc32c_debug_plan_exec_variant(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
+                                                    ctypes.c_void_p(dev_stamps), variant, ctypes.c_void_p(stream)),
+               "crc32c_debug_plan_exec_variant")
 
     def close(self) -> None:
         if self.handle:

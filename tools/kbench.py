@@ -42,10 +42,15 @@ def main():
     g.manual_seed(7)
     bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g) for _ in range(args.nbuf)]
     outs = [torch.zeros(nout, dtype=torch.int32, device=dev) for _ in range(args.nbuf)]
-    variants = [int(v) for v in args.variants.split(",")]
+    # "V" or "V:T" (T = $HDFS_CRC32C_THROTTLE for that context)
+    variants = args.variants.split(",")
     plans = {}
     for v in variants:
-        os.environ["HDFS_CRC32C_KVARIANT"] = str(v)
+        os.environ["HDFS_CRC32C_KVARIANT"] = v.split(":")[0]
+        if ":" in v:
+            os.environ["HDFS_CRC32C_THROTTLE"] = v.split(":")[1]
+        else:
+            os.environ.pop("HDFS_CRC32C_THROTTLE", None)
         ctx = hdfs.Context(0)
         plans[v] = (ctx, ctx.plan(pk))
     stream = torch.cuda.current_stream()
@@ -57,7 +62,7 @@ def main():
         if ref is None:
             ref = got
         if not np.array_equal(got, ref):
-            print("note: variant %d checksums differ (diagnostic variant?)" % v, file=sys.stderr)
+            print("note: variant %s checksums differ (diagnostic variant?)" % v, file=sys.stderr)
     times = {v: [] for v in variants}
     for r in range(args.rounds):
         for v in variants:

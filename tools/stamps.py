@@ -21,6 +21,7 @@ def main():
     from bench import config_packets, load_package
 
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 3  # 3 = production + stamps, 6 = memory-only + stamps
     hdfs = load_package()
     pk, _ = config_packets(cfg, oracle)
     extent = int((pk["payload_off"] + pk["len"]).max())
@@ -34,11 +35,15 @@ def main():
     stamps = torch.zeros(4 * 256 * 2 * 16, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     res = []
+    # placement: which CU / XCD each workgroup ran on (from run 0)
+    placement = None
+    cu_ends = []  # per run: {cu key: last end}
+    wg_ends = []  # per run: per-workgroup last end, by blockIdx
     for rep in range(4):
         for b in range(3):
             plan.exec(bufs[b].data_ptr(), out.data_ptr(), s)
         stamps.zero_()
-        plan.exec_stamped(bufs[3].data_ptr(), out.data_ptr(), stamps.data_ptr(), s)
+        plan.exec_variant(bufs[3].data_ptr(), out.data_ptr(), variant, stamps.data_ptr(), s)
         torch.cuda.synchronize()
         st = stamps.cpu().numpy().reshape(-1, 4)
         st = st[st[:, 0] != 0]
@@ -49,7 +54,9 @@ def main():
         xcc = (st[:, 3] >> 32) & 0xF
         q = lambda a: [round(float(np.percentile(a, x)), 2) for x in (0, 10, 50, 90, 100)]
         wg = np.arange(st.shape[0]) // 16
-        cu = (xcc << 16) | ((st[:, 3] & 0xFFFFFFFF) >> 8)
+        # HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]; tg_id [19:16] is the
+        # workgroup slot on the CU and must not split one CU into several.
+        cu = (xcc << 16) | (((st[:, 3] & 0xFFFFFFFF) >> 8) & 0xFF)
         wg_end = {}
         wg_cu = {}
         for w in np.unique(wg):
@@ -61,6 +68,10 @@ def main():
         for w, c in wg_cu.items():
             by_cu.setdefault(c, []).append(wg_end[w][1])
         pair_gap = [max(v) - min(v) for v in by_cu.values() if len(v) == 2]
+        cu_ends.append({c: max(v) for c, v in by_cu.items()})
+        if placement is None:
+            placement = [wg_cu[w] for w in sorted(wg_cu)]
+        wg_ends.append(np.array([wg_end[w][1] for w in sorted(wg_end)]))
         res.append({
             "wg_end_spread_us_pct": q(np.array(spread_in_wg)),
             "cu_pair_end_gap_us_pct": q(np.array(pair_gap)) if pair_gap else None,
@@ -72,7 +83,20 @@ def main():
             "per_xcd_end_max": [round(float(end[xcc == x].max()), 2) if np.any(xcc == x) else None for x in range(8)],
             "per_xcd_waves": [int(np.sum(xcc == x)) for x in range(8)],
         })
-    print(json.dumps({"config": cfg, "runs": res}, indent=1))
+    # Is a slow CU slow in every run (a property of the CU) or at random?
+    keys = sorted(set.intersection(*[set(d) for d in cu_ends]))
+    m = np.array([[d[k] for k in keys] for d in cu_ends])
+    cc = np.corrcoef(m)
+    wcc = np.corrcoef(np.array([w for w in wg_ends if len(w) == len(wg_ends[0])]))
+    xcd_of = np.array([k >> 16 for k in keys])
+    extra = {"cu_end_corr_between_runs": [round(float(x), 3) for x in cc[np.triu_indices(len(cc), 1)]],
+             "wg_end_corr_between_runs": [round(float(x), 3) for x in wcc[np.triu_indices(len(wcc), 1)]],
+             "cu_mean_end_by_xcd": [round(float(m[:, xcd_of == x].mean()), 2) for x in range(8)],
+             "wg_end_by_blockidx_mod8": [round(float(np.mean([w[i::8].mean() for w in wg_ends])), 2) for i in range(8)],
+             "placement_first_40": [hex(c) for c in placement[:40]],
+             "placement_256_280": [hex(c) for c in placement[256:280]],
+             "wg_end_by_blockidx_decile": [round(float(np.mean([w[i * len(w) // 10:(i + 1) * len(w) // 10].mean() for w in wg_ends])), 2) for i in range(10)]}
+    print(json.dumps({"config": cfg, "variant": variant, "runs": res, "analysis": extra}, indent=1))
 
 
 if __name__ == "__main__":
