@@ -39,8 +39,9 @@ KERNEL_NAME = "hdfs_crc32c_plan_kernel"
 def load_package():
     if "hdfs_crc32c_amd" in sys.modules:
         return sys.modules["hdfs_crc32c_amd"]
-    spec = importlib.util.spec_from_file_location(
-        "hdfs_crc32c_amd", os.path.join(ROOT, "native-hdfs-fuse_amd", "__init__.py"))
+    pkg_dir = os.path.join(ROOT, "native-hdfs-fuse_amd")
+    spec = importlib.util.spec_from_file_location("hdfs_crc32c_amd", os.path.join(pkg_dir, "__init__.py"),
+                                                  submodule_search_locations=[pkg_dir])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["hdfs_crc32c_amd"] = mod
     spec.loader.exec_module(mod)
@@ -60,10 +61,13 @@ def config_packets(name: str, oracle_mod):
     raise SystemExit("unknown config " + name)
 
 
-def c4_rank_packets(oracle_mod, rank: int, world: int):
-    blocks = [b for b in range(32) if b % world == rank]
-    pk = oracle_mod.uniform_packets(64 * len(blocks))
-    return pk, blocks
+def reference_checksums(oracle_mod, payload: np.ndarray, pk, nout: int) -> np.ndarray:
+    """Expected checksums from the reference's crc32c.c (oracle/_ref) when it
+    is built, else the clean-room oracle; multi-threaded over packets."""
+    impl = oracle_mod.Reference() if oracle_mod.Reference.available() else oracle_mod.Oracle()
+    out = np.zeros(max(nout, 1), np.uint32)
+    impl.batch_mt_seconds(payload, pk, out, max(1, min(16, os.cpu_count() or 1)), 1)
+    return out[:nout]
 
 
 def baseline_metric() -> str:
@@ -150,8 +154,13 @@ def main():
     hdfs = load_package()
     hdfs.lib()
 
+    from hdfs_crc32c_amd import shard
+
+    c4_blocks = None
     if args.config == "c4":
-        pk, _blocks = c4_rank_packets(oracle, rank, world)
+        # 128 MiB file = 32 x 4 MiB blocks, block b on rank b mod world
+        c4_blocks = shard.rank_blocks(32, world, rank)
+        pk = oracle.uniform_packets(64 * len(c4_blocks))
         workload = "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
         nbuf = 1
     else:
@@ -166,7 +175,11 @@ def main():
     dev = torch.device("cuda", local_rank)
     # buffer 0: the documented xorshift64 stream (checked against the CPU
     # path below); the rest: device-generated random bytes.
-    payload0 = oracle.xorshift64_bytes(extent, oracle.SEED + rank)
+    if c4_blocks is not None:
+        file_bytes = oracle.xorshift64_bytes(32 * shard.BLOCK_BYTES, oracle.SEED)
+        payload0 = shard.rank_payload(file_bytes, c4_blocks)
+    else:
+        payload0 = oracle.xorshift64_bytes(extent, oracle.SEED + rank)
     bufs = [torch.from_numpy(payload0).to(dev)]
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -183,7 +196,7 @@ def main():
     # correctness gate (outside the timed region): every buffer-0 checksum
     step(0)
     torch.cuda.synchronize()
-    want = (oracle.Reference() if oracle.Reference.available() else oracle.Oracle()).batch(payload0, pk, nout)
+    want = reference_checksums(oracle, payload0, pk, nout)
     got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
     bit_exact = bool(np.array_equal(got0, want))
 
@@ -215,15 +228,28 @@ def main():
         ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         bit_exact = bool(ok.item())
-        # RCCL gather of every rank's checksum array to rank 0 (the path's only exchange)
+    # RCCL gather of every rank's checksum array to rank 0 (the path's only
+    # exchange; timed on its own, outside the kernel's timed region).  For
+    # config 4 rank 0 reassembles the file's checksums in block order and
+    # checks them against the reference over the whole 128 MiB file.
+    gather_ms = None
+    if world > 1 or c4_blocks is not None:
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        gathered = [torch.empty_like(outs[0]) for _ in range(world)] if rank == 0 else None
-        dist.gather(outs[0], gathered, dst=0)
+        if c4_blocks is not None:
+            per_block = 64 * 128
+            full = shard.gather_checksums(outs[0][:nout], 32, per_block, world, rank)
+        else:
+            gathered = [torch.empty_like(outs[0]) for _ in range(world)] if rank == 0 and world > 1 else None
+            if world > 1:
+                dist.gather(outs[0], gathered, dst=0)
+            full = None
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
-    else:
-        gather_ms = None
+        gather_ms = (time.perf_counter() - g0) * 1e3 if world > 1 else None
+        if c4_blocks is not None and rank == 0:
+            whole = oracle.uniform_packets(64 * 32)
+            bit_exact = bit_exact and bool(np.array_equal(full, reference_checksums(oracle, file_bytes, whole,
+                                                                                     64 * 32 * 128)))
 
     total_bytes = nbytes * world * args.steps
     value = total_bytes / elapsed / GIB

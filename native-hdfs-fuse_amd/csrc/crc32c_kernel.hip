@@ -48,22 +48,14 @@ constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
 constexpr uint32_t kStageBytes = (kLdsBytes + 1023u) / 1024u * 1024u;
 static_assert(kStageBytes <= hdfs_crc::kTableAlloc, "staging reads past the device table");
 
-// Kernel modes (template bits).  Production = kModeNt | kModeEarly.
-constexpr int kModeNt = 1;        // payload loads non-temporal (streamed once)
-constexpr int kModeEarly = 2;     // first tile requested before the table staging
-constexpr int kModeStamps = 4;    // DIAGNOSTIC: per-wave timestamps
-constexpr int kModeMemDiag = 8;   // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
-constexpr int kModePipe = 16;     // two tiles per wave: the next tile's loads fly during this tile's lookups
-constexpr int kModeSweep = 32;    // workgroup w takes tiles w, w + G, w + 2G, ...: the chip sweeps memory in order
-constexpr int kModeReverse = 128;  // DIAGNOSTIC: workgroup w takes the range of G - 1 - w
-constexpr int kModeQueue = 64;    // cross-CU balance: chunks from per-XCD queue heads, stealing when drained
-constexpr int kModeValuDiag = 4096;  // DIAGNOSTIC, wrong results: lookup address math only, no LDS reads
-constexpr int kModeLdsDiag = 8192;   // DIAGNOSTIC, wrong results: LDS reads at fixed addresses
-constexpr int kModeCompDiag = 2048;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
-constexpr int kModeEarly2 = 1024;   // first tile requested right BEHIND the table staging, before the barrier
-constexpr int kModeThrottle = 512;  // at most p.throttle tiles of a workgroup in flight (LDS semaphore)
-constexpr int kModeGroup = 256;   // G/2 pairs of workgroups (w, w + G/2: the two on one CU) share one tile range
-                                  // through a global counter; each wave prefetches its next ticket
+// Kernel modes (template bits).  Production = kModeNt.
+constexpr int kModeNt = 1;         // payload loads non-temporal (streamed once)
+constexpr int kModeEarly = 2;      // A/B: first tile requested before the table staging
+constexpr int kModeStamps = 4;     // DIAGNOSTIC: per-wave timestamps
+constexpr int kModeMemDiag = 8;    // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
+constexpr int kModeCompDiag = 16;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
+constexpr int kModeValuDiag = 32;  // DIAGNOSTIC, wrong results: lookup address math only, no LDS reads
+constexpr int kModeLdsDiag = 64;   // DIAGNOSTIC, wrong results: LDS reads at fixed addresses
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -265,76 +257,6 @@ __device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
     return __builtin_amdgcn_readfirstlane(t);
 }
 
-// ---- cross-CU work queue (kModeQueue) -------------------------------------
-// Static per-workgroup ranges leave CUs finishing up to 2x apart (the memory
-// system does not serve CUs evenly).  Instead the tiles are cut into chunks
-// of U = 1 << chunk_shift consecutive tiles; XCD x owns a contiguous 1/8 of
-// the chunks behind its own head counter (one device-scope atomic per chunk,
-// sharded per XCD as MI355X_MICROARCH.md 'dequeue' prescribes) and a
-// workgroup whose XCD is drained steals from the next XCDs' heads.  Inside a
-// workgroup, waves take tiles from an LDS ticket counter: ticket k is tile
-// k mod U of the workgroup's (k / U)-th chunk, whose id sits in an LDS ring
-// entry stamped with its sequence number.  The wave that takes the first
-// ticket of chunk s fetches chunk s + 1, so a fetch overlaps a whole chunk of
-// work; every chunk a ticket refers to is therefore fetched by someone.
-constexpr uint32_t kNoChunk = 0xffffffffu;
-constexpr uint32_t kSlotWordsK = hdfs_crc::kSlotWords;
-constexpr uint32_t kRing = 64;  // a wrap needs 63 chunks taken while one fetch is pending
-
-struct QueueLds {
-    uint64_t ring[kRing];  // (sequence << 32) | chunk id
-    uint32_t ticket;
-    uint32_t exhausted;    // bit x: XCD x's head is drained
-};
-
-// One lane: the next chunk for this workgroup, or kNoChunk.
-__device__ uint32_t queue_fetch(const KParams &p, QueueLds *q, uint32_t nchunks, uint32_t xcc) {
-    uint32_t mask = __atomic_load_n(&q->exhausted, __ATOMIC_RELAXED);
-    for (uint32_t k = 0; k < 8; ++k) {
-        const uint32_t x = (xcc + k) & 7u;
-        if (mask & (1u << x)) continue;
-        const uint32_t lo = uint32_t(uint64_t(nchunks) * x / 8u);
-        const uint32_t hi = uint32_t(uint64_t(nchunks) * (x + 1u) / 8u);
-        if (hi > lo) {
-            const uint32_t c = atomicAdd(p.queue + 32u * x, 1u);
-            if (c < hi - lo) return lo + c;
-        }
-        mask |= 1u << x;
-        atomicOr(&q->exhausted, 1u << x);
-    }
-    return kNoChunk;
-}
-
-__device__ __forceinline__ void ring_put(QueueLds *q, uint32_t seq, uint32_t chunk) {
-    __atomic_store_n(&q->ring[seq % kRing], (uint64_t(seq) << 32) | chunk, __ATOMIC_RELAXED);
-}
-
-// Next tile for this wave, or ntiles when the queue is drained.
-__device__ uint32_t queue_grab(const KParams &p, QueueLds *q, uint32_t nchunks, uint32_t xcc, int lane) {
-    const uint32_t sh = p.chunk_shift;
-    for (;;) {
-        uint32_t k = 0;
-        if (lane == 0) k = atomicAdd(&q->ticket, 1u);
-        k = __builtin_amdgcn_readfirstlane(k);
-        const uint32_t seq = k >> sh, i = k & ((1u << sh) - 1u);
-        if (i == 0 && seq >= 1) {  // chunks 0 and 1 are fetched at start
-            if (lane == 0) ring_put(q, seq + 1u, queue_fetch(p, q, nchunks, xcc));
-        }
-        uint64_t e;
-        for (;;) {
-            e = __atomic_load_n(&q->ring[seq % kRing], __ATOMIC_RELAXED);
-            const uint32_t es = __builtin_amdgcn_readfirstlane(uint32_t(e >> 32));
-            if (es == seq) break;
-            if (es != ~0u && es > seq) return p.ntiles;  // overwritten (cannot happen, see kRing): never spin forever
-            __builtin_amdgcn_s_sleep(1);
-        }
-        const uint32_t c = __builtin_amdgcn_readfirstlane(uint32_t(e));
-        if (c == kNoChunk) return p.ntiles;
-        const uint32_t t = (c << sh) + i;
-        if (t < p.ntiles) return t;  // else: past the end of the last (partial) chunk
-    }
-}
-
 // ---- general path: half a wave per chunk of any length / alignment -------
 __device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
     return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
@@ -415,23 +337,13 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool NT = (MODE & kModeNt) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
-    constexpr bool MEMDIAG = (MODE & kModeMemDiag) != 0;
-    constexpr int DIAG = MEMDIAG ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
-    constexpr bool PIPE = (MODE & kModePipe) != 0;
-    constexpr bool SWEEP = (MODE & kModeSweep) != 0;
-    constexpr bool QUEUE = (MODE & kModeQueue) != 0;
-    constexpr bool GROUP = (MODE & kModeGroup) != 0;
-    constexpr bool THROTTLE = (MODE & kModeThrottle) != 0;
-    constexpr bool EARLY2 = (MODE & kModeEarly2) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
-    const uint32_t wgr = (MODE & kModeReverse) ? gridDim.x - 1u - blockIdx.x : blockIdx.x;  // range owned
+    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     // One LDS array: the tables, then the workgroup's tile counter.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + (QUEUE ? sizeof(QueueLds) : 16)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + 16];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStageBytes);
-    uint32_t *landed = pool_ctr + 1;  // THROTTLE: tiles of this workgroup whose loads have landed
-    QueueLds *qs = reinterpret_cast<QueueLds *>(lds + kStageBytes);
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
 
@@ -443,161 +355,41 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    // SWEEP: the range is over the workgroup's OWN sequence j -> j * G + w.
-    const uint32_t tbeg = SWEEP ? 0u : uint32_t((uint64_t(p.ntiles) * wgr) / gridDim.x);
-    const uint32_t tend = SWEEP ? (p.ntiles > blockIdx.x ? (p.ntiles - blockIdx.x + gridDim.x - 1u) / gridDim.x : 0u)
-                                : uint32_t((uint64_t(p.ntiles) * (wgr + 1)) / gridDim.x);
-    const auto tile_of = [&](uint32_t j) -> FastTile {
-        return tile_at(p, SWEEP ? j * gridDim.x + blockIdx.x : j);
-    };
-    if (threadIdx.x == 0) {
-        *pool_ctr = tbeg + kWaves;
-        *landed = 0;
-    }
-    // THROTTLE: tile j (of the range) may be requested once tiles
-    // 0 .. j - throttle have landed.  The tile of the lowest index not yet
-    // requested can always go, so this never deadlocks.
-    const auto throttle_wait = [&](uint32_t tile) {
-        if (!THROTTLE) return;
-        const uint32_t j = tile - tbeg;
-        if (j < p.throttle) return;
-        for (;;) {
-            const uint32_t l = __builtin_amdgcn_readfirstlane(__atomic_load_n(landed, __ATOMIC_RELAXED));
-            if (l + p.throttle > j) return;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    };
-    const auto throttle_landed = [&]() {
-        if (THROTTLE && lane == 0) atomicAdd(landed, 1u);
-    };
+    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
     uint32_t t = tbeg + wv;
     FastTile ft{0, 0, 0};
     uint4 v[8];
-    // EARLY: request the first tile before the table staging, so its HBM
-    // latency overlaps the 73 KiB L2 -> LDS copy.
+    // EARLY (A/B): request the first tile before the table staging.
     if (EARLY && t < tend) {
-        ft = tile_of(t);
+        ft = tile_at(p, t);
         load_tile<AUX, COMPDIAG>(p, ft, lane, v);
-    }
-    uint32_t nchunks = 0, xcc = 0;
-    if (QUEUE) {
-        nchunks = (p.ntiles + (1u << p.chunk_shift) - 1u) >> p.chunk_shift;
-        xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;  // HW_REG_XCC_ID
-        if (threadIdx.x == 0) {
-            qs->ticket = 0;
-            qs->exhausted = 0;
-            for (uint32_t r = 2; r < kRing; ++r) qs->ring[r] = ~uint64_t(0);
-            ring_put(qs, 0, queue_fetch(p, qs, nchunks, xcc));
-            ring_put(qs, 1, queue_fetch(p, qs, nchunks, xcc));
-        }
     }
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
     for (uint32_t c = wv; c < kStageBytes / 1024u; c += kWaves)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void *)(p.table + c * 1024u + 16u * uint32_t(lane)),
             (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
-    if (EARLY2) {
-        // The first tile's loads queue up behind this wave's staging loads:
-        // wait for all but those 8 (vmcnt counts in issue order), then a bare
-        // barrier (no __syncthreads: its fence would wait for the tile too).
-        if (t < tend) {
-            ft = tile_of(t);
-            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
-        }
-        __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8) expcnt(7) lgkmcnt(15)
-        __builtin_amdgcn_s_barrier();
-    } else {
-        __syncthreads();
-    }
+    __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY && !EARLY2 && !QUEUE && !GROUP && t < tend) {
-        ft = tile_of(t);
-        throttle_wait(t);
+    if (!EARLY && t < tend) {
+        ft = tile_at(p, t);
         load_tile<AUX, COMPDIAG>(p, ft, lane, v);
     }
-    if (GROUP) {
-        // Pair g = w mod ngroups owns tiles [gbeg, gend); its counter is
-        // word g of this launch's slot.  The next ticket's atomic is issued
-        // behind the current tile's loads, so its ~1 us round trip hides
-        // under them.  This launch also clears the slot 32 launches ahead.
-        const uint32_t ngroups = (gridDim.x + 1u) / 2u;
-        const uint32_t g = blockIdx.x % ngroups;
-        const uint32_t gbeg = uint32_t((uint64_t(p.ntiles) * g) / ngroups);
-        const uint32_t gend = uint32_t((uint64_t(p.ntiles) * (g + 1)) / ngroups);
-        uint32_t *ctr = p.queue + 32u * g;
-        if (blockIdx.x == 0 && threadIdx.x < kSlotWordsK) p.queue_next[32u * threadIdx.x] = 0;
-        uint32_t tk = 0;
-        if (lane == 0) tk = atomicAdd(ctr, 1u);
-        t = gbeg + __builtin_amdgcn_readfirstlane(tk);
-        while (t < gend) {
-            ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
-            uint32_t nx = 0;
-            if (lane == 0) nx = atomicAdd(ctr, 1u);
-            finish_tile<DIAG>(p, lds, ft, v, lane);
-            opaque(nx);  // first use of the ticket: its wait lands here, not before the lookups
-            t = gbeg + __builtin_amdgcn_readfirstlane(nx);
-        }
-    } else if (QUEUE) {
-        for (;;) {
-            t = queue_grab(p, qs, nchunks, xcc, lane);
-            if (t >= p.ntiles) break;
-            ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
-            finish_tile<DIAG>(p, lds, ft, v, lane);
-        }
-    } else if (PIPE) {
-        // Two register tiles per wave (a, b): one is always in flight while
-        // the other is looked up, so the CU keeps HBM requests outstanding
-        // through its LDS-bound phases.  Needs ~100 VGPRs: 4 waves per SIMD.
-        uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
-        FastTile fb{0, 0, 0};
-        uint4 vb[8];
-        if (tb < tend) {
-            fb = tile_of(tb);
-            load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
-        }
-        while (t < tend) {
-            finish_tile<DIAG>(p, lds, ft, v, lane);
-            if (tb >= tend) break;
-            t = pool_grab(pool_ctr, lane);
-            if (t < tend) {
-                ft = tile_of(t);
-                load_tile<AUX, COMPDIAG>(p, ft, lane, v);
-            }
-            finish_tile<DIAG>(p, lds, fb, vb, lane);
-            if (t >= tend) break;
-            tb = pool_grab(pool_ctr, lane);
-            if (tb < tend) {
-                fb = tile_of(tb);
-                load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
-            }
-        }
-    } else {
-        while (t < tend) {
-            finish_tile<DIAG>(p, lds, ft, v, lane);
-            throttle_landed();
-            t = pool_grab(pool_ctr, lane);
-            if (t >= tend) break;
-            ft = tile_of(t);
-            throttle_wait(t);
-            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
-        }
+    while (t < tend) {
+        finish_tile<DIAG>(p, lds, ft, v, lane);
+        t = pool_grab(pool_ctr, lane);
+        if (t >= tend) break;
+        ft = tile_at(p, t);
+        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
     }
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
     const uint32_t nwaves = gridDim.x * kWaves;
     const uint32_t npairs = (p.ngen + 1u) >> 1;
     for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair(p, lds, g, lane);
-    if (QUEUE) {
-        // The last workgroup out re-arms this launch's queue slot.
-        __syncthreads();
-        if (threadIdx.x == 0 && atomicAdd(p.queue + 32u * 8u, 1u) == gridDim.x - 1u) {
-            for (uint32_t x = 0; x < 8; ++x) atomicExch(p.queue + 32u * x, 0u);
-            atomicExch(p.queue + 32u * 8u, 0u);
-        }
-    }
     if (STAMPS && lane == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -611,37 +403,16 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"wg1024_pool_nt_early", 1024, 2},          // production
-    {"wg1024_pool_nt", 1024, 2},                // A/B: no early first tile
-    {"wg1024_pool", 1024, 2},                   // A/B: default-policy loads
-    {"wg1024_pool_nt_early_stamps", 1024, 2},   // DIAGNOSTIC: timestamps
-    {"wg1024_pool_nt_early_memonly", 1024, 2},  // DIAGNOSTIC: wrong results, memory ceiling
-    {"wg512_pool_nt_early", 512, 2},            // A/B: 16 waves per CU
-    {"wg1024_pool_nt_early_memonly_stamps", 1024, 2},  // DIAGNOSTIC: both of the above
-    {"wg1024x1_pipe_nt_early", 1024, 1},        // A/B: 1 WG (16 waves) per CU, 2 tiles per wave
-    {"wg512x2_pipe_nt_early", 512, 2},          // A/B: 2 WGs of 8 waves per CU, 2 tiles per wave
-    {"wg1024x1_pipe_nt", 1024, 1},              // A/B: as 7 without the early first tile
-    {"wg1024x1_pool_nt", 1024, 1},              // A/B: 16 waves per CU, one table copy
-    {"wg768x2_pool_nt", 768, 2},                // A/B: 24 waves per CU
-    {"wg512x2_pool_nt", 512, 2},                // A/B: 16 waves per CU, two table copies
-    {"wg1024_pool_nt_sweep", 1024, 2},          // A/B: interleaved tile order
-    {"wg1024_pool_nt_sweep_memonly", 1024, 2},  // DIAGNOSTIC: memory ceiling of 13
-    {"wg1024_pool_nt_memonly", 1024, 2},        // DIAGNOSTIC: memory ceiling of 1
-    {"wg1024_queue_nt", 1024, 2},               // A/B: cross-CU queue
-    {"wg1024_queue_nt_memonly", 1024, 2},       // DIAGNOSTIC: memory ceiling of 16
-    {"wg1024_pool_nt_stamps", 1024, 2},         // DIAGNOSTIC: 1 with timestamps
-    {"wg1024_pool_nt_memonly_stamps", 1024, 2}, // DIAGNOSTIC: 15 with timestamps
-    {"wg1024_pool_nt_memonly_stamps_rev", 1024, 2}, // DIAGNOSTIC: 19 with reversed ranges
-    {"wg1024_pair_nt", 1024, 2},                // A/B: the two workgroups of a CU share a range
-    {"wg1024_pair_nt_memonly", 1024, 2},        // DIAGNOSTIC: memory ceiling of 21
-    {"wg1024_pair_nt_stamps", 1024, 2},         // DIAGNOSTIC: 21 with timestamps
-    {"wg1024_pool_nt_throttle", 1024, 2},       // A/B: $HDFS_CRC32C_THROTTLE tiles in flight per workgroup
-    {"wg1024_pool_nt_throttle_memonly", 1024, 2},  // DIAGNOSTIC: memory ceiling of 24
-    {"wg1024_pool_nt_early2", 1024, 2},         // A/B: first tile behind the staging loads
-    {"wg1024_pool_nt_early2_memonly", 1024, 2}, // DIAGNOSTIC: memory ceiling of 26
-    {"wg1024_pool_compute_only", 1024, 2},      // DIAGNOSTIC: compute ceiling of 1 (no payload loads)
-    {"wg1024_pool_valu_only", 1024, 2},         // DIAGNOSTIC: 28 without the LDS reads
-    {"wg1024_pool_lds_only", 1024, 2},          // DIAGNOSTIC: 28 without the address math
+    {"wg1024_pool_nt", 1024, 2},                // production
+    {"wg1024_pool_nt_early", 1024, 2},          // A/B: first tile before the table staging
+    {"wg1024_pool", 1024, 2},                   // A/B: default-policy payload loads
+    {"wg512_pool_nt", 512, 2},                  // A/B: 16 waves per CU
+    {"wg1024_pool_nt_memonly", 1024, 2},        // DIAGNOSTIC: memory ceiling (no lookups)
+    {"wg1024_pool_nt_compute_only", 1024, 2},   // DIAGNOSTIC: compute ceiling (no payload loads)
+    {"wg1024_pool_nt_valu_only", 1024, 2},      // DIAGNOSTIC: 5 without the LDS reads
+    {"wg1024_pool_nt_lds_only", 1024, 2},       // DIAGNOSTIC: 5 without the address math
+    {"wg1024_pool_nt_stamps", 1024, 2},         // DIAGNOSTIC: 0 with per-wave timestamps
+    {"wg1024_pool_nt_memonly_stamps", 1024, 2}, // DIAGNOSTIC: 4 with per-wave timestamps
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -657,37 +428,16 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{kv.threads, 1, 1};
     switch (variant) {
-    case 1: HDFS_LAUNCH(1024, 8, kModeNt); break;
+    case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly); break;
     case 2: HDFS_LAUNCH(1024, 8, 0); break;
-    case 3: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly | kModeStamps); break;
-    case 4: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly | kModeMemDiag); break;
-    case 5: HDFS_LAUNCH(512, 4, kModeNt | kModeEarly); break;
-    case 6: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly | kModeMemDiag | kModeStamps); break;
-    case 7: HDFS_LAUNCH(1024, 4, kModeNt | kModeEarly | kModePipe); break;
-    case 8: HDFS_LAUNCH(512, 4, kModeNt | kModeEarly | kModePipe); break;
-    case 9: HDFS_LAUNCH(1024, 4, kModeNt | kModePipe); break;
-    case 10: HDFS_LAUNCH(1024, 4, kModeNt); break;
-    case 11: HDFS_LAUNCH(768, 6, kModeNt); break;
-    case 12: HDFS_LAUNCH(512, 4, kModeNt); break;
-    case 13: HDFS_LAUNCH(1024, 8, kModeNt | kModeSweep); break;
-    case 14: HDFS_LAUNCH(1024, 8, kModeNt | kModeSweep | kModeMemDiag); break;
-    case 15: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag); break;
-    case 16: HDFS_LAUNCH(1024, 8, kModeNt | kModeQueue); break;
-    case 17: HDFS_LAUNCH(1024, 8, kModeNt | kModeQueue | kModeMemDiag); break;
-    case 18: HDFS_LAUNCH(1024, 8, kModeNt | kModeStamps); break;
-    case 19: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStamps); break;
-    case 20: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStamps | kModeReverse); break;
-    case 21: HDFS_LAUNCH(1024, 8, kModeNt | kModeGroup); break;
-    case 22: HDFS_LAUNCH(1024, 8, kModeNt | kModeGroup | kModeMemDiag); break;
-    case 23: HDFS_LAUNCH(1024, 8, kModeNt | kModeGroup | kModeStamps); break;
-    case 24: HDFS_LAUNCH(1024, 8, kModeNt | kModeThrottle); break;
-    case 25: HDFS_LAUNCH(1024, 8, kModeNt | kModeThrottle | kModeMemDiag); break;
-    case 26: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly2); break;
-    case 27: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly2 | kModeMemDiag); break;
-    case 28: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag); break;
-    case 29: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
-    case 30: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
-    default: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly); break;
+    case 3: HDFS_LAUNCH(512, 4, kModeNt); break;
+    case 4: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag); break;
+    case 5: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag); break;
+    case 6: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
+    case 7: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
+    case 8: HDFS_LAUNCH(1024, 8, kModeNt | kModeStamps); break;
+    case 9: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStamps); break;
+    default: HDFS_LAUNCH(1024, 8, kModeNt); break;
     }
     return hipGetLastError();
 }

@@ -11,7 +11,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
-#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -78,10 +77,7 @@ struct crc32c_ctx {
     int device = 0;
     int num_cu = 0;
     int variant = 0;  // kernel variant, $HDFS_CRC32C_KVARIANT (A/B measurement only)
-    uint32_t throttle = 0;  // throttled variants: tiles in flight per workgroup, $HDFS_CRC32C_THROTTLE
     uint8_t *d_table = nullptr;
-    LaunchSlot *d_queue = nullptr;  // kQueueSlots launch slots
-    std::atomic<uint32_t> next_queue{0};
     uint32_t c_lg[5];
     uint32_t c_small[4];
     std::mutex mu;
@@ -103,7 +99,7 @@ struct crc32c_multi {
 
 namespace {
 
-KParams params_for(crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
+KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
                    const void *payload, uint32_t *out, uint32_t flags) {
     KParams p;
     p.tiles = static_cast<const FastTile *>(tiles);
@@ -117,11 +113,6 @@ KParams params_for(crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const vo
     std::memcpy(p.c_lg, ctx->c_lg, sizeof p.c_lg);
     std::memcpy(p.c_small, ctx->c_small, sizeof p.c_small);
     p.stamps = nullptr;
-    const uint32_t slot = ctx->next_queue.fetch_add(1) % kQueueSlots;
-    p.queue = ctx->d_queue[slot].w;
-    p.queue_next = ctx->d_queue[(slot + kQueueSlots / 2) % kQueueSlots].w;
-    p.chunk_shift = kQueueChunkShift;
-    p.throttle = ctx->throttle;
     return p;
 }
 
@@ -313,15 +304,11 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
     if (const char *kv = std::getenv("HDFS_CRC32C_KVARIANT")) c->variant = std::atoi(kv);
-    c->throttle = 8;
-    if (const char *th = std::getenv("HDFS_CRC32C_THROTTLE")) c->throttle = uint32_t(std::max(1, std::atoi(th)));
     std::vector<uint8_t> img(kTableAlloc, 0);
     build_lds_image(img.data());
     affine_constants(c->c_lg, c->c_small);
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table), kTableAlloc));
     HIP_TRY(hipMemcpy(c->d_table, img.data(), kTableAlloc, hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_queue), kQueueSlots * sizeof(LaunchSlot)));
-    HIP_TRY(hipMemset(c->d_queue, 0, kQueueSlots * sizeof(LaunchSlot)));
     *out = c.release();
     return 0;
 }
@@ -332,7 +319,6 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
         DeviceGuard guard(ctx->device);
         for (Stage &s : ctx->stage) free_stage(s);
         if (ctx->d_table) (void)hipFree(ctx->d_table);
-        if (ctx->d_queue) (void)hipFree(ctx->d_queue);
     }
     delete ctx;
     return 0;

@@ -27,24 +27,7 @@ struct KParams {
     uint32_t c_lg[5];
     uint32_t c_small[4];
     uint64_t *stamps;  // diagnostic variant only: 4 x u64 per wave
-    uint32_t *queue;       // this launch's LaunchSlot: zero on entry
-    uint32_t *queue_next;  // the slot launch + kQueueSlots/2 will get: zeroed by this launch
-    uint32_t chunk_shift;  // queue work unit = 1 << chunk_shift tiles
-    uint32_t throttle;     // throttled variants: tile loads in flight per workgroup
 };
-
-// Per-launch work-distribution counters: 256 words, each on its own
-// 128-byte line (word i at queue[32 * i]).  Group pools use words
-// 0 .. groups-1; the XCD queue (kModeQueue) uses words 0..7 (heads) and 8
-// (exit counter).  A launch finds its slot zeroed: by hipMemset at context
-// creation, then by the launch kQueueSlots/2 before it (stream order; a slot
-// is reused only after 32 more launches on the context).
-constexpr uint32_t kSlotWords = 256;
-struct LaunchSlot {
-    uint32_t w[kSlotWords * 32];
-};
-constexpr uint32_t kQueueSlots = 64;
-constexpr uint32_t kQueueChunkShift = 4;  // 16 tiles = 128 KiB per queue grab
 
 // Kernel variants; 0 is the production kernel, the others stay built for
 // A/B measurement and diagnostics (tools/kbench.py, tools/stamps.py).
@@ -53,7 +36,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 31;
+constexpr int kNumVariants = 10;
 extern const KernelVariant kVariants[kNumVariants];
 
 // Persistent grid: min(work items / waves per workgroup, kKernelWgPerCu * CUs).

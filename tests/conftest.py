@@ -27,7 +27,8 @@ def load_package():
     """Import native-hdfs-fuse_amd/ (a directory name Python cannot import by name)."""
     if "hdfs_crc32c_amd" in sys.modules:
         return sys.modules["hdfs_crc32c_amd"]
-    spec = importlib.util.spec_from_file_location("hdfs_crc32c_amd", os.path.join(PKG_DIR, "__init__.py"))
+    spec = importlib.util.spec_from_file_location("hdfs_crc32c_amd", os.path.join(PKG_DIR, "__init__.py"),
+                                                  submodule_search_locations=[PKG_DIR])
     mod = importlib.util.module_from_spec(spec)
     sys.modules["hdfs_crc32c_amd"] = mod
     spec.loader.exec_module(mod)

@@ -24,11 +24,11 @@ for s in $STEPS; do
     tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench5) run bench5 600 python bench.py --config c5 --no-cpu ;;
+    bench3) run bench3 600 python bench.py --config c3 --no-cpu --no-host ;;
+    bench4) run bench4 600 python bench.py --config c4 --no-cpu --no-host ;;
     pmc) run pmc 1100 bash tools/pmc_session.sh ;;
-    stamps) run stamps 300 python tools/stamps.py c2 3 ;;
-    stamps6) run stamps6 300 python tools/stamps.py c2 6 ;;
-    stampsv) for v in ${SV:-18 19}; do run stamps_v$v 300 python tools/stamps.py c2 $v; done ;;
-    kbench) run kbench 600 python tools/kbench.py --config c2 --variants ${KV:-0,1,4} ;;
+    stamps) for v in ${SV:-8 9}; do run stamps_v$v 300 python tools/stamps.py c2 $v; done ;;
+    kbench) run kbench 600 python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 --variants ${KV:-0,1} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
             python3 bench.py --steps 50 --warmup 10 --no-cpu --no-host ;;

@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--nbuf", type=int, default=4)
-    ap.add_argument("--variants", default="0,1,2,4,5")
+    ap.add_argument("--variants", default="0,1,2,3,4,5")
     args = ap.parse_args()
 
     import numpy as np
@@ -42,15 +42,10 @@ def main():
     g.manual_seed(7)
     bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g) for _ in range(args.nbuf)]
     outs = [torch.zeros(nout, dtype=torch.int32, device=dev) for _ in range(args.nbuf)]
-    # "V" or "V:T" (T = $HDFS_CRC32C_THROTTLE for that context)
     variants = args.variants.split(",")
     plans = {}
     for v in variants:
-        os.environ["HDFS_CRC32C_KVARIANT"] = v.split(":")[0]
-        if ":" in v:
-            os.environ["HDFS_CRC32C_THROTTLE"] = v.split(":")[1]
-        else:
-            os.environ.pop("HDFS_CRC32C_THROTTLE", None)
+        os.environ["HDFS_CRC32C_KVARIANT"] = v
         ctx = hdfs.Context(0)
         plans[v] = (ctx, ctx.plan(pk))
     stream = torch.cuda.current_stream()

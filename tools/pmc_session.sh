@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/pmc
 mkdir -p $OUT
 export TMPDIR=/tmp
-V="${PMC_VARIANT:-2}"
+V="${PMC_VARIANT:-0}"
 CFG="${PMC_CONFIG:-c2}"
 WL="python3 tools/kbench.py --variants $V --rounds 1 --iters 10 --config $CFG"
 pass() {  # name counters...

@@ -21,7 +21,7 @@ def main():
     from bench import config_packets, load_package
 
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
-    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 3  # 3 = production + stamps, 6 = memory-only + stamps
+    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 8  # 8 = production + stamps, 9 = memory-only + stamps
     hdfs = load_package()
     pk, _ = config_packets(cfg, oracle)
     extent = int((pk["payload_off"] + pk["len"]).max())
@@ -29,7 +29,7 @@ def main():
     dev = torch.device("cuda", 0)
     bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev) for _ in range(4)]
     out = torch.zeros(nout, dtype=torch.int32, device=dev)
-    os.environ["HDFS_CRC32C_KVARIANT"] = "2"
+    os.environ["HDFS_CRC32C_KVARIANT"] = "0"
     ctx = hdfs.Context(0)
     plan = ctx.plan(pk)
     stamps = torch.zeros(4 * 256 * 2 * 16, dtype=torch.int64, device=dev)
