@@ -28,6 +28,7 @@ for s in $STEPS; do
     bench4) run bench4 600 python bench.py --config c4 --no-cpu --no-host ;;
     pmc) run pmc 1100 bash tools/pmc_session.sh ;;
     stamps) for v in ${SV:-8 9}; do run stamps_v$v 300 python tools/stamps.py c2 $v; done ;;
+    tprobe) run tprobe 300 python tools/timing_probe.py ;;
     kbench) run kbench 600 python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 --variants ${KV:-0,1} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
