@@ -95,6 +95,7 @@ def _bind(L):
         "crc32c_last_error": (ctypes.c_char_p, []),
         "crc32c_debug_plan": (i32, [vp, sz, vp, sz, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_debug_lds_image": (sz, [vp, sz, vp, vp]),
+        "crc32c_debug_lds_image_s4": (sz, [vp, sz]),
         "crc32c_debug_plan_exec_variant": (i32, [vp, vp, vp, vp, i32, vp]),
         "crc32c_debug_stream_probe": (i32, [vp, u64, vp, u32, i32, vp]),
     }
@@ -291,3 +292,11 @@ def debug_lds_image():
     c_small = np.zeros(4, np.uint32)
     lib().crc32c_debug_lds_image(_np_ptr(img), n, _np_ptr(c_lg), _np_ptr(c_small))
     return img, c_lg, c_small
+
+
+def debug_lds_image_s4():
+    """The slicing-by-4 kernel's LDS image."""
+    n = int(lib().crc32c_debug_lds_image_s4(None, 0))
+    img = np.zeros(n, np.uint8)
+    lib().crc32c_debug_lds_image_s4(_np_ptr(img), n)
+    return img

@@ -47,6 +47,12 @@ constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
 // device copy is zero-padded to kTableAlloc >= this).
 constexpr uint32_t kStageBytes = (kLdsBytes + 1023u) / 1024u * 1024u;
 static_assert(kStageBytes <= hdfs_crc::kTableAlloc, "staging reads past the device table");
+// The slicing-by-4 kernel's image (crc_math.h): byte tables, N_q, shifts.
+constexpr uint32_t kS4Bytes = uint32_t(hdfs_crc::kS4Bytes);
+constexpr uint32_t kS4NibOff = uint32_t(hdfs_crc::kS4NibOff);
+constexpr uint32_t kS4ShiftOff = uint32_t(hdfs_crc::kS4ShiftOff);
+constexpr uint32_t kS4StageBytes = (kS4Bytes + 1023u) / 1024u * 1024u;
+static_assert(kS4StageBytes <= hdfs_crc::kTableAllocS4, "staging reads past the device table");
 
 // Kernel modes (template bits).  Production = kModeNt.
 constexpr int kModeNt = 1;         // payload loads non-temporal (streamed once)
@@ -56,6 +62,11 @@ constexpr int kModeMemDiag = 8;    // DIAGNOSTIC, wrong results: no lookups (mem
 constexpr int kModeCompDiag = 16;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
 constexpr int kModeValuDiag = 32;  // DIAGNOSTIC, wrong results: lookup address math only, no LDS reads
 constexpr int kModeLdsDiag = 64;   // DIAGNOSTIC, wrong results: LDS reads at fixed addresses
+constexpr int kModeStrided = 128;  // EXPERIMENT (memory-only): lane-contiguous 128-byte loads
+constexpr int kModeHalfDiag = 256;     // EXPERIMENT, wrong results: half of the lookups
+constexpr int kModeQuarterDiag = 512;  // EXPERIMENT, wrong results: three quarters of the lookups
+constexpr int kModeS4 = 1024;     // slicing-by-4 chains + per-column finishing operator (S4 image)
+constexpr int kModePipe = 2048;   // two tiles per wave: the next tile's loads fly during this tile's lookups
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -125,9 +136,69 @@ __device__ __forceinline__ uint32_t piece_lin(const uint8_t *lds, uint4 d, uint3
     return acc;
 }
 
+// (a & mask) | c as ONE v_and_or_b32: left to itself the compiler proves the
+// operands disjoint, turns the OR into an add and splits it in two.
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t mask, uint32_t c) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(mask), "v"(c));
+    return r;
+}
+
+// Per-lane LDS address constants: the lane's column offset, and the same
+// with the base of the S4 image's upper byte-table pair / N_q section.
+struct LaneCols {
+    uint32_t col4;  // (lane & 31) * 4
+    uint32_t hi;    // col4 | 65536
+    uint32_t nib;   // col4 | kS4NibOff
+};
+
+__device__ __forceinline__ LaneCols lane_cols(uint32_t q) {
+    return LaneCols{q << 2, (q << 2) | 65536u, (q << 2) | kS4NibOff};
+}
+
+// Byte j of v into address bits 8..15 and the column base's bytes 0 and 2
+// into bits 0..7 and 16..23 (v_perm_b32: selectors 0-3 = bytes of the
+// second operand, 4-7 = bytes of the first, 0x0C = zero).
+template <int J>
+__device__ __forceinline__ uint32_t byte_addr(uint32_t v, uint32_t base) {
+    return __builtin_amdgcn_perm(v, base, 0x0C020000u | uint32_t(4 + J) << 8);
+}
+
+// One slicing-by-4 step: S(v) ^ next, S(v) = T3[v.b0] ^ T2[v.b1] ^ T1[v.b2]
+// ^ T0[v.b3] (each table replicated over the 32 lane columns, so the 32
+// lanes of a half-wave always hit 32 different banks).
+__device__ __forceinline__ uint32_t s4(const uint8_t *lds, const LaneCols &c, uint32_t v, uint32_t next) {
+    const uint32_t a3 = lds_u32(lds, byte_addr<0>(v, c.hi) + 128u);  // T3: upper pair, odd
+    const uint32_t a2 = lds_u32(lds, byte_addr<1>(v, c.hi));         // T2: upper pair, even
+    const uint32_t a1 = lds_u32(lds, byte_addr<2>(v, c.col4) + 128u);  // T1
+    const uint32_t a0 = lds_u32(lds, byte_addr<3>(v, c.col4));         // T0
+    return xor3(xor3(a3, a2, a1), a0, next);
+}
+
+// lin() of the lane's 16-byte piece with the S4 image: u = S(S(S(d0) ^ d1)
+// ^ d2) ^ d3 is the register after the piece; N_q(u) = Z_{16(31-q)}(S(u))
+// moves it to the block end (8 nibble lookups in the lane's column).
+template <int DIAG>
+__device__ __forceinline__ uint32_t piece_lin_s4(const uint8_t *lds, uint4 d, const LaneCols &c) {
+    if (DIAG == 1) return d.x ^ d.y ^ d.z ^ d.w;
+    const uint32_t u = s4(lds, c, s4(lds, c, s4(lds, c, d.x, d.y), d.z), d.w);
+    const uint32_t xs[8] = {u << 8, u << 4, u, u >> 4, u >> 8, u >> 12, u >> 16, u >> 20};
+    uint32_t r[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) r[t] = lds_u32(lds, and_or(xs[t], 0x0F00u, c.nib) + (t >> 1) * 4096u + (t & 1) * 128u);
+    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
+template <bool S4, int DIAG>
+__device__ __forceinline__ uint32_t piece(const uint8_t *lds, uint4 d, const LaneCols &c) {
+    if (S4) return piece_lin_s4<DIAG>(lds, d, c);
+    return piece_lin<DIAG>(lds, d, c.col4);
+}
+
 // Z^(512*s)(x), s in 1..15, from 8 nibble tables (16 entries each).
+template <bool S4 = false>
 __device__ __forceinline__ uint32_t zshift(const uint8_t *lds, uint32_t s, uint32_t x) {
-    const uint32_t base = kShiftOff + (s - 1u) * 512u;
+    const uint32_t base = (S4 ? kS4ShiftOff : kShiftOff) + (s - 1u) * 512u;
     uint32_t r = 0;
 #pragma unroll
     for (int t = 0; t < 8; ++t) r ^= lds_u32(lds, base + t * 64u + ((x >> (4 * t)) & 15u) * 4u);
@@ -168,7 +239,7 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 // and read zeros without touching memory (lin() of zeros is 0, so they need
 // no mask), every lane uses the same one-VGPR offset plus an immediate, and
 // the instruction stream has no divergent branch.  AUX 2 = non-temporal.
-template <int AUX, bool COMPDIAG = false>
+template <int AUX, bool COMPDIAG = false, bool STRIDED = false>
 __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8]) {
     if (COMPDIAG) {  // synthetic data, no memory traffic
         const uint32_t x = uint32_t(t.src) * 2654435761u + uint32_t(lane) * 40503u;
@@ -179,10 +250,11 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
     const uint32_t nb = t.meta & 0xffu;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src), 0, int(nb * 512u), 0x00020000);
-    const uint32_t voff = 16u * uint32_t(lane);
+    // STRIDED (experiment): lane l reads the 128 contiguous bytes 128l .. 128l+127.
+    const uint32_t voff = (STRIDED ? 128u : 16u) * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (STRIDED ? 16u : 1024u) * i, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
     // Keep the loads ahead of whatever compute follows.
@@ -191,21 +263,27 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
 
 // lin() per piece, then reduce to one lin() per block, combine the blocks of
 // each chunk, store the chunk checksums.
-template <int DIAG>
+template <int DIAG, bool S4 = false>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, FastTile t, const uint4 v[8],
                                             int lane) {
     const uint32_t nb = t.meta & 0xffu;
     const uint32_t lg = (t.meta >> 8) & 0xffu;
-    const uint32_t col4 = uint32_t(lane & 31) << 2;
+    const LaneCols cols = lane_cols(uint32_t(lane & 31));
     const uint32_t h = uint32_t(lane) >> 5;
     uint32_t pc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        pc[i] = piece_lin<DIAG>(lds, v[i], col4);
+        // DIAG 4 / 5 (experiment, wrong results): skip the lookups of 4 / 2 of the 8 pieces.
+        if ((DIAG == 4 && (i & 1)) || (DIAG == 5 && (i & 3) == 3))
+            pc[i] = v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+        else
+            pc[i] = piece<S4, (DIAG >= 4 ? 0 : DIAG)>(lds, v[i], cols);
         opaque(pc[i]);
-        // One piece at a time: keeps the scheduler from hoisting every
-        // piece's 32 LDS reads together (register pressure -> spills).
-        __builtin_amdgcn_sched_barrier(0);
+        // One piece at a time (nibble tables: 32 independent reads each), or
+        // two (S4: a piece is a chain of 4 dependent steps, so two chains
+        // interleave to keep 8 reads in flight): keeps the scheduler from
+        // hoisting every piece's LDS reads together (register pressure).
+        if (!S4 || (i & 1)) __builtin_amdgcn_sched_barrier(0);
     }
 
     // Reduce-scatter over lane bits 0, 1, 3 (8 values -> 1), then all-reduce
@@ -239,7 +317,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     if (lg) {  // chunks of 2^lg blocks: shift each block to the chunk end, XOR them
         const uint32_t nbc = 1u << lg;
         const uint32_t s = nbc - 1u - (blk & (nbc - 1u));
-        if (s) x = zshift(lds, s, x);
+        if (s) x = zshift<S4>(lds, s, x);
         x ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), 32));  // block bit 0 = lane bit 5
         if (lg >= 2) x ^= dpp<kDppXor8>(x);                               // block bit 1 = lane bit 3
         if (lg >= 3) x ^= dpp<kDppXor2>(x);                               // block bit 2 = lane bit 1
@@ -294,6 +372,7 @@ __device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
                       __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
 }
 
+template <bool S4 = false>
 __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t pair, int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
     const uint32_t idx = 2u * pair + h;
@@ -317,10 +396,10 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
             uint32_t w[8];
             load_piece(a0, cbeg, cend, ffend, w);
             load_piece(a0 + 16, cbeg, cend, ffend, w + 4);
-            lin = piece_lin<0>(lds, funnel(w, uint32_t(a & 15u)), q << 2);
+            lin = piece<S4, 0>(lds, funnel(w, uint32_t(a & 15u)), lane_cols(q));
         }
         lin = allreduce32(lin);
-        if (m < nbv) acc = zshift(lds, 1, acc) ^ lin;
+        if (m < nbv) acc = zshift<S4>(lds, 1, acc) ^ lin;
     }
     if (valid && q == 0) {
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
@@ -338,12 +417,18 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
-    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
+    constexpr bool STRIDED = (MODE & kModeStrided) != 0;
+    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3
+                         : (MODE & kModeHalfDiag) ? 4 : (MODE & kModeQuarterDiag) ? 5 : 0;
+    constexpr bool S4 = (MODE & kModeS4) != 0;
+    constexpr bool PIPE = (MODE & kModePipe) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
+    constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
     // One LDS array: the tables, then the workgroup's tile counter.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStageBytes + 16];
-    uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStageBytes);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
+    uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
+    const uint8_t *table = S4 ? p.table_s4 : p.table;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
 
@@ -364,32 +449,60 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     // EARLY (A/B): request the first tile before the table staging.
     if (EARLY && t < tend) {
         ft = tile_at(p, t);
-        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+        load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
     }
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
-    for (uint32_t c = wv; c < kStageBytes / 1024u; c += kWaves)
+    for (uint32_t c = wv; c < kStage / 1024u; c += kWaves)
         __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void *)(p.table + c * 1024u + 16u * uint32_t(lane)),
+            (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
             (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
     if (!EARLY && t < tend) {
         ft = tile_at(p, t);
-        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+        load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
     }
-    while (t < tend) {
-        finish_tile<DIAG>(p, lds, ft, v, lane);
-        t = pool_grab(pool_ctr, lane);
-        if (t >= tend) break;
-        ft = tile_at(p, t);
-        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+    if (PIPE) {
+        // Two register tiles per wave (a = v, b = vb): one is in flight while
+        // the other is looked up.  Needs ~100 VGPRs: 4 waves per SIMD.
+        uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
+        FastTile fb{0, 0, 0};
+        uint4 vb[8];
+        if (tb < tend) {
+            fb = tile_at(p, tb);
+            load_tile<AUX, COMPDIAG, STRIDED>(p, fb, lane, vb);
+        }
+        while (t < tend) {
+            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
+            if (tb >= tend) break;
+            t = pool_grab(pool_ctr, lane);
+            if (t < tend) {
+                ft = tile_at(p, t);
+                load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+            }
+            finish_tile<DIAG, S4>(p, lds, fb, vb, lane);
+            if (t >= tend) break;
+            tb = pool_grab(pool_ctr, lane);
+            if (tb < tend) {
+                fb = tile_at(p, tb);
+                load_tile<AUX, COMPDIAG, STRIDED>(p, fb, lane, vb);
+            }
+        }
+    } else {
+        while (t < tend) {
+            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
+            t = pool_grab(pool_ctr, lane);
+            if (t >= tend) break;
+            ft = tile_at(p, t);
+            load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+        }
     }
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
     const uint32_t nwaves = gridDim.x * kWaves;
     const uint32_t npairs = (p.ngen + 1u) >> 1;
-    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair(p, lds, g, lane);
+    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair<S4>(p, lds, g, lane);
     if (STAMPS && lane == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -413,6 +526,17 @@ const KernelVariant kVariants[kNumVariants] = {
     {"wg1024_pool_nt_lds_only", 1024, 2},       // DIAGNOSTIC: 5 without the address math
     {"wg1024_pool_nt_stamps", 1024, 2},         // DIAGNOSTIC: 0 with per-wave timestamps
     {"wg1024_pool_nt_memonly_stamps", 1024, 2}, // DIAGNOSTIC: 4 with per-wave timestamps
+    {"exp_strided_nt_memonly", 1024, 2},
+    {"exp_strided_memonly", 1024, 2},
+    {"exp_strided_nt_memonly_x1", 1024, 1},
+    {"exp_strided_memonly_x1", 1024, 1},
+    {"exp_nt_memonly_x1", 1024, 1},
+    {"exp_half_lookups", 1024, 2},
+    {"exp_three_quarter_lookups", 1024, 2},
+    {"s4_wg1024x1_nt", 1024, 1},                // slicing-by-4 chains, 1 WG (16 waves) per CU
+    {"s4_wg1024x1_pipe_nt", 1024, 1},           // + two tiles per wave
+    {"s4_wg1024x1_nt_memonly", 1024, 1},        // DIAGNOSTIC: memory ceiling of 17
+    {"s4_wg1024x1_compute_only", 1024, 1},      // DIAGNOSTIC: compute ceiling of 17
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -437,6 +561,17 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 7: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
     case 8: HDFS_LAUNCH(1024, 8, kModeNt | kModeStamps); break;
     case 9: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStamps); break;
+    case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStrided); break;
+    case 11: HDFS_LAUNCH(1024, 8, kModeMemDiag | kModeStrided); break;
+    case 12: HDFS_LAUNCH(1024, 4, kModeNt | kModeMemDiag | kModeStrided); break;
+    case 13: HDFS_LAUNCH(1024, 4, kModeMemDiag | kModeStrided); break;
+    case 14: HDFS_LAUNCH(1024, 4, kModeNt | kModeMemDiag); break;
+    case 15: HDFS_LAUNCH(1024, 8, kModeNt | kModeHalfDiag); break;
+    case 16: HDFS_LAUNCH(1024, 8, kModeNt | kModeQuarterDiag); break;
+    case 17: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4); break;
+    case 18: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModePipe); break;
+    case 19: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeMemDiag); break;
+    case 20: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeCompDiag); break;
     default: HDFS_LAUNCH(1024, 8, kModeNt); break;
     }
     return hipGetLastError();

@@ -78,6 +78,7 @@ struct crc32c_ctx {
     int num_cu = 0;
     int variant = 0;  // kernel variant, $HDFS_CRC32C_KVARIANT (A/B measurement only)
     uint8_t *d_table = nullptr;
+    uint8_t *d_table_s4 = nullptr;
     uint32_t c_lg[5];
     uint32_t c_small[4];
     std::mutex mu;
@@ -107,6 +108,7 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
     p.payload = static_cast<const uint8_t *>(payload);
     p.out = out;
     p.table = ctx->d_table;
+    p.table_s4 = ctx->d_table_s4;
     p.ntiles = ntiles;
     p.ngen = ngen;
     p.flags = flags;
@@ -309,6 +311,10 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     affine_constants(c->c_lg, c->c_small);
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table), kTableAlloc));
     HIP_TRY(hipMemcpy(c->d_table, img.data(), kTableAlloc, hipMemcpyHostToDevice));
+    std::vector<uint8_t> img4(kTableAllocS4, 0);
+    build_lds_image_s4(img4.data());
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4), kTableAllocS4));
+    HIP_TRY(hipMemcpy(c->d_table_s4, img4.data(), kTableAllocS4, hipMemcpyHostToDevice));
     *out = c.release();
     return 0;
 }
@@ -319,6 +325,7 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
         DeviceGuard guard(ctx->device);
         for (Stage &s : ctx->stage) free_stage(s);
         if (ctx->d_table) (void)hipFree(ctx->d_table);
+        if (ctx->d_table_s4) (void)hipFree(ctx->d_table_s4);
     }
     delete ctx;
     return 0;

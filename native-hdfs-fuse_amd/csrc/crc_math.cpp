@@ -3,6 +3,7 @@
 
 #include <cstring>
 #include <mutex>
+#include <vector>
 
 namespace hdfs_crc {
 
@@ -93,6 +94,38 @@ void build_lds_image(uint8_t *dst) {
                 put(kLdsShiftOff + size_t(s - 1) * 512 + size_t(tn) * 64 + n * 4, zs.apply(n << (4 * tn)));
         zs = op_compose(z512, zs);
     }
+}
+
+uint32_t s4_step(uint32_t u) {
+    uint32_t r = u;
+    for (int i = 0; i < 4; ++i) r = append_zero_byte(r);
+    return r;
+}
+
+void build_lds_image_s4(uint8_t *dst) {
+    std::memset(dst, 0, kS4Bytes);
+    auto put = [&](size_t off, uint32_t v) { std::memcpy(dst + off, &v, 4); };
+    // T_m[b]: byte b followed by m zero bytes, from register 0.
+    const uint32_t *t0 = byte_table();
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t v = t0[b];
+        for (int m = 0; m < 4; ++m) {
+            for (int q = 0; q < 32; ++q) put(size_t(m >> 1) * 65536 + size_t(b) * 256 + size_t(m & 1) * 128 + q * 4, v);
+            v = append_zero_byte(v);
+        }
+    }
+    // N_q(n << 4t) = Z_{16 (31 - q)}(S(n << 4t)).
+    for (int q = 0; q < 32; ++q) {
+        const Gf2Op zq = op_zeros(uint64_t(16) * uint64_t(31 - q));
+        for (int t = 0; t < 8; ++t)
+            for (uint32_t n = 0; n < 16; ++n)
+                put(kS4NibOff + size_t(t >> 1) * 4096 + n * 256 + size_t(t & 1) * 128 + q * 4,
+                    zq.apply(s4_step(n << (4 * t))));
+    }
+    // Z^(512 s), as in the nibble image.
+    std::vector<uint8_t> nib(kLdsBytes);
+    build_lds_image(nib.data());
+    std::memcpy(dst + kS4ShiftOff, nib.data() + kLdsShiftOff, kMaxShift * 512);
 }
 
 void affine_constants(uint32_t c_lg[5], uint32_t c_small[4]) {

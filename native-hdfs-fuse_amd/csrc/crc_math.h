@@ -52,6 +52,26 @@ constexpr size_t kLdsBytes = kLdsPosBytes + kMaxShift * 512;
 // Fills `dst` (kLdsBytes) with the LDS image.
 void build_lds_image(uint8_t *dst);
 
+// ---- the slicing-by-4 kernel's LDS image (see DESIGN.md "S4 kernel") ----
+// A lane chains its 16-byte piece d0..d3 through the position-independent
+// slicing-by-4 step S (u = S(S(S(d0) ^ d1) ^ d2) ^ d3) and finishes with one
+// column-specific operator N_q = Z_{16 (31 - q)} o S on u.
+// [0, 131072): byte tables T_m[b] = register after byte b then m zero bytes
+//   (m = 0..3, crc32c.c:50-73's crc32c_table[m]), each replicated over the 32
+//   lane columns: T_m[b] at (m >> 1) * 65536 + b * 256 + (m & 1) * 128 + q * 4.
+// [131072, 147456): N_q on nibble t of u, value n:
+//   131072 + (t >> 1) * 4096 + n * 256 + (t & 1) * 128 + q * 4.
+// [147456, 147456 + 15 * 512): Z^(512 s), s = 1..15, laid out as in the
+//   nibble image's shift section.
+constexpr size_t kS4NibOff = 131072;
+constexpr size_t kS4ShiftOff = 147456;
+constexpr size_t kS4Bytes = kS4ShiftOff + kMaxShift * 512;
+
+// Fills `dst` (kS4Bytes) with the slicing-by-4 LDS image.
+void build_lds_image_s4(uint8_t *dst);
+// S(u): the register after feeding the 4 bytes of u (little-endian) into register 0.
+uint32_t s4_step(uint32_t u);
+
 // crc32c(0, zeros(512 << lg)) for lg = 0..4 and crc32c(0, zeros(r)) for r = 0..3.
 void affine_constants(uint32_t c_lg[5], uint32_t c_small[4]);
 

@@ -14,6 +14,7 @@ constexpr uint32_t kKernelWgPerCu = 2;  // 2 x 73 KiB of LDS per CU
 // Device copy of the LDS image, zero-padded so every staging load of a
 // 1024-thread workgroup (16 B per thread per round) is in bounds.
 constexpr uint32_t kTableAlloc = ((kKernelLdsBytes + 16384 - 1) / 16384) * 16384;
+constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 16384;
 
 struct KParams {
     const FastTile *tiles;
@@ -21,6 +22,7 @@ struct KParams {
     const uint8_t *payload;
     uint32_t *out;
     const uint8_t *table;  // kLdsBytes, staged into LDS by every workgroup
+    const uint8_t *table_s4;  // kS4Bytes: the slicing-by-4 variants' image
     uint32_t ntiles;
     uint32_t ngen;
     uint32_t flags;
@@ -36,7 +38,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 10;
+constexpr int kNumVariants = 21;
 extern const KernelVariant kVariants[kNumVariants];
 
 // Persistent grid: min(work items / waves per workgroup, kKernelWgPerCu * CUs).

@@ -85,3 +85,8 @@ extern "C" size_t crc32c_debug_lds_image(void *dst, size_t cap, uint32_t *c_lg, 
     if (c_lg && c_small) hdfs_crc::affine_constants(c_lg, c_small);
     return hdfs_crc::kLdsBytes;
 }
+
+extern "C" size_t crc32c_debug_lds_image_s4(void *dst, size_t cap) {
+    if (dst && cap >= hdfs_crc::kS4Bytes) hdfs_crc::build_lds_image_s4(static_cast<uint8_t *>(dst));
+    return hdfs_crc::kS4Bytes;
+}

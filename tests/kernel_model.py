@@ -69,3 +69,39 @@ class KernelModel:
         for m in range(nbv):
             acc = self.zshift(1, acc) ^ int(lins[m])
         return acc ^ (0xFFFFFFFF if r >= 4 else self.c_small[r])
+
+
+class KernelModelS4:
+    """The slicing-by-4 variants' arithmetic over their LDS image
+    (``crc32c_debug_lds_image_s4``): per 16-byte lane piece
+    u = S(S(S(d0) ^ d1) ^ d2) ^ d3 from the replicated byte tables, then the
+    column operator N_q(u) from 8 nibble lookups; XOR over the 32 lanes."""
+
+    NIB_OFF = 131072
+    SHIFT_OFF = 147456
+
+    def __init__(self, img: np.ndarray):
+        self.w = img.view("<u4")
+        b = np.arange(256)
+        q = np.arange(32)
+        # t_m[b, q]: byte table m at column q
+        self.t = [self.w[((m >> 1) * 65536 + b[:, None] * 256 + (m & 1) * 128 + q[None, :] * 4) // 4]
+                  for m in range(4)]
+        t = np.arange(8)
+        n = np.arange(16)
+        # nq[q, t, n]
+        self.nq = self.w[(self.NIB_OFF + (t[None, :, None] >> 1) * 4096 + n[None, None, :] * 256
+                          + (t[None, :, None] & 1) * 128 + q[:, None, None] * 4) // 4]
+
+    def s(self, u: np.ndarray, q: np.ndarray) -> np.ndarray:
+        return (self.t[3][u & 0xFF, q] ^ self.t[2][(u >> 8) & 0xFF, q] ^ self.t[1][(u >> 16) & 0xFF, q]
+                ^ self.t[0][(u >> 24) & 0xFF, q])
+
+    def block_lin(self, blocks: np.ndarray) -> np.ndarray:
+        d = np.ascontiguousarray(blocks).view("<u4").reshape(-1, 32, 4)
+        q = np.broadcast_to(np.arange(32)[None, :], d.shape[:2])
+        u = self.s(self.s(self.s(d[..., 0], q) ^ d[..., 1], q) ^ d[..., 2], q) ^ d[..., 3]
+        acc = np.zeros(u.shape, np.uint32)
+        for t in range(8):
+            acc ^= self.nq[q, t, (u >> (4 * t)) & 15]
+        return np.bitwise_xor.reduce(acc, axis=1).astype(np.uint32)

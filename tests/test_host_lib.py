@@ -13,7 +13,7 @@ import pytest
 
 import oracle
 from conftest import ROOT, golden_fill
-from kernel_model import KernelModel
+from kernel_model import KernelModel, KernelModelS4
 
 
 def _declared_functions():
@@ -151,3 +151,22 @@ def test_gpu_entry_points_fail_loudly_without_gpu(hdfs):
     assert ei.value.rc == -19  # -ENODEV: no CPU substitute behind the GPU API
     with pytest.raises(hdfs.Crc32cError):
         hdfs.chunks(np.zeros(1024, np.uint8), 512)
+
+
+def test_s4_image_matches_nibble_image(hdfs, model):
+    """The slicing-by-4 image (byte tables replicated per lane column, the
+    per-column finishing operators N_q, the Z^(512 s) section) computes the
+    same block lin() as the positional nibble image."""
+    img4 = hdfs.debug_lds_image_s4()
+    m4 = KernelModelS4(img4)
+    for t in m4.t:  # every column holds the same byte table
+        assert (t == t[:, :1]).all()
+    rng = np.random.default_rng(11)
+    blocks = rng.integers(0, 256, (64, 512), dtype=np.uint8)
+    blocks[0] = 0
+    blocks[1] = 0xFF
+    assert np.array_equal(m4.block_lin(blocks), model.block_lin(blocks))
+    img, _, _ = hdfs.debug_lds_image()
+    w4 = img4.view("<u4")
+    w = img.view("<u4")
+    assert np.array_equal(w4[KernelModelS4.SHIFT_OFF // 4:], w[65536 // 4:65536 // 4 + w4.size - KernelModelS4.SHIFT_OFF // 4])

@@ -58,6 +58,20 @@ def main():
         q = lambda a, p: round(float(np.percentile(a, p)), 2)
         res.setdefault(name, []).append({"rounds": len(ts), "first5": [round(x, 2) for x in ts[:5]],
                                          "p10": q(ts, 10), "p50": q(ts, 50), "p90": q(ts, 90)})
+    # One continuous stream of launches, an event every 25 launches: the
+    # kernel time as a function of how long the GPU has been running it.
+    n_seg, per = 160, 25
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n_seg + 1)]
+    torch.cuda._sleep(1000000)  # ~idle gap before the burst
+    torch.cuda.synchronize()
+    evs[0].record(s)
+    for k in range(n_seg):
+        for i in range(per):
+            plan.exec(sets["4rand"][i % 4].data_ptr(), outs[i % 4].data_ptr(), s.cuda_stream)
+        evs[k + 1].record(s)
+    torch.cuda.synchronize()
+    seg = [round(evs[k].elapsed_time(evs[k + 1]) / per * 1e3, 1) for k in range(n_seg)]
+    res["continuous_us_per_launch_by_25"] = seg
     print(json.dumps(res, indent=1))
 
 
