@@ -67,6 +67,8 @@ constexpr int kModeHalfDiag = 256;     // EXPERIMENT, wrong results: half of the
 constexpr int kModeQuarterDiag = 512;  // EXPERIMENT, wrong results: three quarters of the lookups
 constexpr int kModeS4 = 1024;     // slicing-by-4 chains + per-column finishing operator (S4 image)
 constexpr int kModePipe = 2048;   // two tiles per wave: the next tile's loads fly during this tile's lookups
+constexpr int kModeEarly2 = 4096; // first tile requested right behind the table staging, bare barrier
+constexpr int kModeTail = 8192;   // the last tiles go through a cross-CU queue (per-XCD heads, stealing)
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -335,6 +337,98 @@ __device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
     return __builtin_amdgcn_readfirstlane(t);
 }
 
+// ---- tail queue (kModeTail) ------------------------------------------------
+// Equal static ranges leave CUs finishing several microseconds apart: the
+// memory system does not serve every CU at the same rate (tools/stamps.py).
+// So only tiles [0, static_tiles) are dealt statically; the rest (the
+// "tail", 1/8 by default) is cut into chunks of C = 1 << chunk_shift tiles,
+// XCD x owns a contiguous 1/8 of the chunks behind its own head counter (one
+// device-scope atomic per chunk, sharded per XCD as MI355X_MICROARCH.md
+// 'dequeue' prescribes), and a workgroup whose XCD is drained steals from
+// the next XCDs' heads.  Inside the workgroup the LDS ticket counter simply
+// runs on past the static range: ticket tend + k is tile k mod C of the
+// workgroup's (k / C)-th tail chunk, whose id sits in an LDS ring entry
+// stamped with its sequence number.  Chunk s is fetched by the wave that
+// takes ticket T_s = tend - L + s C (L = one ticket per wave ahead), or at
+// start when T_s precedes the first grabbed ticket, so every chunk a held
+// ticket refers to is fetched by someone and its ~1 us fetch overlaps L
+// tiles of work.
+constexpr uint32_t kNoChunk = 0xffffffffu;
+constexpr uint32_t kTailEnd = 0xffffffffu;   // queue drained
+constexpr uint32_t kTailSkip = 0xfffffffeu;  // ticket past the end of the last (partial) chunk
+constexpr uint32_t kRing = 64;  // a wrap needs 63 chunks fetched while one ticket is still unresolved
+
+struct TailLds {
+    uint64_t ring[kRing];  // (sequence << 32) | chunk id
+    uint32_t exhausted;    // bit x: XCD x's head is drained
+};
+
+// One lane: the next tail chunk for this workgroup, or kNoChunk.  The own
+// XCD's head first (one returning atomic, its latency hidden by the L-ticket
+// lookahead).  Once that is drained and stealing is on (p.tail_steal), the
+// other heads are read together (device-coherent loads, one round trip) and
+// the fullest one is claimed; a head found drained is never tried again.
+__device__ uint32_t tail_fetch(const KParams &p, TailLds *q, uint32_t nchunks, uint32_t xcc) {
+    uint32_t mask = __atomic_load_n(&q->exhausted, __ATOMIC_RELAXED);
+    const auto lo_of = [&](uint32_t x) { return uint32_t(uint64_t(nchunks) * x / 8u); };
+    const auto len_of = [&](uint32_t x) { return lo_of(x + 1u) - lo_of(x); };
+    if (!(mask & (1u << xcc))) {
+        const uint32_t c = len_of(xcc) ? atomicAdd(p.queue + 32u * xcc, 1u) : 0u;
+        if (c < len_of(xcc)) return lo_of(xcc) + c;
+        mask |= 1u << xcc;
+        atomicOr(&q->exhausted, 1u << xcc);
+    }
+    if (!p.tail_steal) return kNoChunk;
+    for (int attempt = 0; attempt < 8 && mask != 0xffu; ++attempt) {
+        uint32_t taken[8];
+#pragma unroll
+        for (uint32_t x = 0; x < 8; ++x)
+            taken[x] = (mask & (1u << x)) ? 0u
+                                          : __hip_atomic_load(p.queue + 32u * x, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t best = 8, best_rem = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < 8; ++x) {
+            const uint32_t rem = (mask & (1u << x)) || taken[x] >= len_of(x) ? 0u : len_of(x) - taken[x];
+            if (rem == 0) mask |= 1u << x;
+            if (rem > best_rem) {
+                best_rem = rem;
+                best = x;
+            }
+        }
+        if (best == 8) break;
+        const uint32_t c = atomicAdd(p.queue + 32u * best, 1u);
+        if (c < len_of(best)) {
+            atomicOr(&q->exhausted, mask);
+            return lo_of(best) + c;
+        }
+        mask |= 1u << best;
+    }
+    atomicOr(&q->exhausted, 0xffu);
+    return kNoChunk;
+}
+
+__device__ __forceinline__ void ring_put(TailLds *q, uint32_t seq, uint32_t chunk) {
+    __atomic_store_n(&q->ring[seq % kRing], (uint64_t(seq) << 32) | chunk, __ATOMIC_RELAXED);
+}
+
+// Tile of tail ticket k (wave-uniform), kTailEnd or kTailSkip.
+__device__ uint32_t tail_resolve(const KParams &p, TailLds *q, uint32_t k) {
+    const uint32_t seq = k >> p.chunk_shift, i = k & ((1u << p.chunk_shift) - 1u);
+    uint64_t e;
+    for (;;) {
+        e = __atomic_load_n(&q->ring[seq % kRing], __ATOMIC_RELAXED);
+        const uint32_t es = __builtin_amdgcn_readfirstlane(uint32_t(e >> 32));
+        if (es == seq) break;
+        if (es != ~0u && es > seq) return kTailEnd;  // overwritten (cannot happen, see kRing): never spin forever
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const uint32_t c = __builtin_amdgcn_readfirstlane(uint32_t(e));
+    if (c == kNoChunk) return kTailEnd;
+    const uint32_t t = p.static_tiles + (c << p.chunk_shift) + i;
+    return t < p.ntiles ? t : kTailSkip;
+}
+
 // ---- general path: half a wave per chunk of any length / alignment -------
 __device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
     return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
@@ -422,12 +516,15 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
                          : (MODE & kModeHalfDiag) ? 4 : (MODE & kModeQuarterDiag) ? 5 : 0;
     constexpr bool S4 = (MODE & kModeS4) != 0;
     constexpr bool PIPE = (MODE & kModePipe) != 0;
+    constexpr bool EARLY2 = (MODE & kModeEarly2) != 0;
+    constexpr bool TAIL = (MODE & kModeTail) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
     // One LDS array: the tables, then the workgroup's tile counter.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16 + (TAIL ? sizeof(TailLds) : 0)];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
+    TailLds *tq = reinterpret_cast<TailLds *>(lds + kStage + 16);
     const uint8_t *table = S4 ? p.table_s4 : p.table;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
@@ -440,9 +537,25 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
-    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    // TAIL: the ranges cover [0, static_tiles); see "tail queue" above.
+    const uint32_t nstat = TAIL ? p.static_tiles : p.ntiles;
+    const uint32_t tbeg = uint32_t((uint64_t(nstat) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((uint64_t(nstat) * (blockIdx.x + 1)) / gridDim.x);
     if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
+    uint32_t nchunks = 0, xcc = 0;
+    const int64_t trig0 = int64_t(tend) - int64_t(kWaves);  // T_0; T_s = T_0 + s C
+    if (TAIL) {
+        nchunks = ((p.ntiles - p.static_tiles) + (1u << p.chunk_shift) - 1u) >> p.chunk_shift;
+        xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+        if (blockIdx.x == 0 && threadIdx.x < 8) p.queue_next[32u * threadIdx.x] = 0;  // re-arm a later slot
+        if (threadIdx.x == 0) {
+            tq->exhausted = 0;
+            for (uint32_t r = 0; r < kRing; ++r) tq->ring[r] = ~uint64_t(0);
+            // chunks whose trigger ticket no wave will grab
+            for (uint32_t sq = 0; trig0 + int64_t(sq << p.chunk_shift) < int64_t(tbeg + kWaves); ++sq)
+                ring_put(tq, sq, tail_fetch(p, tq, nchunks, xcc));
+        }
+    }
     uint32_t t = tbeg + wv;
     FastTile ft{0, 0, 0};
     uint4 v[8];
@@ -456,10 +569,22 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
             (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
-    __syncthreads();
+    if (EARLY2) {
+        // The first tile's loads queue behind this wave's staging loads: wait
+        // for all but those 8 (vmcnt counts in issue order), then a bare
+        // barrier (__syncthreads' fence would wait for the tile too).
+        if (t < tend) {
+            ft = tile_at(p, t);
+            load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8) expcnt(7) lgkmcnt(15)
+        __builtin_amdgcn_s_barrier();
+    } else {
+        __syncthreads();
+    }
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY && t < tend) {
+    if (!EARLY && !EARLY2 && t < tend) {
         ft = tile_at(p, t);
         load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
     }
@@ -487,6 +612,35 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             if (tb < tend) {
                 fb = tile_at(p, tb);
                 load_tile<AUX, COMPDIAG, STRIDED>(p, fb, lane, vb);
+            }
+        }
+    } else if (TAIL) {
+        // ticket t: static tile t while t < tend, else tail ticket t - tend
+        const auto grab = [&]() {
+            const uint32_t g = pool_grab(pool_ctr, lane);
+            const int64_t w = int64_t(g) - trig0;
+            if (w >= 0 && (uint32_t(w) & ((1u << p.chunk_shift) - 1u)) == 0 && lane == 0)
+                ring_put(tq, uint32_t(w) >> p.chunk_shift, tail_fetch(p, tq, nchunks, xcc));
+            return g;
+        };
+        bool loaded = t < tend;  // the first static tile is in flight already
+        for (;;) {
+            if (!loaded) {
+                const uint32_t tt = tail_resolve(p, tq, t - tend);
+                if (tt == kTailEnd) break;
+                if (tt == kTailSkip) {
+                    t = grab();
+                    continue;
+                }
+                ft = tile_at(p, tt);
+                load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+            }
+            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
+            t = grab();
+            loaded = t < tend;
+            if (loaded) {
+                ft = tile_at(p, t);
+                load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
             }
         }
     } else {
@@ -537,6 +691,14 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_wg1024x1_pipe_nt", 1024, 1},           // + two tiles per wave
     {"s4_wg1024x1_nt_memonly", 1024, 1},        // DIAGNOSTIC: memory ceiling of 17
     {"s4_wg1024x1_compute_only", 1024, 1},      // DIAGNOSTIC: compute ceiling of 17
+    {"s4_wg1024x1_nt_early", 1024, 1},
+    {"s4_wg1024x1_nt_early2", 1024, 1},
+    {"s4_wg1024x1_nt_early_memonly", 1024, 1},
+    {"s4_wg1024x1_nt_early2_memonly", 1024, 1},
+    {"s4_wg1024x1_nt_stamps", 1024, 1},
+    {"s4_wg1024x1_nt_tail", 1024, 1},           // + cross-CU tail queue
+    {"s4_wg1024x1_nt_tail_memonly", 1024, 1},
+    {"s4_wg1024x1_nt_tail_stamps", 1024, 1},
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -572,6 +734,14 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 18: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModePipe); break;
     case 19: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeMemDiag); break;
     case 20: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeCompDiag); break;
+    case 21: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly); break;
+    case 22: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly2); break;
+    case 23: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly | kModeMemDiag); break;
+    case 24: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly2 | kModeMemDiag); break;
+    case 25: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeStamps); break;
+    case 26: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeTail); break;
+    case 27: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeTail | kModeMemDiag); break;
+    case 28: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeTail | kModeStamps); break;
     default: HDFS_LAUNCH(1024, 8, kModeNt); break;
     }
     return hipGetLastError();
