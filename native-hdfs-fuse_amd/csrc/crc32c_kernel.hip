@@ -54,21 +54,16 @@ constexpr uint32_t kS4ShiftOff = uint32_t(hdfs_crc::kS4ShiftOff);
 constexpr uint32_t kS4StageBytes = (kS4Bytes + 1023u) / 1024u * 1024u;
 static_assert(kS4StageBytes <= hdfs_crc::kTableAllocS4, "staging reads past the device table");
 
-// Kernel modes (template bits).  Production = kModeNt.
+// Kernel modes (template bits).  Production = kModeS4 | kModeNt.
 constexpr int kModeNt = 1;         // payload loads non-temporal (streamed once)
-constexpr int kModeEarly = 2;      // A/B: first tile requested before the table staging
-constexpr int kModeStamps = 4;     // DIAGNOSTIC: per-wave timestamps
-constexpr int kModeMemDiag = 8;    // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
-constexpr int kModeCompDiag = 16;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
-constexpr int kModeValuDiag = 32;  // DIAGNOSTIC, wrong results: lookup address math only, no LDS reads
-constexpr int kModeLdsDiag = 64;   // DIAGNOSTIC, wrong results: LDS reads at fixed addresses
-constexpr int kModeStrided = 128;  // EXPERIMENT (memory-only): lane-contiguous 128-byte loads
-constexpr int kModeHalfDiag = 256;     // EXPERIMENT, wrong results: half of the lookups
-constexpr int kModeQuarterDiag = 512;  // EXPERIMENT, wrong results: three quarters of the lookups
-constexpr int kModeS4 = 1024;     // slicing-by-4 chains + per-column finishing operator (S4 image)
-constexpr int kModePipe = 2048;   // two tiles per wave: the next tile's loads fly during this tile's lookups
-constexpr int kModeEarly2 = 4096; // first tile requested right behind the table staging, bare barrier
-constexpr int kModeTail = 8192;   // the last tiles go through a cross-CU queue (per-XCD heads, stealing)
+constexpr int kModeS4 = 2;         // slicing-by-4 chains + per-column finishing operator (S4 image)
+constexpr int kModeEarly2 = 4;     // A/B: first tile requested right behind the table staging, bare barrier
+constexpr int kModePipe = 8;       // A/B: two tiles per wave, the next in flight during the lookups
+constexpr int kModeStamps = 16;    // DIAGNOSTIC: per-wave timestamps
+constexpr int kModeMemDiag = 32;   // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
+constexpr int kModeCompDiag = 64;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
+constexpr int kModeValuDiag = 128; // DIAGNOSTIC, wrong results (nibble kernel): address math only, no LDS reads
+constexpr int kModeLdsDiag = 256;  // DIAGNOSTIC, wrong results (nibble kernel): LDS reads at fixed addresses
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -241,7 +236,7 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 // and read zeros without touching memory (lin() of zeros is 0, so they need
 // no mask), every lane uses the same one-VGPR offset plus an immediate, and
 // the instruction stream has no divergent branch.  AUX 2 = non-temporal.
-template <int AUX, bool COMPDIAG = false, bool STRIDED = false>
+template <int AUX, bool COMPDIAG = false>
 __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8]) {
     if (COMPDIAG) {  // synthetic data, no memory traffic
         const uint32_t x = uint32_t(t.src) * 2654435761u + uint32_t(lane) * 40503u;
@@ -252,11 +247,10 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
     const uint32_t nb = t.meta & 0xffu;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src), 0, int(nb * 512u), 0x00020000);
-    // STRIDED (experiment): lane l reads the 128 contiguous bytes 128l .. 128l+127.
-    const uint32_t voff = (STRIDED ? 128u : 16u) * uint32_t(lane);
+    const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (STRIDED ? 16u : 1024u) * i, 0, AUX);
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
     // Keep the loads ahead of whatever compute follows.
@@ -275,11 +269,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     uint32_t pc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        // DIAG 4 / 5 (experiment, wrong results): skip the lookups of 4 / 2 of the 8 pieces.
-        if ((DIAG == 4 && (i & 1)) || (DIAG == 5 && (i & 3) == 3))
-            pc[i] = v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
-        else
-            pc[i] = piece<S4, (DIAG >= 4 ? 0 : DIAG)>(lds, v[i], cols);
+        pc[i] = piece<S4, DIAG>(lds, v[i], cols);
         opaque(pc[i]);
         // One piece at a time (nibble tables: 32 independent reads each), or
         // two (S4: a piece is a chain of 4 dependent steps, so two chains
@@ -335,98 +325,6 @@ __device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
     uint32_t t = 0;
     if (lane == 0) t = atomicAdd(pool_ctr, 1u);
     return __builtin_amdgcn_readfirstlane(t);
-}
-
-// ---- tail queue (kModeTail) ------------------------------------------------
-// Equal static ranges leave CUs finishing several microseconds apart: the
-// memory system does not serve every CU at the same rate (tools/stamps.py).
-// So only tiles [0, static_tiles) are dealt statically; the rest (the
-// "tail", 1/8 by default) is cut into chunks of C = 1 << chunk_shift tiles,
-// XCD x owns a contiguous 1/8 of the chunks behind its own head counter (one
-// device-scope atomic per chunk, sharded per XCD as MI355X_MICROARCH.md
-// 'dequeue' prescribes), and a workgroup whose XCD is drained steals from
-// the next XCDs' heads.  Inside the workgroup the LDS ticket counter simply
-// runs on past the static range: ticket tend + k is tile k mod C of the
-// workgroup's (k / C)-th tail chunk, whose id sits in an LDS ring entry
-// stamped with its sequence number.  Chunk s is fetched by the wave that
-// takes ticket T_s = tend - L + s C (L = one ticket per wave ahead), or at
-// start when T_s precedes the first grabbed ticket, so every chunk a held
-// ticket refers to is fetched by someone and its ~1 us fetch overlaps L
-// tiles of work.
-constexpr uint32_t kNoChunk = 0xffffffffu;
-constexpr uint32_t kTailEnd = 0xffffffffu;   // queue drained
-constexpr uint32_t kTailSkip = 0xfffffffeu;  // ticket past the end of the last (partial) chunk
-constexpr uint32_t kRing = 64;  // a wrap needs 63 chunks fetched while one ticket is still unresolved
-
-struct TailLds {
-    uint64_t ring[kRing];  // (sequence << 32) | chunk id
-    uint32_t exhausted;    // bit x: XCD x's head is drained
-};
-
-// One lane: the next tail chunk for this workgroup, or kNoChunk.  The own
-// XCD's head first (one returning atomic, its latency hidden by the L-ticket
-// lookahead).  Once that is drained and stealing is on (p.tail_steal), the
-// other heads are read together (device-coherent loads, one round trip) and
-// the fullest one is claimed; a head found drained is never tried again.
-__device__ uint32_t tail_fetch(const KParams &p, TailLds *q, uint32_t nchunks, uint32_t xcc) {
-    uint32_t mask = __atomic_load_n(&q->exhausted, __ATOMIC_RELAXED);
-    const auto lo_of = [&](uint32_t x) { return uint32_t(uint64_t(nchunks) * x / 8u); };
-    const auto len_of = [&](uint32_t x) { return lo_of(x + 1u) - lo_of(x); };
-    if (!(mask & (1u << xcc))) {
-        const uint32_t c = len_of(xcc) ? atomicAdd(p.queue + 32u * xcc, 1u) : 0u;
-        if (c < len_of(xcc)) return lo_of(xcc) + c;
-        mask |= 1u << xcc;
-        atomicOr(&q->exhausted, 1u << xcc);
-    }
-    if (!p.tail_steal) return kNoChunk;
-    for (int attempt = 0; attempt < 8 && mask != 0xffu; ++attempt) {
-        uint32_t taken[8];
-#pragma unroll
-        for (uint32_t x = 0; x < 8; ++x)
-            taken[x] = (mask & (1u << x)) ? 0u
-                                          : __hip_atomic_load(p.queue + 32u * x, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t best = 8, best_rem = 0;
-#pragma unroll
-        for (uint32_t x = 0; x < 8; ++x) {
-            const uint32_t rem = (mask & (1u << x)) || taken[x] >= len_of(x) ? 0u : len_of(x) - taken[x];
-            if (rem == 0) mask |= 1u << x;
-            if (rem > best_rem) {
-                best_rem = rem;
-                best = x;
-            }
-        }
-        if (best == 8) break;
-        const uint32_t c = atomicAdd(p.queue + 32u * best, 1u);
-        if (c < len_of(best)) {
-            atomicOr(&q->exhausted, mask);
-            return lo_of(best) + c;
-        }
-        mask |= 1u << best;
-    }
-    atomicOr(&q->exhausted, 0xffu);
-    return kNoChunk;
-}
-
-__device__ __forceinline__ void ring_put(TailLds *q, uint32_t seq, uint32_t chunk) {
-    __atomic_store_n(&q->ring[seq % kRing], (uint64_t(seq) << 32) | chunk, __ATOMIC_RELAXED);
-}
-
-// Tile of tail ticket k (wave-uniform), kTailEnd or kTailSkip.
-__device__ uint32_t tail_resolve(const KParams &p, TailLds *q, uint32_t k) {
-    const uint32_t seq = k >> p.chunk_shift, i = k & ((1u << p.chunk_shift) - 1u);
-    uint64_t e;
-    for (;;) {
-        e = __atomic_load_n(&q->ring[seq % kRing], __ATOMIC_RELAXED);
-        const uint32_t es = __builtin_amdgcn_readfirstlane(uint32_t(e >> 32));
-        if (es == seq) break;
-        if (es != ~0u && es > seq) return kTailEnd;  // overwritten (cannot happen, see kRing): never spin forever
-        __builtin_amdgcn_s_sleep(1);
-    }
-    const uint32_t c = __builtin_amdgcn_readfirstlane(uint32_t(e));
-    if (c == kNoChunk) return kTailEnd;
-    const uint32_t t = p.static_tiles + (c << p.chunk_shift) + i;
-    return t < p.ntiles ? t : kTailSkip;
 }
 
 // ---- general path: half a wave per chunk of any length / alignment -------
@@ -508,23 +406,18 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
 template <int THREADS, int WPS, int MODE>
 __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams p) {
     constexpr bool NT = (MODE & kModeNt) != 0;
-    constexpr bool EARLY = (MODE & kModeEarly) != 0;
+    constexpr bool S4 = (MODE & kModeS4) != 0;
+    constexpr bool EARLY2 = (MODE & kModeEarly2) != 0;
+    constexpr bool PIPE = (MODE & kModePipe) != 0;
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
-    constexpr bool STRIDED = (MODE & kModeStrided) != 0;
-    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3
-                         : (MODE & kModeHalfDiag) ? 4 : (MODE & kModeQuarterDiag) ? 5 : 0;
-    constexpr bool S4 = (MODE & kModeS4) != 0;
-    constexpr bool PIPE = (MODE & kModePipe) != 0;
-    constexpr bool EARLY2 = (MODE & kModeEarly2) != 0;
-    constexpr bool TAIL = (MODE & kModeTail) != 0;
+    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
     // One LDS array: the tables, then the workgroup's tile counter.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16 + (TAIL ? sizeof(TailLds) : 0)];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
-    TailLds *tq = reinterpret_cast<TailLds *>(lds + kStage + 16);
     const uint8_t *table = S4 ? p.table_s4 : p.table;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
@@ -537,33 +430,12 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    // TAIL: the ranges cover [0, static_tiles); see "tail queue" above.
-    const uint32_t nstat = TAIL ? p.static_tiles : p.ntiles;
-    const uint32_t tbeg = uint32_t((uint64_t(nstat) * blockIdx.x) / gridDim.x);
-    const uint32_t tend = uint32_t((uint64_t(nstat) * (blockIdx.x + 1)) / gridDim.x);
+    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
     if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
-    uint32_t nchunks = 0, xcc = 0;
-    const int64_t trig0 = int64_t(tend) - int64_t(kWaves);  // T_0; T_s = T_0 + s C
-    if (TAIL) {
-        nchunks = ((p.ntiles - p.static_tiles) + (1u << p.chunk_shift) - 1u) >> p.chunk_shift;
-        xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20) & 7u;  // HW_REG_XCC_ID
-        if (blockIdx.x == 0 && threadIdx.x < 8) p.queue_next[32u * threadIdx.x] = 0;  // re-arm a later slot
-        if (threadIdx.x == 0) {
-            tq->exhausted = 0;
-            for (uint32_t r = 0; r < kRing; ++r) tq->ring[r] = ~uint64_t(0);
-            // chunks whose trigger ticket no wave will grab
-            for (uint32_t sq = 0; trig0 + int64_t(sq << p.chunk_shift) < int64_t(tbeg + kWaves); ++sq)
-                ring_put(tq, sq, tail_fetch(p, tq, nchunks, xcc));
-        }
-    }
     uint32_t t = tbeg + wv;
     FastTile ft{0, 0, 0};
     uint4 v[8];
-    // EARLY (A/B): request the first tile before the table staging.
-    if (EARLY && t < tend) {
-        ft = tile_at(p, t);
-        load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
-    }
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
     for (uint32_t c = wv; c < kStage / 1024u; c += kWaves)
         __builtin_amdgcn_global_load_lds(
@@ -575,7 +447,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         // barrier (__syncthreads' fence would wait for the tile too).
         if (t < tend) {
             ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
         }
         __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8) expcnt(7) lgkmcnt(15)
         __builtin_amdgcn_s_barrier();
@@ -584,19 +456,19 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     }
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY && !EARLY2 && t < tend) {
+    if (!EARLY2 && t < tend) {
         ft = tile_at(p, t);
-        load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
     }
     if (PIPE) {
         // Two register tiles per wave (a = v, b = vb): one is in flight while
-        // the other is looked up.  Needs ~100 VGPRs: 4 waves per SIMD.
+        // the other is looked up.
         uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
         FastTile fb{0, 0, 0};
         uint4 vb[8];
         if (tb < tend) {
             fb = tile_at(p, tb);
-            load_tile<AUX, COMPDIAG, STRIDED>(p, fb, lane, vb);
+            load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
         }
         while (t < tend) {
             finish_tile<DIAG, S4>(p, lds, ft, v, lane);
@@ -604,43 +476,14 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             t = pool_grab(pool_ctr, lane);
             if (t < tend) {
                 ft = tile_at(p, t);
-                load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+                load_tile<AUX, COMPDIAG>(p, ft, lane, v);
             }
             finish_tile<DIAG, S4>(p, lds, fb, vb, lane);
             if (t >= tend) break;
             tb = pool_grab(pool_ctr, lane);
             if (tb < tend) {
                 fb = tile_at(p, tb);
-                load_tile<AUX, COMPDIAG, STRIDED>(p, fb, lane, vb);
-            }
-        }
-    } else if (TAIL) {
-        // ticket t: static tile t while t < tend, else tail ticket t - tend
-        const auto grab = [&]() {
-            const uint32_t g = pool_grab(pool_ctr, lane);
-            const int64_t w = int64_t(g) - trig0;
-            if (w >= 0 && (uint32_t(w) & ((1u << p.chunk_shift) - 1u)) == 0 && lane == 0)
-                ring_put(tq, uint32_t(w) >> p.chunk_shift, tail_fetch(p, tq, nchunks, xcc));
-            return g;
-        };
-        bool loaded = t < tend;  // the first static tile is in flight already
-        for (;;) {
-            if (!loaded) {
-                const uint32_t tt = tail_resolve(p, tq, t - tend);
-                if (tt == kTailEnd) break;
-                if (tt == kTailSkip) {
-                    t = grab();
-                    continue;
-                }
-                ft = tile_at(p, tt);
-                load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
-            }
-            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
-            t = grab();
-            loaded = t < tend;
-            if (loaded) {
-                ft = tile_at(p, t);
-                load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+                load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
             }
         }
     } else {
@@ -649,7 +492,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             t = pool_grab(pool_ctr, lane);
             if (t >= tend) break;
             ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG, STRIDED>(p, ft, lane, v);
+            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
         }
     }
 
@@ -670,35 +513,18 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"wg1024_pool_nt", 1024, 2},                // production
-    {"wg1024_pool_nt_early", 1024, 2},          // A/B: first tile before the table staging
-    {"wg1024_pool", 1024, 2},                   // A/B: default-policy payload loads
-    {"wg512_pool_nt", 512, 2},                  // A/B: 16 waves per CU
-    {"wg1024_pool_nt_memonly", 1024, 2},        // DIAGNOSTIC: memory ceiling (no lookups)
-    {"wg1024_pool_nt_compute_only", 1024, 2},   // DIAGNOSTIC: compute ceiling (no payload loads)
-    {"wg1024_pool_nt_valu_only", 1024, 2},      // DIAGNOSTIC: 5 without the LDS reads
-    {"wg1024_pool_nt_lds_only", 1024, 2},       // DIAGNOSTIC: 5 without the address math
-    {"wg1024_pool_nt_stamps", 1024, 2},         // DIAGNOSTIC: 0 with per-wave timestamps
-    {"wg1024_pool_nt_memonly_stamps", 1024, 2}, // DIAGNOSTIC: 4 with per-wave timestamps
-    {"exp_strided_nt_memonly", 1024, 2},
-    {"exp_strided_memonly", 1024, 2},
-    {"exp_strided_nt_memonly_x1", 1024, 1},
-    {"exp_strided_memonly_x1", 1024, 1},
-    {"exp_nt_memonly_x1", 1024, 1},
-    {"exp_half_lookups", 1024, 2},
-    {"exp_three_quarter_lookups", 1024, 2},
-    {"s4_wg1024x1_nt", 1024, 1},                // slicing-by-4 chains, 1 WG (16 waves) per CU
-    {"s4_wg1024x1_pipe_nt", 1024, 1},           // + two tiles per wave
-    {"s4_wg1024x1_nt_memonly", 1024, 1},        // DIAGNOSTIC: memory ceiling of 17
-    {"s4_wg1024x1_compute_only", 1024, 1},      // DIAGNOSTIC: compute ceiling of 17
-    {"s4_wg1024x1_nt_early", 1024, 1},
-    {"s4_wg1024x1_nt_early2", 1024, 1},
-    {"s4_wg1024x1_nt_early_memonly", 1024, 1},
-    {"s4_wg1024x1_nt_early2_memonly", 1024, 1},
-    {"s4_wg1024x1_nt_stamps", 1024, 1},
-    {"s4_wg1024x1_nt_tail", 1024, 1},           // + cross-CU tail queue
-    {"s4_wg1024x1_nt_tail_memonly", 1024, 1},
-    {"s4_wg1024x1_nt_tail_stamps", 1024, 1},
+    {"s4_wg1024x1_nt", 1024, 1},                // production: slicing-by-4 chains, 16 waves per CU
+    {"nibble_wg1024x2_nt", 1024, 2},            // A/B: positional nibble tables, 32 waves per CU
+    {"s4_wg1024x1_nt_early2", 1024, 1},         // A/B: first tile right behind the table staging
+    {"s4_wg1024x1_nt_pipe", 1024, 1},           // A/B: two tiles per wave
+    {"s4_wg1024x1_nt_memonly", 1024, 1},        // DIAGNOSTIC: memory ceiling of 0 (no lookups)
+    {"s4_wg1024x1_nt_compute_only", 1024, 1},   // DIAGNOSTIC: compute ceiling of 0 (no payload loads)
+    {"nibble_wg1024x2_nt_memonly", 1024, 2},    // DIAGNOSTIC: memory ceiling of 1
+    {"nibble_wg1024x2_nt_compute_only", 1024, 2},  // DIAGNOSTIC: compute ceiling of 1
+    {"s4_wg1024x1_nt_stamps", 1024, 1},         // DIAGNOSTIC: 0 with per-wave timestamps
+    {"s4_wg1024x1_nt_memonly_stamps", 1024, 1}, // DIAGNOSTIC: 4 with per-wave timestamps
+    {"nibble_wg1024x2_nt_valu_only", 1024, 2},  // DIAGNOSTIC: 7 without the LDS reads
+    {"nibble_wg1024x2_nt_lds_only", 1024, 2},   // DIAGNOSTIC: 7 without the address math
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -713,36 +539,20 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{kv.threads, 1, 1};
+    constexpr int kS4Nt = kModeS4 | kModeNt;
     switch (variant) {
-    case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeEarly); break;
-    case 2: HDFS_LAUNCH(1024, 8, 0); break;
-    case 3: HDFS_LAUNCH(512, 4, kModeNt); break;
-    case 4: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag); break;
-    case 5: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag); break;
-    case 6: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
-    case 7: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
-    case 8: HDFS_LAUNCH(1024, 8, kModeNt | kModeStamps); break;
-    case 9: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStamps); break;
-    case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag | kModeStrided); break;
-    case 11: HDFS_LAUNCH(1024, 8, kModeMemDiag | kModeStrided); break;
-    case 12: HDFS_LAUNCH(1024, 4, kModeNt | kModeMemDiag | kModeStrided); break;
-    case 13: HDFS_LAUNCH(1024, 4, kModeMemDiag | kModeStrided); break;
-    case 14: HDFS_LAUNCH(1024, 4, kModeNt | kModeMemDiag); break;
-    case 15: HDFS_LAUNCH(1024, 8, kModeNt | kModeHalfDiag); break;
-    case 16: HDFS_LAUNCH(1024, 8, kModeNt | kModeQuarterDiag); break;
-    case 17: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4); break;
-    case 18: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModePipe); break;
-    case 19: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeMemDiag); break;
-    case 20: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeCompDiag); break;
-    case 21: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly); break;
-    case 22: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly2); break;
-    case 23: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly | kModeMemDiag); break;
-    case 24: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeEarly2 | kModeMemDiag); break;
-    case 25: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeStamps); break;
-    case 26: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeTail); break;
-    case 27: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeTail | kModeMemDiag); break;
-    case 28: HDFS_LAUNCH(1024, 4, kModeNt | kModeS4 | kModeTail | kModeStamps); break;
-    default: HDFS_LAUNCH(1024, 8, kModeNt); break;
+    case 1: HDFS_LAUNCH(1024, 8, kModeNt); break;
+    case 2: HDFS_LAUNCH(1024, 4, kS4Nt | kModeEarly2); break;
+    case 3: HDFS_LAUNCH(1024, 4, kS4Nt | kModePipe); break;
+    case 4: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag); break;
+    case 5: HDFS_LAUNCH(1024, 4, kS4Nt | kModeCompDiag); break;
+    case 6: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag); break;
+    case 7: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag); break;
+    case 8: HDFS_LAUNCH(1024, 4, kS4Nt | kModeStamps); break;
+    case 9: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeStamps); break;
+    case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
+    case 11: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
+    default: HDFS_LAUNCH(1024, 4, kS4Nt); break;
     }
     return hipGetLastError();
 }

@@ -5,7 +5,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -80,11 +79,6 @@ struct crc32c_ctx {
     int variant = 0;  // kernel variant, $HDFS_CRC32C_KVARIANT (A/B measurement only)
     uint8_t *d_table = nullptr;
     uint8_t *d_table_s4 = nullptr;
-    LaunchSlot *d_queue = nullptr;  // kQueueSlots tail-queue launch slots
-    std::atomic<uint32_t> next_queue{0};
-    uint32_t tail_64ths = 8;  // tail-queue share of the tiles in 1/64 units ($HDFS_CRC32C_TAIL, A/B only)
-    uint32_t chunk_shift = 2;  // tail chunk = 4 tiles ($HDFS_CRC32C_TAIL_CHUNK_SHIFT, A/B only)
-    uint32_t tail_steal = 0;   // $HDFS_CRC32C_TAIL_STEAL (A/B only)
     uint32_t c_lg[5];
     uint32_t c_small[4];
     std::mutex mu;
@@ -106,7 +100,7 @@ struct crc32c_multi {
 
 namespace {
 
-KParams params_for(crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
+KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
                    const void *payload, uint32_t *out, uint32_t flags) {
     KParams p;
     p.tiles = static_cast<const FastTile *>(tiles);
@@ -121,12 +115,6 @@ KParams params_for(crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const vo
     std::memcpy(p.c_lg, ctx->c_lg, sizeof p.c_lg);
     std::memcpy(p.c_small, ctx->c_small, sizeof p.c_small);
     p.stamps = nullptr;
-    const uint32_t slot = ctx->next_queue.fetch_add(1) % kQueueSlots;
-    p.queue = ctx->d_queue[slot].w;
-    p.queue_next = ctx->d_queue[(slot + kQueueSlots / 2) % kQueueSlots].w;
-    p.static_tiles = ntiles - uint32_t((uint64_t(ntiles) * ctx->tail_64ths) / 64u);
-    p.chunk_shift = ctx->chunk_shift;
-    p.tail_steal = ctx->tail_steal;
     return p;
 }
 
@@ -327,12 +315,6 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     build_lds_image_s4(img4.data());
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4), kTableAllocS4));
     HIP_TRY(hipMemcpy(c->d_table_s4, img4.data(), kTableAllocS4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_queue), kQueueSlots * sizeof(LaunchSlot)));
-    HIP_TRY(hipMemset(c->d_queue, 0, kQueueSlots * sizeof(LaunchSlot)));
-    if (const char *tl = std::getenv("HDFS_CRC32C_TAIL")) c->tail_64ths = uint32_t(std::min(64, std::max(0, std::atoi(tl))));
-    if (const char *st = std::getenv("HDFS_CRC32C_TAIL_STEAL")) c->tail_steal = std::atoi(st) != 0;
-    if (const char *cs = std::getenv("HDFS_CRC32C_TAIL_CHUNK_SHIFT"))
-        c->chunk_shift = uint32_t(std::min(6, std::max(0, std::atoi(cs))));
     *out = c.release();
     return 0;
 }
@@ -344,7 +326,6 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
         for (Stage &s : ctx->stage) free_stage(s);
         if (ctx->d_table) (void)hipFree(ctx->d_table);
         if (ctx->d_table_s4) (void)hipFree(ctx->d_table_s4);
-        if (ctx->d_queue) (void)hipFree(ctx->d_queue);
     }
     delete ctx;
     return 0;

@@ -194,3 +194,30 @@ def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     # shifting the payload by one chunk shifts the checksum vector by one
     got2 = run_dev(hdfs, gpu_ctx, np.ascontiguousarray(payload[512:]), oracle.uniform_packets(4095))
     assert np.array_equal(got2[:127], got[1:128])
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_every_product_kernel_variant(hdfs, golden, orc, variant, monkeypatch):
+    """Both table schemes (0 = slicing-by-4 chains, production; 1 = positional
+    nibble tables) and the A/B loop shapes (2, 3) are bit-exact: golden
+    config-2 digest, mixed bpc and a ragged batch through the general path."""
+    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
+    ctx = hdfs.Context(0)
+    try:
+        for name in ("c2_4096_packets", "c5_mixed_bpc_96", "ragged_tail_257"):
+            spec = [b for b in golden["batches"] if b["name"] == name][0]
+            pk = golden_batch_packets(spec)
+            payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+            got = run_dev(hdfs, ctx, payload, pk)
+            assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"], name
+        rng = np.random.default_rng(variant)
+        pk = oracle.mixed_packets(24)
+        pk["len"] = rng.integers(0, 65537, pk.size).astype(np.uint32)
+        pk["payload_off"] = np.arange(pk.size, dtype=np.uint64) * np.uint64(65536 + 48) + np.uint64(16)
+        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 99 + variant)
+        got = run_dev(hdfs, ctx, payload, pk)
+        assert np.array_equal(got, orc.batch(payload, pk, hdfs.total_checksums(pk)))
+    finally:
+        ctx.close()
