@@ -34,6 +34,10 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 KERNEL_NAME = "hdfs_crc32c_plan_kernel"
+# Template instance of the production variant (crc32c_kernel.hip, kVariants[0]:
+# 1024 threads, 4 waves/SIMD, kModeS4 | kModeNt); PMC traffic is only reported
+# from a summary of this exact kernel.
+PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<1024, 4, 3>"
 
 
 def load_package():
@@ -81,7 +85,7 @@ def baseline_metric() -> str:
 def latest_pmc(profile_dir: str):
     """HBM bytes per launch of the kernel from the committed rocprofv3 PMC
     summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
-    files = sorted(glob.glob(os.path.join(profile_dir, "*pmc*.json")))
+    files = sorted(glob.glob(os.path.join(profile_dir, "*pmc_c*.json")))
     if not files:
         return None
     try:
@@ -269,7 +273,8 @@ def main():
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"))
         traffic = None
-        if pmc and pmc.get("kernel") == KERNEL_NAME and pmc.get("config") == args.config:
+        if (pmc and pmc.get("config") == args.config
+                and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
         cpu = None if args.no_cpu else cpu_baseline(oracle, pk, payload0, args.cpu_seconds)
         line = {

@@ -31,8 +31,8 @@ def load(pmc_dir: str):
                 key = (os.path.basename(os.path.dirname(f)), row["Dispatch_Id"])
                 per[row["Counter_Name"]][key].append(float(row["Counter_Value"]))
                 durations[key] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
-                meta = {k: row[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count",
-                                            "SGPR_Count", "Scratch_Size")}
+                meta = {k: row[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
+                                            "VGPR_Count", "SGPR_Count", "Scratch_Size")}
     out = {}
     for c, d in per.items():
         vals = [sum(v) for v in d.values()]
