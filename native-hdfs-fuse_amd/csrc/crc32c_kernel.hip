@@ -14,11 +14,18 @@
 //    (16 B per lane) = two 512-byte blocks; lane q of each half owns bytes
 //    16q .. 16q+15 of its block in EVERY instruction.  Loads are
 //    non-temporal buffer loads bounded by the tile (partial tiles read zeros).
-//  * The Castagnoli tables live in LDS as positional NIBBLE tables, one
-//    128-byte row per nibble value with one 4-byte column per lane: the 32
-//    lanes of a ds_read_b32 group always hit 32 different banks (bank =
-//    column), so every lookup is conflict-free whatever the data.
-//    2 lookups per byte, 64 KiB of LDS (see crc_math.h for the layout).
+//  * Lookups, production (kModeS4): each lane chains its 16-byte piece
+//    d0..d3 through the slicing-by-4 step S (crc32c.c's crc32c_table[0..3],
+//    one 4-byte column per lane so the 32 lanes of a half-wave always hit 32
+//    different banks): u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-
+//    specific operator N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the
+//    piece's contribution to the block end.  20 LDS lookups + 37 VALU per
+//    16 bytes; 152 KiB of LDS, one 1024-thread workgroup per CU.
+//  * Lookups, A/B variant 1: positional NIBBLE tables, one 128-byte row per
+//    (byte position, nibble value), 2 lookups per byte: 32 lookups + 60 VALU
+//    per 16 bytes, 72 KiB, two workgroups per CU.  The kernel is power-capped
+//    (1.4 kW) when both HBM and LDS/VALU run flat out, so the 38 % fewer
+//    instructions of S4 turn into clock: 44 us vs 49-51 us sustained.
 //  * Wave-level reduction: each lane's per-piece value is XOR-reduced over
 //    the 32 lanes of its block with a DPP reduce-scatter, which also packs
 //    the 16 block results of a tile into 16 lanes for one coalesced store.
