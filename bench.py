@@ -149,9 +149,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # One process per GPU over RCCL (the "nccl" backend).  BENCH_DIST_BACKEND=gloo
+    # rehearses the N > 1 path with ranks sharing the visible GPUs (their
+    # collectives then go through host memory); never used for a measurement.
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     import oracle
 
@@ -225,11 +234,12 @@ def main():
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)  # avg per launch, on the launch stream
 
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # where collectives run
     if world > 1:
-        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(tt[0]), float(tt[1])
-        ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=dev)
+        ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         bit_exact = bool(ok.item())
     # RCCL gather of every rank's checksum array to rank 0 (the path's only
@@ -242,11 +252,12 @@ def main():
         g0 = time.perf_counter()
         if c4_blocks is not None:
             per_block = 64 * 128
-            full = shard.gather_checksums(outs[0][:nout], 32, per_block, world, rank)
+            full = shard.gather_checksums(outs[0][:nout].to(cdev), 32, per_block, world, rank)
         else:
-            gathered = [torch.empty_like(outs[0]) for _ in range(world)] if rank == 0 and world > 1 else None
+            send = outs[0].to(cdev)
+            gathered = [torch.empty_like(send) for _ in range(world)] if rank == 0 and world > 1 else None
             if world > 1:
-                dist.gather(outs[0], gathered, dst=0)
+                dist.gather(send, gathered, dst=0)
             full = None
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3 if world > 1 else None
@@ -287,7 +298,8 @@ def main():
             "config": {"workload": workload, "config": args.config, "packets_per_rank": int(pk.size),
                        "packet_bytes": int(pk["len"][0]), "bytes_per_checksum": sorted(set(int(x) for x in pk["bpc"])),
                        "payload_bytes_per_rank": nbytes, "checksums_per_rank": nout,
-                       "parallelism": "dp%d (independent shards, RCCL gather of checksums after timing)" % world},
+                       "parallelism": "dp%d (independent shards, %s gather of checksums after timing)"
+                                      % (world, "RCCL" if backend == "nccl" else backend + " rehearsal")},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "kernel": KERNEL_NAME, "kernel_avg_us": round(kernel_ms * 1e3, 2),

@@ -42,8 +42,16 @@ extern "C" {
  * ------------------------------------------------------------------------- */
 uint32_t crc32c(uint32_t crc, const void *buf, size_t len);
 
-/* Checksum flags. */
+/* Hadoop's CHECKSUM_CRC32 on the host: zlib's crc32(crc, buf, len) (reflected
+ * polynomial 0xEDB88320, same conditioning and incremental semantics as
+ * crc32c above).  The reference has no implementation (hadooprpc.c:629-631). */
+uint32_t hdfs_crc32(uint32_t crc, const void *buf, size_t len);
+
+/* Checksum flags (batch entry points). */
 #define CRC32C_BIG_ENDIAN 0x1u /* store htonl(crc), the wire order of hadooprpc.c:71-75 */
+#define CRC32C_TYPE_CRC32 0x2u /* Hadoop CHECKSUM_CRC32 (IEEE 802.3 / zlib polynomial)
+                                  instead of CHECKSUM_CRC32C; the reference returns
+                                  -ENOSYS for it (hadooprpc.c:629-631) */
 
 /* One packet of a batch: `len` payload bytes starting `payload_off` bytes into
  * the batch payload buffer, cut into chunks of `bpc` bytes

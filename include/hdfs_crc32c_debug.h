@@ -27,10 +27,13 @@ int crc32c_debug_plan(const crc32c_packet *pkts, size_t npkts, void *tiles, size
  * lg = 0..4, and crc32c(0, zeros(r)), r = 0..3. */
 size_t crc32c_debug_lds_image(void *dst, size_t cap, uint32_t *c_lg5, uint32_t *c_small4);
 
-/* The slicing-by-4 kernel's LDS image (byte tables T0..T3 replicated over
+/* The slicing-by-4 kernel's LDS image for the checksum type in `flags`
+ * (byte tables T0..T3 replicated over
  * the 32 lane columns, the per-column finishing operators N_q, the Z^(512 s)
  * shifts); returns its size and fills dst when cap is large enough. */
-size_t crc32c_debug_lds_image_s4(void *dst, size_t cap);
+size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags);
+/* The affine constants of the checksum type in `flags` (CRC32C_TYPE_CRC32 or not). */
+void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_small4);
 
 /* Diagnostic launch of a plan with an explicit kernel variant (see
  * kernel_abi.h kVariants; variants 3 and 6 write per-wave timestamps,

@@ -26,6 +26,7 @@ LIB_PATH = os.path.join(HERE, "libhdfs_crc32c.so")
 INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
 
 CRC32C_BIG_ENDIAN = 0x1
+CRC32C_TYPE_CRC32 = 0x2  # Hadoop CHECKSUM_CRC32 (zlib polynomial) instead of CRC32C
 
 PACKET_DTYPE = np.dtype(
     [("payload_off", "<u8"), ("out_idx", "<u8"), ("len", "<u4"), ("bpc", "<u4")], align=True
@@ -95,7 +96,9 @@ def _bind(L):
         "crc32c_last_error": (ctypes.c_char_p, []),
         "crc32c_debug_plan": (i32, [vp, sz, vp, sz, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_debug_lds_image": (sz, [vp, sz, vp, vp]),
-        "crc32c_debug_lds_image_s4": (sz, [vp, sz]),
+        "crc32c_debug_lds_image_s4": (sz, [vp, sz, u32]),
+        "crc32c_debug_affine_constants": (None, [u32, vp, vp]),
+        "hdfs_crc32": (u32, [u32, vp, sz]),
         "crc32c_debug_plan_exec_variant": (i32, [vp, vp, vp, vp, i32, vp]),
         "crc32c_debug_stream_probe": (i32, [vp, u64, vp, u32, i32, vp]),
     }
@@ -123,6 +126,12 @@ def as_packets(pkts) -> np.ndarray:
 def crc32c(data, crc: int = 0) -> int:
     a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
     return int(lib().crc32c(crc & 0xFFFFFFFF, _np_ptr(a), a.nbytes))
+
+
+def hdfs_crc32(data, crc: int = 0) -> int:
+    """Hadoop CHECKSUM_CRC32 on the host (zlib-compatible crc32)."""
+    a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
+    return int(lib().hdfs_crc32(crc & 0xFFFFFFFF, _np_ptr(a), a.nbytes))
 
 
 def nchunks(length: int, bpc: int) -> int:
@@ -294,9 +303,16 @@ def debug_lds_image():
     return img, c_lg, c_small
 
 
-def debug_lds_image_s4():
-    """The slicing-by-4 kernel's LDS image."""
-    n = int(lib().crc32c_debug_lds_image_s4(None, 0))
+def debug_lds_image_s4(flags: int = 0):
+    """The slicing-by-4 kernel's LDS image (CRC32C, or CRC32 with CRC32C_TYPE_CRC32)."""
+    n = int(lib().crc32c_debug_lds_image_s4(None, 0, flags))
     img = np.zeros(n, np.uint8)
-    lib().crc32c_debug_lds_image_s4(_np_ptr(img), n)
+    lib().crc32c_debug_lds_image_s4(_np_ptr(img), n, flags)
     return img
+
+
+def debug_affine_constants(flags: int = 0):
+    c_lg = np.zeros(5, np.uint32)
+    c_small = np.zeros(4, np.uint32)
+    lib().crc32c_debug_affine_constants(flags, _np_ptr(c_lg), _np_ptr(c_small))
+    return c_lg, c_small

@@ -105,6 +105,39 @@ extern "C" uint32_t crc32c(uint32_t crc, const void *buf, size_t len) {
     return ~reg_update_sw(r, p, len);
 }
 
+namespace {
+uint32_t g_ieee[8][256];
+std::once_flag g_ieee_once;
+
+void init_ieee() {
+    const uint32_t *t0 = hdfs_crc::byte_table(hdfs_crc::kPolyIeee);
+    for (int b = 0; b < 256; ++b) {
+        g_ieee[0][b] = t0[b];
+        for (int k = 1; k < 8; ++k) g_ieee[k][b] = (g_ieee[k - 1][b] >> 8) ^ t0[g_ieee[k - 1][b] & 0xffu];
+    }
+}
+}  // namespace
+
+extern "C" uint32_t hdfs_crc32(uint32_t crc, const void *buf, size_t len) {
+    // Slicing-by-8 over the IEEE tables (x86 has no CRC32 instruction for
+    // this polynomial); little-endian host, as crc32c.c:75-77 assumes too.
+    std::call_once(g_ieee_once, init_ieee);
+    const uint8_t *p = static_cast<const uint8_t *>(buf);
+    uint32_t r = ~crc;
+    size_t n = len;
+    for (; n && (reinterpret_cast<uintptr_t>(p) & 7u); --n) r = (r >> 8) ^ g_ieee[0][(r ^ *p++) & 0xffu];
+    for (; n >= 8; n -= 8, p += 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        w ^= r;
+        r = g_ieee[7][w & 0xff] ^ g_ieee[6][(w >> 8) & 0xff] ^ g_ieee[5][(w >> 16) & 0xff] ^
+            g_ieee[4][(w >> 24) & 0xff] ^ g_ieee[3][(w >> 32) & 0xff] ^ g_ieee[2][(w >> 40) & 0xff] ^
+            g_ieee[1][(w >> 48) & 0xff] ^ g_ieee[0][w >> 56];
+    }
+    for (; n; --n) r = (r >> 8) ^ g_ieee[0][(r ^ *p++) & 0xffu];
+    return ~r;
+}
+
 extern "C" uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc) {
     // roundup(len, bpc) (hadooprpc.c:639, roundup.h:7-11).
     return bpc ? (len + bpc - 1) / bpc : 0;

@@ -77,10 +77,11 @@ struct crc32c_ctx {
     int device = 0;
     int num_cu = 0;
     int variant = 0;  // kernel variant, $HDFS_CRC32C_KVARIANT (A/B measurement only)
-    uint8_t *d_table = nullptr;
-    uint8_t *d_table_s4 = nullptr;
-    uint32_t c_lg[5];
-    uint32_t c_small[4];
+    // per checksum type (0 = CRC32C, 1 = CRC32 / CRC32C_TYPE_CRC32)
+    uint8_t *d_table[2] = {nullptr, nullptr};
+    uint8_t *d_table_s4[2] = {nullptr, nullptr};
+    uint32_t c_lg[2][5];
+    uint32_t c_small[2][4];
     std::mutex mu;
     Stage stage[2];
 };
@@ -107,13 +108,14 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
     p.gen = static_cast<const GenItem *>(gen);
     p.payload = static_cast<const uint8_t *>(payload);
     p.out = out;
-    p.table = ctx->d_table;
-    p.table_s4 = ctx->d_table_s4;
+    const int ty = (flags & CRC32C_TYPE_CRC32) ? 1 : 0;
+    p.table = ctx->d_table[ty];
+    p.table_s4 = ctx->d_table_s4[ty];
     p.ntiles = ntiles;
     p.ngen = ngen;
     p.flags = flags;
-    std::memcpy(p.c_lg, ctx->c_lg, sizeof p.c_lg);
-    std::memcpy(p.c_small, ctx->c_small, sizeof p.c_small);
+    std::memcpy(p.c_lg, ctx->c_lg[ty], sizeof p.c_lg);
+    std::memcpy(p.c_small, ctx->c_small[ty], sizeof p.c_small);
     p.stamps = nullptr;
     return p;
 }
@@ -122,6 +124,13 @@ int launch(const crc32c_ctx *ctx, const KParams &p, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
     if (!items) return 0;
     HIP_TRY(launch_plan_kernel(p, ctx->variant, uint32_t(ctx->num_cu), stream));
+    return 0;
+}
+
+constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32;
+
+int check_flags(uint32_t flags) {
+    if (flags & ~kKnownFlags) return fail(-EINVAL, "unknown flags 0x%x", flags & ~kKnownFlags);
     return 0;
 }
 
@@ -306,15 +315,18 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
     if (const char *kv = std::getenv("HDFS_CRC32C_KVARIANT")) c->variant = std::atoi(kv);
-    std::vector<uint8_t> img(kTableAlloc, 0);
-    build_lds_image(img.data());
-    affine_constants(c->c_lg, c->c_small);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table), kTableAlloc));
-    HIP_TRY(hipMemcpy(c->d_table, img.data(), kTableAlloc, hipMemcpyHostToDevice));
-    std::vector<uint8_t> img4(kTableAllocS4, 0);
-    build_lds_image_s4(img4.data());
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4), kTableAllocS4));
-    HIP_TRY(hipMemcpy(c->d_table_s4, img4.data(), kTableAllocS4, hipMemcpyHostToDevice));
+    for (int ty = 0; ty < 2; ++ty) {
+        const uint32_t poly = ty ? kPolyIeee : kPoly;
+        std::vector<uint8_t> img(kTableAlloc, 0);
+        build_lds_image(img.data(), poly);
+        affine_constants(c->c_lg[ty], c->c_small[ty], poly);
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table[ty]), kTableAlloc));
+        HIP_TRY(hipMemcpy(c->d_table[ty], img.data(), kTableAlloc, hipMemcpyHostToDevice));
+        std::vector<uint8_t> img4(kTableAllocS4, 0);
+        build_lds_image_s4(img4.data(), poly);
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4));
+        HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4, hipMemcpyHostToDevice));
+    }
     *out = c.release();
     return 0;
 }
@@ -324,8 +336,10 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
     {
         DeviceGuard guard(ctx->device);
         for (Stage &s : ctx->stage) free_stage(s);
-        if (ctx->d_table) (void)hipFree(ctx->d_table);
-        if (ctx->d_table_s4) (void)hipFree(ctx->d_table_s4);
+        for (int ty = 0; ty < 2; ++ty) {
+            if (ctx->d_table[ty]) (void)hipFree(ctx->d_table[ty]);
+            if (ctx->d_table_s4[ty]) (void)hipFree(ctx->d_table_s4[ty]);
+        }
     }
     delete ctx;
     return 0;
@@ -335,7 +349,8 @@ int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts,
                        crc32c_plan **out) {
     if (!ctx || !out) return fail(-EINVAL, "ctx/out == NULL");
     *out = nullptr;
-    int rc = check_packets(pkts, npkts);
+    int rc = check_flags(flags);
+    if (!rc) rc = check_packets(pkts, npkts);
     if (rc) return rc;
     HostPlan hp;
     rc = build_plan(pkts, npkts, &hp);
@@ -417,7 +432,8 @@ int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, 
 int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
                       uint32_t *out, uint32_t flags) {
     if (!ctx) return fail(-EINVAL, "ctx == NULL");
-    int rc = check_packets(pkts, npkts);
+    int rc = check_flags(flags);
+    if (!rc) rc = check_packets(pkts, npkts);
     if (rc) return rc;
     if (npkts && (!payload || !out)) return fail(-EINVAL, "payload/out == NULL");
     std::lock_guard<std::mutex> lock(ctx->mu);

@@ -12,7 +12,10 @@
 
 namespace hdfs_crc {
 
-constexpr uint32_t kPoly = 0x82f63b78u;  // crc32c.c:43
+constexpr uint32_t kPoly = 0x82f63b78u;      // CRC32C, Castagnoli (crc32c.c:43)
+constexpr uint32_t kPolyIeee = 0xedb88320u;  // CRC32, IEEE 802.3 / zlib (Hadoop's CHECKSUM_CRC32)
+// Both are reflected CRCs with init ~0 and final ~0; everything below takes
+// the polynomial as a parameter (only these two are supported).
 
 // 32x32 GF(2) matrix stored as the images of the 32 unit vectors.
 struct Gf2Op {
@@ -25,15 +28,15 @@ struct Gf2Op {
     }
 };
 
-const uint32_t *byte_table();               // T0[b]: register after one byte b from register 0
-uint32_t append_zero_byte(uint32_t reg);     // linear register, one zero byte appended
+const uint32_t *byte_table(uint32_t poly = kPoly);            // T0[b]: register after byte b from register 0
+uint32_t append_zero_byte(uint32_t reg, uint32_t poly = kPoly);  // linear register, one zero byte appended
 Gf2Op op_identity();
-Gf2Op op_compose(const Gf2Op &a, const Gf2Op &b);  // a after b
-Gf2Op op_zeros(uint64_t nbytes);                   // append nbytes zero bytes
+Gf2Op op_compose(const Gf2Op &a, const Gf2Op &b);           // a after b
+Gf2Op op_zeros(uint64_t nbytes, uint32_t poly = kPoly);      // append nbytes zero bytes
 
-// Linear part of CRC32C over bytes with register starting at 0 (no
-// conditioning): crc32c(0, M) == lin(M) ^ crc32c(0, zeros(len)).
-uint32_t lin_bytes(const uint8_t *p, size_t n, uint32_t reg = 0);
+// Linear part of the CRC over bytes with register starting at 0 (no
+// conditioning): crc(0, M) == lin(M) ^ crc(0, zeros(len)).
+uint32_t lin_bytes(const uint8_t *p, size_t n, uint32_t reg = 0, uint32_t poly = kPoly);
 
 // ---- the GPU's LDS image (see DESIGN.md "LDS layout") ----
 // [0, 65536): positional nibble tables of one 512-byte block.  Lane column q
@@ -50,7 +53,7 @@ constexpr int kMaxShift = 15;
 constexpr size_t kLdsBytes = kLdsPosBytes + kMaxShift * 512;
 
 // Fills `dst` (kLdsBytes) with the LDS image.
-void build_lds_image(uint8_t *dst);
+void build_lds_image(uint8_t *dst, uint32_t poly = kPoly);
 
 // ---- the slicing-by-4 kernel's LDS image (see DESIGN.md "S4 kernel") ----
 // A lane chains its 16-byte piece d0..d3 through the position-independent
@@ -68,11 +71,11 @@ constexpr size_t kS4ShiftOff = 147456;
 constexpr size_t kS4Bytes = kS4ShiftOff + kMaxShift * 512;
 
 // Fills `dst` (kS4Bytes) with the slicing-by-4 LDS image.
-void build_lds_image_s4(uint8_t *dst);
+void build_lds_image_s4(uint8_t *dst, uint32_t poly = kPoly);
 // S(u): the register after feeding the 4 bytes of u (little-endian) into register 0.
-uint32_t s4_step(uint32_t u);
+uint32_t s4_step(uint32_t u, uint32_t poly = kPoly);
 
-// crc32c(0, zeros(512 << lg)) for lg = 0..4 and crc32c(0, zeros(r)) for r = 0..3.
-void affine_constants(uint32_t c_lg[5], uint32_t c_small[4]);
+// crc(0, zeros(512 << lg)) for lg = 0..4 and crc(0, zeros(r)) for r = 0..3.
+void affine_constants(uint32_t c_lg[5], uint32_t c_small[4], uint32_t poly = kPoly);
 
 }  // namespace hdfs_crc

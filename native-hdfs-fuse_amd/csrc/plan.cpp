@@ -1,5 +1,6 @@
 // plan.cpp -- see plan.h.
 #include "plan.h"
+#include "hdfs_crc32c.h"
 
 #include <cerrno>
 #include <cstring>
@@ -86,7 +87,13 @@ extern "C" size_t crc32c_debug_lds_image(void *dst, size_t cap, uint32_t *c_lg, 
     return hdfs_crc::kLdsBytes;
 }
 
-extern "C" size_t crc32c_debug_lds_image_s4(void *dst, size_t cap) {
-    if (dst && cap >= hdfs_crc::kS4Bytes) hdfs_crc::build_lds_image_s4(static_cast<uint8_t *>(dst));
+extern "C" size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags) {
+    const uint32_t poly = (flags & CRC32C_TYPE_CRC32) ? hdfs_crc::kPolyIeee : hdfs_crc::kPoly;
+    if (dst && cap >= hdfs_crc::kS4Bytes) hdfs_crc::build_lds_image_s4(static_cast<uint8_t *>(dst), poly);
     return hdfs_crc::kS4Bytes;
+}
+
+extern "C" void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg, uint32_t *c_small) {
+    const uint32_t poly = (flags & CRC32C_TYPE_CRC32) ? hdfs_crc::kPolyIeee : hdfs_crc::kPoly;
+    hdfs_crc::affine_constants(c_lg, c_small, poly);
 }

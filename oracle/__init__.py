@@ -236,3 +236,27 @@ def total_checksums(pkts: np.ndarray) -> int:
         return 0
     per = (pkts["len"].astype(np.uint64) + pkts["bpc"].astype(np.uint64) - 1) // pkts["bpc"].astype(np.uint64)
     return int((pkts["out_idx"] + per).max())
+
+
+# ---- Hadoop CHECKSUM_CRC32 ("next" row 3) ------------
+# The reference has no CRC32 implementation (hadooprpc.c:629-631 returns
+# -ENOSYS).  Hadoop's CHECKSUM_CRC32 is java.util.zip.CRC32, i.e. zlib's
+# crc32; Python's zlib module (the system zlib) is the independent oracle,
+# applied per chunk exactly as the CRC32C loop of hadooprpc.c:733-742.
+def zlib_chunks(packet: np.ndarray, bpc: int) -> np.ndarray:
+    import zlib
+
+    b = np.ascontiguousarray(packet, dtype=np.uint8).tobytes()
+    return np.array([zlib.crc32(b[i:i + bpc]) for i in range(0, len(b), bpc)], dtype=np.uint32)
+
+
+def zlib_batch(payload: np.ndarray, pkts: np.ndarray, nout: int) -> np.ndarray:
+    import zlib
+
+    out = np.zeros(max(nout, 1), dtype=np.uint32)
+    mv = memoryview(np.ascontiguousarray(payload, dtype=np.uint8))
+    for p in pkts:
+        off, n, bpc, oi = int(p["payload_off"]), int(p["len"]), int(p["bpc"]), int(p["out_idx"])
+        for i, c in enumerate(range(0, n, bpc)):
+            out[oi + i] = zlib.crc32(mv[off + c:off + min(c + bpc, n)])
+    return out[:nout]

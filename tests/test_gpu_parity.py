@@ -221,3 +221,33 @@ def test_every_product_kernel_variant(hdfs, golden, orc, variant, monkeypatch):
         assert np.array_equal(got, orc.batch(payload, pk, hdfs.total_checksums(pk)))
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_crc32_type_matches_zlib(hdfs, variant, monkeypatch):
+    """CHECKSUM_CRC32 (CRC32C_TYPE_CRC32): same kernel, zlib-polynomial tables;
+    per-chunk results equal zlib.crc32 (the reference returns -ENOSYS here,
+    hadooprpc.c:629-631).  Fast tiles, mixed bpc, ragged tails, unaligned
+    packets, big-endian output, host path."""
+    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
+    ctx = hdfs.Context(0)
+    try:
+        T = hdfs.CRC32C_TYPE_CRC32
+        pk = oracle.uniform_packets(64)
+        payload = oracle.xorshift64_bytes(64 * 65536, 77)
+        want = oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk))
+        assert np.array_equal(run_dev(hdfs, ctx, payload, pk, T), want)
+        be = run_dev(hdfs, ctx, payload, pk, T | hdfs.CRC32C_BIG_ENDIAN)
+        assert np.array_equal(be, want.byteswap())
+        rng = np.random.default_rng(40 + variant)
+        pk = oracle.mixed_packets(30)
+        pk["len"] = rng.integers(0, 65537, pk.size).astype(np.uint32)
+        pk["payload_off"] = np.arange(pk.size, dtype=np.uint64) * np.uint64(65536 + 40) + np.uint64(3)
+        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 81 + variant)
+        want = oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk))
+        assert np.array_equal(run_dev(hdfs, ctx, payload, pk, T), want)
+        assert np.array_equal(ctx.batch_host(payload, pk, T), want)
+    finally:
+        ctx.close()

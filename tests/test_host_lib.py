@@ -170,3 +170,44 @@ def test_s4_image_matches_nibble_image(hdfs, model):
     w4 = img4.view("<u4")
     w = img.view("<u4")
     assert np.array_equal(w4[KernelModelS4.SHIFT_OFF // 4:], w[65536 // 4:65536 // 4 + w4.size - KernelModelS4.SHIFT_OFF // 4])
+
+
+# ---- CHECKSUM_CRC32 (zlib polynomial) ------------------------------------
+def test_hdfs_crc32_matches_zlib(hdfs):
+    import zlib
+
+    assert hdfs.hdfs_crc32(b"123456789") == 0xCBF43926  # the CRC-32 check value
+    assert hdfs.hdfs_crc32(b"") == 0
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 70000, dtype=np.uint8)
+    for off, n in [(0, 1), (1, 7), (3, 8), (5, 513), (0, 65536), (7, 69993)]:
+        assert hdfs.hdfs_crc32(buf[off:off + n]) == zlib.crc32(buf[off:off + n].tobytes()), (off, n)
+    # incremental, as crc32c(crc, ...)
+    assert hdfs.hdfs_crc32(buf[100:300], hdfs.hdfs_crc32(buf[:100])) == zlib.crc32(buf[:300].tobytes())
+
+
+@pytest.mark.parametrize("lg", [0, 2, 4])
+def test_crc32_tables_match_zlib(hdfs, lg):
+    """The CRC32 images (nibble and S4) and constants give zlib's per-chunk CRC32."""
+    img, _, _ = hdfs.debug_lds_image()  # layout only; CRC32 contents below
+    c_lg, c_small = hdfs.debug_affine_constants(hdfs.CRC32C_TYPE_CRC32)
+    img4 = hdfs.debug_lds_image_s4(hdfs.CRC32C_TYPE_CRC32)
+    m4 = KernelModelS4(img4)
+    bpc = 512 << lg
+    data = oracle.xorshift64_bytes(bpc * 4, 300 + lg)
+    data[:bpc] = 0
+    lins = m4.block_lin(data.reshape(-1, 512)).reshape(-1, 1 << lg)
+    # combine the blocks of a chunk with Z^(512 s) from the image's shift section
+    zm = KernelModel(np.concatenate([np.zeros(65536, np.uint8), img4[KernelModelS4.SHIFT_OFF:]]), c_lg, c_small)
+    got = []
+    for c in range(lins.shape[0]):
+        x = 0
+        for m in range(1 << lg):
+            s = (1 << lg) - 1 - m
+            x ^= zm.zshift(s, int(lins[c, m])) if s else int(lins[c, m])
+        got.append(x ^ int(c_lg[lg]))
+    assert np.array_equal(np.array(got, np.uint32), oracle.zlib_chunks(data, bpc))
+    for r in range(4):
+        import zlib
+        assert int(c_small[r]) == zlib.crc32(bytes(r))
+    assert img.size > 0
