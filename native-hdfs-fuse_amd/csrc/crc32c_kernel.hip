@@ -71,6 +71,8 @@ constexpr int kModeMemDiag = 32;   // DIAGNOSTIC, wrong results: no lookups (mem
 constexpr int kModeCompDiag = 64;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
 constexpr int kModeValuDiag = 128; // DIAGNOSTIC, wrong results (nibble kernel): address math only, no LDS reads
 constexpr int kModeLdsDiag = 256;  // DIAGNOSTIC, wrong results (nibble kernel): LDS reads at fixed addresses
+constexpr int kModeRotate = 512;   // A/B: workgroup w walks its range starting at a w-dependent rotation
+constexpr int kModeGstride = 1024; // A/B: static grid-stride per wave: wave g takes tiles g, g + W, g + 2W, ...
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -419,6 +421,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
     constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
+    constexpr bool ROTATE = (MODE & kModeRotate) != 0;
+    constexpr bool GSTRIDE = (MODE & kModeGstride) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
@@ -441,6 +445,17 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
     if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
     uint32_t t = tbeg + wv;
+    // ROTATE: ticket t -> tile tbeg + (t - tbeg + rot) mod n, rot spread over
+    // the range by a golden-ratio step, so that at any moment the CUs stream
+    // from different offsets of their ranges (HBM channel spread).
+    const uint32_t nrange = tend - tbeg;
+    const uint32_t rot = nrange ? uint32_t((uint64_t(blockIdx.x) * 2654435769u >> 32) * nrange >> 32) : 0u;
+    const auto tile_of = [&](uint32_t tk) -> FastTile {
+        if (!ROTATE) return tile_at(p, tk);
+        uint32_t j = tk - tbeg + rot;
+        if (j >= nrange) j -= nrange;
+        return tile_at(p, tbeg + j);
+    };
     FastTile ft{0, 0, 0};
     uint4 v[8];
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
@@ -453,7 +468,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         // for all but those 8 (vmcnt counts in issue order), then a bare
         // barrier (__syncthreads' fence would wait for the tile too).
         if (t < tend) {
-            ft = tile_at(p, t);
+            ft = tile_of(t);
             load_tile<AUX, COMPDIAG>(p, ft, lane, v);
         }
         __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8) expcnt(7) lgkmcnt(15)
@@ -463,18 +478,26 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     }
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY2 && t < tend) {
-        ft = tile_at(p, t);
+    if (!EARLY2 && !GSTRIDE && t < tend) {
+        ft = tile_of(t);
         load_tile<AUX, COMPDIAG>(p, ft, lane, v);
     }
-    if (PIPE) {
+    if (GSTRIDE) {
+        // t was loaded as tbeg + wv above only when !GSTRIDE: restart here.
+        const uint32_t W = gridDim.x * kWaves;
+        for (uint32_t g = blockIdx.x * kWaves + wv; g < p.ntiles; g += W) {
+            ft = tile_at(p, g);
+            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
+        }
+    } else if (PIPE) {
         // Two register tiles per wave (a = v, b = vb): one is in flight while
         // the other is looked up.
         uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
         FastTile fb{0, 0, 0};
         uint4 vb[8];
         if (tb < tend) {
-            fb = tile_at(p, tb);
+            fb = tile_of(tb);
             load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
         }
         while (t < tend) {
@@ -482,14 +505,14 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             if (tb >= tend) break;
             t = pool_grab(pool_ctr, lane);
             if (t < tend) {
-                ft = tile_at(p, t);
+                ft = tile_of(t);
                 load_tile<AUX, COMPDIAG>(p, ft, lane, v);
             }
             finish_tile<DIAG, S4>(p, lds, fb, vb, lane);
             if (t >= tend) break;
             tb = pool_grab(pool_ctr, lane);
             if (tb < tend) {
-                fb = tile_at(p, tb);
+                fb = tile_of(tb);
                 load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
             }
         }
@@ -498,7 +521,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             finish_tile<DIAG, S4>(p, lds, ft, v, lane);
             t = pool_grab(pool_ctr, lane);
             if (t >= tend) break;
-            ft = tile_at(p, t);
+            ft = tile_of(t);
             load_tile<AUX, COMPDIAG>(p, ft, lane, v);
         }
     }
@@ -532,6 +555,11 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_wg1024x1_nt_memonly_stamps", 1024, 1}, // DIAGNOSTIC: 4 with per-wave timestamps
     {"nibble_wg1024x2_nt_valu_only", 1024, 2},  // DIAGNOSTIC: 7 without the LDS reads
     {"nibble_wg1024x2_nt_lds_only", 1024, 2},   // DIAGNOSTIC: 7 without the address math
+    {"s4_wg1024x1_nt_rotate", 1024, 1},         // A/B: rotated walk of each range
+    {"s4_wg1024x1_nt_rotate_memonly", 1024, 1}, // DIAGNOSTIC: memory ceiling of 12
+    {"s4_wg1024x1_nt_gstride", 1024, 1},        // A/B: static grid-stride per wave
+    {"s4_wg1024x1_nt_gstride_memonly", 1024, 1},
+    {"s4_wg1024x2_nt_gstride_memonly_512thr", 512, 2},
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -559,6 +587,11 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 9: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeStamps); break;
     case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
     case 11: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
+    case 12: HDFS_LAUNCH(1024, 4, kS4Nt | kModeRotate); break;
+    case 13: HDFS_LAUNCH(1024, 4, kS4Nt | kModeRotate | kModeMemDiag); break;
+    case 14: HDFS_LAUNCH(1024, 4, kS4Nt | kModeGstride); break;
+    case 15: HDFS_LAUNCH(1024, 4, kS4Nt | kModeGstride | kModeMemDiag); break;
+    case 16: HDFS_LAUNCH(512, 4, kModeNt | kModeGstride | kModeMemDiag); break;
     default: HDFS_LAUNCH(1024, 4, kS4Nt); break;
     }
     return hipGetLastError();

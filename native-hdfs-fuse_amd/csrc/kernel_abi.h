@@ -37,7 +37,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 12;
+constexpr int kNumVariants = 17;
 extern const KernelVariant kVariants[kNumVariants];
 
 // Persistent grid: min(work items / waves per workgroup, wg_per_cu * CUs) of the variant.
