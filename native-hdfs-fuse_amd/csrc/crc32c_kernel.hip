@@ -71,11 +71,7 @@ constexpr int kModeMemDiag = 32;   // DIAGNOSTIC, wrong results: no lookups (mem
 constexpr int kModeCompDiag = 64;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
 constexpr int kModeValuDiag = 128; // DIAGNOSTIC, wrong results (nibble kernel): address math only, no LDS reads
 constexpr int kModeLdsDiag = 256;  // DIAGNOSTIC, wrong results (nibble kernel): LDS reads at fixed addresses
-constexpr int kModeRotate = 512;   // A/B: workgroup w walks its range starting at a w-dependent rotation
-constexpr int kModeGstride = 1024; // A/B: static grid-stride per wave: wave g takes tiles g, g + W, g + 2W, ...
-constexpr int kModeGlobalLd = 2048; // EXPERIMENT (full tiles only): global_load nt instead of bounded buffer loads
-constexpr int kModeNoStage = 4096;  // DIAGNOSTIC (memory-only): no table staging
-constexpr int kModeFastStage = 8192;  // S4: replicate the byte tables with LDS writes from a compact copy
+constexpr int kModeNoStage = 512;   // DIAGNOSTIC (memory-only): no table staging
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -248,20 +244,8 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 // and read zeros without touching memory (lin() of zeros is 0, so they need
 // no mask), every lane uses the same one-VGPR offset plus an immediate, and
 // the instruction stream has no divergent branch.  AUX 2 = non-temporal.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
-template <int AUX, bool COMPDIAG = false, bool GLOBALLD = false>
+template <int AUX, bool COMPDIAG = false>
 __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8]) {
-    if (GLOBALLD) {  // experiment: no bounds (full tiles only)
-        const u32x4_t *src = reinterpret_cast<const u32x4_t *>(p.payload + t.src) + lane;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const u32x4_t r = __builtin_nontemporal_load(src + 64 * i);
-            v[i] = make_uint4(r[0], r[1], r[2], r[3]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        return;
-    }
     if (COMPDIAG) {  // synthetic data, no memory traffic
         const uint32_t x = uint32_t(t.src) * 2654435761u + uint32_t(lane) * 40503u;
 #pragma unroll
@@ -436,11 +420,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
     constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
-    constexpr bool ROTATE = (MODE & kModeRotate) != 0;
-    constexpr bool GSTRIDE = (MODE & kModeGstride) != 0;
-    constexpr bool GLOBALLD = (MODE & kModeGlobalLd) != 0;
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
-    constexpr bool FASTSTAGE = S4 && (MODE & kModeFastStage) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
@@ -463,39 +443,10 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
     if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
     uint32_t t = tbeg + wv;
-    // ROTATE: ticket t -> tile tbeg + (t - tbeg + rot) mod n, rot spread over
-    // the range by a golden-ratio step, so that at any moment the CUs stream
-    // from different offsets of their ranges (HBM channel spread).
-    const uint32_t nrange = tend - tbeg;
-    const uint32_t rot = nrange ? uint32_t((uint64_t(blockIdx.x) * 2654435769u >> 32) * nrange >> 32) : 0u;
-    const auto tile_of = [&](uint32_t tk) -> FastTile {
-        if (!ROTATE) return tile_at(p, tk);
-        uint32_t j = tk - tbeg + rot;
-        if (j >= nrange) j -= nrange;
-        return tile_at(p, tbeg + j);
-    };
     FastTile ft{0, 0, 0};
     uint4 v[8];
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
-    if (FASTSTAGE) {
-        // The 1024 byte-table rows (T_m[b], 32 columns = 8 x 16 B each) are
-        // written with ds_write_b128 from a compact 4 KiB copy: item k = row
-        // k >> 3, chunk k & 7, rows ordered (b, m) so that the 16 lanes of one
-        // write pass cover rows (b, 0) and (b, 1) -- 256 contiguous bytes, 64
-        // different banks.  The N_q and shift sections (distinct per column)
-        // still come by LDS-DMA.
-        static_assert(!FASTSTAGE || THREADS == 1024, "fast staging assumes 1024 threads");
-        const uint32_t *compact = reinterpret_cast<const uint32_t *>(table + hdfs_crc::kS4CompactOff);
-#pragma unroll
-        for (uint32_t it = 0; it < 8; ++it) {
-            const uint32_t item = it * 1024u + threadIdx.x;
-            const uint32_t row = item >> 3, chunk = item & 7u, b = row >> 2, m = row & 3u;
-            const uint32_t e = compact[m * 256u + b];
-            *reinterpret_cast<uint4 *>(lds + (m >> 1) * 65536u + b * 256u + (m & 1u) * 128u + chunk * 16u) =
-                make_uint4(e, e, e, e);
-        }
-    }
-    for (uint32_t c = wv + (FASTSTAGE ? kS4NibOff / 1024u : 0u); !NOSTAGE && c < kStage / 1024u; c += kWaves)
+    for (uint32_t c = wv; !NOSTAGE && c < kStage / 1024u; c += kWaves)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
             (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
@@ -504,8 +455,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         // for all but those 8 (vmcnt counts in issue order), then a bare
         // barrier (__syncthreads' fence would wait for the tile too).
         if (t < tend) {
-            ft = tile_of(t);
-            load_tile<AUX, COMPDIAG, GLOBALLD>(p, ft, lane, v);
+            ft = tile_at(p, t);
+            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
             __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0): staging loads and LDS writes done
         } else {
             __builtin_amdgcn_s_waitcnt(0x0070);  // no tile in flight: vmcnt(0) lgkmcnt(0)
@@ -516,42 +467,34 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     }
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY2 && !GSTRIDE && t < tend) {
-        ft = tile_of(t);
-        load_tile<AUX, COMPDIAG, GLOBALLD>(p, ft, lane, v);
+    if (!EARLY2 && t < tend) {
+        ft = tile_at(p, t);
+        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
     }
-    if (GSTRIDE) {
-        // t was loaded as tbeg + wv above only when !GSTRIDE: restart here.
-        const uint32_t W = gridDim.x * kWaves;
-        for (uint32_t g = blockIdx.x * kWaves + wv; g < p.ntiles; g += W) {
-            ft = tile_at(p, g);
-            load_tile<AUX, COMPDIAG, GLOBALLD>(p, ft, lane, v);
-            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
-        }
-    } else if (PIPE) {
+    if (PIPE) {
         // Two register tiles per wave (a = v, b = vb): one is in flight while
         // the other is looked up.
         uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
         FastTile fb{0, 0, 0};
         uint4 vb[8];
         if (tb < tend) {
-            fb = tile_of(tb);
-            load_tile<AUX, COMPDIAG, GLOBALLD>(p, fb, lane, vb);
+            fb = tile_at(p, tb);
+            load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
         }
         while (t < tend) {
             finish_tile<DIAG, S4>(p, lds, ft, v, lane);
             if (tb >= tend) break;
             t = pool_grab(pool_ctr, lane);
             if (t < tend) {
-                ft = tile_of(t);
-                load_tile<AUX, COMPDIAG, GLOBALLD>(p, ft, lane, v);
+                ft = tile_at(p, t);
+                load_tile<AUX, COMPDIAG>(p, ft, lane, v);
             }
             finish_tile<DIAG, S4>(p, lds, fb, vb, lane);
             if (t >= tend) break;
             tb = pool_grab(pool_ctr, lane);
             if (tb < tend) {
-                fb = tile_of(tb);
-                load_tile<AUX, COMPDIAG, GLOBALLD>(p, fb, lane, vb);
+                fb = tile_at(p, tb);
+                load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
             }
         }
     } else {
@@ -559,8 +502,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             finish_tile<DIAG, S4>(p, lds, ft, v, lane);
             t = pool_grab(pool_ctr, lane);
             if (t >= tend) break;
-            ft = tile_of(t);
-            load_tile<AUX, COMPDIAG, GLOBALLD>(p, ft, lane, v);
+            ft = tile_at(p, t);
+            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
         }
     }
 
@@ -593,19 +536,7 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_wg1024x1_nt_memonly_stamps", 1024, 1}, // DIAGNOSTIC: 4 with per-wave timestamps
     {"nibble_wg1024x2_nt_valu_only", 1024, 2},  // DIAGNOSTIC: 7 without the LDS reads
     {"nibble_wg1024x2_nt_lds_only", 1024, 2},   // DIAGNOSTIC: 7 without the address math
-    {"s4_wg1024x1_nt_rotate", 1024, 1},         // A/B: rotated walk of each range
-    {"s4_wg1024x1_nt_rotate_memonly", 1024, 1}, // DIAGNOSTIC: memory ceiling of 12
-    {"s4_wg1024x1_nt_gstride", 1024, 1},        // A/B: static grid-stride per wave
-    {"s4_wg1024x1_nt_gstride_memonly", 1024, 1},
-    {"s4_wg1024x2_nt_gstride_memonly_512thr", 512, 2},
-    {"s4_wg1024x1_globalld", 1024, 1},
-    {"s4_wg1024x1_globalld_memonly", 1024, 1},
-    {"s4_wg1024x1_memonly_nostage", 1024, 1},
-    {"s4_wg1024x1_memonly_nostage_stamps", 1024, 1},
-    {"s4_wg1024x1_nt_faststage", 1024, 1},      // A/B: tables replicated by LDS writes
-    {"s4_wg1024x1_nt_faststage_memonly", 1024, 1},
-    {"s4_wg1024x1_nt_faststage_stamps", 1024, 1},
-    {"s4_wg1024x1_nt_faststage_early2", 1024, 1},
+    {"s4_wg1024x1_nt_memonly_nostage", 1024, 1},  // DIAGNOSTIC: 4 without the table staging
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -633,19 +564,7 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 9: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeStamps); break;
     case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
     case 11: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
-    case 12: HDFS_LAUNCH(1024, 4, kS4Nt | kModeRotate); break;
-    case 13: HDFS_LAUNCH(1024, 4, kS4Nt | kModeRotate | kModeMemDiag); break;
-    case 14: HDFS_LAUNCH(1024, 4, kS4Nt | kModeGstride); break;
-    case 15: HDFS_LAUNCH(1024, 4, kS4Nt | kModeGstride | kModeMemDiag); break;
-    case 16: HDFS_LAUNCH(512, 4, kModeNt | kModeGstride | kModeMemDiag); break;
-    case 17: HDFS_LAUNCH(1024, 4, kS4Nt | kModeGlobalLd); break;
-    case 18: HDFS_LAUNCH(1024, 4, kS4Nt | kModeGlobalLd | kModeMemDiag); break;
-    case 19: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeNoStage); break;
-    case 20: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeNoStage | kModeStamps); break;
-    case 21: HDFS_LAUNCH(1024, 4, kS4Nt | kModeFastStage); break;
-    case 22: HDFS_LAUNCH(1024, 4, kS4Nt | kModeFastStage | kModeMemDiag); break;
-    case 23: HDFS_LAUNCH(1024, 4, kS4Nt | kModeFastStage | kModeStamps); break;
-    case 24: HDFS_LAUNCH(1024, 4, kS4Nt | kModeFastStage | kModeEarly2); break;
+    case 12: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeNoStage); break;
     default: HDFS_LAUNCH(1024, 4, kS4Nt); break;
     }
     return hipGetLastError();

@@ -324,10 +324,6 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         HIP_TRY(hipMemcpy(c->d_table[ty], img.data(), kTableAlloc, hipMemcpyHostToDevice));
         std::vector<uint8_t> img4(kTableAllocS4, 0);
         build_lds_image_s4(img4.data(), poly);
-        for (uint32_t m = 0; m < 4; ++m)  // compact T_m[b] (column 0 of the replicated tables)
-            for (uint32_t b = 0; b < 256; ++b)
-                std::memcpy(img4.data() + kS4CompactOff + (m * 256 + b) * 4,
-                            img4.data() + (m >> 1) * 65536 + b * 256 + (m & 1) * 128, 4);
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4));
         HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4, hipMemcpyHostToDevice));
     }

@@ -13,12 +13,7 @@ constexpr uint32_t kKernelShiftOff = uint32_t(kLdsShiftOff);
 // Device copy of the LDS image, zero-padded so every staging load of a
 // 1024-thread workgroup (16 B per thread per round) is in bounds.
 constexpr uint32_t kTableAlloc = ((kKernelLdsBytes + 16384 - 1) / 16384) * 16384;
-// S4 device image: the LDS image (staged by LDS-DMA, rounded up to 1 KiB),
-// then the byte tables T0..T3 once more in compact form (4 x 256 dwords) for
-// the fast-staging variant, which replicates them over the lane columns with
-// LDS writes instead of copying all 32 replicas from L2.
-constexpr uint32_t kS4CompactOff = ((uint32_t(kS4Bytes) + 1023u) / 1024u) * 1024u;
-constexpr uint32_t kTableAllocS4 = ((kS4CompactOff + 4096u + 16384u - 1u) / 16384u) * 16384u;
+constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 16384;
 
 struct KParams {
     const FastTile *tiles;
@@ -42,7 +37,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 25;
+constexpr int kNumVariants = 13;
 extern const KernelVariant kVariants[kNumVariants];
 
 // Persistent grid: min(work items / waves per workgroup, wg_per_cu * CUs) of the variant.
