@@ -270,6 +270,26 @@ def main():
     value = total_bytes / elapsed / GIB
     achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
 
+    # Read-side verification (crc32c_plan_verify) of buffer 0 against its
+    # checksums, timed the same way (rank 0, reported beside the main line).
+    verify = None
+    if rank == 0:
+        res = torch.zeros(2, dtype=torch.int32, device=dev)
+        for _ in range(3):
+            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), sptr)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        nv = 20
+        for _ in range(nv):
+            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), sptr)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(np.uint32)
+        verify = {"gib_s": round(nbytes * nv / (e0.elapsed_time(e1) * 1e-3) / GIB, 1),
+                  "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
+                  "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF)}
+
     host = None
     if rank == 0 and not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
@@ -307,6 +327,7 @@ def main():
             "cpu_baseline": cpu,
             "bit_exact_vs_reference": bit_exact,
             "host_resident_gib_s": host,
+            "verify": verify,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         }
         print(json.dumps(line), flush=True)

@@ -110,6 +110,18 @@ uint64_t crc32c_plan_nchecksums(const crc32c_plan *plan);
 /* Payload bytes the plan checksums (sum of packet lengths). */
 uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
 
+/* Verification, the read side ("next" row 1): a DataNode
+ * sends each packet's checksums ahead of its data (received by
+ * hadoop_rpc_receive_packets, src/hadooprpc.c:497-584; the reference asks for
+ * none, src/fuse.c:1608-1609).  Computes every checksum of the plan's batch on
+ * the GPU and compares it with dev_expected[same index] (in wire order when
+ * the plan was created with CRC32C_BIG_ENDIAN) instead of storing it.
+ * dev_result: 2 device u32s, set by this call (asynchronously on `stream`):
+ * [0] = mismatching checksums, [1] = lowest mismatching index (0xffffffff
+ * when none). */
+int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
+                       uint32_t *dev_result, void *stream);
+
 /* One-shot device batch: builds a plan, runs it on `stream` and waits for it. */
 int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,
                       uint32_t *dev_out, uint32_t flags, void *stream);
@@ -122,6 +134,12 @@ int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, 
  * ------------------------------------------------------------------------- */
 int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
                       uint32_t *out, uint32_t flags);
+
+/* Host-resident verification (blocking): returns the number of checksums that
+ * differ from expected[] (>= 0; only indices the packets cover are compared),
+ * or -errno; *first_bad = the lowest such index (UINT64_MAX when none). */
+int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                           const uint32_t *expected, uint32_t flags, uint64_t *first_bad);
 
 /* The reference's per-packet loop (hadooprpc.c:733-742) on one host packet:
  * out receives ceil(len / bpc) checksums.  Uses the process-wide default
@@ -140,6 +158,34 @@ int crc32c_multi_create(const int *devices, int ndevices, crc32c_multi **out);
 int crc32c_multi_destroy(crc32c_multi *m);
 int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_packet *pkts, size_t npkts,
                             uint32_t group_packets, uint32_t *out, uint32_t flags);
+
+/* ---------------------------------------------------------------------------
+ * 6. Host-side companions of the checksum path.
+ * ------------------------------------------------------------------------- */
+
+/* Batched packet framing ("next" row 2).  hadoop_rpc_send_packet sends every
+ * packet as PLEN (u32 BE) | HLEN (u16 BE) | PacketHeaderProto | checksums
+ * (u32 BE each) | data with 1 + 1 + 1 + n sendto calls (src/hadooprpc.c:
+ * 596-664, 733-748).  This writes the prefixes (everything but the data) of
+ * a whole batch back to back into `out`, so each packet can go out as one
+ * sendmsg of two iovecs: out + prefix_off[i] .. prefix_off[i+1], then its
+ * data.  Per packet i: offsetInBlock = block_offset + payload_off[i] -
+ * payload_off[0], seqno = first_seqno + i (0 at a block start,
+ * hadooprpc.c:825), lastPacketInBlock = (len == 0), dataLen = len;
+ * PLEN = 4 + checksum_len * nchunks + len (hadooprpc.c:640).
+ * `sums` holds each packet's checksums at out_idx (host order, or wire order
+ * with CRC32C_BIG_ENDIAN in flags); checksum_len is 4 (CRC32C / CRC32) or 0
+ * (CHECKSUM_NULL).  prefix_off (optional) receives npkts + 1 offsets.
+ * Returns the bytes written, or the bytes needed when `out` is NULL or `cap`
+ * is too small (nothing written then); 0 on invalid arguments. */
+size_t crc32c_frame_packets(const crc32c_packet *pkts, size_t npkts, const uint32_t *sums, uint32_t flags,
+                            uint64_t block_offset, int64_t first_seqno, uint32_t checksum_len, uint8_t *out,
+                            size_t cap, uint64_t *prefix_off);
+
+/* OpBlockChecksumResponseProto.md5 ("next" row 4, datatransfer.proto:262-267):
+ * MD5 over a block's checksums as big-endian bytes (`sums` in host order, or
+ * wire order with CRC32C_BIG_ENDIAN). */
+void crc32c_block_md5(const uint32_t *sums, size_t n, uint32_t flags, uint8_t md5[16]);
 
 /* Last error text of the calling thread (static storage, never NULL). */
 const char *crc32c_last_error(void);

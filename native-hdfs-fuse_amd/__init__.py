@@ -97,6 +97,10 @@ def _bind(L):
         "crc32c_debug_plan": (i32, [vp, sz, vp, sz, vp, sz, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_debug_lds_image": (sz, [vp, sz, vp, vp]),
         "crc32c_debug_lds_image_s4": (sz, [vp, sz, u32]),
+        "crc32c_plan_verify": (i32, [vp, vp, vp, vp, vp]),
+        "crc32c_frame_packets": (sz, [vp, sz, vp, u32, u64, ctypes.c_int64, u32, vp, sz, vp]),
+        "crc32c_block_md5": (None, [vp, sz, u32, vp]),
+        "crc32c_verify_host": (ctypes.c_int64, [vp, vp, vp, sz, vp, u32, vp]),
         "crc32c_debug_affine_constants": (None, [u32, vp, vp]),
         "hdfs_crc32": (u32, [u32, vp, sz]),
         "crc32c_debug_plan_exec_variant": (i32, [vp, vp, vp, vp, i32, vp]),
@@ -132,6 +136,31 @@ def hdfs_crc32(data, crc: int = 0) -> int:
     """Hadoop CHECKSUM_CRC32 on the host (zlib-compatible crc32)."""
     a = np.ascontiguousarray(np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else data)
     return int(lib().hdfs_crc32(crc & 0xFFFFFFFF, _np_ptr(a), a.nbytes))
+
+
+def frame_packets(pkts, sums: np.ndarray, flags: int = 0, block_offset: int = 0, first_seqno: int = 0,
+                  checksum_len: int = 4):
+    """Per-packet send prefixes (PLEN | HLEN | PacketHeaderProto | checksums) of
+    a batch: (bytes, offsets[npkts + 1])."""
+    pkts = as_packets(pkts)
+    sums = np.ascontiguousarray(sums, dtype=np.uint32)
+    need = int(lib().crc32c_frame_packets(_np_ptr(pkts), pkts.size, _np_ptr(sums), flags, block_offset,
+                                          first_seqno, checksum_len, None, 0, None))
+    out = np.zeros(max(need, 1), np.uint8)
+    offs = np.zeros(pkts.size + 1, np.uint64)
+    got = int(lib().crc32c_frame_packets(_np_ptr(pkts), pkts.size, _np_ptr(sums), flags, block_offset,
+                                         first_seqno, checksum_len, _np_ptr(out), out.size, _np_ptr(offs)))
+    if got != need:
+        raise Crc32cError(-errno.EINVAL, "crc32c_frame_packets")
+    return out[:need].tobytes(), offs
+
+
+def block_md5(sums: np.ndarray, flags: int = 0) -> bytes:
+    """OpBlockChecksumResponseProto.md5 of a block's checksums."""
+    sums = np.ascontiguousarray(sums, dtype=np.uint32)
+    md5 = np.zeros(16, np.uint8)
+    lib().crc32c_block_md5(_np_ptr(sums), sums.size, flags, _np_ptr(md5))
+    return md5.tobytes()
 
 
 def nchunks(length: int, bpc: int) -> int:
@@ -190,6 +219,18 @@ class Context:
                "crc32c_batch_host")
         return out[:n]
 
+    def verify_host(self, payload: np.ndarray, pkts, expected: np.ndarray, flags: int = 0):
+        """Host-resident verification: (number of mismatching checksums, lowest bad index or None)."""
+        pkts = as_packets(pkts)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        expected = np.ascontiguousarray(expected, dtype=np.uint32)
+        first = ctypes.c_uint64(0)
+        rc = lib().crc32c_verify_host(self.handle, _np_ptr(payload), _np_ptr(pkts), pkts.size, _np_ptr(expected),
+                                      flags, ctypes.byref(first))
+        if rc < 0:
+            _check(int(rc), "crc32c_verify_host")
+        return int(rc), (None if first.value == 0xFFFFFFFFFFFFFFFF else int(first.value))
+
     def chunks_dev(self, pkts, dev_payload: int, dev_out: int, flags: int = 0, stream: int = 0) -> None:
         pkts = as_packets(pkts)
         _check(lib().crc32c_chunks_dev(self.handle, _np_ptr(pkts), pkts.size, ctypes.c_void_p(dev_payload),
@@ -212,6 +253,11 @@ class Plan:
     def exec(self, dev_payload: int, dev_out: int, stream: int = 0) -> None:
         _check(lib().crc32c_plan_exec(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
                                       ctypes.c_void_p(stream)), "crc32c_plan_exec")
+
+    def verify(self, dev_payload: int, dev_expected: int, dev_result: int, stream: int = 0) -> None:
+        """Compare instead of store: dev_result[0] = mismatches, [1] = lowest bad index (async)."""
+        _check(lib().crc32c_plan_verify(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_expected),
+                                        ctypes.c_void_p(dev_result), ctypes.c_void_p(stream)), "crc32c_plan_verify")
 
     def exec_variant(self, dev_payload: int, dev_out: int, variant: int, dev_stamps: int = 0, stream: int = 0) -> None:
         """Diagnostic: run an explicit kernel variant (3/6 write per-wave timestamps)."""

@@ -237,6 +237,20 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
     return (flags & 1u) ? __builtin_bswap32(crc) : crc;  // htonl on the wire, hadooprpc.c:71-75
 }
 
+// Checksum `idx` of the batch: stored, or (verification) compared with the
+// expected value; a mismatch bumps result[0] and lowers result[1].
+__device__ __forceinline__ void emit(const KParams &p, uint32_t idx, uint32_t crc) {
+    const uint32_t v = out_order(crc, p.flags);
+    if (p.expect) {
+        if (v != p.expect[idx]) {
+            atomicAdd(p.result, 1u);
+            atomicMin(p.result + 1, idx);
+        }
+    } else {
+        p.out[idx] = v;
+    }
+}
+
 // ---- fast path: one wave, 16 blocks of full chunks -----------------------
 // Loads of one tile: instruction i reads 1 KiB contiguous (blocks 2i, 2i+1)
 // through a buffer descriptor whose range is the tile's nb * 512 valid
@@ -325,7 +339,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     }
     const uint32_t crc = x ^ p.c_lg[lg];
     const bool rep = ((lane & 0x14) == 0) && ((blk & ((1u << lg) - 1u)) == 0) && blk < nb;
-    if (rep) p.out[t.out + (blk >> lg)] = out_order(crc, p.flags);
+    if (rep) emit(p, t.out + (blk >> lg), crc);
 }
 
 // One tile index from the workgroup's LDS counter (one ds_add_rtn per wave).
@@ -403,7 +417,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
     }
     if (valid && q == 0) {
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
-        p.out[g.out] = out_order(crc, p.flags);
+        emit(p, g.out, crc);
     }
 }
 

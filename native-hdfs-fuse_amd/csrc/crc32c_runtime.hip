@@ -117,6 +117,8 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
     std::memcpy(p.c_lg, ctx->c_lg[ty], sizeof p.c_lg);
     std::memcpy(p.c_small, ctx->c_small[ty], sizeof p.c_small);
     p.stamps = nullptr;
+    p.expect = nullptr;
+    p.result = nullptr;
     return p;
 }
 
@@ -386,6 +388,51 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
     const KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload,
                                  dev_out, plan->flags);
     return launch(plan->ctx, p, static_cast<hipStream_t>(stream));
+}
+
+int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
+                       uint32_t *dev_result, void *stream) {
+    if (!plan) return fail(-EINVAL, "plan == NULL");
+    if (!dev_result) return fail(-EINVAL, "result == NULL");
+    DeviceGuard guard(plan->ctx->device);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result), 0, 1, s));
+    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));
+    if (plan->nchecksums == 0) return 0;
+    if (!dev_payload || !dev_expected) return fail(-EINVAL, "payload/expected == NULL");
+    if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
+        return fail(-EINVAL, "device payload must be 16-byte aligned");
+    KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, nullptr,
+                           plan->flags);
+    p.expect = dev_expected;
+    p.result = dev_result;
+    return launch(plan->ctx, p, s);
+}
+
+int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                           const uint32_t *expected, uint32_t flags, uint64_t *first_bad) {
+    if (first_bad) *first_bad = UINT64_MAX;
+    if (!ctx) return fail(-EINVAL, "ctx == NULL");
+    uint64_t n = 0;
+    for (size_t i = 0; i < npkts; ++i)
+        if (pkts && pkts[i].bpc) n = std::max<uint64_t>(n, pkts[i].out_idx + crc32c_nchunks(pkts[i].len, pkts[i].bpc));
+    if (n && !expected) return fail(-EINVAL, "expected == NULL");
+    std::vector<uint32_t> got(std::max<uint64_t>(n, 1));
+    int rc = crc32c_batch_host(ctx, payload, pkts, npkts, got.data(), flags);
+    if (rc) return rc;
+    // Only the indices the packets cover are compared (gaps between packets are not checksums).
+    int64_t bad = 0;
+    uint64_t first = UINT64_MAX;
+    for (size_t i = 0; i < npkts; ++i) {
+        const uint64_t k0 = pkts[i].out_idx, k1 = k0 + crc32c_nchunks(pkts[i].len, pkts[i].bpc);
+        for (uint64_t k = k0; k < k1; ++k)
+            if (got[k] != expected[k]) {
+                ++bad;
+                first = std::min(first, k);
+            }
+    }
+    if (first_bad) *first_bad = first;
+    return bad;
 }
 
 int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,

@@ -28,6 +28,10 @@ struct KParams {
     uint32_t c_lg[5];
     uint32_t c_small[4];
     uint64_t *stamps;  // diagnostic variant only: 4 x u64 per wave
+    // Verification (crc32c_plan_verify): compare with expect[] instead of
+    // storing to out[]; result[0] += mismatches, result[1] = min bad index.
+    const uint32_t *expect;
+    uint32_t *result;
 };
 
 // Kernel variants; 0 is the production kernel, the others stay built for

@@ -251,3 +251,58 @@ def test_crc32_type_matches_zlib(hdfs, variant, monkeypatch):
         assert np.array_equal(ctx.batch_host(payload, pk, T), want)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_verify_reports_mismatches(hdfs, orc, variant, monkeypatch):
+    """Read-side verification (crc32c_plan_verify / crc32c_verify_host): no
+    mismatch on intact data; a corrupted payload byte or expected checksum is
+    counted and the lowest bad index reported; wire-order expectations with
+    CRC32C_BIG_ENDIAN; fast tiles and general-path chunks."""
+    torch = _torch()
+    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
+    ctx = hdfs.Context(0)
+    try:
+        rng = np.random.default_rng(60 + variant)
+        pk = oracle.mixed_packets(40)
+        pk["len"] = rng.integers(1, 65537, pk.size).astype(np.uint32)
+        pk["len"][:20] = 65536  # fast tiles
+        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 5 + variant)
+        n = hdfs.total_checksums(pk)
+        stream = torch.cuda.current_stream()
+        for flags in (0, hdfs.CRC32C_BIG_ENDIAN):
+            want = orc.batch(payload, pk, n, big_endian=bool(flags))
+            plan = hdfs.Plan(ctx, pk, flags)
+            dev = torch.from_numpy(payload).cuda()
+            exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+            res = torch.zeros(2, dtype=torch.int32, device="cuda")
+
+            def verify():
+                plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+                stream.synchronize()
+                r = res.cpu().numpy().view(np.uint32)
+                return int(r[0]), int(r[1])
+
+            assert verify() == (0, 0xFFFFFFFF)
+            # corrupt one payload byte inside packet 25 (a general-path packet) -> its chunk
+            p25 = pk[25]
+            off = int(p25["len"]) // 2
+            dev[int(p25["payload_off"]) + off] ^= 0x01
+            bad_idx = int(p25["out_idx"]) + off // int(p25["bpc"])
+            assert verify() == (1, bad_idx)
+            dev[int(p25["payload_off"]) + off] ^= 0x01
+            # corrupt expected checksums 7 (fast tile) and bad_idx
+            exp[7] ^= 0x100
+            exp[bad_idx] ^= 0x1
+            assert verify() == (2, 7)
+            plan.close()
+            # host path
+            cnt, first = ctx.verify_host(payload, pk, want, flags)
+            assert (cnt, first) == (0, None)
+            w2 = want.copy()
+            w2[[3, n - 1]] ^= 1
+            assert ctx.verify_host(payload, pk, w2, flags) == (2, 3)
+    finally:
+        ctx.close()
