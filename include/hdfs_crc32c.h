@@ -118,7 +118,11 @@ uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
  * the plan was created with CRC32C_BIG_ENDIAN) instead of storing it.
  * dev_result: 2 device u32s, set by this call (asynchronously on `stream`):
  * [0] = mismatching checksums, [1] = lowest mismatching index (0xffffffff
- * when none). */
+ * when none).  One launch: the last workgroup to finish publishes the result
+ * (no separate reset of dev_result).  A plan's verify launches must not run
+ * concurrently with each other (they share the plan's device scratch);
+ * serialise them on one stream.  Kernel variants other than 0 and 1
+ * ($HDFS_CRC32C_KVARIANT, A/B only) return -EINVAL. */
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream);
 

@@ -47,6 +47,11 @@ namespace {
 using hdfs_crc::FastTile;
 using hdfs_crc::GenItem;
 using hdfs_crc::KParams;
+using hdfs_crc::kMaxHeads;
+using hdfs_crc::kHeadStride;
+using hdfs_crc::kTicketWord;
+using hdfs_crc::kVCountWord;
+using hdfs_crc::kVFirstWord;
 
 constexpr uint32_t kLdsBytes = hdfs_crc::kKernelLdsBytes;
 constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
@@ -72,6 +77,10 @@ constexpr int kModeCompDiag = 64;  // DIAGNOSTIC, wrong results: no payload load
 constexpr int kModeValuDiag = 128; // DIAGNOSTIC, wrong results (nibble kernel): address math only, no LDS reads
 constexpr int kModeLdsDiag = 256;  // DIAGNOSTIC, wrong results (nibble kernel): LDS reads at fixed addresses
 constexpr int kModeNoStage = 512;   // DIAGNOSTIC (memory-only): no table staging
+constexpr int kModeVerify = 1024;   // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
+constexpr int kModeDyn = 2048;      // dynamic tile scheduler (per-wave prefetched grabs, stealing) instead of static ranges
+constexpr int kModeStriped = 8192;  // scheduler heads striped over the tiles (one sweep front)
+constexpr int kModeSchedWave = 4096;  // last wave of the workgroup schedules: static share, then head grabs; LDS ring
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -85,6 +94,21 @@ __device__ __forceinline__ FastTile tile_at(const KParams &p, uint32_t i) {
     r.src = t->src;
     r.out = t->out;
     r.meta = t->meta;
+    return r;
+}
+
+// Descriptor prefetch through the VECTOR memory path: issued behind a tile's
+// payload loads it is the youngest vmcnt entry, so the lookups never wait for
+// it (a scalar load would: lgkmcnt also counts the LDS lookups, and scalar
+// loads return out of order).  Every lane loads the same 16 bytes.
+__device__ __forceinline__ uint4 tile_prefetch(const KParams &p, uint32_t i) {
+    return *reinterpret_cast<const uint4 *>(p.tiles + i);
+}
+__device__ __forceinline__ FastTile tile_from(uint4 d) {
+    FastTile r;
+    r.src = (uint64_t(__builtin_amdgcn_readfirstlane(d.y)) << 32) | __builtin_amdgcn_readfirstlane(d.x);
+    r.out = __builtin_amdgcn_readfirstlane(d.z);
+    r.meta = __builtin_amdgcn_readfirstlane(d.w);
     return r;
 }
 
@@ -237,17 +261,281 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
     return (flags & 1u) ? __builtin_bswap32(crc) : crc;  // htonl on the wire, hadooprpc.c:71-75
 }
 
-// Checksum `idx` of the batch: stored, or (verification) compared with the
-// expected value; a mismatch bumps result[0] and lowers result[1].
-__device__ __forceinline__ void emit(const KParams &p, uint32_t idx, uint32_t crc) {
+// Checksum `idx` of the batch: stored, or (VERIFY) compared with the
+// expected value; a mismatch bumps the workgroup's LDS count and lowers its
+// LDS first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish).
+template <bool VERIFY>
+__device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc) {
     const uint32_t v = out_order(crc, p.flags);
-    if (p.expect) {
+    if (VERIFY) {
         if (v != p.expect[idx]) {
-            atomicAdd(p.result, 1u);
-            atomicMin(p.result + 1, idx);
+            atomicAdd(vacc, 1u);
+            atomicMin(vacc + 1, idx);
         }
     } else {
         p.out[idx] = v;
+    }
+}
+
+// Fast-path verification: the expected value was prefetched with the tile.
+__device__ __forceinline__ void check(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t ev) {
+    if (out_order(crc, p.flags) != ev) {
+        atomicAdd(vacc, 1u);
+        atomicMin(vacc + 1, idx);
+    }
+}
+
+// ---- launch-wide scheduler / verification state (kernel_abi.h slots) ----
+__device__ __forceinline__ uint32_t *head_ptr(uint32_t *sched, uint32_t h) { return sched + h * kHeadStride; }
+
+// Start of a launch, one thread of workgroup 0: restore the OTHER slot of the
+// pair (used by the previous launch, which has completed) for the next launch.
+__device__ __forceinline__ void reset_next_slot(const KParams &p) {
+    uint32_t *s = p.sched_next;
+#pragma unroll
+    for (uint32_t h = 0; h < kMaxHeads; ++h) atomicExch(head_ptr(s, h), 0u);
+    atomicExch(s + kTicketWord, 0u);
+    atomicExch(s + kVCountWord, 0u);
+    atomicExch(s + kVFirstWord, 0xffffffffu);
+}
+
+// End of a verification launch, thread 0 of every workgroup: fold the
+// workgroup's count / first-bad index into the slot, take a ticket, and let
+// the last workgroup publish the totals to p.result[0..1] (threadfence
+// reduction; no host-side reset of the result is needed).
+__device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
+    uint32_t *s = p.sched;
+    const uint32_t cnt = vacc[0], first = vacc[1];
+    if (cnt) {
+        atomicAdd(s + kVCountWord, cnt);
+        atomicMin(s + kVFirstWord, first);
+    }
+    __threadfence();
+    const uint32_t ticket = atomicAdd(s + kTicketWord, 1u);
+    if (ticket == gridDim.x - 1u) {
+        __threadfence();
+        p.result[0] = atomicAdd(s + kVCountWord, 0u);
+        p.result[1] = atomicAdd(s + kVFirstWord, 0u);
+    }
+}
+
+// Dynamic tile scheduler.  Every wave's first tile is static (tile = global
+// wave index); the other D tiles are split into p.nheads contiguous ranges,
+// each handed out one tile per returning atomicAdd on its head (memory-side
+// atomics, ~1 us under load, so each grab is issued one tile ahead, right
+// behind that tile's loads).  A wave pulls from its home head; when the head
+// runs dry it probes every head in one 16-lane instruction and steals from
+// the one with the most tiles left (odd and even XCDs are not served HBM
+// equally, so static ranges finish several us apart).
+struct DynSched {
+    uint32_t first;  // tiles [0, first) are the static first tiles
+    uint32_t dyn;    // dynamic tiles
+    uint32_t heads;
+    bool striped = false;  // head h's i-th tile: first + i * heads + h (one sweep front) instead of a sub-range
+    __device__ __forceinline__ uint32_t base(uint32_t h) const {
+        return striped ? first + h : first + uint32_t((uint64_t(dyn) * h) / heads);
+    }
+    __device__ __forceinline__ uint32_t len(uint32_t h) const {
+        if (striped) return h < dyn ? (dyn - h + heads - 1) / heads : 0u;
+        return uint32_t((uint64_t(dyn) * (h + 1)) / heads) - uint32_t((uint64_t(dyn) * h) / heads);
+    }
+    __device__ __forceinline__ uint32_t step() const { return striped ? heads : 1u; }
+};
+constexpr uint32_t kNoTile = 0xffffffffu;
+
+// ---- scheduler wave (kModeSchedWave) --------------------------------------
+// The workgroup's last wave hands tile indices to the other (worker) waves
+// through an LDS ring; it is the only wave that touches the scheduler heads,
+// so the ~6 us latency of a memory-side atomic under full HBM load stays off
+// the workers' vector-memory queues.  It first feeds the workgroup's static
+// share (tiles [0, static_tiles) split evenly over the workgroups), then grabs
+// p.grab_unit tiles per lane from kGrabLanes heads per instruction (lane l of
+// workgroup b pulls head (b + l) % nheads, so every head drains at the chip's
+// average rate; a lane whose head runs dry retires), keeping about
+// p.ring_target tiles queued ahead of the workers.
+constexpr uint32_t kRingSlots = 64;     // LDS ring entries: u64 {tag << 32 | tile}
+constexpr uint32_t kGrabLanes = 16;
+constexpr uint32_t kRingBytes = kRingSlots * 8 + 16;  // ring + {taken}
+
+// Slot tags: 2*pos + 1 = tile of ring position pos published; 2*pos = slot
+// free for position pos (its reader of pos - kRingSlots has read it).  Slot
+// i starts free for position i.  Tag and tile travel in one 64-bit LDS word,
+// so relaxed accesses suffice (an acquire/release would also wait for the
+// wave's outstanding global loads and checksum stores).
+struct Ring {
+    uint64_t *slot;   // kRingSlots
+    uint32_t *taken;  // positions reserved by workers
+};
+
+__device__ __forceinline__ uint32_t lds_ld(uint32_t *a) {
+    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint64_t *ring_slot(const Ring &r, uint32_t pos) { return r.slot + (pos & (kRingSlots - 1)); }
+
+// Scheduler: publish `tile` at ring position pos once its slot is free.
+__device__ __forceinline__ void ring_push(const Ring &r, uint32_t pos, uint32_t tile) {
+    uint64_t *sl = ring_slot(r, pos);
+    while (uint32_t(__hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 32) != 2u * pos)
+        __builtin_amdgcn_s_sleep(1);
+    __hip_atomic_store(sl, (uint64_t(2u * pos + 1u) << 32) | tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Worker: the tile at ring position k (waits until it is published), then
+// frees the slot for position k + kRingSlots.
+__device__ __forceinline__ uint32_t ring_pop(const Ring &r, uint32_t k) {
+    uint64_t *sl = ring_slot(r, k);
+    uint64_t v;
+    for (;;) {
+        v = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (uint32_t(v >> 32) == 2u * k + 1u) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
+        __hip_atomic_store(sl, uint64_t(2u * (k + kRingSlots)) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return uint32_t(v);
+}
+
+__device__ __forceinline__ uint32_t ring_reserve(const Ring &r, int lane) {
+    uint32_t k = 0;
+    if (lane == 0) k = __hip_atomic_fetch_add(r.taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(k);
+}
+
+// Scheduler: lanes l < n publish tile[l] (per lane) at ring positions pos + l,
+// once all n slots are free (one LDS read per lane per check, one write).
+__device__ __forceinline__ void ring_push_batch(const Ring &r, uint32_t pos, uint32_t n, uint32_t tile, int lane) {
+    const bool mine = uint32_t(lane) < n;
+    const uint32_t q = pos + uint32_t(lane);
+    uint64_t *sl = ring_slot(r, q);
+    for (;;) {
+        bool busy = false;
+        if (mine) busy = uint32_t(__hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 32) != 2u * q;
+        if (__builtin_amdgcn_ballot_w64(busy) == 0) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (mine) __hip_atomic_store(sl, (uint64_t(2u * q + 1u) << 32) | tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Inclusive prefix sum over the wave's lanes (wave-uniform control flow).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d));
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+// st (DIAGNOSTIC, stamps builds): [0] grabs, [1] summed grab round trip,
+// [2] longest grab round trip (s_memrealtime ticks, 100 MHz), [3] time of the
+// first grab.
+template <bool STATS>
+__device__ __forceinline__ void sched_wave(const KParams &p, const Ring &r, const DynSched &ds, uint32_t sbeg,
+                                           uint32_t send, uint32_t workers, int lane, uint64_t *st) {
+    uint32_t pos = 0;
+    uint32_t sc = sbeg;
+    const uint32_t target = min(p.ring_target, 48u);
+    // Static share first, published in batches, kept ~target ahead of the workers
+    // (signed: workers may have reserved positions not published yet).
+    while (sc < send) {
+        const int32_t ahead = int32_t(pos - lds_ld(r.taken));
+        if (ahead >= int32_t(target)) {
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const uint32_t n = min(send - sc, uint32_t(int32_t(target) - ahead));
+        ring_push_batch(r, pos, n, sc + uint32_t(lane), lane);
+        pos += n;
+        sc += n;
+    }
+    // lane l pulls head (b + l) % heads: with one lane per head, every
+    // workgroup pulls every head and the heads run dry together.
+    const uint32_t lanes = min(ds.heads, kGrabLanes);
+    const uint32_t hl = (blockIdx.x + uint32_t(lane)) % ds.heads;
+    bool active = uint32_t(lane) < lanes && ds.dyn > 0 && ds.len(hl) > 0;
+    const uint32_t unit = min(p.grab_unit, 64u / lanes);  // one batch fits the ring
+    while (__builtin_amdgcn_ballot_w64(active) != 0) {
+        while (int32_t(pos - lds_ld(r.taken)) >= int32_t(target)) __builtin_amdgcn_s_sleep(2);
+        uint64_t t0 = 0;
+        if (STATS) t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t g = 0;
+        if (active) g = atomicAdd(head_ptr(p.sched, hl), unit);
+        if (STATS) {
+            g = __builtin_amdgcn_readfirstlane(g) == 0xdeadbeefu ? 1u : g;  // forces the wait here
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+            if (st[0] == 0) st[3] = t0;
+            st[0] += 1;
+            st[1] += dt;
+            st[2] = dt > st[2] ? dt : st[2];
+        }
+        // lane l got tiles base(hl) + g .. + cnt - 1
+        const uint32_t n = ds.len(hl);
+        const uint32_t cnt = active ? (g < n ? min(unit, n - g) : 0u) : 0u;
+        if (active && g + unit >= n) active = false;
+        const uint32_t incl = wave_incl_scan(cnt, lane);
+        const uint32_t off = incl - cnt;
+        const uint32_t m = __builtin_amdgcn_readlane(incl, 63);
+        if (m == 0) continue;
+        // slots pos .. pos + m - 1 must be free; then every lane writes its tiles
+        {
+            const bool mine = uint32_t(lane) < m;
+            const uint32_t q = pos + uint32_t(lane);
+            for (;;) {
+                bool busy = false;
+                if (mine)
+                    busy = uint32_t(__hip_atomic_load(ring_slot(r, q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                                    32) != 2u * q;
+                if (__builtin_amdgcn_ballot_w64(busy) == 0) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        const uint32_t b = ds.base(hl) + g * ds.step();
+        for (uint32_t u = 0; u < unit; ++u)
+            if (u < cnt) {
+                const uint32_t q = pos + off + u;
+                __hip_atomic_store(ring_slot(r, q), (uint64_t(2u * q + 1u) << 32) | (b + u * ds.step()),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        pos += m;
+    }
+    ring_push_batch(r, pos, workers, kNoTile, lane);
+}
+
+__device__ __forceinline__ uint32_t head_grab(uint32_t *sched, uint32_t h, int lane) {
+    uint32_t r = 0;
+    if (lane == 0) r = atomicAdd(head_ptr(sched, h), 1u);
+    return r;
+}
+
+// Resolves a grab issued on `home` (raw lane-0 result r); on a dry head,
+// steals.  Terminates: a failed steal means another wave took the tile, and
+// heads only grow.
+__device__ __forceinline__ uint32_t dyn_next(uint32_t *sched, const DynSched &ds, uint32_t &home, uint32_t r,
+                                             int lane) {
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (r < ds.len(home)) return ds.base(home) + r * ds.step();
+    for (;;) {
+        uint32_t rem = 0;
+        if (lane < int(ds.heads)) {
+            const uint32_t h = uint32_t(lane);
+            const uint32_t c = atomicAdd(head_ptr(sched, h), 0u);
+            const uint32_t n = ds.len(h);
+            rem = c < n ? n - c : 0u;
+        }
+        uint32_t best = 0, bh = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < ds.heads; ++h) {
+            const uint32_t x = __builtin_amdgcn_readlane(rem, h);
+            if (x > best) {
+                best = x;
+                bh = h;
+            }
+        }
+        if (best == 0) return kNoTile;
+        home = bh;
+        const uint32_t g = __builtin_amdgcn_readfirstlane(head_grab(sched, home, lane));
+        if (g < ds.len(home)) return ds.base(home) + g * ds.step();
     }
 }
 
@@ -258,8 +546,17 @@ __device__ __forceinline__ void emit(const KParams &p, uint32_t idx, uint32_t cr
 // and read zeros without touching memory (lin() of zeros is 0, so they need
 // no mask), every lane uses the same one-VGPR offset plus an immediate, and
 // the instruction stream has no divergent branch.  AUX 2 = non-temporal.
-template <int AUX, bool COMPDIAG = false>
-__device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8]) {
+// Block of the tile whose lin() lane `lane` holds after finish_tile's
+// reduce-scatter, and whether the lane emits that block's chunk checksum.
+__device__ __forceinline__ uint32_t rep_block(int lane) {
+    return 2u * (((lane & 8) ? 1u : 0u) + ((lane & 2) ? 2u : 0u) + ((lane & 1) ? 4u : 0u)) + (uint32_t(lane) >> 5);
+}
+__device__ __forceinline__ bool rep_lane(int lane, uint32_t blk, uint32_t nb, uint32_t lg) {
+    return ((lane & 0x14) == 0) && ((blk & ((1u << lg) - 1u)) == 0) && blk < nb;
+}
+
+template <int AUX, bool COMPDIAG, bool VERIFY>
+__device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
     if (COMPDIAG) {  // synthetic data, no memory traffic
         const uint32_t x = uint32_t(t.src) * 2654435761u + uint32_t(lane) * 40503u;
 #pragma unroll
@@ -275,19 +572,22 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
+    if (VERIFY) {  // the expected checksum this lane compares, fetched with the tile
+        const uint32_t lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
+        if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];  // default policy: the next tile reads the rest of the line
+    }
     // Keep the loads ahead of whatever compute follows.
     __builtin_amdgcn_sched_barrier(0);
 }
 
 // lin() per piece, then reduce to one lin() per block, combine the blocks of
 // each chunk, store the chunk checksums.
-template <int DIAG, bool S4 = false>
-__device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, FastTile t, const uint4 v[8],
-                                            int lane) {
+template <int DIAG, bool S4, bool VERIFY>
+__device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            const uint4 v[8], uint32_t ev, int lane) {
     const uint32_t nb = t.meta & 0xffu;
     const uint32_t lg = (t.meta >> 8) & 0xffu;
     const LaneCols cols = lane_cols(uint32_t(lane & 31));
-    const uint32_t h = uint32_t(lane) >> 5;
     uint32_t pc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -326,7 +626,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     }
     x ^= swz_xor<4>(x);
     x ^= swz_xor<16>(x);
-    const uint32_t blk = 2u * ((b3 ? 1u : 0u) + (b1 ? 2u : 0u) + (b0 ? 4u : 0u)) + h;
+    const uint32_t blk = rep_block(lane);
 
     if (lg) {  // chunks of 2^lg blocks: shift each block to the chunk end, XOR them
         const uint32_t nbc = 1u << lg;
@@ -338,8 +638,13 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
         if (lg >= 4) x ^= dpp<kDppXor1>(x);                               // block bit 3 = lane bit 0
     }
     const uint32_t crc = x ^ p.c_lg[lg];
-    const bool rep = ((lane & 0x14) == 0) && ((blk & ((1u << lg) - 1u)) == 0) && blk < nb;
-    if (rep) emit(p, t.out + (blk >> lg), crc);
+    if (rep_lane(lane, blk, nb, lg)) {
+        const uint32_t idx = t.out + (blk >> lg);
+        if (VERIFY)
+            check(p, vacc, idx, crc, ev);
+        else
+            emit<false>(p, vacc, idx, crc);
+    }
 }
 
 // One tile index from the workgroup's LDS counter (one ds_add_rtn per wave).
@@ -386,8 +691,9 @@ __device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
                       __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
 }
 
-template <bool S4 = false>
-__device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t pair, int lane) {
+template <bool S4, bool VERIFY>
+__device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
+                                         int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
     const uint32_t idx = 2u * pair + h;
     const bool valid = idx < p.ngen;
@@ -417,7 +723,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
     }
     if (valid && q == 0) {
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
-        emit(p, g.out, crc);
+        emit<VERIFY>(p, vacc, g.out, crc);
     }
 }
 
@@ -435,12 +741,23 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
     constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
+    constexpr bool VERIFY = (MODE & kModeVerify) != 0;
+    constexpr bool DYN = (MODE & kModeDyn) != 0;
+    constexpr bool SCHEDW = (MODE & kModeSchedWave) != 0;
+    constexpr bool STRIPED = (MODE & kModeStriped) != 0;
+    static_assert(!DYN || (!EARLY2 && !PIPE), "the dynamic scheduler has its own tile loop");
+    static_assert(!SCHEDW || (!EARLY2 && !PIPE && !DYN), "the scheduler wave has its own tile loop");
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
-    // One LDS array: the tables, then the workgroup's tile counter.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
+    // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
+    // its mismatch count and first bad index.
+    constexpr uint32_t kRingLds = SCHEDW ? kRingBytes : 0u;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16 + kRingLds];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
+    uint32_t *vacc = pool_ctr + 1;
+    const Ring ring{reinterpret_cast<uint64_t *>(lds + kStage + 16),
+                    reinterpret_cast<uint32_t *>(lds + kStage + 16 + kRingSlots * 8)};
     const uint8_t *table = S4 ? p.table_s4 : p.table;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
@@ -453,12 +770,38 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
-    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
-    if (threadIdx.x == 0) *pool_ctr = tbeg + kWaves;
-    uint32_t t = tbeg + wv;
+    // (DYN: every tile index below p.ntiles is valid; first tile = global wave index.)
+    const uint32_t tbeg = DYN ? 0u : uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = DYN ? p.ntiles : uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    DynSched ds{0, 0, 1};
+    uint32_t home = 0;
+    if (DYN) {
+        const uint32_t nw = gridDim.x * kWaves;
+        ds.first = min(p.ntiles, nw);
+        ds.dyn = p.ntiles - ds.first;
+        ds.heads = p.nheads;
+        home = (blockIdx.x * kWaves + wv) % ds.heads;
+    }
+    if (SCHEDW) {
+        ds.first = p.static_tiles;
+        ds.dyn = p.ntiles - p.static_tiles;
+        ds.heads = p.nheads;
+        ds.striped = STRIPED;
+        for (uint32_t i = threadIdx.x; i < kRingSlots; i += THREADS) ring.slot[i] = uint64_t(2u * i) << 32;
+        if (threadIdx.x == 0) *ring.taken = 0;
+    }
+    if ((DYN || SCHEDW || VERIFY) && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
+    if (threadIdx.x == 0) {
+        *pool_ctr = tbeg + kWaves;
+        if (VERIFY) {
+            vacc[0] = 0;
+            vacc[1] = 0xffffffffu;
+        }
+    }
+    uint32_t t = DYN ? blockIdx.x * kWaves + wv : tbeg + wv;
     FastTile ft{0, 0, 0};
     uint4 v[8];
+    uint32_t ev = 0;  // VERIFY: expected checksum prefetched with the tile
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
     for (uint32_t c = wv; !NOSTAGE && c < kStage / 1024u; c += kWaves)
         __builtin_amdgcn_global_load_lds(
@@ -470,7 +813,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         // barrier (__syncthreads' fence would wait for the tile too).
         if (t < tend) {
             ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+            load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
             __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0): staging loads and LDS writes done
         } else {
             __builtin_amdgcn_s_waitcnt(0x0070);  // no tile in flight: vmcnt(0) lgkmcnt(0)
@@ -481,58 +824,114 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     }
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY2 && t < tend) {
+    if (!EARLY2 && !SCHEDW && t < tend) {
         ft = tile_at(p, t);
-        load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+        load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
     }
-    if (PIPE) {
+    uint64_t sstat[4] = {0, 0, 0, 0};
+    if (SCHEDW) {
+        constexpr uint32_t kWorkers = kWaves - 1;
+        if (wv == kWorkers) {
+            const uint32_t sbeg = uint32_t((uint64_t(p.static_tiles) * blockIdx.x) / gridDim.x);
+            const uint32_t send = uint32_t((uint64_t(p.static_tiles) * (blockIdx.x + 1)) / gridDim.x);
+            sched_wave<STAMPS>(p, ring, ds, sbeg, send, kWorkers, lane, sstat);
+        } else {
+            // The next tile index is popped as soon as this tile's loads are
+            // out, and its descriptor fetched behind them (tile_prefetch).
+            t = ring_pop(ring, ring_reserve(ring, lane));
+            uint4 dn = make_uint4(0, 0, 0, 0);
+            if (t != kNoTile) dn = tile_prefetch(p, t);
+            while (t != kNoTile) {
+                ft = tile_from(dn);
+                load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
+                const uint32_t k = ring_reserve(ring, lane);
+                uint32_t tn;
+                if (STAMPS) {
+                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                    tn = ring_pop(ring, k);
+                    sstat[1] += __builtin_amdgcn_s_memrealtime() - w0;  // worker: time waiting on the ring
+                    sstat[0] += 1;
+                } else {
+                    tn = ring_pop(ring, k);
+                }
+                dn = tile_prefetch(p, tn != kNoTile ? tn : 0u);  // unconditional: keeps vmcnt counts exact
+                __builtin_amdgcn_sched_barrier(0);
+                finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
+                t = tn;
+            }
+        }
+    } else if (PIPE) {
         // Two register tiles per wave (a = v, b = vb): one is in flight while
         // the other is looked up.
         uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
         FastTile fb{0, 0, 0};
         uint4 vb[8];
+        uint32_t evb = 0;
         if (tb < tend) {
             fb = tile_at(p, tb);
-            load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
+            load_tile<AUX, COMPDIAG, VERIFY>(p, fb, lane, vb, evb);
         }
         while (t < tend) {
-            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
+            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
             if (tb >= tend) break;
             t = pool_grab(pool_ctr, lane);
             if (t < tend) {
                 ft = tile_at(p, t);
-                load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+                load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
             }
-            finish_tile<DIAG, S4>(p, lds, fb, vb, lane);
+            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, fb, vb, evb, lane);
             if (t >= tend) break;
             tb = pool_grab(pool_ctr, lane);
             if (tb < tend) {
                 fb = tile_at(p, tb);
-                load_tile<AUX, COMPDIAG>(p, fb, lane, vb);
+                load_tile<AUX, COMPDIAG, VERIFY>(p, fb, lane, vb, evb);
             }
+        }
+    } else if (DYN) {
+        // The first tile's loads are in flight; the grab for the next one
+        // goes right behind them and is resolved after the lookups.
+        while (t < tend) {
+            uint32_t r = ds.dyn ? head_grab(p.sched, home, lane) : 0u;
+            __builtin_amdgcn_sched_barrier(0);
+            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
+            // The grab's result is first read here, after the lookups (keeps
+            // its vmcnt wait from moving in front of them).
+            __builtin_amdgcn_sched_barrier(0);
+            opaque(r);
+            t = ds.dyn ? dyn_next(p.sched, ds, home, r, lane) : kNoTile;
+            if (t >= tend) break;
+            ft = tile_at(p, t);
+            load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
         }
     } else {
         while (t < tend) {
-            finish_tile<DIAG, S4>(p, lds, ft, v, lane);
+            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
             t = pool_grab(pool_ctr, lane);
             if (t >= tend) break;
             ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG>(p, ft, lane, v);
+            load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
         }
     }
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
     const uint32_t nwaves = gridDim.x * kWaves;
     const uint32_t npairs = (p.ngen + 1u) >> 1;
-    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair<S4>(p, lds, g, lane);
+    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair<S4, VERIFY>(p, lds, vacc, g, lane);
+    if (VERIFY) {
+        __syncthreads();
+        if (threadIdx.x == 0) verify_finish(p, vacc);
+    }
     if (STAMPS && lane == 0) {
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
         const uint32_t xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
-        p.stamps[4 * wave + 0] = t_start;
-        p.stamps[4 * wave + 1] = t_staged;
-        p.stamps[4 * wave + 2] = t_end;
-        p.stamps[4 * wave + 3] = (uint64_t(xcc_id) << 32) | hw_id;
+        constexpr uint32_t kW = SCHEDW ? 8u : 4u;  // scheduler-wave builds add sstat[0..3]
+        p.stamps[kW * wave + 0] = t_start;
+        p.stamps[kW * wave + 1] = t_staged;
+        p.stamps[kW * wave + 2] = t_end;
+        p.stamps[kW * wave + 3] = (uint64_t(xcc_id) << 32) | hw_id;
+        if (SCHEDW)
+            for (int i = 0; i < 4; ++i) p.stamps[kW * wave + 4 + i] = sstat[i];
     }
 }
 
@@ -551,6 +950,43 @@ const KernelVariant kVariants[kNumVariants] = {
     {"nibble_wg1024x2_nt_valu_only", 1024, 2},  // DIAGNOSTIC: 7 without the LDS reads
     {"nibble_wg1024x2_nt_lds_only", 1024, 2},   // DIAGNOSTIC: 7 without the address math
     {"s4_wg1024x1_nt_memonly_nostage", 1024, 1},  // DIAGNOSTIC: 4 without the table staging
+    {"s4_wg512x1_nt", 512, 1},                  // A/B: 0 with 8 waves per CU
+    {"s4_wg512x1_nt_pipe", 512, 1},             // A/B: 8 waves per CU, two tiles per wave
+    {"s4_wg768x1_nt", 768, 1},                  // A/B: 0 with 12 waves per CU
+    {"s4_wg512x1_nt_memonly", 512, 1},          // DIAGNOSTIC: memory ceiling of 13
+    {"s4_wg640x1_nt", 640, 1},                  // A/B: 0 with 10 waves per CU
+    {"s4_wg896x1_nt", 896, 1},                  // A/B: 0 with 14 waves per CU
+    {"s4_wg768x1_nt_memonly", 768, 1},          // DIAGNOSTIC: memory ceiling of 15
+    {"s4_wg768x1_nt_early2", 768, 1},           // A/B: 15 with the first tile right behind the staging
+    {"s4_wg1024x1_nt_dyn", 1024, 1, 16},        // A/B: 0 with the dynamic tile scheduler
+    {"s4_wg768x1_nt_dyn", 768, 1, 16},          // A/B: 15 with the dynamic tile scheduler
+    {"s4_wg768x1_nt_dyn_memonly", 768, 1, 16},  // DIAGNOSTIC: memory ceiling of 22
+    {"s4_wg768x1_nt_dyn_stamps", 768, 1, 16},   // DIAGNOSTIC: 22 with per-wave timestamps
+    {"s4_wg768x1_nt_dyn32", 768, 1, 32},        // A/B: 22 with 32 heads
+    {"s4_wg768x1_nt_dyn8", 768, 1, 8},          // A/B: 22 with 8 heads
+    {"s4_wg832x1_nt_schedw50", 832, 1, 16, 50},  // A/B: 12 worker waves + scheduler wave, half the tiles static
+    {"s4_wg832x1_nt_schedw25", 832, 1, 16, 25},  // A/B: same, a quarter static
+    {"s4_wg832x1_nt_schedw50_memonly", 832, 1, 16, 50},  // DIAGNOSTIC: memory ceiling of 27
+    {"s4_wg832x1_nt_schedw50_stamps", 832, 1, 16, 50},   // DIAGNOSTIC: 27 with per-wave timestamps
+    {"s4_wg832x1_nt_schedw50_t36u4", 832, 1, 16, 50, 36, 4},  // A/B: 27, deeper pipeline
+    {"s4_wg832x1_nt_schedw50_t48u4", 832, 1, 16, 50, 48, 4},  // A/B: 27, deeper still
+    {"s4_wg832x1_nt_schedw75_t36u4", 832, 1, 16, 75, 36, 4},  // A/B: 31 with 3/4 static
+    {"s4_wg832x1_nt_schedw50_t36u4_memonly", 832, 1, 16, 50, 36, 4},  // DIAGNOSTIC: memory ceiling of 31
+    {"s4_wg832x1_nt_schedw100", 832, 1, 16, 100, 20, 2},  // DIAGNOSTIC: 27 with every tile static (ring only)
+    {"s4_wg832x1_nt_schedw0", 832, 1, 16, 0, 36, 4},      // A/B: 27 with every tile dynamic
+    {"s4_wg832x1_nt_schedw50_h8t2u1", 832, 1, 8, 50, 2, 1},    // A/B: small queue
+    {"s4_wg832x1_nt_schedw50_h8t6u1", 832, 1, 8, 50, 6, 1},
+    {"s4_wg832x1_nt_schedw50_h12t6u1", 832, 1, 12, 50, 6, 1},
+    {"s4_wg832x1_nt_schedw25_h8t6u1", 832, 1, 8, 25, 6, 1},
+    {"s4_wg832x1_nt_schedw0_h8t6u1", 832, 1, 8, 0, 6, 1},
+    {"s4_wg832x1_nt_schedw50_h8t6u1_memonly", 832, 1, 8, 50, 6, 1},  // DIAGNOSTIC: memory ceiling of 38
+    {"s4_wg832x1_nt_schedw50_h8t6u1_stamps", 832, 1, 8, 50, 6, 1},   // DIAGNOSTIC: 38 with stamps
+    {"s4_wg832x1_nt_schedw50_h8t6u1_striped", 832, 1, 8, 50, 6, 1},  // A/B: 38 with striped heads
+    {"s4_wg832x1_nt_schedw25_h8t6u1_striped", 832, 1, 8, 25, 6, 1},
+    {"s4_wg832x1_nt_schedw0_h8t6u1_striped", 832, 1, 8, 0, 6, 1},
+    {"s4_wg832x1_nt_schedw0_h16t6u1_striped", 832, 1, 16, 0, 6, 1},
+    {"s4_wg832x1_nt_schedw0_h8t6u1_striped_memonly", 832, 1, 8, 0, 6, 1},  // DIAGNOSTIC: memory ceiling of 46
+    {"s4_wg832x1_nt_schedw0_h8t6u1_striped_stamps", 832, 1, 8, 0, 6, 1},   // DIAGNOSTIC: 46 with stamps
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -566,6 +1002,19 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{kv.threads, 1, 1};
     constexpr int kS4Nt = kModeS4 | kModeNt;
+    if ((kv.heads || p.expect) && (!p.sched || !p.sched_next)) return hipErrorInvalidValue;
+    if (kv.heads && (p.nheads == 0 || p.nheads > kMaxHeads)) return hipErrorInvalidValue;
+    if (p.expect) {  // verification: the production kernel (or the nibble A/B kernel) in compare mode
+        if (!p.result) return hipErrorInvalidValue;
+        switch (variant) {
+        case 0: HDFS_LAUNCH(1024, 4, kS4Nt | kModeVerify); break;
+        case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeVerify); break;
+        case 21: HDFS_LAUNCH(1024, 4, kS4Nt | kModeDyn | kModeVerify); break;
+        case 22: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn | kModeVerify); break;
+        default: return hipErrorInvalidValue;  // diagnostic variants do not verify
+        }
+        return hipGetLastError();
+    }
     switch (variant) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt); break;
     case 2: HDFS_LAUNCH(1024, 4, kS4Nt | kModeEarly2); break;
@@ -579,6 +1028,43 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
     case 11: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
     case 12: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeNoStage); break;
+    case 13: HDFS_LAUNCH(512, 2, kS4Nt); break;
+    case 14: HDFS_LAUNCH(512, 2, kS4Nt | kModePipe); break;
+    case 15: HDFS_LAUNCH(768, 3, kS4Nt); break;
+    case 16: HDFS_LAUNCH(512, 2, kS4Nt | kModeMemDiag); break;
+    case 17: HDFS_LAUNCH(640, 3, kS4Nt); break;
+    case 18: HDFS_LAUNCH(896, 4, kS4Nt); break;
+    case 19: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag); break;
+    case 20: HDFS_LAUNCH(768, 3, kS4Nt | kModeEarly2); break;
+    case 21: HDFS_LAUNCH(1024, 4, kS4Nt | kModeDyn); break;
+    case 22: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn); break;
+    case 23: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn | kModeMemDiag); break;
+    case 24: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn | kModeStamps); break;
+    case 25: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn); break;
+    case 26: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn); break;
+    case 27: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 28: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 29: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeMemDiag); break;
+    case 30: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStamps); break;
+    case 31: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 32: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 33: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 34: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeMemDiag); break;
+    case 35: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 36: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 37:
+    case 38:
+    case 39:
+    case 40:
+    case 41: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
+    case 42: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeMemDiag); break;
+    case 43: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStamps); break;
+    case 44:
+    case 45:
+    case 46:
+    case 47: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStriped); break;
+    case 48: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStriped | kModeMemDiag); break;
+    case 49: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStriped | kModeStamps); break;
     default: HDFS_LAUNCH(1024, 4, kS4Nt); break;
     }
     return hipGetLastError();

@@ -57,6 +57,13 @@ struct DeviceGuard {
 
 constexpr size_t kSliceBytes = 32ull << 20;  // host pipeline slice (whole packets)
 
+// The two device scheduler slots (kernel_abi.h) of one launch sequence that
+// the GPU runs in order: a plan, or a host-pipeline stage.
+struct SchedSlots {
+    uint32_t *d = nullptr;  // 2 * kSlotWords u32
+    int cur = 0;
+};
+
 struct Stage {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -69,6 +76,7 @@ struct Stage {
     bool pending = false;
     // packets of the slice in flight: (global out_idx, local out index, count)
     std::vector<uint64_t> scatter;
+    SchedSlots sched;  // this stage's launches are serialised on its stream
 };
 
 }  // namespace
@@ -88,6 +96,14 @@ struct crc32c_ctx {
 
 struct crc32c_plan {
     crc32c_ctx *ctx = nullptr;
+    // Launches of a plan share its scheduler slots, so they are kept in GPU
+    // order: a launch on another stream than the previous one first waits
+    // for the previous one (last_done).
+    std::mutex mu;
+    SchedSlots sched;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t last_done = nullptr;
+    bool launched = false;
     FastTile *d_tiles = nullptr;
     GenItem *d_gen = nullptr;
     uint32_t ntiles = 0, ngen = 0;
@@ -119,14 +135,66 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
     p.stamps = nullptr;
     p.expect = nullptr;
     p.result = nullptr;
+    p.sched = nullptr;
+    p.sched_next = nullptr;
+    p.nheads = 0;
+    p.static_tiles = 0;
+    p.ring_target = 0;
+    p.grab_unit = 0;
     return p;
 }
 
-int launch(const crc32c_ctx *ctx, const KParams &p, hipStream_t stream) {
+int alloc_slots(SchedSlots &s) {
+    if (s.d) return 0;
+    std::vector<uint32_t> init(2 * kSlotWords);
+    init_sched_slots(init.data());
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d), init.size() * sizeof(uint32_t)));
+    HIP_TRY(hipMemcpy(s.d, init.data(), init.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Launches p on `stream`.  Kernels that use the scheduler slots (dynamic
+// variants, verification) take the current slot, reset the other one, and
+// the pair flips; the caller keeps launches on `slots` in GPU order.
+int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
     if (!items) return 0;
+    const bool sched = kVariants[ctx->variant].heads || p.expect;
+    p.nheads = kVariants[ctx->variant].heads;
+    p.static_tiles = uint32_t(uint64_t(p.ntiles) * kVariants[ctx->variant].static_pct / 100);
+    p.ring_target = kVariants[ctx->variant].ring_target;
+    p.grab_unit = kVariants[ctx->variant].grab_unit;
+    if (sched) {
+        int rc = alloc_slots(slots);
+        if (rc) return rc;
+        p.sched = slots.d + slots.cur * kSlotWords;
+        p.sched_next = slots.d + (slots.cur ^ 1) * kSlotWords;
+    }
     HIP_TRY(launch_plan_kernel(p, ctx->variant, uint32_t(ctx->num_cu), stream));
+    if (sched) slots.cur ^= 1;
     return 0;
+}
+
+// Orders the plan's next launch on `stream` after everything it launched
+// before: when the stream changes, an event recorded on the previous stream
+// now (it covers that stream's launches so far) is waited on.  Same stream:
+// nothing to do (stream order).  Caller holds plan->mu.
+int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
+    if (plan->launched && plan->last_stream != stream) {
+        if (!plan->last_done) HIP_TRY(hipEventCreateWithFlags(&plan->last_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(plan->last_done, plan->last_stream));
+        HIP_TRY(hipStreamWaitEvent(stream, plan->last_done, 0));
+    }
+    plan->last_stream = stream;
+    plan->launched = true;
+    return 0;
+}
+
+int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
+    std::lock_guard<std::mutex> lock(plan->mu);
+    int rc = order_plan_launch(plan, stream);
+    if (rc) return rc;
+    return launch(plan->ctx, p, plan->sched, stream);
 }
 
 constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32;
@@ -168,6 +236,7 @@ void free_stage(Stage &s) {
     if (s.d_out) (void)hipFree(s.d_out);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.sched.d) (void)hipFree(s.sched.d);
     s = Stage();
 }
 
@@ -268,7 +337,7 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, desc_bytes, hipMemcpyHostToDevice, s.stream));
         const KParams p = params_for(ctx, s.d_desc, uint32_t(plan.tiles.size()), s.d_desc + plan.tiles.size() * 16,
                                      uint32_t(plan.gen.size()), s.d_payload, s.d_out, flags);
-        rc = launch(ctx, p, s.stream);
+        rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nout * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));
@@ -317,6 +386,7 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
     if (const char *kv = std::getenv("HDFS_CRC32C_KVARIANT")) c->variant = std::atoi(kv);
+    if (c->variant < 0 || c->variant >= kNumVariants) c->variant = 0;
     for (int ty = 0; ty < 2; ++ty) {
         const uint32_t poly = ty ? kPolyIeee : kPoly;
         std::vector<uint8_t> img(kTableAlloc, 0);
@@ -387,7 +457,7 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
     DeviceGuard guard(plan->ctx->device);
     const KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload,
                                  dev_out, plan->flags);
-    return launch(plan->ctx, p, static_cast<hipStream_t>(stream));
+    return launch_plan(plan, p, static_cast<hipStream_t>(stream));
 }
 
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
@@ -396,17 +466,21 @@ int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_
     if (!dev_result) return fail(-EINVAL, "result == NULL");
     DeviceGuard guard(plan->ctx->device);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result), 0, 1, s));
-    HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));
-    if (plan->nchecksums == 0) return 0;
+    if (uint64_t(plan->ntiles) + plan->ngen == 0) {  // nothing to compare: no launch, set the result directly
+        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result), 0, 1, s));
+        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));
+        return 0;
+    }
     if (!dev_payload || !dev_expected) return fail(-EINVAL, "payload/expected == NULL");
     if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
         return fail(-EINVAL, "device payload must be 16-byte aligned");
+    if (!variant_verifies(plan->ctx->variant))
+        return fail(-EINVAL, "kernel variant %d has no verification mode", plan->ctx->variant);
     KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, nullptr,
                            plan->flags);
     p.expect = dev_expected;
     p.result = dev_result;
-    return launch(plan->ctx, p, s);
+    return launch_plan(plan, p, s);
 }
 
 int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
@@ -443,7 +517,23 @@ int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, u
     KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, dev_out,
                            plan->flags);
     p.stamps = dev_stamps;
-    HIP_TRY(launch_plan_kernel(p, variant, uint32_t(plan->ctx->num_cu), static_cast<hipStream_t>(stream)));
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lock(plan->mu);
+    if (variant < 0 || variant >= kNumVariants) return fail(-EINVAL, "no kernel variant %d", variant);
+    p.nheads = kVariants[variant].heads;
+    p.static_tiles = uint32_t(uint64_t(p.ntiles) * kVariants[variant].static_pct / 100);
+    p.ring_target = kVariants[variant].ring_target;
+    p.grab_unit = kVariants[variant].grab_unit;
+    if (kVariants[variant].heads) {
+        int rc = alloc_slots(plan->sched);
+        if (rc) return rc;
+        rc = order_plan_launch(plan, s);
+        if (rc) return rc;
+        p.sched = plan->sched.d + plan->sched.cur * kSlotWords;
+        p.sched_next = plan->sched.d + (plan->sched.cur ^ 1) * kSlotWords;
+    }
+    HIP_TRY(launch_plan_kernel(p, variant, uint32_t(plan->ctx->num_cu), s));
+    if (kVariants[variant].heads) plan->sched.cur ^= 1;
     return 0;
 }
 
@@ -453,6 +543,8 @@ int crc32c_plan_destroy(crc32c_plan *plan) {
         DeviceGuard guard(plan->ctx->device);
         if (plan->d_tiles) (void)hipFree(plan->d_tiles);
         if (plan->d_gen) (void)hipFree(plan->d_gen);
+        if (plan->sched.d) (void)hipFree(plan->sched.d);
+        if (plan->last_done) (void)hipEventDestroy(plan->last_done);
     }
     delete plan;
     return 0;

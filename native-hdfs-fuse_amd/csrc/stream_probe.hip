@@ -10,6 +10,12 @@ namespace {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
 // Grid-stride read of 16 B per lane, UNROLL loads in flight per lane,
 // XOR-folded so nothing is dead; one dword per thread written at the end.
 template <int UNROLL, bool NT>
@@ -21,7 +27,7 @@ __global__ __launch_bounds__(256) void probe_read(const u32x4 *__restrict__ src,
     for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
         u32x4 v[UNROLL];
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) v[u] = NT ? __builtin_nontemporal_load(src + i + u * stride) : src[i + u * stride];
+        for (int u = 0; u < UNROLL; ++u) v[u] = ld16<NT>(src + i + u * stride);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
@@ -32,17 +38,67 @@ __global__ __launch_bounds__(256) void probe_read(const u32x4 *__restrict__ src,
     out[tid] = acc;
 }
 
+// Tile-shaped reads like the CRC kernel's: a wave reads one tile of UNROLL
+// consecutive KiB (one 1 KiB wave instruction each).  RANGE: every workgroup
+// owns an equal contiguous range of tiles and its waves take them round-
+// robin; otherwise the chip's waves take tiles grid-stride.
+template <int THREADS, int UNROLL, bool RANGE>
+__global__ __launch_bounds__(THREADS) void probe_tiles(const u32x4 *__restrict__ src, uint64_t bytes, uint32_t *out) {
+    constexpr uint32_t kWaves = THREADS / 64;
+    constexpr uint64_t kTile = 1024ull * UNROLL;
+    const uint64_t ntiles = bytes / kTile;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint64_t t, tend, step;
+    if (RANGE) {
+        t = ntiles * blockIdx.x / gridDim.x + wv;
+        tend = ntiles * (blockIdx.x + 1) / gridDim.x;
+        step = kWaves;
+    } else {
+        t = uint64_t(blockIdx.x) * kWaves + wv;
+        tend = ntiles;
+        step = uint64_t(gridDim.x) * kWaves;
+    }
+    uint32_t acc = 0;
+    for (; t < tend; t += step) {
+        const u32x4 *p = src + t * (kTile / 16) + lane;
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) v[u] = __builtin_nontemporal_load(p + 64 * u);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    out[blockIdx.x * THREADS + threadIdx.x] = acc;
+}
+
 }  // namespace
 
+// shape: 0-3 grid-stride (256 threads; unroll 4 / 8 / 4 nt / 16);
+// 4-7 grid-stride nt, unroll 2 / 8 / 16 / 1;
+// 8-15 tile probes, 1024 threads: 8 KiB tiles range / stride, 4 KiB range /
+// stride, then 512 threads: 8 KiB range / stride, 4 KiB range / stride.
 extern "C" int crc32c_debug_stream_probe(const void *dev_src, uint64_t bytes, uint32_t *dev_out, uint32_t grid,
                                          int shape, void *stream) {
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const uint64_t n16 = bytes / 16;
+    const u32x4 *src = (const u32x4 *)dev_src;
     switch (shape) {
-    case 0: hipLaunchKernelGGL((probe_read<4, false>), dim3(grid), dim3(256), 0, s, (const u32x4 *)dev_src, n16, dev_out); break;
-    case 1: hipLaunchKernelGGL((probe_read<8, false>), dim3(grid), dim3(256), 0, s, (const u32x4 *)dev_src, n16, dev_out); break;
-    case 2: hipLaunchKernelGGL((probe_read<4, true>), dim3(grid), dim3(256), 0, s, (const u32x4 *)dev_src, n16, dev_out); break;
-    default: hipLaunchKernelGGL((probe_read<16, false>), dim3(grid), dim3(256), 0, s, (const u32x4 *)dev_src, n16, dev_out); break;
+    case 0: hipLaunchKernelGGL((probe_read<4, false>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 1: hipLaunchKernelGGL((probe_read<8, false>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 2: hipLaunchKernelGGL((probe_read<4, true>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 3: hipLaunchKernelGGL((probe_read<16, false>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 4: hipLaunchKernelGGL((probe_read<2, true>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 5: hipLaunchKernelGGL((probe_read<8, true>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 6: hipLaunchKernelGGL((probe_read<16, true>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 7: hipLaunchKernelGGL((probe_read<1, true>), dim3(grid), dim3(256), 0, s, src, n16, dev_out); break;
+    case 8: hipLaunchKernelGGL((probe_tiles<1024, 8, true>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out); break;
+    case 9: hipLaunchKernelGGL((probe_tiles<1024, 8, false>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out); break;
+    case 10: hipLaunchKernelGGL((probe_tiles<1024, 4, true>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out); break;
+    case 11: hipLaunchKernelGGL((probe_tiles<1024, 4, false>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out); break;
+    case 12: hipLaunchKernelGGL((probe_tiles<512, 8, true>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
+    case 13: hipLaunchKernelGGL((probe_tiles<512, 8, false>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
+    case 14: hipLaunchKernelGGL((probe_tiles<512, 4, true>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
+    case 15: hipLaunchKernelGGL((probe_tiles<512, 4, false>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
+    default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }

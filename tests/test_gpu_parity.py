@@ -196,7 +196,7 @@ def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     assert np.array_equal(got2[:127], got[1:128])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 15, 21, 22, 27, 39, 41, 44, 46, 47])
 def test_every_product_kernel_variant(hdfs, golden, orc, variant, monkeypatch):
     """Both table schemes (0 = slicing-by-4 chains, production; 1 = positional
     nibble tables) and the A/B loop shapes (2, 3) are bit-exact: golden
@@ -253,7 +253,7 @@ def test_crc32_type_matches_zlib(hdfs, variant, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 22])
 def test_verify_reports_mismatches(hdfs, orc, variant, monkeypatch):
     """Read-side verification (crc32c_plan_verify / crc32c_verify_host): no
     mismatch on intact data; a corrupted payload byte or expected checksum is

@@ -21,15 +21,16 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
   case $s in
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) run tests ${T_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${T_ARGS:-} ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench5) run bench5 600 python bench.py --config c5 --no-cpu ;;
     bench3) run bench3 600 python bench.py --config c3 --no-cpu --no-host ;;
     bench4) run bench4 600 python bench.py --config c4 --no-cpu --no-host ;;
     pmc) run pmc 1100 bash tools/pmc_session.sh ;;
-    stamps) for v in ${SV:-8 9}; do run stamps_v$v 300 python tools/stamps.py c2 $v; done ;;
+    stamps) for v in ${SV:-8 9}; do run stamps_v$v 300 python tools/stamps.py c2 $v ${SW:-16}; done ;;
     tprobe) run tprobe 300 python tools/timing_probe.py ;;
-    kbench) run kbench 600 python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ;;
+    sweep) run sweep 300 python tools/probe_sweep.py ;;
+    kbench) run kbench ${KB_TIMEOUT:-600} python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ${KB_ARGS:-} ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 --variants ${KV:-0,1} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
             python3 bench.py --steps 50 --warmup 10 --no-cpu --no-host ;;

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--nbuf", type=int, default=4)
     ap.add_argument("--variants", default="0,1,2,3,4,5")
+    ap.add_argument("--verify", action="store_true", help="also time crc32c_plan_verify (variant 0) as 'verify'")
     args = ap.parse_args()
 
     import numpy as np
@@ -59,7 +60,28 @@ def main():
         if not np.array_equal(got, ref):
             print("note: variant %s checksums differ (diagnostic variant?)" % v, file=sys.stderr)
     times = {v: [] for v in variants}
+    if args.verify:
+        vplan = plans[variants[0]][1]
+        exps = [torch.zeros_like(o) for o in outs]
+        for i in range(args.nbuf):  # expected checksums of every buffer (diagnostic variants overwrite outs)
+            vplan.exec(bufs[i].data_ptr(), exps[i].data_ptr(), stream.cuda_stream)
+        vres = torch.zeros(2, dtype=torch.int32, device=dev)
+        times["verify"] = []
     for r in range(args.rounds):
+        if args.verify:
+            for i in range(3):
+                vplan.verify(bufs[i % args.nbuf].data_ptr(), exps[i % args.nbuf].data_ptr(), vres.data_ptr(),
+                             stream.cuda_stream)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(args.iters):
+                b = i % args.nbuf
+                vplan.verify(bufs[b].data_ptr(), exps[b].data_ptr(), vres.data_ptr(), stream.cuda_stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times["verify"].append(e0.elapsed_time(e1) / args.iters * 1e3)
+            assert vres.cpu().tolist() == [0, -1], vres
         for v in variants:
             plan = plans[v][1]
             for i in range(3):
@@ -105,7 +127,7 @@ def main():
                 tt.append(e0.elapsed_time(e1) / args.iters * 1e3)
             res["probe_s%d_g%d" % (shape, grid)] = {"us": round(min(tt), 2),
                                                     "GBps": round(extent / (min(tt) * 1e-6) / 1e9, 1)}
-    for v in variants:
+    for v in times:
         t = sorted(times[v])
         res[v] = {"median_us": round(t[len(t) // 2], 2), "min_us": round(t[0], 2),
                   "GBps_median": round(nbytes / (t[len(t) // 2] * 1e-6) / 1e9, 1),

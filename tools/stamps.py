@@ -22,6 +22,7 @@ def main():
 
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     variant = int(sys.argv[2]) if len(sys.argv) > 2 else 8  # 8 = production + stamps, 9 = memory-only + stamps
+    wpg = int(sys.argv[3]) if len(sys.argv) > 3 else 16  # waves per workgroup of that variant (24: 12)
     hdfs = load_package()
     pk, _ = config_packets(cfg, oracle)
     extent = int((pk["payload_off"] + pk["len"]).max())
@@ -53,7 +54,7 @@ def main():
         end = (st[:, 2] - t0) / 100.0
         xcc = (st[:, 3] >> 32) & 0xF
         q = lambda a: [round(float(np.percentile(a, x)), 2) for x in (0, 10, 50, 90, 100)]
-        wg = np.arange(st.shape[0]) // 16
+        wg = np.arange(st.shape[0]) // wpg
         # HW_ID: cu_id [11:8], sh_id [12], se_id [15:13]; tg_id [19:16] is the
         # workgroup slot on the CU and must not split one CU into several.
         cu = (xcc << 16) | (((st[:, 3] & 0xFFFFFFFF) >> 8) & 0xFF)
@@ -82,6 +83,8 @@ def main():
             "end_us_pct": q(end),
             "per_xcd_end_max": [round(float(end[xcc == x].max()), 2) if np.any(xcc == x) else None for x in range(8)],
             "per_xcd_waves": [int(np.sum(xcc == x)) for x in range(8)],
+            "xcc_of_block_0_to_7": [int(xcc[wg == b][0]) if np.any(wg == b) else None for b in range(8)],
+            "group_mean_end": [round(float(np.mean([wg_end[w][1] for w in wg_end if w % 8 == g])), 2) for g in range(8)],
         })
     # Is a slow CU slow in every run (a property of the CU) or at random?
     keys = sorted(set.intersection(*[set(d) for d in cu_ends]))
