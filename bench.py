@@ -34,10 +34,10 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 KERNEL_NAME = "hdfs_crc32c_plan_kernel"
-# Template instance of the production variant (crc32c_kernel.hip, kVariants[0]:
-# 1024 threads, 4 waves/SIMD, kModeS4 | kModeNt); PMC traffic is only reported
-# from a summary of this exact kernel.
-PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<1024, 4, 3>"
+# Template instance of the production variant on a full batch (crc32c_kernel.hip,
+# kVariants[0]: 768 threads, 3 waves/SIMD, kModeS4 | kModeNt); PMC traffic is
+# only reported from a summary of this exact kernel.
+PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<768, 3, 3>"
 
 
 def load_package():
@@ -270,19 +270,20 @@ def main():
     value = total_bytes / elapsed / GIB
     achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
 
-    # Read-side verification (crc32c_plan_verify) of buffer 0 against its
-    # checksums, timed the same way (rank 0, reported beside the main line).
+    # Read-side verification (crc32c_plan_verify) of the rotating buffers
+    # against their checksums (outs[b] now holds buffer b's), timed the same
+    # way (rank 0, reported beside the main line).
     verify = None
     if rank == 0:
         res = torch.zeros(2, dtype=torch.int32, device=dev)
-        for _ in range(3):
-            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), sptr)
+        for i in range(3):
+            plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         nv = 20
-        for _ in range(nv):
-            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), sptr)
+        for i in range(nv):
+            plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         e1.record(stream)
         torch.cuda.synchronize()
         r = res.cpu().numpy().view(np.uint32)

@@ -20,7 +20,8 @@
 //    different banks): u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-
 //    specific operator N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the
 //    piece's contribution to the block end.  20 LDS lookups + 37 VALU per
-//    16 bytes; 152 KiB of LDS, one 1024-thread workgroup per CU.
+//    16 bytes; 152 KiB of LDS, one workgroup per CU, 12 waves (768 threads):
+//    16 waves keep 33 % more bytes in flight per CU and stream 2-3 % slower.
 //  * Lookups, A/B variant 1: positional NIBBLE tables, one 128-byte row per
 //    (byte position, nibble value), 2 lookups per byte: 32 lookups + 60 VALU
 //    per 16 bytes, 72 KiB, two workgroups per CU.  The kernel is power-capped
@@ -33,10 +34,15 @@
 //    Z^(512*s) (nibble tables in LDS) and XORed across the blocks of a chunk.
 //  * Work distribution: each workgroup owns an equal range of 8 KiB tiles;
 //    its waves pull tiles from an LDS counter (the SIMD arbiter's age
-//    priority makes static per-wave assignment finish 2x apart).
+//    priority makes static per-wave assignment finish 2x apart).  Batches too
+//    small to give every CU 12 tiles run with 8, 4, 2 or 1 waves per
+//    workgroup so that they still spread over all CUs.
 //  * Tails / odd bpc / unaligned chunks: half a wave per chunk, the chunk is
 //    right-aligned into zero-prefixed virtual 512-byte blocks (leading zeros
 //    do not change lin), Horner-combined with Z^512.
+//  * Verification (crc32c_plan_verify): the same kernel compares instead of
+//    storing; the expected values are fetched with the tile and the last
+//    workgroup publishes the launch's result (threadfence reduction).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -47,8 +53,6 @@ namespace {
 using hdfs_crc::FastTile;
 using hdfs_crc::GenItem;
 using hdfs_crc::KParams;
-using hdfs_crc::kMaxHeads;
-using hdfs_crc::kHeadStride;
 using hdfs_crc::kTicketWord;
 using hdfs_crc::kVCountWord;
 using hdfs_crc::kVFirstWord;
@@ -67,20 +71,14 @@ constexpr uint32_t kS4StageBytes = (kS4Bytes + 1023u) / 1024u * 1024u;
 static_assert(kS4StageBytes <= hdfs_crc::kTableAllocS4, "staging reads past the device table");
 
 // Kernel modes (template bits).  Production = kModeS4 | kModeNt.
-constexpr int kModeNt = 1;         // payload loads non-temporal (streamed once)
-constexpr int kModeS4 = 2;         // slicing-by-4 chains + per-column finishing operator (S4 image)
-constexpr int kModeEarly2 = 4;     // A/B: first tile requested right behind the table staging, bare barrier
-constexpr int kModePipe = 8;       // A/B: two tiles per wave, the next in flight during the lookups
-constexpr int kModeStamps = 16;    // DIAGNOSTIC: per-wave timestamps
-constexpr int kModeMemDiag = 32;   // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
-constexpr int kModeCompDiag = 64;  // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
-constexpr int kModeValuDiag = 128; // DIAGNOSTIC, wrong results (nibble kernel): address math only, no LDS reads
-constexpr int kModeLdsDiag = 256;  // DIAGNOSTIC, wrong results (nibble kernel): LDS reads at fixed addresses
-constexpr int kModeNoStage = 512;   // DIAGNOSTIC (memory-only): no table staging
-constexpr int kModeVerify = 1024;   // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
-constexpr int kModeDyn = 2048;      // dynamic tile scheduler (per-wave prefetched grabs, stealing) instead of static ranges
-constexpr int kModeStriped = 8192;  // scheduler heads striped over the tiles (one sweep front)
-constexpr int kModeSchedWave = 4096;  // last wave of the workgroup schedules: static share, then head grabs; LDS ring
+constexpr int kModeNt = 1;          // payload loads non-temporal (streamed once)
+constexpr int kModeS4 = 2;          // slicing-by-4 chains + per-column finishing operator (S4 image)
+constexpr int kModeStamps = 4;      // DIAGNOSTIC: per-wave timestamps
+constexpr int kModeMemDiag = 8;     // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
+constexpr int kModeCompDiag = 16;   // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
+constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table staging
+constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
+constexpr int kModeDescPf = 128;    // A/B: next tile grabbed at load time, its descriptor prefetched (vector path)
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -97,10 +95,10 @@ __device__ __forceinline__ FastTile tile_at(const KParams &p, uint32_t i) {
     return r;
 }
 
-// Descriptor prefetch through the VECTOR memory path: issued behind a tile's
-// payload loads it is the youngest vmcnt entry, so the lookups never wait for
-// it (a scalar load would: lgkmcnt also counts the LDS lookups, and scalar
-// loads return out of order).  Every lane loads the same 16 bytes.
+// A/B (kModeDescPf): the descriptor through the VECTOR memory path, issued
+// behind a tile's payload loads so the lookups never wait for it (a scalar
+// load would: lgkmcnt also counts the LDS lookups, and scalar loads return
+// out of order).  Every lane loads the same 16 bytes.
 __device__ __forceinline__ uint4 tile_prefetch(const KParams &p, uint32_t i) {
     return *reinterpret_cast<const uint4 *>(p.tiles + i);
 }
@@ -131,9 +129,7 @@ __device__ __forceinline__ uint32_t lds_u32(const uint8_t *lds, uint32_t off) {
 // Byte k of the piece: low nibble row at k*4096 + n*256, high nibble row at
 // 128 + k*256 + n*4096; the lane's column is col*4.  Shifting the dword so
 // the byte sits in bits 8..15 makes both row offsets a single v_and_or.
-// DIAG (diagnostic builds only, wrong results): 1 = the lookups are
-// skipped (memory ceiling), 2 = address arithmetic without the LDS reads
-// (VALU share), 3 = LDS reads at data-independent addresses (LDS share).
+// DIAG 1 (diagnostic builds only, wrong results): the lookups are skipped.
 template <int DIAG>
 __device__ __forceinline__ uint32_t piece_lin(const uint8_t *lds, uint4 d, uint32_t col4) {
     uint32_t acc = 0;
@@ -150,15 +146,8 @@ __device__ __forceinline__ uint32_t piece_lin(const uint8_t *lds, uint4 d, uint3
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             const uint32_t k = 4 * w + t;
-            const uint32_t a0 = DIAG == 3 ? col4 : ((xs[t] & 0x0F00u) | col4);
-            const uint32_t a1 = DIAG == 3 ? col4 : ((xs[t] & 0xF000u) | col4);
-            if (DIAG == 2) {
-                r[2 * t] = a0;
-                r[2 * t + 1] = a1;
-            } else {
-                r[2 * t] = lds_u32(lds, a0 + k * 4096u);
-                r[2 * t + 1] = lds_u32(lds, a1 + 128u + k * 256u);
-            }
+            r[2 * t] = lds_u32(lds, ((xs[t] & 0x0F00u) | col4) + k * 4096u);
+            r[2 * t + 1] = lds_u32(lds, ((xs[t] & 0xF000u) | col4) + 128u + k * 256u);
         }
         acc = xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], acc));
     }
@@ -261,291 +250,64 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
     return (flags & 1u) ? __builtin_bswap32(crc) : crc;  // htonl on the wire, hadooprpc.c:71-75
 }
 
-// Checksum `idx` of the batch: stored, or (VERIFY) compared with the
-// expected value; a mismatch bumps the workgroup's LDS count and lowers its
-// LDS first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish).
+// A mismatch (VERIFY): bump the workgroup's LDS count and lower its LDS
+// first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish).
+__device__ __forceinline__ void mismatch(uint32_t *vacc, uint32_t idx) {
+    atomicAdd(vacc, 1u);
+    atomicMin(vacc + 1, idx);
+}
+
+// Checksum `idx` of the batch: stored, or (VERIFY) compared with `expect`.
 template <bool VERIFY>
-__device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc) {
+__device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t expect) {
     const uint32_t v = out_order(crc, p.flags);
     if (VERIFY) {
-        if (v != p.expect[idx]) {
-            atomicAdd(vacc, 1u);
-            atomicMin(vacc + 1, idx);
-        }
+        if (v != expect) mismatch(vacc, idx);
     } else {
         p.out[idx] = v;
     }
 }
 
-// Fast-path verification: the expected value was prefetched with the tile.
-__device__ __forceinline__ void check(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t ev) {
-    if (out_order(crc, p.flags) != ev) {
-        atomicAdd(vacc, 1u);
-        atomicMin(vacc + 1, idx);
-    }
-}
-
-// ---- launch-wide scheduler / verification state (kernel_abi.h slots) ----
-__device__ __forceinline__ uint32_t *head_ptr(uint32_t *sched, uint32_t h) { return sched + h * kHeadStride; }
-
-// Start of a launch, one thread of workgroup 0: restore the OTHER slot of the
-// pair (used by the previous launch, which has completed) for the next launch.
+// ---- launch-wide verification state (kernel_abi.h slots) -----------------
+// Start of a verification launch, one thread of workgroup 0: restore the
+// OTHER slot of the pair (used by the previous launch, which has completed)
+// for the next launch.
 __device__ __forceinline__ void reset_next_slot(const KParams &p) {
     uint32_t *s = p.sched_next;
-#pragma unroll
-    for (uint32_t h = 0; h < kMaxHeads; ++h) atomicExch(head_ptr(s, h), 0u);
     atomicExch(s + kTicketWord, 0u);
     atomicExch(s + kVCountWord, 0u);
     atomicExch(s + kVFirstWord, 0xffffffffu);
 }
 
+// Waits until every vector-memory operation of the wave has completed; for a
+// returning device-scope atomic that means it has been performed.
+__device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // End of a verification launch, thread 0 of every workgroup: fold the
 // workgroup's count / first-bad index into the slot, take a ticket, and let
-// the last workgroup publish the totals to p.result[0..1] (threadfence
-// reduction; no host-side reset of the result is needed).
+// the last workgroup publish the totals to p.result[0..1] (no host-side reset
+// of the result is needed).  Every word of the slot is only ever touched by
+// device-scope atomics, which are performed in one place, so ordering needs
+// only completion waits, no cache fences (a __threadfence() is an L2
+// writeback + invalidate, ~3.5 us each on the launch's critical tail).
 __device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
     uint32_t *s = p.sched;
     const uint32_t cnt = vacc[0], first = vacc[1];
     if (cnt) {
-        atomicAdd(s + kVCountWord, cnt);
-        atomicMin(s + kVFirstWord, first);
+        uint32_t a = atomicAdd(s + kVCountWord, cnt);
+        uint32_t b = atomicMin(s + kVFirstWord, first);
+        asm volatile("" : "+v"(a), "+v"(b));  // returning forms: the wait below covers them
+        wait_vmem();
     }
-    __threadfence();
     const uint32_t ticket = atomicAdd(s + kTicketWord, 1u);
     if (ticket == gridDim.x - 1u) {
-        __threadfence();
+        // every other workgroup's adds completed before its ticket
         p.result[0] = atomicAdd(s + kVCountWord, 0u);
         p.result[1] = atomicAdd(s + kVFirstWord, 0u);
     }
 }
 
-// Dynamic tile scheduler.  Every wave's first tile is static (tile = global
-// wave index); the other D tiles are split into p.nheads contiguous ranges,
-// each handed out one tile per returning atomicAdd on its head (memory-side
-// atomics, ~1 us under load, so each grab is issued one tile ahead, right
-// behind that tile's loads).  A wave pulls from its home head; when the head
-// runs dry it probes every head in one 16-lane instruction and steals from
-// the one with the most tiles left (odd and even XCDs are not served HBM
-// equally, so static ranges finish several us apart).
-struct DynSched {
-    uint32_t first;  // tiles [0, first) are the static first tiles
-    uint32_t dyn;    // dynamic tiles
-    uint32_t heads;
-    bool striped = false;  // head h's i-th tile: first + i * heads + h (one sweep front) instead of a sub-range
-    __device__ __forceinline__ uint32_t base(uint32_t h) const {
-        return striped ? first + h : first + uint32_t((uint64_t(dyn) * h) / heads);
-    }
-    __device__ __forceinline__ uint32_t len(uint32_t h) const {
-        if (striped) return h < dyn ? (dyn - h + heads - 1) / heads : 0u;
-        return uint32_t((uint64_t(dyn) * (h + 1)) / heads) - uint32_t((uint64_t(dyn) * h) / heads);
-    }
-    __device__ __forceinline__ uint32_t step() const { return striped ? heads : 1u; }
-};
-constexpr uint32_t kNoTile = 0xffffffffu;
-
-// ---- scheduler wave (kModeSchedWave) --------------------------------------
-// The workgroup's last wave hands tile indices to the other (worker) waves
-// through an LDS ring; it is the only wave that touches the scheduler heads,
-// so the ~6 us latency of a memory-side atomic under full HBM load stays off
-// the workers' vector-memory queues.  It first feeds the workgroup's static
-// share (tiles [0, static_tiles) split evenly over the workgroups), then grabs
-// p.grab_unit tiles per lane from kGrabLanes heads per instruction (lane l of
-// workgroup b pulls head (b + l) % nheads, so every head drains at the chip's
-// average rate; a lane whose head runs dry retires), keeping about
-// p.ring_target tiles queued ahead of the workers.
-constexpr uint32_t kRingSlots = 64;     // LDS ring entries: u64 {tag << 32 | tile}
-constexpr uint32_t kGrabLanes = 16;
-constexpr uint32_t kRingBytes = kRingSlots * 8 + 16;  // ring + {taken}
-
-// Slot tags: 2*pos + 1 = tile of ring position pos published; 2*pos = slot
-// free for position pos (its reader of pos - kRingSlots has read it).  Slot
-// i starts free for position i.  Tag and tile travel in one 64-bit LDS word,
-// so relaxed accesses suffice (an acquire/release would also wait for the
-// wave's outstanding global loads and checksum stores).
-struct Ring {
-    uint64_t *slot;   // kRingSlots
-    uint32_t *taken;  // positions reserved by workers
-};
-
-__device__ __forceinline__ uint32_t lds_ld(uint32_t *a) {
-    return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ uint64_t *ring_slot(const Ring &r, uint32_t pos) { return r.slot + (pos & (kRingSlots - 1)); }
-
-// Scheduler: publish `tile` at ring position pos once its slot is free.
-__device__ __forceinline__ void ring_push(const Ring &r, uint32_t pos, uint32_t tile) {
-    uint64_t *sl = ring_slot(r, pos);
-    while (uint32_t(__hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 32) != 2u * pos)
-        __builtin_amdgcn_s_sleep(1);
-    __hip_atomic_store(sl, (uint64_t(2u * pos + 1u) << 32) | tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Worker: the tile at ring position k (waits until it is published), then
-// frees the slot for position k + kRingSlots.
-__device__ __forceinline__ uint32_t ring_pop(const Ring &r, uint32_t k) {
-    uint64_t *sl = ring_slot(r, k);
-    uint64_t v;
-    for (;;) {
-        v = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (uint32_t(v >> 32) == 2u * k + 1u) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
-        __hip_atomic_store(sl, uint64_t(2u * (k + kRingSlots)) << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return uint32_t(v);
-}
-
-__device__ __forceinline__ uint32_t ring_reserve(const Ring &r, int lane) {
-    uint32_t k = 0;
-    if (lane == 0) k = __hip_atomic_fetch_add(r.taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return __builtin_amdgcn_readfirstlane(k);
-}
-
-// Scheduler: lanes l < n publish tile[l] (per lane) at ring positions pos + l,
-// once all n slots are free (one LDS read per lane per check, one write).
-__device__ __forceinline__ void ring_push_batch(const Ring &r, uint32_t pos, uint32_t n, uint32_t tile, int lane) {
-    const bool mine = uint32_t(lane) < n;
-    const uint32_t q = pos + uint32_t(lane);
-    uint64_t *sl = ring_slot(r, q);
-    for (;;) {
-        bool busy = false;
-        if (mine) busy = uint32_t(__hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> 32) != 2u * q;
-        if (__builtin_amdgcn_ballot_w64(busy) == 0) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (mine) __hip_atomic_store(sl, (uint64_t(2u * q + 1u) << 32) | tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Inclusive prefix sum over the wave's lanes (wave-uniform control flow).
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = static_cast<uint32_t>(__shfl_up(static_cast<int>(x), d));
-        if (lane >= d) x += y;
-    }
-    return x;
-}
-
-// st (DIAGNOSTIC, stamps builds): [0] grabs, [1] summed grab round trip,
-// [2] longest grab round trip (s_memrealtime ticks, 100 MHz), [3] time of the
-// first grab.
-template <bool STATS>
-__device__ __forceinline__ void sched_wave(const KParams &p, const Ring &r, const DynSched &ds, uint32_t sbeg,
-                                           uint32_t send, uint32_t workers, int lane, uint64_t *st) {
-    uint32_t pos = 0;
-    uint32_t sc = sbeg;
-    const uint32_t target = min(p.ring_target, 48u);
-    // Static share first, published in batches, kept ~target ahead of the workers
-    // (signed: workers may have reserved positions not published yet).
-    while (sc < send) {
-        const int32_t ahead = int32_t(pos - lds_ld(r.taken));
-        if (ahead >= int32_t(target)) {
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        const uint32_t n = min(send - sc, uint32_t(int32_t(target) - ahead));
-        ring_push_batch(r, pos, n, sc + uint32_t(lane), lane);
-        pos += n;
-        sc += n;
-    }
-    // lane l pulls head (b + l) % heads: with one lane per head, every
-    // workgroup pulls every head and the heads run dry together.
-    const uint32_t lanes = min(ds.heads, kGrabLanes);
-    const uint32_t hl = (blockIdx.x + uint32_t(lane)) % ds.heads;
-    bool active = uint32_t(lane) < lanes && ds.dyn > 0 && ds.len(hl) > 0;
-    const uint32_t unit = min(p.grab_unit, 64u / lanes);  // one batch fits the ring
-    while (__builtin_amdgcn_ballot_w64(active) != 0) {
-        while (int32_t(pos - lds_ld(r.taken)) >= int32_t(target)) __builtin_amdgcn_s_sleep(2);
-        uint64_t t0 = 0;
-        if (STATS) t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t g = 0;
-        if (active) g = atomicAdd(head_ptr(p.sched, hl), unit);
-        if (STATS) {
-            g = __builtin_amdgcn_readfirstlane(g) == 0xdeadbeefu ? 1u : g;  // forces the wait here
-            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
-            if (st[0] == 0) st[3] = t0;
-            st[0] += 1;
-            st[1] += dt;
-            st[2] = dt > st[2] ? dt : st[2];
-        }
-        // lane l got tiles base(hl) + g .. + cnt - 1
-        const uint32_t n = ds.len(hl);
-        const uint32_t cnt = active ? (g < n ? min(unit, n - g) : 0u) : 0u;
-        if (active && g + unit >= n) active = false;
-        const uint32_t incl = wave_incl_scan(cnt, lane);
-        const uint32_t off = incl - cnt;
-        const uint32_t m = __builtin_amdgcn_readlane(incl, 63);
-        if (m == 0) continue;
-        // slots pos .. pos + m - 1 must be free; then every lane writes its tiles
-        {
-            const bool mine = uint32_t(lane) < m;
-            const uint32_t q = pos + uint32_t(lane);
-            for (;;) {
-                bool busy = false;
-                if (mine)
-                    busy = uint32_t(__hip_atomic_load(ring_slot(r, q), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >>
-                                    32) != 2u * q;
-                if (__builtin_amdgcn_ballot_w64(busy) == 0) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        const uint32_t b = ds.base(hl) + g * ds.step();
-        for (uint32_t u = 0; u < unit; ++u)
-            if (u < cnt) {
-                const uint32_t q = pos + off + u;
-                __hip_atomic_store(ring_slot(r, q), (uint64_t(2u * q + 1u) << 32) | (b + u * ds.step()),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-        pos += m;
-    }
-    ring_push_batch(r, pos, workers, kNoTile, lane);
-}
-
-__device__ __forceinline__ uint32_t head_grab(uint32_t *sched, uint32_t h, int lane) {
-    uint32_t r = 0;
-    if (lane == 0) r = atomicAdd(head_ptr(sched, h), 1u);
-    return r;
-}
-
-// Resolves a grab issued on `home` (raw lane-0 result r); on a dry head,
-// steals.  Terminates: a failed steal means another wave took the tile, and
-// heads only grow.
-__device__ __forceinline__ uint32_t dyn_next(uint32_t *sched, const DynSched &ds, uint32_t &home, uint32_t r,
-                                             int lane) {
-    r = __builtin_amdgcn_readfirstlane(r);
-    if (r < ds.len(home)) return ds.base(home) + r * ds.step();
-    for (;;) {
-        uint32_t rem = 0;
-        if (lane < int(ds.heads)) {
-            const uint32_t h = uint32_t(lane);
-            const uint32_t c = atomicAdd(head_ptr(sched, h), 0u);
-            const uint32_t n = ds.len(h);
-            rem = c < n ? n - c : 0u;
-        }
-        uint32_t best = 0, bh = 0;
-#pragma unroll
-        for (uint32_t h = 0; h < ds.heads; ++h) {
-            const uint32_t x = __builtin_amdgcn_readlane(rem, h);
-            if (x > best) {
-                best = x;
-                bh = h;
-            }
-        }
-        if (best == 0) return kNoTile;
-        home = bh;
-        const uint32_t g = __builtin_amdgcn_readfirstlane(head_grab(sched, home, lane));
-        if (g < ds.len(home)) return ds.base(home) + g * ds.step();
-    }
-}
-
 // ---- fast path: one wave, 16 blocks of full chunks -----------------------
-// Loads of one tile: instruction i reads 1 KiB contiguous (blocks 2i, 2i+1)
-// through a buffer descriptor whose range is the tile's nb * 512 valid
-// bytes.  Lanes of blocks a partial tile does not have fall outside the range
-// and read zeros without touching memory (lin() of zeros is 0, so they need
-// no mask), every lane uses the same one-VGPR offset plus an immediate, and
-// the instruction stream has no divergent branch.  AUX 2 = non-temporal.
 // Block of the tile whose lin() lane `lane` holds after finish_tile's
 // reduce-scatter, and whether the lane emits that block's chunk checksum.
 __device__ __forceinline__ uint32_t rep_block(int lane) {
@@ -555,6 +317,13 @@ __device__ __forceinline__ bool rep_lane(int lane, uint32_t blk, uint32_t nb, ui
     return ((lane & 0x14) == 0) && ((blk & ((1u << lg) - 1u)) == 0) && blk < nb;
 }
 
+// Loads of one tile: instruction i reads 1 KiB contiguous (blocks 2i, 2i+1)
+// through a buffer descriptor whose range is the tile's nb * 512 valid
+// bytes.  Lanes of blocks a partial tile does not have fall outside the range
+// and read zeros without touching memory (lin() of zeros is 0, so they need
+// no mask), every lane uses the same one-VGPR offset plus an immediate, and
+// the instruction stream has no divergent branch.  AUX 2 = non-temporal.
+// VERIFY: the expected checksum the lane compares is fetched with the tile.
 template <int AUX, bool COMPDIAG, bool VERIFY>
 __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
     if (COMPDIAG) {  // synthetic data, no memory traffic
@@ -572,16 +341,16 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
-    if (VERIFY) {  // the expected checksum this lane compares, fetched with the tile
+    if (VERIFY) {  // default policy: the next tile's lanes read the rest of the line
         const uint32_t lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
-        if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];  // default policy: the next tile reads the rest of the line
+        if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];
     }
     // Keep the loads ahead of whatever compute follows.
     __builtin_amdgcn_sched_barrier(0);
 }
 
 // lin() per piece, then reduce to one lin() per block, combine the blocks of
-// each chunk, store the chunk checksums.
+// each chunk, store (or compare) the chunk checksums.
 template <int DIAG, bool S4, bool VERIFY>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             const uint4 v[8], uint32_t ev, int lane) {
@@ -602,7 +371,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
 
     // Reduce-scatter over lane bits 0, 1, 3 (8 values -> 1), then all-reduce
     // over lane bits 2 and 4.  Afterwards lane l holds lin() of block
-    // blk = 2*i + h with i = b3 + 2*b1 + 4*b0 (b = bits of l).
+    // rep_block(l) = 2*i + h with i = b3 + 2*b1 + 4*b0 (b = bits of l).
     const bool b0 = lane & 1, b1 = lane & 2, b3 = lane & 8;
     uint32_t u[4];
 #pragma unroll
@@ -638,13 +407,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
         if (lg >= 4) x ^= dpp<kDppXor1>(x);                               // block bit 3 = lane bit 0
     }
     const uint32_t crc = x ^ p.c_lg[lg];
-    if (rep_lane(lane, blk, nb, lg)) {
-        const uint32_t idx = t.out + (blk >> lg);
-        if (VERIFY)
-            check(p, vacc, idx, crc, ev);
-        else
-            emit<false>(p, vacc, idx, crc);
-    }
+    if (rep_lane(lane, blk, nb, lg)) emit<VERIFY>(p, vacc, t.out + (blk >> lg), crc, ev);
 }
 
 // One tile index from the workgroup's LDS counter (one ds_add_rtn per wave).
@@ -723,7 +486,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
     }
     if (valid && q == 0) {
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
-        emit<VERIFY>(p, vacc, g.out, crc);
+        emit<VERIFY>(p, vacc, g.out, crc, VERIFY ? p.expect[g.out] : 0u);
     }
 }
 
@@ -735,29 +498,20 @@ template <int THREADS, int WPS, int MODE>
 __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams p) {
     constexpr bool NT = (MODE & kModeNt) != 0;
     constexpr bool S4 = (MODE & kModeS4) != 0;
-    constexpr bool EARLY2 = (MODE & kModeEarly2) != 0;
-    constexpr bool PIPE = (MODE & kModePipe) != 0;
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
-    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : (MODE & kModeValuDiag) ? 2 : (MODE & kModeLdsDiag) ? 3 : 0;
+    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : 0;
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
     constexpr bool VERIFY = (MODE & kModeVerify) != 0;
-    constexpr bool DYN = (MODE & kModeDyn) != 0;
-    constexpr bool SCHEDW = (MODE & kModeSchedWave) != 0;
-    constexpr bool STRIPED = (MODE & kModeStriped) != 0;
-    static_assert(!DYN || (!EARLY2 && !PIPE), "the dynamic scheduler has its own tile loop");
-    static_assert(!SCHEDW || (!EARLY2 && !PIPE && !DYN), "the scheduler wave has its own tile loop");
+    constexpr bool DESCPF = (MODE & kModeDescPf) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
     // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
     // its mismatch count and first bad index.
-    constexpr uint32_t kRingLds = SCHEDW ? kRingBytes : 0u;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16 + kRingLds];
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
-    const Ring ring{reinterpret_cast<uint64_t *>(lds + kStage + 16),
-                    reinterpret_cast<uint32_t *>(lds + kStage + 16 + kRingSlots * 8)};
     const uint8_t *table = S4 ? p.table_s4 : p.table;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
@@ -770,27 +524,9 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    // (DYN: every tile index below p.ntiles is valid; first tile = global wave index.)
-    const uint32_t tbeg = DYN ? 0u : uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
-    const uint32_t tend = DYN ? p.ntiles : uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
-    DynSched ds{0, 0, 1};
-    uint32_t home = 0;
-    if (DYN) {
-        const uint32_t nw = gridDim.x * kWaves;
-        ds.first = min(p.ntiles, nw);
-        ds.dyn = p.ntiles - ds.first;
-        ds.heads = p.nheads;
-        home = (blockIdx.x * kWaves + wv) % ds.heads;
-    }
-    if (SCHEDW) {
-        ds.first = p.static_tiles;
-        ds.dyn = p.ntiles - p.static_tiles;
-        ds.heads = p.nheads;
-        ds.striped = STRIPED;
-        for (uint32_t i = threadIdx.x; i < kRingSlots; i += THREADS) ring.slot[i] = uint64_t(2u * i) << 32;
-        if (threadIdx.x == 0) *ring.taken = 0;
-    }
-    if ((DYN || SCHEDW || VERIFY) && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
+    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
     if (threadIdx.x == 0) {
         *pool_ctr = tbeg + kWaves;
         if (VERIFY) {
@@ -798,110 +534,35 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             vacc[1] = 0xffffffffu;
         }
     }
-    uint32_t t = DYN ? blockIdx.x * kWaves + wv : tbeg + wv;
+    uint32_t t = tbeg + wv;
     FastTile ft{0, 0, 0};
     uint4 v[8];
-    uint32_t ev = 0;  // VERIFY: expected checksum prefetched with the tile
+    uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
     for (uint32_t c = wv; !NOSTAGE && c < kStage / 1024u; c += kWaves)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
             (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
-    if (EARLY2) {
-        // The first tile's loads queue behind this wave's staging loads: wait
-        // for all but those 8 (vmcnt counts in issue order), then a bare
-        // barrier (__syncthreads' fence would wait for the tile too).
-        if (t < tend) {
-            ft = tile_at(p, t);
-            load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
-            __builtin_amdgcn_s_waitcnt(0x0078);  // vmcnt(8) expcnt(7) lgkmcnt(0): staging loads and LDS writes done
-        } else {
-            __builtin_amdgcn_s_waitcnt(0x0070);  // no tile in flight: vmcnt(0) lgkmcnt(0)
-        }
-        __builtin_amdgcn_s_barrier();
-    } else {
-        __syncthreads();
-    }
+    __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (!EARLY2 && !SCHEDW && t < tend) {
+    if (t < tend) {
         ft = tile_at(p, t);
         load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
     }
-    uint64_t sstat[4] = {0, 0, 0, 0};
-    if (SCHEDW) {
-        constexpr uint32_t kWorkers = kWaves - 1;
-        if (wv == kWorkers) {
-            const uint32_t sbeg = uint32_t((uint64_t(p.static_tiles) * blockIdx.x) / gridDim.x);
-            const uint32_t send = uint32_t((uint64_t(p.static_tiles) * (blockIdx.x + 1)) / gridDim.x);
-            sched_wave<STAMPS>(p, ring, ds, sbeg, send, kWorkers, lane, sstat);
-        } else {
-            // The next tile index is popped as soon as this tile's loads are
-            // out, and its descriptor fetched behind them (tile_prefetch).
-            t = ring_pop(ring, ring_reserve(ring, lane));
-            uint4 dn = make_uint4(0, 0, 0, 0);
-            if (t != kNoTile) dn = tile_prefetch(p, t);
-            while (t != kNoTile) {
-                ft = tile_from(dn);
-                load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
-                const uint32_t k = ring_reserve(ring, lane);
-                uint32_t tn;
-                if (STAMPS) {
-                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                    tn = ring_pop(ring, k);
-                    sstat[1] += __builtin_amdgcn_s_memrealtime() - w0;  // worker: time waiting on the ring
-                    sstat[0] += 1;
-                } else {
-                    tn = ring_pop(ring, k);
-                }
-                dn = tile_prefetch(p, tn != kNoTile ? tn : 0u);  // unconditional: keeps vmcnt counts exact
-                __builtin_amdgcn_sched_barrier(0);
-                finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
-                t = tn;
-            }
-        }
-    } else if (PIPE) {
-        // Two register tiles per wave (a = v, b = vb): one is in flight while
-        // the other is looked up.
-        uint32_t tb = t < tend ? pool_grab(pool_ctr, lane) : tend;
-        FastTile fb{0, 0, 0};
-        uint4 vb[8];
-        uint32_t evb = 0;
-        if (tb < tend) {
-            fb = tile_at(p, tb);
-            load_tile<AUX, COMPDIAG, VERIFY>(p, fb, lane, vb, evb);
-        }
+    if (DESCPF) {
+        // (the first tile's loads are already out)
+        uint32_t tn = t < tend ? pool_grab(pool_ctr, lane) : tend;
+        uint4 dn = tile_prefetch(p, tn < tend ? tn : 0u);
         while (t < tend) {
-            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
-            if (tb >= tend) break;
-            t = pool_grab(pool_ctr, lane);
-            if (t < tend) {
-                ft = tile_at(p, t);
-                load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
-            }
-            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, fb, vb, evb, lane);
-            if (t >= tend) break;
-            tb = pool_grab(pool_ctr, lane);
-            if (tb < tend) {
-                fb = tile_at(p, tb);
-                load_tile<AUX, COMPDIAG, VERIFY>(p, fb, lane, vb, evb);
-            }
-        }
-    } else if (DYN) {
-        // The first tile's loads are in flight; the grab for the next one
-        // goes right behind them and is resolved after the lookups.
-        while (t < tend) {
-            uint32_t r = ds.dyn ? head_grab(p.sched, home, lane) : 0u;
             __builtin_amdgcn_sched_barrier(0);
             finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
-            // The grab's result is first read here, after the lookups (keeps
-            // its vmcnt wait from moving in front of them).
-            __builtin_amdgcn_sched_barrier(0);
-            opaque(r);
-            t = ds.dyn ? dyn_next(p.sched, ds, home, r, lane) : kNoTile;
+            t = tn;
             if (t >= tend) break;
-            ft = tile_at(p, t);
+            ft = tile_from(dn);
             load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
+            tn = pool_grab(pool_ctr, lane);
+            dn = tile_prefetch(p, tn < tend ? tn : 0u);  // unconditional: keeps vmcnt counts exact
         }
     } else {
         while (t < tend) {
@@ -925,147 +586,98 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
         const uint32_t xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
-        constexpr uint32_t kW = SCHEDW ? 8u : 4u;  // scheduler-wave builds add sstat[0..3]
-        p.stamps[kW * wave + 0] = t_start;
-        p.stamps[kW * wave + 1] = t_staged;
-        p.stamps[kW * wave + 2] = t_end;
-        p.stamps[kW * wave + 3] = (uint64_t(xcc_id) << 32) | hw_id;
-        if (SCHEDW)
-            for (int i = 0; i < 4; ++i) p.stamps[kW * wave + 4 + i] = sstat[i];
+        p.stamps[4 * wave + 0] = t_start;
+        p.stamps[4 * wave + 1] = t_staged;
+        p.stamps[4 * wave + 2] = t_end;
+        p.stamps[4 * wave + 3] = (uint64_t(xcc_id) << 32) | hw_id;
     }
 }
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"s4_wg1024x1_nt", 1024, 1},                // production: slicing-by-4 chains, 16 waves per CU
+    {"s4_nt", 768, 1},                          // production: slicing-by-4 chains, 12 waves per CU (fewer for small batches)
     {"nibble_wg1024x2_nt", 1024, 2},            // A/B: positional nibble tables, 32 waves per CU
-    {"s4_wg1024x1_nt_early2", 1024, 1},         // A/B: first tile right behind the table staging
-    {"s4_wg1024x1_nt_pipe", 1024, 1},           // A/B: two tiles per wave
-    {"s4_wg1024x1_nt_memonly", 1024, 1},        // DIAGNOSTIC: memory ceiling of 0 (no lookups)
-    {"s4_wg1024x1_nt_compute_only", 1024, 1},   // DIAGNOSTIC: compute ceiling of 0 (no payload loads)
-    {"nibble_wg1024x2_nt_memonly", 1024, 2},    // DIAGNOSTIC: memory ceiling of 1
-    {"nibble_wg1024x2_nt_compute_only", 1024, 2},  // DIAGNOSTIC: compute ceiling of 1
-    {"s4_wg1024x1_nt_stamps", 1024, 1},         // DIAGNOSTIC: 0 with per-wave timestamps
-    {"s4_wg1024x1_nt_memonly_stamps", 1024, 1}, // DIAGNOSTIC: 4 with per-wave timestamps
-    {"nibble_wg1024x2_nt_valu_only", 1024, 2},  // DIAGNOSTIC: 7 without the LDS reads
-    {"nibble_wg1024x2_nt_lds_only", 1024, 2},   // DIAGNOSTIC: 7 without the address math
-    {"s4_wg1024x1_nt_memonly_nostage", 1024, 1},  // DIAGNOSTIC: 4 without the table staging
+    {"s4_wg1024x1_nt", 1024, 1},                // A/B: 0 with 16 waves per CU (round-1 production)
+    {"s4_wg768x1_nt_memonly", 768, 1},          // DIAGNOSTIC: memory ceiling of 0 (no lookups)
+    {"s4_wg768x1_nt_compute_only", 768, 1},     // DIAGNOSTIC: compute ceiling of 0 (no payload loads)
+    {"s4_wg768x1_nt_stamps", 768, 1},           // DIAGNOSTIC: 0 with per-wave timestamps
+    {"s4_wg768x1_nt_memonly_stamps", 768, 1},   // DIAGNOSTIC: 3 with per-wave timestamps
+    {"s4_wg768x1_nt_memonly_nostage", 768, 1},  // DIAGNOSTIC: 3 without the table staging
+    {"s4_wg768x1_nt_descpf", 768, 1},           // A/B: 0 with the next descriptor prefetched (vector path)
     {"s4_wg512x1_nt", 512, 1},                  // A/B: 0 with 8 waves per CU
-    {"s4_wg512x1_nt_pipe", 512, 1},             // A/B: 8 waves per CU, two tiles per wave
-    {"s4_wg768x1_nt", 768, 1},                  // A/B: 0 with 12 waves per CU
-    {"s4_wg512x1_nt_memonly", 512, 1},          // DIAGNOSTIC: memory ceiling of 13
-    {"s4_wg640x1_nt", 640, 1},                  // A/B: 0 with 10 waves per CU
-    {"s4_wg896x1_nt", 896, 1},                  // A/B: 0 with 14 waves per CU
-    {"s4_wg768x1_nt_memonly", 768, 1},          // DIAGNOSTIC: memory ceiling of 15
-    {"s4_wg768x1_nt_early2", 768, 1},           // A/B: 15 with the first tile right behind the staging
-    {"s4_wg1024x1_nt_dyn", 1024, 1, 16},        // A/B: 0 with the dynamic tile scheduler
-    {"s4_wg768x1_nt_dyn", 768, 1, 16},          // A/B: 15 with the dynamic tile scheduler
-    {"s4_wg768x1_nt_dyn_memonly", 768, 1, 16},  // DIAGNOSTIC: memory ceiling of 22
-    {"s4_wg768x1_nt_dyn_stamps", 768, 1, 16},   // DIAGNOSTIC: 22 with per-wave timestamps
-    {"s4_wg768x1_nt_dyn32", 768, 1, 32},        // A/B: 22 with 32 heads
-    {"s4_wg768x1_nt_dyn8", 768, 1, 8},          // A/B: 22 with 8 heads
-    {"s4_wg832x1_nt_schedw50", 832, 1, 16, 50},  // A/B: 12 worker waves + scheduler wave, half the tiles static
-    {"s4_wg832x1_nt_schedw25", 832, 1, 16, 25},  // A/B: same, a quarter static
-    {"s4_wg832x1_nt_schedw50_memonly", 832, 1, 16, 50},  // DIAGNOSTIC: memory ceiling of 27
-    {"s4_wg832x1_nt_schedw50_stamps", 832, 1, 16, 50},   // DIAGNOSTIC: 27 with per-wave timestamps
-    {"s4_wg832x1_nt_schedw50_t36u4", 832, 1, 16, 50, 36, 4},  // A/B: 27, deeper pipeline
-    {"s4_wg832x1_nt_schedw50_t48u4", 832, 1, 16, 50, 48, 4},  // A/B: 27, deeper still
-    {"s4_wg832x1_nt_schedw75_t36u4", 832, 1, 16, 75, 36, 4},  // A/B: 31 with 3/4 static
-    {"s4_wg832x1_nt_schedw50_t36u4_memonly", 832, 1, 16, 50, 36, 4},  // DIAGNOSTIC: memory ceiling of 31
-    {"s4_wg832x1_nt_schedw100", 832, 1, 16, 100, 20, 2},  // DIAGNOSTIC: 27 with every tile static (ring only)
-    {"s4_wg832x1_nt_schedw0", 832, 1, 16, 0, 36, 4},      // A/B: 27 with every tile dynamic
-    {"s4_wg832x1_nt_schedw50_h8t2u1", 832, 1, 8, 50, 2, 1},    // A/B: small queue
-    {"s4_wg832x1_nt_schedw50_h8t6u1", 832, 1, 8, 50, 6, 1},
-    {"s4_wg832x1_nt_schedw50_h12t6u1", 832, 1, 12, 50, 6, 1},
-    {"s4_wg832x1_nt_schedw25_h8t6u1", 832, 1, 8, 25, 6, 1},
-    {"s4_wg832x1_nt_schedw0_h8t6u1", 832, 1, 8, 0, 6, 1},
-    {"s4_wg832x1_nt_schedw50_h8t6u1_memonly", 832, 1, 8, 50, 6, 1},  // DIAGNOSTIC: memory ceiling of 38
-    {"s4_wg832x1_nt_schedw50_h8t6u1_stamps", 832, 1, 8, 50, 6, 1},   // DIAGNOSTIC: 38 with stamps
-    {"s4_wg832x1_nt_schedw50_h8t6u1_striped", 832, 1, 8, 50, 6, 1},  // A/B: 38 with striped heads
-    {"s4_wg832x1_nt_schedw25_h8t6u1_striped", 832, 1, 8, 25, 6, 1},
-    {"s4_wg832x1_nt_schedw0_h8t6u1_striped", 832, 1, 8, 0, 6, 1},
-    {"s4_wg832x1_nt_schedw0_h16t6u1_striped", 832, 1, 16, 0, 6, 1},
-    {"s4_wg832x1_nt_schedw0_h8t6u1_striped_memonly", 832, 1, 8, 0, 6, 1},  // DIAGNOSTIC: memory ceiling of 46
-    {"s4_wg832x1_nt_schedw0_h8t6u1_striped_stamps", 832, 1, 8, 0, 6, 1},   // DIAGNOSTIC: 46 with stamps
+    {"s4_wg768x1_nt_fixed", 768, 1},            // A/B: 0 without the small-batch shapes
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
+
+namespace {
+constexpr int kS4Nt = kModeS4 | kModeNt;
+
+// Waves per workgroup of the production kernel: 12, or for batches too small
+// to give every CU 12 work items, the largest of 8 / 4 / 2 / 1 that still
+// gives every CU one item per wave (so the batch spreads over all CUs).
+uint32_t production_waves(uint64_t items, uint32_t num_cu) {
+    if (items >= uint64_t(12) * num_cu) return 12;
+    for (uint32_t w : {8u, 4u, 2u})
+        if (items >= uint64_t(w) * num_cu) return w;
+    return 1;
+}
+
+template <int M>
+hipError_t launch_production(const KParams &p, uint64_t items, uint32_t num_cu, hipStream_t stream) {
+    const uint32_t w = production_waves(items, num_cu);
+    uint64_t grid = (items + w - 1) / w;
+    if (grid > num_cu) grid = num_cu;
+    if (grid == 0) grid = 1;
+    const dim3 g{uint32_t(grid), 1, 1}, b{w * 64u, 1, 1};
+    switch (w) {
+    case 12: HDFS_LAUNCH(768, 3, M); break;
+    case 8: HDFS_LAUNCH(512, 2, M); break;
+    case 4: HDFS_LAUNCH(256, 1, M); break;
+    case 2: HDFS_LAUNCH(128, 1, M); break;
+    default: HDFS_LAUNCH(64, 1, M); break;
+    }
+    return hipGetLastError();
+}
+}  // namespace
 
 hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream) {
     if (variant < 0 || variant >= kNumVariants) variant = 0;
     const KernelVariant &kv = kVariants[variant];
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
+    if (variant == 0) {
+        if (p.expect) {
+            if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
+            return launch_production<kS4Nt | kModeVerify>(p, items, num_cu, stream);
+        }
+        return launch_production<kS4Nt>(p, items, num_cu, stream);
+    }
     const uint64_t waves = uint64_t(kv.threads / 64);
     uint64_t grid = (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * kv.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{kv.threads, 1, 1};
-    constexpr int kS4Nt = kModeS4 | kModeNt;
-    if ((kv.heads || p.expect) && (!p.sched || !p.sched_next)) return hipErrorInvalidValue;
-    if (kv.heads && (p.nheads == 0 || p.nheads > kMaxHeads)) return hipErrorInvalidValue;
-    if (p.expect) {  // verification: the production kernel (or the nibble A/B kernel) in compare mode
-        if (!p.result) return hipErrorInvalidValue;
+    if (p.expect) {  // verification: the A/B kernels 1 and 2 also have a compare mode
+        if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
         switch (variant) {
-        case 0: HDFS_LAUNCH(1024, 4, kS4Nt | kModeVerify); break;
         case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeVerify); break;
-        case 21: HDFS_LAUNCH(1024, 4, kS4Nt | kModeDyn | kModeVerify); break;
-        case 22: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn | kModeVerify); break;
+        case 2: HDFS_LAUNCH(1024, 4, kS4Nt | kModeVerify); break;
         default: return hipErrorInvalidValue;  // diagnostic variants do not verify
         }
         return hipGetLastError();
     }
     switch (variant) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt); break;
-    case 2: HDFS_LAUNCH(1024, 4, kS4Nt | kModeEarly2); break;
-    case 3: HDFS_LAUNCH(1024, 4, kS4Nt | kModePipe); break;
-    case 4: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag); break;
-    case 5: HDFS_LAUNCH(1024, 4, kS4Nt | kModeCompDiag); break;
-    case 6: HDFS_LAUNCH(1024, 8, kModeNt | kModeMemDiag); break;
-    case 7: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag); break;
-    case 8: HDFS_LAUNCH(1024, 4, kS4Nt | kModeStamps); break;
-    case 9: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeStamps); break;
-    case 10: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeValuDiag); break;
-    case 11: HDFS_LAUNCH(1024, 8, kModeNt | kModeCompDiag | kModeLdsDiag); break;
-    case 12: HDFS_LAUNCH(1024, 4, kS4Nt | kModeMemDiag | kModeNoStage); break;
-    case 13: HDFS_LAUNCH(512, 2, kS4Nt); break;
-    case 14: HDFS_LAUNCH(512, 2, kS4Nt | kModePipe); break;
-    case 15: HDFS_LAUNCH(768, 3, kS4Nt); break;
-    case 16: HDFS_LAUNCH(512, 2, kS4Nt | kModeMemDiag); break;
-    case 17: HDFS_LAUNCH(640, 3, kS4Nt); break;
-    case 18: HDFS_LAUNCH(896, 4, kS4Nt); break;
-    case 19: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag); break;
-    case 20: HDFS_LAUNCH(768, 3, kS4Nt | kModeEarly2); break;
-    case 21: HDFS_LAUNCH(1024, 4, kS4Nt | kModeDyn); break;
-    case 22: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn); break;
-    case 23: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn | kModeMemDiag); break;
-    case 24: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn | kModeStamps); break;
-    case 25: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn); break;
-    case 26: HDFS_LAUNCH(768, 3, kS4Nt | kModeDyn); break;
-    case 27: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 28: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 29: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeMemDiag); break;
-    case 30: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStamps); break;
-    case 31: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 32: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 33: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 34: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeMemDiag); break;
-    case 35: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 36: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 37:
-    case 38:
-    case 39:
-    case 40:
-    case 41: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave); break;
-    case 42: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeMemDiag); break;
-    case 43: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStamps); break;
-    case 44:
-    case 45:
-    case 46:
-    case 47: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStriped); break;
-    case 48: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStriped | kModeMemDiag); break;
-    case 49: HDFS_LAUNCH(832, 4, kS4Nt | kModeSchedWave | kModeStriped | kModeStamps); break;
-    default: HDFS_LAUNCH(1024, 4, kS4Nt); break;
+    case 2: HDFS_LAUNCH(1024, 4, kS4Nt); break;
+    case 3: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag); break;
+    case 4: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompDiag); break;
+    case 5: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps); break;
+    case 6: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeStamps); break;
+    case 7: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeNoStage); break;
+    case 8: HDFS_LAUNCH(768, 3, kS4Nt | kModeDescPf); break;
+    case 9: HDFS_LAUNCH(512, 2, kS4Nt); break;
+    default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
 }

@@ -137,10 +137,6 @@ KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, co
     p.result = nullptr;
     p.sched = nullptr;
     p.sched_next = nullptr;
-    p.nheads = 0;
-    p.static_tiles = 0;
-    p.ring_target = 0;
-    p.grab_unit = 0;
     return p;
 }
 
@@ -153,17 +149,13 @@ int alloc_slots(SchedSlots &s) {
     return 0;
 }
 
-// Launches p on `stream`.  Kernels that use the scheduler slots (dynamic
-// variants, verification) take the current slot, reset the other one, and
-// the pair flips; the caller keeps launches on `slots` in GPU order.
+// Launches p on `stream`.  Verification launches take the current slot,
+// reset the other one, and the pair flips; the caller keeps launches on
+// `slots` in GPU order.
 int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
     if (!items) return 0;
-    const bool sched = kVariants[ctx->variant].heads || p.expect;
-    p.nheads = kVariants[ctx->variant].heads;
-    p.static_tiles = uint32_t(uint64_t(p.ntiles) * kVariants[ctx->variant].static_pct / 100);
-    p.ring_target = kVariants[ctx->variant].ring_target;
-    p.grab_unit = kVariants[ctx->variant].grab_unit;
+    const bool sched = p.expect != nullptr;
     if (sched) {
         int rc = alloc_slots(slots);
         if (rc) return rc;
@@ -517,23 +509,8 @@ int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, u
     KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, dev_out,
                            plan->flags);
     p.stamps = dev_stamps;
-    const hipStream_t s = static_cast<hipStream_t>(stream);
-    std::lock_guard<std::mutex> lock(plan->mu);
     if (variant < 0 || variant >= kNumVariants) return fail(-EINVAL, "no kernel variant %d", variant);
-    p.nheads = kVariants[variant].heads;
-    p.static_tiles = uint32_t(uint64_t(p.ntiles) * kVariants[variant].static_pct / 100);
-    p.ring_target = kVariants[variant].ring_target;
-    p.grab_unit = kVariants[variant].grab_unit;
-    if (kVariants[variant].heads) {
-        int rc = alloc_slots(plan->sched);
-        if (rc) return rc;
-        rc = order_plan_launch(plan, s);
-        if (rc) return rc;
-        p.sched = plan->sched.d + plan->sched.cur * kSlotWords;
-        p.sched_next = plan->sched.d + (plan->sched.cur ^ 1) * kSlotWords;
-    }
-    HIP_TRY(launch_plan_kernel(p, variant, uint32_t(plan->ctx->num_cu), s));
-    if (kVariants[variant].heads) plan->sched.cur ^= 1;
+    HIP_TRY(launch_plan_kernel(p, variant, uint32_t(plan->ctx->num_cu), static_cast<hipStream_t>(stream)));
     return 0;
 }
 

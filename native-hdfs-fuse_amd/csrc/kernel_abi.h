@@ -35,28 +35,21 @@ struct KParams {
     uint32_t *result;
     // Scheduler slot of this launch (kSlotWords u32s, see below) and the
     // other slot of the pair, which this launch resets for the next one.
+    // Verification slot of this launch (kSlotWords u32s) and the other slot
+    // of the pair, which this launch resets for the next one.
     uint32_t *sched;
     uint32_t *sched_next;
-    uint32_t nheads;  // dynamic scheduler heads in use (<= kMaxHeads)
-    uint32_t static_tiles;  // scheduler-wave variants: tiles [0, static_tiles) are split statically
-    uint32_t ring_target;   // scheduler-wave variants: tiles queued ahead before the next grab
-    uint32_t grab_unit;     // scheduler-wave variants: tiles per lane per grab
 };
 
-// Device scratch of one launch ("slot"), u32 words.  Launches of one plan
-// (or one host-pipeline stage) alternate between two slots and are
-// serialised on the GPU, so a launch may reset the slot its predecessor used.
-//   heads: up to kMaxHeads tile counters of the dynamic scheduler, 8 KiB
-//          apart so they do not share a memory channel's atomic unit; 0 at
-//          launch start;
-//   ticket / vcount / vfirst: verification's grid-wide merge; 0 / 0 / ~0 at
-//          launch start, restored by the launch's last workgroup.
-constexpr uint32_t kMaxHeads = 32;
-constexpr uint32_t kHeadStride = 17408;  // 68 KiB: heads spread over memory channels
-constexpr uint32_t kTicketWord = kMaxHeads * kHeadStride;
-constexpr uint32_t kVCountWord = kTicketWord + 32;
-constexpr uint32_t kVFirstWord = kTicketWord + 64;
-constexpr uint32_t kSlotWords = kTicketWord + 96;
+// Device state of one verification launch ("slot"), u32 words, each on its
+// own 128-B line: the grid-wide merge of the workgroups' mismatch counts.
+// Launches of one plan (or one host-pipeline stage) alternate between two
+// slots and run in GPU order, so a launch resets the slot its predecessor
+// used: {ticket, vcount, vfirst} = {0, 0, ~0} at launch start.
+constexpr uint32_t kTicketWord = 0;
+constexpr uint32_t kVCountWord = 32;
+constexpr uint32_t kVFirstWord = 64;
+constexpr uint32_t kSlotWords = 96;
 
 // Fills two slots' initial state (2 * kSlotWords words).
 inline void init_sched_slots(uint32_t *w) {
@@ -71,17 +64,14 @@ struct KernelVariant {
     const char *name;
     uint32_t threads;
     uint32_t wg_per_cu;
-    uint32_t heads = 0;  // dynamic scheduler heads (0: static tile ranges, no scheduler slots)
-    uint32_t static_pct = 0;  // scheduler-wave variants: share of the tiles split statically
-    uint32_t ring_target = 20;
-    uint32_t grab_unit = 2;
 };
-constexpr int kNumVariants = 50;
+constexpr int kNumVariants = 11;
 // Variants whose verification mode is built (crc32c_plan_verify).
-inline bool variant_verifies(int v) { return v == 0 || v == 1 || v == 21 || v == 22; }
+inline bool variant_verifies(int v) { return v >= 0 && v <= 2; }
 extern const KernelVariant kVariants[kNumVariants];
 
-// Persistent grid: min(work items / waves per workgroup, wg_per_cu * CUs) of the variant.
+// Persistent grid: min(work items / waves per workgroup, wg_per_cu * CUs) of the
+// variant; variant 0 also picks its waves per workgroup by batch size.
 hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream);
 
 }  // namespace hdfs_crc

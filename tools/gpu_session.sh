@@ -27,7 +27,7 @@ for s in $STEPS; do
     bench3) run bench3 600 python bench.py --config c3 --no-cpu --no-host ;;
     bench4) run bench4 600 python bench.py --config c4 --no-cpu --no-host ;;
     pmc) run pmc 1100 bash tools/pmc_session.sh ;;
-    stamps) for v in ${SV:-8 9}; do run stamps_v$v 300 python tools/stamps.py c2 $v ${SW:-16}; done ;;
+    stamps) for v in ${SV:-5 6}; do run stamps_v$v 300 python tools/stamps.py c2 $v ${SW:-12}; done ;;
     tprobe) run tprobe 300 python tools/timing_probe.py ;;
     sweep) run sweep 300 python tools/probe_sweep.py ;;
     kbench) run kbench ${KB_TIMEOUT:-600} python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ${KB_ARGS:-} ;;

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--nbuf", type=int, default=4)
     ap.add_argument("--variants", default="0,1,2,3,4,5")
-    ap.add_argument("--verify", action="store_true", help="also time crc32c_plan_verify (variant 0) as 'verify'")
+    ap.add_argument("--verify", action="store_true", help="also time crc32c_plan_verify of variants 0-2 as 'verify_<v>'")
     args = ap.parse_args()
 
     import numpy as np
@@ -60,15 +60,17 @@ def main():
         if not np.array_equal(got, ref):
             print("note: variant %s checksums differ (diagnostic variant?)" % v, file=sys.stderr)
     times = {v: [] for v in variants}
-    if args.verify:
-        vplan = plans[variants[0]][1]
+    vvars = [v for v in variants if int(v) in (0, 1, 2)] if args.verify else []  # variants with a compare mode
+    if vvars:
         exps = [torch.zeros_like(o) for o in outs]
         for i in range(args.nbuf):  # expected checksums of every buffer (diagnostic variants overwrite outs)
-            vplan.exec(bufs[i].data_ptr(), exps[i].data_ptr(), stream.cuda_stream)
+            plans[vvars[0]][1].exec(bufs[i].data_ptr(), exps[i].data_ptr(), stream.cuda_stream)
         vres = torch.zeros(2, dtype=torch.int32, device=dev)
-        times["verify"] = []
+        for v in vvars:
+            times["verify_" + v] = []
     for r in range(args.rounds):
-        if args.verify:
+        for v in vvars:
+            vplan = plans[v][1]
             for i in range(3):
                 vplan.verify(bufs[i % args.nbuf].data_ptr(), exps[i % args.nbuf].data_ptr(), vres.data_ptr(),
                              stream.cuda_stream)
@@ -80,7 +82,7 @@ def main():
                 vplan.verify(bufs[b].data_ptr(), exps[b].data_ptr(), vres.data_ptr(), stream.cuda_stream)
             e1.record(stream)
             torch.cuda.synchronize()
-            times["verify"].append(e0.elapsed_time(e1) / args.iters * 1e3)
+            times["verify_" + v].append(e0.elapsed_time(e1) / args.iters * 1e3)
             assert vres.cpu().tolist() == [0, -1], vres
         for v in variants:
             plan = plans[v][1]

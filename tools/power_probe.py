@@ -4,7 +4,7 @@ kernel variant.  For each variant, ~1.5 s of back-to-back launches is queued
 on the stream; rocm-smi is sampled while they run; the average launch time
 comes from HIP events around the whole burst.
 
-    python tools/power_probe.py [--variants 0,4,5] [--launches 30000]
+    python tools/power_probe.py [--variants 0,3,4] [--launches 30000]
 """
 from __future__ import annotations
 
@@ -33,7 +33,7 @@ def smi():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,4,5")
+    ap.add_argument("--variants", default="0,3,4")
     ap.add_argument("--launches", type=int, default=30000)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--external-smi", action="store_true", help="power is sampled by tools/power_probe.sh")

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
     sleep 0.3
   done ) > gpurun_out/smi.log 2>&1 &
 spid=$!
-timeout -k 10 300 python tools/power_probe.py --external-smi --launches ${LAUNCHES:-60000} --variants ${PV:-0,4,5} > gpurun_out/pp.log 2>&1
+timeout -k 10 300 python tools/power_probe.py --external-smi --launches ${LAUNCHES:-60000} --variants ${PV:-0,3,4} > gpurun_out/pp.log 2>&1
 rc=$?
 kill $spid 2>/dev/null
 wait $spid 2>/dev/null

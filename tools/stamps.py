@@ -21,8 +21,8 @@ def main():
     from bench import config_packets, load_package
 
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
-    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 8  # 8 = production + stamps, 9 = memory-only + stamps
-    wpg = int(sys.argv[3]) if len(sys.argv) > 3 else 16  # waves per workgroup of that variant (24: 12)
+    variant = int(sys.argv[2]) if len(sys.argv) > 2 else 5  # 5 = production + stamps, 6 = memory-only + stamps
+    wpg = int(sys.argv[3]) if len(sys.argv) > 3 else 12  # waves per workgroup of that variant
     hdfs = load_package()
     pk, _ = config_packets(cfg, oracle)
     extent = int((pk["payload_off"] + pk["len"]).max())
