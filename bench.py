@@ -134,8 +134,11 @@ def cpu_baseline(oracle_mod, pk, payload_np: np.ndarray, seconds: float):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    # Defaults measure the steady state: the first ~500 back-to-back launches
+    # ride a power-management transient (boost, then an overshooting clamp at
+    # the 1.4 kW package cap).  2500 launches take ~0.1 s.
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--nbuf", type=int, default=4, help="rotating payload buffers (defeat the 256 MiB L3)")
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
@@ -276,12 +279,12 @@ def main():
     verify = None
     if rank == 0:
         res = torch.zeros(2, dtype=torch.int32, device=dev)
-        for i in range(3):
+        for i in range(50):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        nv = 20
+        nv = 200
         for i in range(nv):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         e1.record(stream)

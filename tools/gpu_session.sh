@@ -33,7 +33,7 @@ for s in $STEPS; do
     kbench) run kbench ${KB_TIMEOUT:-600} python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ${KB_ARGS:-} ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 --variants ${KV:-0,1} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-            python3 bench.py --steps 50 --warmup 10 --no-cpu --no-host ;;
+            python3 bench.py --no-cpu --no-host ;;
   esac
 done
 echo "session done"
