@@ -294,7 +294,7 @@ def main():
                   "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
                   "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF)}
 
-    host = None
+    host = h2d = None
     if rank == 0 and not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
         hp = pinned.numpy()
@@ -304,6 +304,16 @@ def main():
         for _ in range(reps):
             ctx.batch_host(hp, pk)
         host = round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2)
+        # the PCIe ceiling of that path: a plain pinned H2D copy of the same bytes
+        dst = torch.empty(pinned.numel(), dtype=torch.uint8, device=dev)
+        dst.copy_(pinned, non_blocking=True)
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(pinned, non_blocking=True)
+        torch.cuda.synchronize()
+        h2d = round(pinned.numel() * reps / (time.perf_counter() - h0) / GIB, 2)
+        del dst
 
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"))
@@ -331,6 +341,7 @@ def main():
             "cpu_baseline": cpu,
             "bit_exact_vs_reference": bit_exact,
             "host_resident_gib_s": host,
+            "host_h2d_copy_gib_s": h2d,
             "verify": verify,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         }

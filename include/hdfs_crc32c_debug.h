@@ -36,18 +36,21 @@ size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags);
 void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_small4);
 
 /* Diagnostic launch of a plan with an explicit kernel variant (see
- * kernel_abi.h kVariants; variants 3 and 6 write per-wave timestamps,
+ * crc32c_kernel.hip kVariants): variants 5 and 6 write per-wave timestamps,
  * 4 x u64 per wave: s_memrealtime at start, after table staging, at exit;
  * XCC_ID << 32 | HW_ID, into dev_stamps, which must then hold 4 * (waves
- * launched) entries; variants 4 and 6 compute WRONG checksums on purpose
- * (memory-only ceiling)). */
+ * launched) entries; variants 3, 4, 6 and 7 compute WRONG checksums on
+ * purpose (memory-only / compute-only ceilings). */
 int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
                                    uint64_t *dev_stamps, int variant, void *stream);
 
-/* DIAGNOSTIC: plain streaming read of `bytes` device bytes (grid x 256
- * threads, grid-stride, 16 B per lane; shape 0/1/3 = 4/8/16 loads in flight
- * per lane, 2 = 4 non-temporal loads); writes grid*256 dwords to dev_out.
- * Prices the HBM read roofline this device actually delivers. */
+/* DIAGNOSTIC: plain streaming read of `bytes` device bytes; writes one
+ * dword per thread to dev_out (at most 2^20 dwords).  Shapes 0-7: grid x 256
+ * threads, grid-stride, 16 B per lane, 4 / 8 / 4 nt / 16 / 2 nt / 8 nt /
+ * 16 nt / 1 nt loads in flight per lane; shapes 8-15: tile reads like the
+ * CRC kernel's (1024 or 512 threads, 8 or 4 KiB per wave, per-workgroup
+ * ranges or grid-stride tiles), see stream_probe.hip.  Prices the HBM read
+ * roofline this device actually delivers (tools/probe_sweep.py). */
 int crc32c_debug_stream_probe(const void *dev_src, uint64_t bytes, uint32_t *dev_out, uint32_t grid, int shape,
                               void *stream);
 

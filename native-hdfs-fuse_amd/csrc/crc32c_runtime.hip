@@ -55,7 +55,17 @@ struct DeviceGuard {
     }
 };
 
-constexpr size_t kSliceBytes = 32ull << 20;  // host pipeline slice (whole packets)
+constexpr size_t kSliceBytes = 32ull << 20;  // host pipeline slice (whole packets), default
+
+// Host pipeline slice size: kSliceBytes, or $HDFS_CRC32C_SLICE_MB (A/B only).
+size_t slice_bytes() {
+    static const size_t v = [] {
+        const char *e = std::getenv("HDFS_CRC32C_SLICE_MB");
+        const long mb = e ? std::atol(e) : 0;
+        return mb > 0 && mb <= 1024 ? size_t(mb) << 20 : kSliceBytes;
+    }();
+    return v;
+}
 
 // The two device scheduler slots (kernel_abi.h) of one launch sequence that
 // the GPU runs in order: a plan, or a host-pipeline stage.
@@ -268,10 +278,10 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
     std::vector<crc32c_packet> local;
     HostPlan plan;
     while (i < npkts) {
-        // Slice = consecutive packets totalling about kSliceBytes.
+        // Slice = consecutive packets totalling about slice_bytes().
         size_t j = i;
         uint64_t bytes = 0, lo = UINT64_MAX, hi = 0;
-        while (j < npkts && (j == i || bytes + pkts[j].len <= kSliceBytes)) {
+        while (j < npkts && (j == i || bytes + pkts[j].len <= slice_bytes())) {
             bytes += pkts[j].len;
             if (pkts[j].len) {
                 lo = std::min<uint64_t>(lo, pkts[j].payload_off);
