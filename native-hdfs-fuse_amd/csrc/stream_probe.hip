@@ -70,6 +70,38 @@ __global__ __launch_bounds__(THREADS) void probe_tiles(const u32x4 *__restrict__
     out[blockIdx.x * THREADS + threadIdx.x] = acc;
 }
 
+// Tile reads handed out dynamically: each wave takes GRAB consecutive 8 KiB
+// tiles per atomicAdd on one device counter (DYN) or the same tiles in the
+// same per-wave order statically (grid-stride over groups of GRAB tiles), so
+// the two differ only in who decides the order.
+template <int GRAB, bool DYN>
+__global__ __launch_bounds__(1024) void probe_dyn(const u32x4 *__restrict__ src, uint64_t bytes, uint32_t *out,
+                                                  uint32_t *ctr) {
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t ngroups = bytes / (8192ull * GRAB);
+    const uint64_t nw = uint64_t(gridDim.x) * 16;
+    uint64_t g = uint64_t(blockIdx.x) * 16 + wv;
+    uint32_t acc = 0;
+    for (;;) {
+        if (DYN) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(ctr, 1u);
+            g = __builtin_amdgcn_readfirstlane(t);
+        }
+        if (g >= ngroups) break;
+        for (int k = 0; k < GRAB; ++k) {
+            const u32x4 *p = src + (g * GRAB + k) * 512 + lane;
+            u32x4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(p + 64 * u);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+        if (!DYN) g += nw;
+    }
+    out[blockIdx.x * 1024 + threadIdx.x] = acc;
+}
+
 }  // namespace
 
 // shape: 0-3 grid-stride (256 threads; unroll 4 / 8 / 4 nt / 16);
@@ -98,6 +130,20 @@ extern "C" int crc32c_debug_stream_probe(const void *dev_src, uint64_t bytes, ui
     case 13: hipLaunchKernelGGL((probe_tiles<512, 8, false>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
     case 14: hipLaunchKernelGGL((probe_tiles<512, 4, true>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
     case 15: hipLaunchKernelGGL((probe_tiles<512, 4, false>), dim3(grid), dim3(512), 0, s, src, bytes, dev_out); break;
+    case 16:
+    case 17:
+    case 18:
+    case 19: {
+        // the counter lives past the per-thread outputs (grid <= 256 here)
+        uint32_t *ctr = dev_out + (1u << 20) - 64;
+        if (grid > 256) return -22;
+        if (hipMemsetAsync(ctr, 0, 4, s) != hipSuccess) return -5;
+        if (shape == 16) hipLaunchKernelGGL((probe_dyn<1, true>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out, ctr);
+        if (shape == 17) hipLaunchKernelGGL((probe_dyn<1, false>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out, ctr);
+        if (shape == 18) hipLaunchKernelGGL((probe_dyn<4, true>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out, ctr);
+        if (shape == 19) hipLaunchKernelGGL((probe_dyn<4, false>), dim3(grid), dim3(1024), 0, s, src, bytes, dev_out, ctr);
+        break;
+    }
     default: return -22;
     }
     return hipGetLastError() == hipSuccess ? 0 : -5;

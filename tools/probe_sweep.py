@@ -30,6 +30,10 @@ SHAPES = {  # shape id -> (name, grids)
     13: ("t512_8k_stride", (256, 512, 1024)),
     14: ("t512_4k_range", (256, 512, 1024)),
     15: ("t512_4k_stride", (256, 512, 1024)),
+    16: ("t1024_8k_dyn1", (256,)),
+    17: ("t1024_8k_static1", (256,)),
+    18: ("t1024_8k_dyn4", (256,)),
+    19: ("t1024_8k_static4", (256,)),
 }
 
 
@@ -38,6 +42,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--nbuf", type=int, default=4)
+    ap.add_argument("--shapes", default="", help="comma-separated shape ids (default: all)")
     args = ap.parse_args()
     import torch
 
@@ -57,6 +62,8 @@ def main():
     res = {}
     for r in range(args.rounds):
         for shape, (name, grids) in SHAPES.items():
+            if args.shapes and str(shape) not in args.shapes.split(","):
+                continue
             for grid in grids:
                 def go(i):
                     rc = L.crc32c_debug_stream_probe(bufs[i % args.nbuf].data_ptr(), extent, out.data_ptr(), grid, shape,
