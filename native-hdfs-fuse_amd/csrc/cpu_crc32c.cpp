@@ -6,10 +6,14 @@
 // host path for single calls; batches go to the GPU (crc32c_gpu.hip).
 //
 // Two host implementations, chosen once by CPUID:
-//  * SSE4.2 `crc32` instruction; buffers >= 3 * kStripe bytes run three
-//    independent register chains over three consecutive stripes and merge
-//    them with a precomputed "append kStripe zero bytes" operator
-//    (crc32c.c:249-289 uses the same idea with two fixed stripe sizes).
+//  * SSE4.2 `crc32` instruction (3-cycle latency, 1 per cycle): the buffer
+//    is consumed in groups of three consecutive stripes, run as three
+//    independent register chains and merged with precomputed "append S zero
+//    bytes" operators (crc32c.c:249-289 uses the same idea with two stripe
+//    sizes, 8192 and 256).  A cascade of stripe sizes 8192 / 1024 / 336 /
+//    168 also covers the sizes the checksum loop actually passes: a 512-byte
+//    chunk is three 168-byte chains + 8 bytes, about half the latency of one
+//    64-step chain (the reference's path for 512 B, crc32c.c:293-299).
 //  * portable slicing-by-8 tables (crc32c.c:78-107's fallback role).
 #include <cstring>
 #include <mutex>
@@ -21,10 +25,11 @@ namespace {
 
 using hdfs_crc::Gf2Op;
 
-constexpr size_t kStripe = 1024;
+constexpr size_t kStripes[] = {8192, 1024, 336, 168};
+constexpr int kNumStripes = 4;
 
 uint32_t g_slice[8][256];
-uint32_t g_stripe_shift[4][256];  // Z^kStripe applied to byte k of a register
+uint32_t g_stripe_shift[kNumStripes][4][256];  // Z^stripe applied to byte k of a register
 bool g_have_sse42 = false;
 std::once_flag g_once;
 
@@ -34,18 +39,20 @@ void init_once() {
         g_slice[0][b] = t0[b];
         for (int k = 1; k < 8; ++k) g_slice[k][b] = (g_slice[k - 1][b] >> 8) ^ t0[g_slice[k - 1][b] & 0xffu];
     }
-    const Gf2Op z = hdfs_crc::op_zeros(kStripe);
-    for (int k = 0; k < 4; ++k)
-        for (uint32_t b = 0; b < 256; ++b) g_stripe_shift[k][b] = z.apply(b << (8 * k));
+    for (int s = 0; s < kNumStripes; ++s) {
+        const Gf2Op z = hdfs_crc::op_zeros(kStripes[s]);
+        for (int k = 0; k < 4; ++k)
+            for (uint32_t b = 0; b < 256; ++b) g_stripe_shift[s][k][b] = z.apply(b << (8 * k));
+    }
 #if defined(__x86_64__) || defined(__i386__)
     __builtin_cpu_init();
     g_have_sse42 = __builtin_cpu_supports("sse4.2");
 #endif
 }
 
-inline uint32_t stripe_shift(uint32_t r) {
-    return g_stripe_shift[0][r & 0xff] ^ g_stripe_shift[1][(r >> 8) & 0xff] ^ g_stripe_shift[2][(r >> 16) & 0xff] ^
-           g_stripe_shift[3][r >> 24];
+inline uint32_t stripe_shift(int s, uint32_t r) {
+    const uint32_t(&t)[4][256] = g_stripe_shift[s];
+    return t[0][r & 0xff] ^ t[1][(r >> 8) & 0xff] ^ t[2][(r >> 16) & 0xff] ^ t[3][r >> 24];
 }
 
 // Register update over raw bytes (no conditioning), portable.
@@ -64,25 +71,31 @@ uint32_t reg_update_sw(uint32_t r, const uint8_t *p, size_t n) {
 }
 
 #if defined(__x86_64__)
+// Three chains over the stripes [p, p+S), [p+S, p+2S), [p+2S, p+3S); the
+// first continues r, the other two start from 0 and are shifted into place.
+template <int SI>
+__attribute__((target("sse4.2"))) inline uint64_t three_stripes(uint64_t r, const uint8_t *p) {
+    constexpr size_t S = kStripes[SI];
+    uint64_t a = r, b = 0, c = 0;
+    for (size_t i = 0; i < S; i += 8) {
+        uint64_t wa, wb, wc;
+        std::memcpy(&wa, p + i, 8);
+        std::memcpy(&wb, p + S + i, 8);
+        std::memcpy(&wc, p + 2 * S + i, 8);
+        a = __builtin_ia32_crc32di(a, wa);
+        b = __builtin_ia32_crc32di(b, wb);
+        c = __builtin_ia32_crc32di(c, wc);
+    }
+    return stripe_shift(SI, stripe_shift(SI, uint32_t(a)) ^ uint32_t(b)) ^ uint32_t(c);
+}
+
 __attribute__((target("sse4.2"))) uint32_t reg_update_hw(uint32_t r32, const uint8_t *p, size_t n) {
     uint64_t r = r32;
     for (; n && (reinterpret_cast<uintptr_t>(p) & 7u); --n) r = __builtin_ia32_crc32qi(uint32_t(r), *p++);
-    while (n >= 3 * kStripe) {
-        uint64_t a = r, b = 0, c = 0;
-        const uint8_t *pa = p, *pb = p + kStripe, *pc = p + 2 * kStripe;
-        for (size_t i = 0; i < kStripe; i += 8) {
-            uint64_t wa, wb, wc;
-            std::memcpy(&wa, pa + i, 8);
-            std::memcpy(&wb, pb + i, 8);
-            std::memcpy(&wc, pc + i, 8);
-            a = __builtin_ia32_crc32di(a, wa);
-            b = __builtin_ia32_crc32di(b, wb);
-            c = __builtin_ia32_crc32di(c, wc);
-        }
-        r = stripe_shift(stripe_shift(uint32_t(a)) ^ uint32_t(b)) ^ uint32_t(c);
-        p += 3 * kStripe;
-        n -= 3 * kStripe;
-    }
+    for (; n >= 3 * kStripes[0]; n -= 3 * kStripes[0], p += 3 * kStripes[0]) r = three_stripes<0>(r, p);
+    for (; n >= 3 * kStripes[1]; n -= 3 * kStripes[1], p += 3 * kStripes[1]) r = three_stripes<1>(r, p);
+    for (; n >= 3 * kStripes[2]; n -= 3 * kStripes[2], p += 3 * kStripes[2]) r = three_stripes<2>(r, p);
+    for (; n >= 3 * kStripes[3]; n -= 3 * kStripes[3], p += 3 * kStripes[3]) r = three_stripes<3>(r, p);
     for (; n >= 8; n -= 8, p += 8) {
         uint64_t w;
         std::memcpy(&w, p, 8);

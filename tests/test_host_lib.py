@@ -45,10 +45,12 @@ def test_scalar_dropin_known_answers(hdfs, golden):
 
 
 def test_scalar_dropin_random_vs_oracle(hdfs, orc):
-    # sizes around the 3 x 1024-byte stripe path and unaligned starts
+    # sizes around the three-stripe groups (3 x 168 / 336 / 1024 / 8192 bytes)
+    # and their cascades, with unaligned starts
     rng = np.random.default_rng(1)
-    buf = oracle.xorshift64_bytes(1 << 16, 33)
-    for n in list(range(0, 40)) + [3071, 3072, 3073, 6144, 9999, 65000]:
+    buf = oracle.xorshift64_bytes(1 << 17, 33)
+    for n in list(range(0, 40)) + [503, 504, 505, 511, 512, 513, 1007, 1008, 1009, 1024, 1512, 3071, 3072, 3073,
+                                   4096, 6144, 9999, 24575, 24576, 24577, 65000, 65536, 100000]:
         off = int(rng.integers(0, 16))
         crc = int(rng.integers(0, 2**32))
         seg = buf[off:off + n]
