@@ -42,7 +42,7 @@
 //    do not change lin), Horner-combined with Z^512.
 //  * Verification (crc32c_plan_verify): the same kernel compares instead of
 //    storing; the expected values are fetched with the tile and the last
-//    workgroup publishes the launch's result (threadfence reduction).
+//    workgroup publishes the launch's result (sharded ticket reduction).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -53,6 +53,8 @@ namespace {
 using hdfs_crc::FastTile;
 using hdfs_crc::GenItem;
 using hdfs_crc::KParams;
+using hdfs_crc::kShardWord;
+using hdfs_crc::kTicketShards;
 using hdfs_crc::kTicketWord;
 using hdfs_crc::kVCountWord;
 using hdfs_crc::kVFirstWord;
@@ -277,6 +279,8 @@ __device__ __forceinline__ void reset_next_slot(const KParams &p) {
     atomicExch(s + kTicketWord, 0u);
     atomicExch(s + kVCountWord, 0u);
     atomicExch(s + kVFirstWord, 0xffffffffu);
+#pragma unroll
+    for (uint32_t i = 0; i < kTicketShards; ++i) atomicExch(s + kShardWord + 32 * i, 0u);
 }
 
 // Waits until every vector-memory operation of the wave has completed; for a
@@ -299,9 +303,13 @@ __device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *
         asm volatile("" : "+v"(a), "+v"(b));  // returning forms: the wait below covers them
         wait_vmem();
     }
-    const uint32_t ticket = atomicAdd(s + kTicketWord, 1u);
-    if (ticket == gridDim.x - 1u) {
-        // every other workgroup's adds completed before its ticket
+    // shard ticket, then (last of the shard) the global ticket
+    const uint32_t shard = blockIdx.x % kTicketShards;
+    const uint32_t shards = min(gridDim.x, kTicketShards);
+    const uint32_t in_shard = (gridDim.x - shard + kTicketShards - 1u) / kTicketShards;
+    if (atomicAdd(s + kShardWord + 32u * shard, 1u) != in_shard - 1u) return;
+    if (atomicAdd(s + kTicketWord, 1u) == shards - 1u) {
+        // every other workgroup's adds completed before its tickets
         p.result[0] = atomicAdd(s + kVCountWord, 0u);
         p.result[1] = atomicAdd(s + kVFirstWord, 0u);
     }

@@ -33,8 +33,6 @@ struct KParams {
     // result[1] = min bad index.
     const uint32_t *expect;
     uint32_t *result;
-    // Scheduler slot of this launch (kSlotWords u32s, see below) and the
-    // other slot of the pair, which this launch resets for the next one.
     // Verification slot of this launch (kSlotWords u32s) and the other slot
     // of the pair, which this launch resets for the next one.
     uint32_t *sched;
@@ -45,11 +43,16 @@ struct KParams {
 // own 128-B line: the grid-wide merge of the workgroups' mismatch counts.
 // Launches of one plan (or one host-pipeline stage) alternate between two
 // slots and run in GPU order, so a launch resets the slot its predecessor
-// used: {ticket, vcount, vfirst} = {0, 0, ~0} at launch start.
+// used: {ticket, vcount, vfirst, shard tickets} = {0, 0, ~0, 0} at launch
+// start.  Workgroup b first takes a ticket in shard b % kTicketShards; the
+// last of a shard takes one of the global ticket (one counter per 32
+// workgroups instead of one for all 256: every add to one word serialises).
+constexpr uint32_t kTicketShards = 8;
 constexpr uint32_t kTicketWord = 0;
 constexpr uint32_t kVCountWord = 32;
 constexpr uint32_t kVFirstWord = 64;
-constexpr uint32_t kSlotWords = 96;
+constexpr uint32_t kShardWord = 96;  // + 32 * shard
+constexpr uint32_t kSlotWords = kShardWord + 32 * kTicketShards;
 
 // Fills two slots' initial state (2 * kSlotWords words).
 inline void init_sched_slots(uint32_t *w) {
