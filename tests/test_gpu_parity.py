@@ -336,3 +336,34 @@ def test_small_batch_shapes(hdfs, gpu_ctx, orc, npkts):
     stream.synchronize()
     assert res.cpu().numpy().view(np.uint32).tolist() == [1, n // 2]
     plan.close()
+
+
+def test_plan_launches_across_streams(hdfs, gpu_ctx, orc):
+    """A plan's verification launches share its device slots, so the library
+    keeps a plan's launches in GPU order when the caller alternates streams
+    (crc32c_plan_verify doc): exec and verify interleaved on two streams give
+    the oracle's checksums and exact mismatch counts every time."""
+    torch = _torch()
+    pk = oracle.uniform_packets(64)
+    payload = oracle.xorshift64_bytes(64 * 65536, 71)
+    want = orc.batch(payload, pk, 64 * 128)
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    bad = exp.clone()
+    bad[[5, 4000]] ^= 1
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.zeros(64 * 128, dtype=torch.int32, device="cuda") for _ in range(8)]
+    results = [torch.zeros(2, dtype=torch.int32, device="cuda") for _ in range(16)]
+    for i in range(16):
+        s = streams[i % 2].cuda_stream
+        plan.verify(dev.data_ptr(), (bad if i % 3 == 0 else exp).data_ptr(), results[i].data_ptr(), s)
+        if i % 2 == 0:
+            plan.exec(dev.data_ptr(), outs[i // 2].data_ptr(), s)
+    torch.cuda.synchronize()
+    for i in range(16):
+        got = results[i].cpu().numpy().view(np.uint32).tolist()
+        assert got == ([2, 5] if i % 3 == 0 else [0, 0xFFFFFFFF]), i
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want)
+    plan.close()
