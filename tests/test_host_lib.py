@@ -57,6 +57,21 @@ def test_scalar_dropin_random_vs_oracle(hdfs, orc):
         assert hdfs.crc32c(seg, crc) == orc.crc32c(seg, crc), n
 
 
+@pytest.mark.skipif(not oracle.Reference.available(), reason="reference build not present")
+def test_scalar_dropin_matches_reference_build(hdfs):
+    """The drop-in against the reference's own crc32c.c (oracle/_ref): random
+    lengths across every stripe size, random alignment and incoming crc."""
+    ref = oracle.Reference()
+    rng = np.random.default_rng(77)
+    buf = oracle.xorshift64_bytes(1 << 17, 78)
+    for _ in range(400):
+        off = int(rng.integers(0, 64))
+        n = int(rng.choice([int(rng.integers(0, 2048)), int(rng.integers(2048, 70000))]))
+        crc = int(rng.integers(0, 2**32))
+        seg = buf[off:off + n]
+        assert hdfs.crc32c(seg, crc) == ref.crc32c(seg, crc), (off, n)
+
+
 def test_nchunks_and_packetize(hdfs, orc):
     assert hdfs.nchunks(65536, 512) == 128
     assert hdfs.nchunks(65537, 512) == 129
