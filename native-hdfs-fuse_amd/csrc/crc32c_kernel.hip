@@ -34,9 +34,9 @@
 //    Z^(512*s) (nibble tables in LDS) and XORed across the blocks of a chunk.
 //  * Work distribution: each workgroup owns an equal range of 8 KiB tiles;
 //    its waves pull tiles from an LDS counter (the SIMD arbiter's age
-//    priority makes static per-wave assignment finish 2x apart).  Batches too
-//    small to give every CU 12 tiles run with 8, 4, 2 or 1 waves per
-//    workgroup so that they still spread over all CUs.
+//    priority makes static per-wave assignment finish 2x apart).  A batch with
+//    fewer tiles than CUs x 12 still runs one 12-wave workgroup per CU (or
+//    per tile): the idle waves share the table staging.
 //  * Tails / odd bpc / unaligned chunks: half a wave per chunk, the chunk is
 //    right-aligned into zero-prefixed virtual 512-byte blocks (leading zeros
 //    do not change lin), Horner-combined with Z^512.
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"s4_nt", 768, 1},                          // production: slicing-by-4 chains, 12 waves per CU (fewer for small batches)
+    {"s4_nt", 768, 1},                          // production: slicing-by-4 chains, 12 waves per CU
     {"nibble_wg1024x2_nt", 1024, 2},            // A/B: positional nibble tables, 32 waves per CU
     {"s4_wg1024x1_nt", 1024, 1},                // A/B: 0 with 16 waves per CU (round-1 production)
     {"s4_wg768x1_nt_memonly", 768, 1},          // DIAGNOSTIC: memory ceiling of 0 (no lookups)
@@ -613,7 +613,8 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_wg768x1_nt_memonly_nostage", 768, 1},  // DIAGNOSTIC: 3 without the table staging
     {"s4_wg768x1_nt_descpf", 768, 1},           // A/B: 0 with the next descriptor prefetched (vector path)
     {"s4_wg512x1_nt", 512, 1},                  // A/B: 0 with 8 waves per CU
-    {"s4_wg768x1_nt_fixed", 768, 1},            // A/B: 0 without the small-batch shapes
+    {"s4_wg768x1_nt_fixed", 768, 1},            // A/B: 0 on ceil(items / 12) workgroups (concentrated)
+    {"s4_nt_shapes", 768, 1},                   // A/B: 0 with 8/4/2/1 waves per workgroup for small batches
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -621,10 +622,21 @@ const KernelVariant kVariants[kNumVariants] = {
 namespace {
 constexpr int kS4Nt = kModeS4 | kModeNt;
 
-// Waves per workgroup of the production kernel: 12, or for batches too small
-// to give every CU 12 work items, the largest of 8 / 4 / 2 / 1 that still
-// gives every CU one item per wave (so the batch spreads over all CUs).
-uint32_t production_waves(uint64_t items, uint32_t num_cu) {
+// Production grid: one 12-wave workgroup per CU, or one per work item when
+// there are fewer items than CUs.  A small batch leaves most waves without a
+// tile; they still share the table staging, which is what bounds a small
+// launch (one wave alone issues 152 LDS-DMA instructions).
+template <int M>
+hipError_t launch_production(const KParams &p, uint64_t items, uint32_t num_cu, hipStream_t stream) {
+    const uint64_t grid = items < num_cu ? (items ? items : 1) : num_cu;
+    const dim3 g{uint32_t(grid), 1, 1}, b{768, 1, 1};
+    HDFS_LAUNCH(768, 3, M);
+    return hipGetLastError();
+}
+
+// A/B (variant 11): waves per workgroup by batch size, 12 or the largest of
+// 8 / 4 / 2 / 1 that still gives every CU one item per wave.
+uint32_t shape_waves(uint64_t items, uint32_t num_cu) {
     if (items >= uint64_t(12) * num_cu) return 12;
     for (uint32_t w : {8u, 4u, 2u})
         if (items >= uint64_t(w) * num_cu) return w;
@@ -632,8 +644,8 @@ uint32_t production_waves(uint64_t items, uint32_t num_cu) {
 }
 
 template <int M>
-hipError_t launch_production(const KParams &p, uint64_t items, uint32_t num_cu, hipStream_t stream) {
-    const uint32_t w = production_waves(items, num_cu);
+hipError_t launch_shapes(const KParams &p, uint64_t items, uint32_t num_cu, hipStream_t stream) {
+    const uint32_t w = shape_waves(items, num_cu);
     uint64_t grid = (items + w - 1) / w;
     if (grid > num_cu) grid = num_cu;
     if (grid == 0) grid = 1;
@@ -660,6 +672,7 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
         }
         return launch_production<kS4Nt>(p, items, num_cu, stream);
     }
+    if (variant == 11 && !p.expect) return launch_shapes<kS4Nt>(p, items, num_cu, stream);
     const uint64_t waves = uint64_t(kv.threads / 64);
     uint64_t grid = (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * kv.wg_per_cu;

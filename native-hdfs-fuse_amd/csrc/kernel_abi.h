@@ -68,13 +68,14 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 11;
+constexpr int kNumVariants = 12;
 // Variants whose verification mode is built (crc32c_plan_verify).
 inline bool variant_verifies(int v) { return v >= 0 && v <= 2; }
 extern const KernelVariant kVariants[kNumVariants];
 
 // Persistent grid: min(work items / waves per workgroup, wg_per_cu * CUs) of the
-// variant; variant 0 also picks its waves per workgroup by batch size.
+// variant; variant 0 runs one 12-wave workgroup per CU, min(items, CUs) of
+// them, and variant 11 picks its waves per workgroup by batch size.
 hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream);
 
 }  // namespace hdfs_crc

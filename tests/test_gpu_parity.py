@@ -196,11 +196,12 @@ def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     assert np.array_equal(got2[:127], got[1:128])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9, 10])
+@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9, 10, 11])
 def test_every_product_kernel_variant(hdfs, golden, orc, variant, monkeypatch):
     """Both table schemes (0 = slicing-by-4 chains, production; 1 = positional
     nibble tables) and the A/B shapes (2 = 16 waves per CU, 8 = descriptor
-    prefetch, 9 = 8 waves, 10 = no small-batch shapes) are bit-exact: golden
+    prefetch, 9 = 8 waves, 10 = concentrated grid, 11 = small-batch shapes of
+    8 / 4 / 2 / 1 waves per workgroup) are bit-exact: golden
     config-2 digest, mixed bpc and a ragged batch through the general path."""
     monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
     ctx = hdfs.Context(0)
@@ -310,11 +311,10 @@ def test_verify_reports_mismatches(hdfs, orc, variant, monkeypatch):
 
 
 @pytest.mark.parametrize("npkts", [1, 3, 75, 138, 263, 388])
-def test_small_batch_shapes(hdfs, gpu_ctx, orc, npkts):
-    """The production kernel runs batches too small to give every CU 12 tiles
-    with 8 / 4 / 2 / 1 waves per workgroup (8 KiB tiles, 8 per 64 KiB packet:
-    these sizes hit every shape on a 256-CU MI355X), plus a ragged packet and
-    a general-path packet; every shape bit-exact, exec and verify."""
+def test_small_batches(hdfs, gpu_ctx, orc, npkts):
+    """Batches with fewer tiles than waves on the chip (8 KiB tiles, 8 per
+    64 KiB packet: from 8 tiles on 8 workgroups to 3104 on 256), each with a
+    ragged general-path packet: bit-exact, exec and verify."""
     torch = _torch()
     pk = oracle.uniform_packets(npkts)
     pk["len"][-1] = 65536 - 100  # ragged tail

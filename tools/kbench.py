@@ -4,7 +4,7 @@
 rotating over NBUF buffers; reports per-variant median/min kernel time and
 GB/s, and checks every variant's checksums against variant 0.
 
-    python tools/kbench.py [--rounds 7] [--iters 20] [--config c2|c5|c3]
+    python tools/kbench.py [--rounds 7] [--iters 20] [--config c2|c5|c3|pN]
 """
 from __future__ import annotations
 
@@ -34,7 +34,11 @@ def main():
     from bench import config_packets, load_package
 
     hdfs = load_package()
-    pk, workload = config_packets(args.config, oracle)
+    if args.config.startswith("p"):  # pN: N uniform 64 KiB packets, 512 B chunks
+        n = int(args.config[1:])
+        pk, workload = oracle.uniform_packets(n), "%d x 64KiB packets, 512B chunks" % n
+    else:
+        pk, workload = config_packets(args.config, oracle)
     nbytes = int(pk["len"].astype(np.int64).sum())
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)
