@@ -319,11 +319,13 @@ def chunks(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:
 # --- helpers ----------------------------------------------------------------
 def total_checksums(pkts) -> int:
     pkts = as_packets(pkts)
-    live = pkts[pkts["len"] > 0]
-    if live.size == 0:
+    if pkts.size == 0:
         return 0
-    per = (live["len"].astype(np.uint64) + live["bpc"].astype(np.uint64) - 1) // live["bpc"].astype(np.uint64)
-    return int((live["out_idx"] + per).max())
+    ln = pkts["len"].astype(np.int64)
+    bpc = np.maximum(pkts["bpc"].astype(np.int64), 1)
+    end = pkts["out_idx"].astype(np.int64) + (ln + bpc - 1) // bpc
+    end[ln == 0] = 0
+    return int(end.max())
 
 
 def debug_plan(pkts):

@@ -55,7 +55,7 @@ struct DeviceGuard {
     }
 };
 
-constexpr size_t kSliceBytes = 32ull << 20;  // host pipeline slice (whole packets), default
+constexpr size_t kSliceBytes = 64ull << 20;  // host pipeline slice (whole packets), default
 
 // Host pipeline slice size: kSliceBytes, or $HDFS_CRC32C_SLICE_MB (A/B only).
 size_t slice_bytes() {
@@ -76,11 +76,17 @@ struct SchedSlots {
 
 struct Stage {
     hipStream_t stream = nullptr;
+    hipEvent_t copied = nullptr;  // the slice's H2D payload copy (on the context's copy stream) is done
     hipEvent_t done = nullptr;
     uint8_t *h_payload = nullptr, *d_payload = nullptr;
     size_t payload_cap = 0;
+    // Work descriptors: pinned host memory the kernel reads in place (d_desc
+    // is its device mapping).  A slice's 64 KiB of descriptors are not worth
+    // a copy of their own: on the copy stream each copy adds ~25 us.
     uint8_t *h_desc = nullptr, *d_desc = nullptr;
     size_t desc_cap = 0;
+    // Checksums: written by the kernel straight into pinned host memory
+    // (d_out is h_out's mapping), which saves a D2H copy on the tail.
     uint32_t *h_out = nullptr, *d_out = nullptr;
     size_t out_cap = 0;
     bool pending = false;
@@ -101,6 +107,11 @@ struct crc32c_ctx {
     uint32_t c_lg[2][5];
     uint32_t c_small[2][4];
     std::mutex mu;
+    // Host pipeline: every stage's H2D copies go on one copy stream, so they
+    // run back to back at the full link rate while the other stage's kernel
+    // and D2H run on its own stream.  Two copies on two streams would share
+    // the link, finish together and leave it idle while both stages drain.
+    hipStream_t copy_stream = nullptr;
     Stage stage[2];
 };
 
@@ -228,15 +239,31 @@ int grow_pinned_pair(T **h, T **d, size_t *cap, size_t need) {
     return 0;
 }
 
+// Pinned, device-mapped host buffer of at least `need` bytes.
+template <typename T>
+int grow_mapped(T **h, T **d, size_t *cap, size_t need) {
+    if (*cap >= need) return 0;
+    if (*h) (void)hipHostFree(*h);
+    *h = nullptr;
+    *d = nullptr;
+    *cap = 0;
+    const size_t c = std::max(need, size_t(4096));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(h), c * sizeof(T), hipHostMallocMapped));
+    void *dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, *h, 0));
+    *d = static_cast<T *>(dp);
+    *cap = c;
+    return 0;
+}
+
 void free_stage(Stage &s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.h_payload) (void)hipHostFree(s.h_payload);
     if (s.d_payload) (void)hipFree(s.d_payload);
-    if (s.h_desc) (void)hipHostFree(s.h_desc);
-    if (s.d_desc) (void)hipFree(s.d_desc);
-    if (s.h_out) (void)hipHostFree(s.h_out);
-    if (s.d_out) (void)hipFree(s.d_out);
+    if (s.h_desc) (void)hipHostFree(s.h_desc);  // d_desc is its mapping
+    if (s.h_out) (void)hipHostFree(s.h_out);  // d_out is its mapping
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.sched.d) (void)hipFree(s.sched.d);
     s = Stage();
@@ -266,10 +293,12 @@ bool is_pinned(const void *p) {
 int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_packet *pkts, size_t npkts,
                       uint32_t *out, uint32_t flags) {
     DeviceGuard guard(ctx->device);
+    if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     for (Stage &s : ctx->stage) {
         if (!s.stream) {
             HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
         }
     }
     const bool pinned = npkts && is_pinned(payload);
@@ -301,18 +330,32 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         const size_t stage_bytes = ranged ? size_t(hi - lo) : size_t(bytes + 16 * (j - i));
         rc = grow_pinned_pair(&s.h_payload, &s.d_payload, &s.payload_cap, stage_bytes + 16);
         if (rc) return rc;
+        // 1. The payload copy goes first: it needs no plan, and the copy
+        //    stream runs the slices' copies back to back.  (This stage's
+        //    previous kernel is done: drain_stage waited for it.)
         local.assign(pkts + i, pkts + j);
-        uint64_t nout = 0, gather_off = 0;
+        const uint8_t *src = s.h_payload;
+        if (ranged) {
+            for (crc32c_packet &pk : local) pk.payload_off -= lo;
+            if (pinned)
+                src = payload + lo;
+            else
+                std::memcpy(s.h_payload, payload + lo, size_t(hi - lo));
+        } else {
+            uint64_t gather_off = 0;
+            for (crc32c_packet &pk : local) {
+                std::memcpy(s.h_payload + gather_off, payload + pk.payload_off, pk.len);
+                pk.payload_off = gather_off;
+                gather_off = (gather_off + pk.len + 15) & ~uint64_t(15);
+            }
+        }
+        HIP_TRY(hipMemcpyAsync(s.d_payload, src, stage_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+        HIP_TRY(hipEventRecord(s.copied, ctx->copy_stream));
+        // 2. Plan and descriptors while the copy runs.
+        uint64_t nout = 0;
         s.scatter.clear();
         for (size_t k = 0; k < local.size(); ++k) {
             const uint64_t n = crc32c_nchunks(local[k].len, local[k].bpc);
-            if (ranged) {
-                local[k].payload_off -= lo;
-            } else {
-                std::memcpy(s.h_payload + gather_off, payload + pkts[i + k].payload_off, local[k].len);
-                local[k].payload_off = gather_off;
-                gather_off = (gather_off + local[k].len + 15) & ~uint64_t(15);
-            }
             s.scatter.push_back(pkts[i + k].out_idx);
             s.scatter.push_back(nout);
             s.scatter.push_back(n);
@@ -322,26 +365,18 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         rc = build_plan(local.data(), local.size(), &plan);
         if (rc) return fail(rc, "invalid packet in batch");
         const size_t desc_bytes = (plan.tiles.size() + plan.gen.size()) * 16;
-        rc = grow_pinned_pair(&s.h_desc, &s.d_desc, &s.desc_cap, desc_bytes + 16);
+        rc = grow_mapped(&s.h_desc, &s.d_desc, &s.desc_cap, desc_bytes + 16);
         if (rc) return rc;
-        rc = grow_pinned_pair(&s.h_out, &s.d_out, &s.out_cap, size_t(nout) + 1);
+        rc = grow_mapped(&s.h_out, &s.d_out, &s.out_cap, size_t(nout) + 1);
         if (rc) return rc;
         std::memcpy(s.h_desc, plan.tiles.data(), plan.tiles.size() * 16);
         std::memcpy(s.h_desc + plan.tiles.size() * 16, plan.gen.data(), plan.gen.size() * 16);
-        const uint8_t *src = s.h_payload;
-        if (ranged) {
-            if (pinned)
-                src = payload + lo;
-            else
-                std::memcpy(s.h_payload, payload + lo, size_t(hi - lo));
-        }
-        HIP_TRY(hipMemcpyAsync(s.d_payload, src, stage_bytes, hipMemcpyHostToDevice, s.stream));
-        HIP_TRY(hipMemcpyAsync(s.d_desc, s.h_desc, desc_bytes, hipMemcpyHostToDevice, s.stream));
+        // 3. Kernel and checksums on the stage's stream, after the copy.
+        HIP_TRY(hipStreamWaitEvent(s.stream, s.copied, 0));
         const KParams p = params_for(ctx, s.d_desc, uint32_t(plan.tiles.size()), s.d_desc + plan.tiles.size() * 16,
                                      uint32_t(plan.gen.size()), s.d_payload, s.d_out, flags);
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, nout * sizeof(uint32_t), hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));
         s.pending = true;
         which ^= 1;
@@ -410,6 +445,10 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
     {
         DeviceGuard guard(ctx->device);
         for (Stage &s : ctx->stage) free_stage(s);
+        if (ctx->copy_stream) {
+            (void)hipStreamSynchronize(ctx->copy_stream);
+            (void)hipStreamDestroy(ctx->copy_stream);
+        }
         for (int ty = 0; ty < 2; ++ty) {
             if (ctx->d_table[ty]) (void)hipFree(ctx->d_table[ty]);
             if (ctx->d_table_s4[ty]) (void)hipFree(ctx->d_table_s4[ty]);
@@ -565,6 +604,7 @@ int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet 
     std::lock_guard<std::mutex> lock(ctx->mu);
     rc = batch_host_locked(ctx, static_cast<const uint8_t *>(payload), pkts, npkts, out, flags);
     if (rc) {
+        if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
         for (Stage &s : ctx->stage) {
             s.pending = false;
             s.scatter.clear();
