@@ -151,15 +151,25 @@ def test_random_batches(hdfs, gpu_ctx, orc):
 
 def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
     torch = _torch()
-    pk = oracle.uniform_packets(700)  # ~44 MiB: crosses the 32 MiB slice size
-    payload = oracle.xorshift64_bytes(700 * 65536, 42)
-    want = orc.batch(payload, pk, 700 * 128)
+    """crc32c_batch_host over 64 MiB slices on two alternating stages: 3
+    slices (~137 MiB, so each stage is reused), from pageable memory (pinned
+    staging) and from pinned memory (copied in place), then mixed bpc with
+    ragged tails, then scattered packets through the gather path (2
+    slices)."""
+    n = 2200
+    pk = oracle.uniform_packets(n)
+    payload = oracle.xorshift64_bytes(n * 65536, 42)
+    want = orc.batch(payload, pk, n * 128)
     assert np.array_equal(gpu_ctx.batch_host(payload, pk), want)
     pinned = torch.from_numpy(payload).pin_memory()
     got = gpu_ctx.batch_host(pinned.numpy(), pk)
     assert np.array_equal(got, want)
+    pkm = oracle.mixed_packets(n)
+    pkm["len"][::7] -= 100
+    wantm = orc.batch(payload, pkm, oracle.total_checksums(pkm))
+    assert np.array_equal(gpu_ctx.batch_host(pinned.numpy(), pkm), wantm)
     # scattered packets (gather path) with out_idx in reverse order
-    pk2 = oracle.uniform_packets(50, pkt_len=30000, stride=65536)
+    pk2 = oracle.uniform_packets(n, pkt_len=40000, stride=65536)
     pk2["out_idx"] = pk2["out_idx"][::-1].copy()
     want2 = orc.batch(payload, pk2, oracle.total_checksums(pk2))
     assert np.array_equal(gpu_ctx.batch_host(payload, pk2), want2)
