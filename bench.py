@@ -294,6 +294,35 @@ def main():
                   "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
                   "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF)}
 
+    # Independent batches on two streams (rank 0, beside the main line, which
+    # stays one stream so that one step = one launch): the next launch's
+    # workgroups start on the CUs the previous one has released.
+    two_streams = None
+    if rank == 0 and nbuf > 1:
+        ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
+
+        def two(n):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for s in ss:
+                s.wait_event(e0)
+            for i in range(n):
+                plan.exec(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), ss[i % 2].cuda_stream)
+            for s in ss:
+                ej = torch.cuda.Event()
+                ej.record(s)
+                stream.wait_event(ej)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) * 1e-3
+
+        two(200)
+        n2 = 1000
+        dt = two(n2)
+        two_streams = {"gib_s": round(nbytes * n2 / dt / GIB, 1), "us_per_batch": round(dt / n2 * 1e6, 2),
+                       "batches": n2}
+
     host = h2d = None
     if rank == 0 and not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
@@ -344,6 +373,7 @@ def main():
             "host_resident_gib_s": host,
             "host_h2d_copy_gib_s": h2d,
             "verify": verify,
+            "two_streams": two_streams,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         }
         print(json.dumps(line), flush=True)

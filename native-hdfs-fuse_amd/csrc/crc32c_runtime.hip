@@ -117,9 +117,9 @@ struct crc32c_ctx {
 
 struct crc32c_plan {
     crc32c_ctx *ctx = nullptr;
-    // Launches of a plan share its scheduler slots, so they are kept in GPU
-    // order: a launch on another stream than the previous one first waits
-    // for the previous one (last_done).
+    // Verify launches of a plan share its scheduler slots, so they are kept
+    // in GPU order: one on another stream than the previous one first waits
+    // for it (last_done).  Exec launches are not ordered.
     std::mutex mu;
     SchedSlots sched;
     hipStream_t last_stream = nullptr;
@@ -205,8 +205,10 @@ int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
 
 int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     std::lock_guard<std::mutex> lock(plan->mu);
-    int rc = order_plan_launch(plan, stream);
-    if (rc) return rc;
+    if (p.expect) {  // only verify launches use the plan's scheduler slots
+        int rc = order_plan_launch(plan, stream);
+        if (rc) return rc;
+    }
     return launch(plan->ctx, p, plan->sched, stream);
 }
 

@@ -150,12 +150,12 @@ def test_random_batches(hdfs, gpu_ctx, orc):
 
 
 def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
-    torch = _torch()
     """crc32c_batch_host over 64 MiB slices on two alternating stages: 3
     slices (~137 MiB, so each stage is reused), from pageable memory (pinned
     staging) and from pinned memory (copied in place), then mixed bpc with
     ragged tails, then scattered packets through the gather path (2
     slices)."""
+    torch = _torch()
     n = 2200
     pk = oracle.uniform_packets(n)
     payload = oracle.xorshift64_bytes(n * 65536, 42)
@@ -350,9 +350,11 @@ def test_small_batches(hdfs, gpu_ctx, orc, npkts):
 
 def test_plan_launches_across_streams(hdfs, gpu_ctx, orc):
     """A plan's verification launches share its device slots, so the library
-    keeps a plan's launches in GPU order when the caller alternates streams
+    keeps them in GPU order when the caller alternates streams
     (crc32c_plan_verify doc): exec and verify interleaved on two streams give
-    the oracle's checksums and exact mismatch counts every time."""
+    the oracle's checksums and exact mismatch counts every time.  Exec
+    launches are not ordered: eight different payloads through one plan on
+    two streams at once each get their own checksums."""
     torch = _torch()
     pk = oracle.uniform_packets(64)
     payload = oracle.xorshift64_bytes(64 * 65536, 71)
@@ -376,4 +378,12 @@ def test_plan_launches_across_streams(hdfs, gpu_ctx, orc):
         assert got == ([2, 5] if i % 3 == 0 else [0, 0xFFFFFFFF]), i
     for o in outs:
         assert np.array_equal(o.cpu().numpy().view(np.uint32), want)
+    pays = [oracle.xorshift64_bytes(64 * 65536, 200 + k) for k in range(8)]
+    devs = [torch.from_numpy(x).cuda() for x in pays]
+    torch.cuda.synchronize()
+    for k in range(8):
+        plan.exec(devs[k].data_ptr(), outs[k].data_ptr(), streams[k % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for k in range(8):
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), orc.batch(pays[k], pk, 64 * 128)), k
     plan.close()
