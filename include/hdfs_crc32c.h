@@ -68,6 +68,10 @@ typedef struct crc32c_packet {
 /* Number of checksums of one packet: roundup(len, bpc) (hadooprpc.c:639). */
 uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc);
 
+/* Length of the checksum array a batch fills: max over packets with len > 0
+ * of out_idx + crc32c_nchunks(len, bpc) (0 for none; bpc == 0 counts as 1). */
+uint64_t crc32c_batch_nchecksums(const crc32c_packet *pkts, size_t npkts);
+
 /* Packet lengths hadoop_rpc_send_packets produces for one block write of
  * `len` bytes starting at `blockoffset` (hadooprpc.c:827-857), including the
  * final empty packet.  Writes up to `max` lengths; returns the count. */

@@ -79,6 +79,7 @@ def _bind(L):
         "crc32c": (u32, [u32, vp, sz]),
         "crc32c_nchunks": (u64, [u64, u32]),
         "crc32c_packetize": (u64, [u64, u64, u32, u32, vp, u64]),
+        "crc32c_batch_nchecksums": (u64, [vp, sz]),
         "crc32c_device_count": (i32, []),
         "crc32c_ctx_create": (i32, [i32, pp]),
         "crc32c_ctx_destroy": (i32, [vp]),
@@ -319,13 +320,7 @@ def chunks(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:
 # --- helpers ----------------------------------------------------------------
 def total_checksums(pkts) -> int:
     pkts = as_packets(pkts)
-    if pkts.size == 0:
-        return 0
-    ln = pkts["len"].astype(np.int64)
-    bpc = np.maximum(pkts["bpc"].astype(np.int64), 1)
-    end = pkts["out_idx"].astype(np.int64) + (ln + bpc - 1) // bpc
-    end[ln == 0] = 0
-    return int(end.max())
+    return int(lib().crc32c_batch_nchecksums(_np_ptr(pkts), pkts.size))
 
 
 def debug_plan(pkts):

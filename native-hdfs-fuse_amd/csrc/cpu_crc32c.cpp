@@ -156,6 +156,16 @@ extern "C" uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc) {
     return bpc ? (len + bpc - 1) / bpc : 0;
 }
 
+extern "C" uint64_t crc32c_batch_nchecksums(const crc32c_packet *pkts, size_t npkts) {
+    uint64_t n = 0;
+    for (size_t i = 0; pkts && i < npkts; ++i)
+        if (pkts[i].len) {
+            const uint64_t end = pkts[i].out_idx + crc32c_nchunks(pkts[i].len, pkts[i].bpc ? pkts[i].bpc : 1);
+            if (end > n) n = end;
+        }
+    return n;
+}
+
 extern "C" uint64_t crc32c_packetize(uint64_t len, uint64_t blockoffset, uint32_t packetsize, uint32_t bpc,
                                      uint64_t *lens, uint64_t max) {
     // hadooprpc.c:827-857.  A packet that would start off a chunk boundary

@@ -81,6 +81,25 @@ def test_nchunks_and_packetize(hdfs, orc):
         assert hdfs.packetize(*args) == orc.packetize(*args), args
 
 
+def test_batch_nchecksums(hdfs):
+    """crc32c_batch_nchecksums (the checksum array length of a batch): the
+    oracle's count on full batches; with empty packets (which own no
+    checksum) and reversed out_idx, the max end over non-empty packets."""
+    rng = np.random.default_rng(17)
+    assert hdfs.total_checksums(np.zeros(0, oracle.PACKET_DTYPE)) == 0
+    for pk in [oracle.uniform_packets(4096), oracle.mixed_packets(96), next(c for n, c in _cases() if n == "odd")]:
+        assert hdfs.total_checksums(pk) == oracle.total_checksums(pk)
+    for _ in range(20):
+        n = int(rng.integers(1, 50))
+        pk = oracle.mixed_packets(n)
+        pk["len"] = rng.integers(0, 70000, n)
+        pk["len"][rng.random(n) < 0.2] = 0
+        pk["out_idx"] = pk["out_idx"][::-1].copy()
+        live = pk[pk["len"] > 0]
+        want = oracle.total_checksums(live) if live.size else 0
+        assert hdfs.total_checksums(pk) == want
+
+
 def _cases():
     yield "c2_shape", oracle.uniform_packets(64)
     yield "mixed", oracle.mixed_packets(24)
