@@ -298,7 +298,7 @@ def main():
     # stays one stream so that one step = one launch): the next launch's
     # workgroups start on the CUs the previous one has released.
     two_streams = None
-    if rank == 0 and nbuf > 1:
+    if rank == 0 and world == 1 and nbuf > 1:
         ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
 
         def two(n):
@@ -324,7 +324,7 @@ def main():
                        "batches": n2}
 
     host = h2d = None
-    if rank == 0 and not args.no_host and args.config != "c4":
+    if rank == 0 and world == 1 and not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
         hp = pinned.numpy()
         hout = np.zeros(max(nout, 1), np.uint32)  # caller-owned output, as hadooprpc.c's packet buffer
@@ -351,7 +351,8 @@ def main():
         if (pmc and pmc.get("config") == args.config
                 and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
-        cpu = None if args.no_cpu else cpu_baseline(oracle, pk, payload0, args.cpu_seconds)
+        # the CPU baseline is an N = 1 figure (timed on rank 0's host cores)
+        cpu = None if args.no_cpu or world > 1 else cpu_baseline(oracle, pk, payload0, args.cpu_seconds)
         line = {
             "metric": baseline_metric(),
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
