@@ -323,26 +323,43 @@ def main():
         two_streams = {"gib_s": round(nbytes * n2 / dt / GIB, 1), "us_per_batch": round(dt / n2 * 1e6, 2),
                        "batches": n2}
 
+    # Host-resident rate (crc32c_batch_host: pinned host batch -> GPU ->
+    # checksums in host memory), every rank at once on its own GPU and PCIe
+    # link; the node-level rate is all ranks' bytes / the slowest rank's time.
+    # Beside it, the link's ceiling: a plain pinned H2D copy of the same bytes.
     host = h2d = None
-    if rank == 0 and world == 1 and not args.no_host and args.config != "c4":
+    if not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
         hp = pinned.numpy()
         hout = np.zeros(max(nout, 1), np.uint32)  # caller-owned output, as hadooprpc.c's packet buffer
         ctx.batch_host(hp, pk, out=hout)  # warm (allocates staging)
-        h0 = time.perf_counter()
         reps = 5
+
+        def slowest(dt):
+            if world > 1:
+                t = torch.tensor([dt], dtype=torch.float64, device=cdev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dt = float(t[0])
+            return dt
+
+        if world > 1:
+            dist.barrier()
+        h0 = time.perf_counter()
         for _ in range(reps):
             ctx.batch_host(hp, pk, out=hout)
-        host = round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2)
-        # the PCIe ceiling of that path: a plain pinned H2D copy of the same bytes
+        host = round(world * nbytes * reps / slowest(time.perf_counter() - h0) / GIB, 2)
+        if not np.array_equal(hout[:nout], want):
+            bit_exact = False
         dst = torch.empty(pinned.numel(), dtype=torch.uint8, device=dev)
         dst.copy_(pinned, non_blocking=True)
         torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
         h0 = time.perf_counter()
         for _ in range(reps):
             dst.copy_(pinned, non_blocking=True)
         torch.cuda.synchronize()
-        h2d = round(pinned.numel() * reps / (time.perf_counter() - h0) / GIB, 2)
+        h2d = round(world * pinned.numel() * reps / slowest(time.perf_counter() - h0) / GIB, 2)
         del dst
 
     if rank == 0:
@@ -373,6 +390,7 @@ def main():
             "bit_exact_vs_reference": bit_exact,
             "host_resident_gib_s": host,
             "host_h2d_copy_gib_s": h2d,
+            "host_resident_ranks": world if host is not None else None,
             "verify": verify,
             "two_streams": two_streams,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
