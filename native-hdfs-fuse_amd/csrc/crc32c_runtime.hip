@@ -55,7 +55,10 @@ struct DeviceGuard {
     }
 };
 
-constexpr size_t kSliceBytes = 64ull << 20;  // host pipeline slice (whole packets), default
+constexpr size_t kSliceBytes = 64ull << 20;
+// Scattered packets from pinned memory are copied run by run when the runs
+// average at least this much (each copy costs ~15 us on the copy engine).
+constexpr uint64_t kMinRunBytes = 1ull << 20;  // host pipeline slice (whole packets), default
 
 // Host pipeline slice size: kSliceBytes, or $HDFS_CRC32C_SLICE_MB (A/B only).
 size_t slice_bytes() {
@@ -307,6 +310,9 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
     size_t i = 0;
     int which = 0;
     std::vector<crc32c_packet> local;
+    std::vector<std::pair<uint64_t, uint64_t>> runs;  // [begin, end) payload ranges copied one by one
+    std::vector<uint32_t> run_of;                     // run of each packet of the slice
+    std::vector<uint64_t> run_dst;                    // device offset of each run
     HostPlan plan;
     while (i < npkts) {
         // Slice = consecutive packets totalling about slice_bytes().
@@ -326,23 +332,63 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         if (lo == UINT64_MAX) lo = hi = 0;
         lo &= ~uint64_t(15);  // keep every packet's 16-byte phase (fast-path alignment)
         // Contiguous-enough slices move as one range (direct from pinned
-        // memory, else through the pinned staging buffer); scattered
-        // packets are gathered packet by packet into the staging buffer.
+        // memory, else through the pinned staging buffer).  Scattered
+        // packets from pinned memory move as one copy per contiguous run when
+        // the runs are long (an HDFS block per run, e.g. crc32c_multi's
+        // round-robin shards); otherwise they are gathered packet by packet
+        // into the staging buffer by the CPU.
         const bool ranged = (hi - lo) <= bytes + bytes / 4 + 4096;
-        const size_t stage_bytes = ranged ? size_t(hi - lo) : size_t(bytes + 16 * (j - i));
+        runs.clear();
+        run_of.assign(j - i, 0);
+        if (!ranged && pinned) {
+            for (size_t k = i; k < j; ++k) {
+                if (!pkts[k].len) continue;
+                const uint64_t b0 = pkts[k].payload_off, b1 = b0 + pkts[k].len;
+                if (!runs.empty() && b0 >= runs.back().second && b0 <= runs.back().second + 4096)
+                    runs.back().second = b1;
+                else
+                    runs.emplace_back(b0, b1);
+                run_of[k - i] = uint32_t(runs.size() - 1);
+            }
+            if (runs.empty() || bytes / runs.size() < kMinRunBytes) runs.clear();
+        }
+        const bool by_runs = !runs.empty();
+        size_t stage_bytes = ranged ? size_t(hi - lo) : size_t(bytes + 16 * (j - i));
+        if (by_runs) {
+            stage_bytes = 0;
+            for (const auto &r : runs) stage_bytes += size_t(r.second - (r.first & ~uint64_t(15))) + 16;
+        }
         rc = grow_pinned_pair(&s.h_payload, &s.d_payload, &s.payload_cap, stage_bytes + 16);
         if (rc) return rc;
         // 1. The payload copy goes first: it needs no plan, and the copy
         //    stream runs the slices' copies back to back.  (This stage's
         //    previous kernel is done: drain_stage waited for it.)
         local.assign(pkts + i, pkts + j);
-        const uint8_t *src = s.h_payload;
         if (ranged) {
             for (crc32c_packet &pk : local) pk.payload_off -= lo;
+            const uint8_t *src = s.h_payload;
             if (pinned)
                 src = payload + lo;
             else
                 std::memcpy(s.h_payload, payload + lo, size_t(hi - lo));
+            HIP_TRY(hipMemcpyAsync(s.d_payload, src, stage_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+        } else if (by_runs) {
+            // run r (from a0 = its start rounded down to 16) lands at
+            // run_dst[r], keeping its 16-byte phase (fast-path alignment)
+            run_dst.resize(runs.size());
+            uint64_t dst = 0;
+            for (size_t r = 0; r < runs.size(); ++r) {
+                const uint64_t a0 = runs[r].first & ~uint64_t(15);
+                HIP_TRY(hipMemcpyAsync(s.d_payload + dst, payload + a0, size_t(runs[r].second - a0),
+                                       hipMemcpyHostToDevice, ctx->copy_stream));
+                run_dst[r] = dst;
+                dst += (runs[r].second - a0 + 15) & ~uint64_t(15);
+            }
+            for (size_t k = 0; k < local.size(); ++k) {
+                crc32c_packet &pk = local[k];
+                const uint32_t r = run_of[k];
+                pk.payload_off = pk.len ? run_dst[r] + (pk.payload_off - (runs[r].first & ~uint64_t(15))) : 0;
+            }
         } else {
             uint64_t gather_off = 0;
             for (crc32c_packet &pk : local) {
@@ -350,8 +396,8 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
                 pk.payload_off = gather_off;
                 gather_off = (gather_off + pk.len + 15) & ~uint64_t(15);
             }
+            HIP_TRY(hipMemcpyAsync(s.d_payload, s.h_payload, stage_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
         }
-        HIP_TRY(hipMemcpyAsync(s.d_payload, src, stage_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
         HIP_TRY(hipEventRecord(s.copied, ctx->copy_stream));
         // 2. Plan and descriptors while the copy runs.
         uint64_t nout = 0;

@@ -175,6 +175,38 @@ def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
     assert np.array_equal(gpu_ctx.batch_host(payload, pk2), want2)
 
 
+def test_host_path_pinned_runs(hdfs, gpu_ctx, orc):
+    """Scattered packets from pinned memory in long contiguous runs go H2D one
+    copy per run (crc32c_batch_host): 4 MiB blocks taken in a shuffled
+    order (runs going backwards in memory), one block starting 5 bytes off
+    16-byte alignment (general path), ragged and mixed-bpc packets, empty
+    packets between runs, a 100-byte gap merged into its run; the same
+    batch from pageable memory (CPU gather) must give the same checksums."""
+    torch = _torch()
+    nblk = 40  # 160 MiB: 3 slices of 64 MiB
+    payload = oracle.xorshift64_bytes(nblk * (4 << 20) + 4096, 77)
+    pinned = torch.from_numpy(payload).pin_memory()
+    rng = np.random.default_rng(5)
+    order = rng.permutation(nblk)
+    rows, out = [], 0
+    for j, b in enumerate(order):
+        base = int(b) * (4 << 20) + (5 if j == 3 else 0)
+        for p in range(64):
+            ln = 65536 - (100 if p == 63 else 0)
+            bpc = (512, 1024, 4096)[(j + p) % 3] if j % 4 == 1 else 512
+            off = base + p * 65536 + (100 if (j == 7 and p == 10) else 0)
+            if j == 7 and p >= 10:
+                ln = min(ln, base + 64 * 65536 - off)
+            rows.append((off, out, ln, bpc))
+            out += (ln + bpc - 1) // bpc
+        rows.append((0, out, 0, 512))  # an empty packet between runs
+    pk = np.array(rows, hdfs.PACKET_DTYPE)
+    want = orc.batch(payload, pk, oracle.total_checksums(pk))
+    got = gpu_ctx.batch_host(pinned.numpy(), pk)
+    assert np.array_equal(got, want)
+    assert np.array_equal(gpu_ctx.batch_host(payload, pk), want)
+
+
 def test_chunks_default_context(hdfs, orc):
     pkt = oracle.xorshift64_bytes(65536, 99)
     assert np.array_equal(hdfs.chunks(pkt, 512), orc.chunks(pkt, 512))

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--packets", default="1024,4096,16384")
+    ap.add_argument("--shuffle-blocks", action="store_true",
+                    help="packets in 4 MiB blocks taken in a shuffled order (scattered pinned runs)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -42,8 +44,16 @@ def main():
     hp = pinned.numpy()
     dst = torch.empty(big, dtype=torch.uint8, device=dev)
     res = {}
-    for n in sizes:  # warm: staging buffers, plans
+    def packets(n):
         pk = oracle.uniform_packets(n)
+        if args.shuffle_blocks and n >= 64:
+            perm = np.random.default_rng(n).permutation(n // 64)
+            pk = pk.reshape(-1, 64)[perm].reshape(-1).copy()
+            pk["out_idx"] = np.arange(n, dtype=np.uint64) * 128
+        return pk
+
+    for n in sizes:  # warm: staging buffers, plans
+        pk = packets(n)
         out = np.zeros(hdfs.total_checksums(pk), np.uint32)
         ctx.batch_host(hp, pk, out=out)
         dst[: n * 65536].copy_(pinned[: n * 65536], non_blocking=True)
@@ -51,7 +61,7 @@ def main():
     for _ in range(args.rounds):
         for n in sizes:
             nb = n * 65536
-            pk = oracle.uniform_packets(n)
+            pk = packets(n)
             out = np.zeros(hdfs.total_checksums(pk), np.uint32)
             t0 = time.perf_counter()
             for _ in range(args.reps):
@@ -71,7 +81,8 @@ def main():
         r["copy_gib_s"] = round(nb / (r["copy_ms"] * 1e-3) / GIB, 2)
         r["host_ms"] = round(r["host_ms"], 3)
         r["copy_ms"] = round(r["copy_ms"], 3)
-    print(json.dumps({"slice_mb": os.environ.get("HDFS_CRC32C_SLICE_MB", "default"), "sizes": res}))
+    print(json.dumps({"slice_mb": os.environ.get("HDFS_CRC32C_SLICE_MB", "default"),
+                      "shuffled_blocks": args.shuffle_blocks, "sizes": res}))
     ctx.close()
 
 
