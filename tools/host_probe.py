@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--packets", default="1024,4096,16384")
+    ap.add_argument("--pageable", action="store_true", help="batch_host from pageable memory (CPU staging copy)")
     ap.add_argument("--shuffle-blocks", action="store_true",
                     help="packets in 4 MiB blocks taken in a shuffled order (scattered pinned runs)")
     args = ap.parse_args()
@@ -41,7 +42,7 @@ def main():
     big = max(sizes) * 65536
     pinned = torch.empty(big, dtype=torch.uint8).pin_memory()
     pinned.numpy()[:] = np.frombuffer(oracle.xorshift64_bytes(big, 11), np.uint8)
-    hp = pinned.numpy()
+    hp = pinned.numpy().copy() if args.pageable else pinned.numpy()
     dst = torch.empty(big, dtype=torch.uint8, device=dev)
     res = {}
     def packets(n):
@@ -82,7 +83,7 @@ def main():
         r["host_ms"] = round(r["host_ms"], 3)
         r["copy_ms"] = round(r["copy_ms"], 3)
     print(json.dumps({"slice_mb": os.environ.get("HDFS_CRC32C_SLICE_MB", "default"),
-                      "shuffled_blocks": args.shuffle_blocks, "sizes": res}))
+                      "shuffled_blocks": args.shuffle_blocks, "pageable": args.pageable, "sizes": res}))
     ctx.close()
 
 
