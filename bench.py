@@ -144,6 +144,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--two-streams", action="store_true",
+                    help="also time 1000 batches alternated over two streams (their launches overlap, so a "
+                         "rocprofv3 run of the bench would average overlapped durations: off by default)")
     args = ap.parse_args()
 
     import torch
@@ -294,11 +297,11 @@ def main():
                   "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
                   "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF)}
 
-    # Independent batches on two streams (rank 0, beside the main line, which
-    # stays one stream so that one step = one launch): the next launch's
-    # workgroups start on the CUs the previous one has released.
+    # Independent batches on two streams (opt-in, rank 0, beside the main
+    # line, which stays one stream so that one step = one launch): the next
+    # launch's workgroups start on the CUs the previous one has released.
     two_streams = None
-    if rank == 0 and world == 1 and nbuf > 1:
+    if args.two_streams and rank == 0 and world == 1 and nbuf > 1:
         ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
 
         def two(n):
