@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -55,10 +56,13 @@ struct DeviceGuard {
     }
 };
 
-constexpr size_t kSliceBytes = 64ull << 20;
+constexpr size_t kSliceBytes = 64ull << 20;  // host pipeline slice (whole packets), default
 // Scattered packets from pinned memory are copied run by run when the runs
 // average at least this much (each copy costs ~15 us on the copy engine).
-constexpr uint64_t kMinRunBytes = 1ull << 20;  // host pipeline slice (whole packets), default
+constexpr uint64_t kMinRunBytes = 1ull << 20;
+// The first slice of a pageable batch is staged and copied in pieces of this
+// size, so that the copy engine starts after one piece instead of a slice.
+constexpr size_t kFirstPieceBytes = 8ull << 20;
 
 // Host pipeline slice size: kSliceBytes, or $HDFS_CRC32C_SLICE_MB (A/B only).
 size_t slice_bytes() {
@@ -109,6 +113,46 @@ void copy_range(uint8_t *dst, const uint8_t *src, size_t n) {
         const size_t lo = b * 64, hi = std::min(n, e * 64);
         if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
     });
+}
+
+// Staging copy of a large range in pieces: copy_threads() threads each copy
+// their share of piece 0, 1, ... in turn; when every share of piece p is in,
+// the calling thread (also a copier) hands the piece to ready(offset, size),
+// which queues its H2D copy.  Threads are started once per call.
+template <class R>
+void copy_range_pipelined(uint8_t *dst, const uint8_t *src, size_t n, size_t piece, R ready) {
+    const unsigned t = n < (8u << 20) ? 1u : copy_threads();
+    const size_t npieces = (n + piece - 1) / piece;
+    std::vector<std::atomic<unsigned>> done(npieces);
+    for (auto &d : done) d.store(0, std::memory_order_relaxed);
+    auto work = [&](unsigned k) {
+        for (size_t p = 0; p < npieces; ++p) {
+            const size_t b = p * piece, e = std::min(n, b + piece);
+            const size_t lines = (e - b + 63) / 64;
+            const size_t lo = b + lines * k / t * 64, hi = std::min(e, b + lines * (k + 1) / t * 64);
+            if (hi > lo) std::memcpy(dst + lo, src + lo, hi - lo);
+            done[p].fetch_add(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    th.reserve(t - 1);
+    for (unsigned k = 1; k < t; ++k) th.emplace_back(work, k);
+    // the calling thread: its own share, then publish pieces as they complete
+    size_t next = 0;
+    for (size_t p = 0; p < npieces; ++p) {
+        const size_t b = p * piece, e = std::min(n, b + piece);
+        const size_t lines = (e - b + 63) / 64;
+        const size_t hi = std::min(e, b + lines / t * 64);
+        if (hi > b) std::memcpy(dst + b, src + b, hi - b);
+        done[p].fetch_add(1, std::memory_order_release);
+        for (; next <= p && done[next].load(std::memory_order_acquire) == t; ++next)
+            ready(next * piece, std::min(n, next * piece + piece) - next * piece);
+    }
+    for (; next < npieces; ++next) {
+        while (done[next].load(std::memory_order_acquire) != t) std::this_thread::yield();
+        ready(next * piece, std::min(n, next * piece + piece) - next * piece);
+    }
+    for (auto &x : th) x.join();
 }
 
 // The two device scheduler slots (kernel_abi.h) of one launch sequence that
@@ -408,12 +452,25 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         local.assign(pkts + i, pkts + j);
         if (ranged) {
             for (crc32c_packet &pk : local) pk.payload_off -= lo;
-            const uint8_t *src = s.h_payload;
-            if (pinned)
-                src = payload + lo;
-            else
-                copy_range(s.h_payload, payload + lo, size_t(hi - lo));
-            HIP_TRY(hipMemcpyAsync(s.d_payload, src, stage_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+            if (pinned) {
+                HIP_TRY(hipMemcpyAsync(s.d_payload, payload + lo, stage_bytes, hipMemcpyHostToDevice,
+                                       ctx->copy_stream));
+            } else if (i == 0) {
+                // nothing to overlap the first slice's staging with: copy it
+                // H2D piece by piece as the pieces are staged
+                hipError_t err = hipSuccess;
+                copy_range_pipelined(s.h_payload, payload + lo, stage_bytes, kFirstPieceBytes,
+                                     [&](size_t o, size_t n) {
+                                         if (err == hipSuccess)
+                                             err = hipMemcpyAsync(s.d_payload + o, s.h_payload + o, n,
+                                                                  hipMemcpyHostToDevice, ctx->copy_stream);
+                                     });
+                HIP_TRY(err);
+            } else {
+                copy_range(s.h_payload, payload + lo, stage_bytes);
+                HIP_TRY(hipMemcpyAsync(s.d_payload, s.h_payload, stage_bytes, hipMemcpyHostToDevice,
+                                       ctx->copy_stream));
+            }
         } else if (by_runs) {
             // run r (from a0 = its start rounded down to 16) lands at
             // run_dst[r], keeping its 16-byte phase (fast-path alignment)
