@@ -144,6 +144,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak (default): every rank checksums its own config batch; strong: the config-2/5 batch's "
+                         "packets are split evenly over the ranks (SURVEY.md section 8e)")
     ap.add_argument("--two-streams", action="store_true",
                     help="also time 1000 batches alternated over two streams (their launches overlap, so a "
                          "rocprofv3 run of the bench would average overlapped durations: off by default)")
@@ -184,6 +187,14 @@ def main():
         nbuf = 1
     else:
         pk, workload = config_packets(args.config, oracle)
+        if args.scaling == "strong" and world > 1:
+            if args.config not in ("c2", "c5") or pk.size % world:
+                raise SystemExit("--scaling strong needs config c2/c5 and a rank count dividing %d" % pk.size)
+            per = pk.size // world
+            pk = pk[rank * per:(rank + 1) * per].copy()  # this rank's packets, rebased
+            pk["payload_off"] -= pk["payload_off"][0]
+            pk["out_idx"] -= pk["out_idx"][0]
+            workload += ", strong scaling: packets split over %d ranks" % world
         nbuf = args.nbuf if args.config != "c3" else 1
     nbytes = int(pk["len"].astype(np.int64).sum())
     extent = int((pk["payload_off"] + pk["len"]).max())
@@ -377,7 +388,8 @@ def main():
             "metric": baseline_metric(),
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "higher_is_better": True, "scaling": "strong" if args.config == "c4" or (args.scaling == "strong" and world > 1) else "weak",
+            "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (xorshift64 stream + device random bytes, %d rotating %d MiB buffers per rank)"
                     % (nbuf, extent >> 20),
             "config": {"workload": workload, "config": args.config, "packets_per_rank": int(pk.size),
