@@ -52,22 +52,15 @@ def load_package():
     return mod
 
 
-def config_packets(name: str, oracle_mod):
-    """Packet descriptors of one rank's batch, per BASELINE.json configs."""
-    if name == "c2":  # 4096 x 64 KiB, bpc 512
-        return oracle_mod.uniform_packets(4096), "4096 x 64KiB packets, 512B chunks (BASELINE config 2)"
-    if name == "c3":  # one 4 MiB block
-        return oracle_mod.uniform_packets(64), "one 4MiB block as 64 x 64KiB packets, 512B chunks (config 3)"
-    if name == "c4":  # 128 MiB file = 32 blocks round-robin over the ranks
-        return None, "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
-    if name == "c5":
-        return oracle_mod.mixed_packets(4096), "4096 x 64KiB packets, bpc cycling 512/1024/4096 (config 5)"
-    raise SystemExit("unknown config " + name)
-
-
-def reference_checksums(oracle_mod, payload: np.ndarray, pk, nout: int) -> np.ndarray:
+# ---- the CPU reference leg: the only place bench.py touches oracle/ --------
+# The reference's own crc32c.c (oracle/_ref) is the checker of the GPU
+# results (outside the timed region) and the timed CPU baseline; nothing it
+# computes is measured as or passed off for the product's output.
+def reference_checksums(payload: np.ndarray, pk, nout: int) -> np.ndarray:
     """Expected checksums from the reference's crc32c.c (oracle/_ref) when it
     is built, else the clean-room oracle; multi-threaded over packets."""
+    import oracle as oracle_mod
+
     impl = oracle_mod.Reference() if oracle_mod.Reference.available() else oracle_mod.Oracle()
     out = np.zeros(max(nout, 1), np.uint32)
     impl.batch_mt_seconds(payload, pk, out, max(1, min(16, os.cpu_count() or 1)), 1)
@@ -96,11 +89,13 @@ def latest_pmc(profile_dir: str):
         return None
 
 
-def cpu_baseline(oracle_mod, pk, payload_np: np.ndarray, seconds: float):
+def cpu_baseline(pk, payload_np: np.ndarray, seconds: float):
     """The reference's own crc32c.c (oracle/_ref, kind "reference") or the
     clean-room oracle (kind "port"), per chunk as hadooprpc.c:739-742, on
     the host cores of this box: bounded sample = the same batch, repeated
     until `seconds` of wall time per thread count."""
+    import oracle as oracle_mod
+
     try:
         impl = oracle_mod.Reference()
         kind = "reference"
@@ -171,22 +166,21 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    import oracle
-
     hdfs = load_package()
     hdfs.lib()
 
     from hdfs_crc32c_amd import shard
+    from hdfs_crc32c_amd.workloads import config_packets, synthetic_bytes, uniform_packets
 
     c4_blocks = None
     if args.config == "c4":
         # 128 MiB file = 32 x 4 MiB blocks, block b on rank b mod world
         c4_blocks = shard.rank_blocks(32, world, rank)
-        pk = oracle.uniform_packets(64 * len(c4_blocks))
+        pk = uniform_packets(64 * len(c4_blocks))
         workload = "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
         nbuf = 1
     else:
-        pk, workload = config_packets(args.config, oracle)
+        pk, workload = config_packets(args.config)
         if args.scaling == "strong" and world > 1:
             if args.config not in ("c2", "c5") or pk.size % world:
                 raise SystemExit("--scaling strong needs config c2/c5 and a rank count dividing %d" % pk.size)
@@ -203,13 +197,13 @@ def main():
     ctx = hdfs.Context(local_rank)
     plan = ctx.plan(pk)
     dev = torch.device("cuda", local_rank)
-    # buffer 0: the documented xorshift64 stream (checked against the CPU
+    # buffer 0: PCG64 host bytes (checked against the CPU
     # path below); the rest: device-generated random bytes.
     if c4_blocks is not None:
-        file_bytes = oracle.xorshift64_bytes(32 * shard.BLOCK_BYTES, oracle.SEED)
+        file_bytes = synthetic_bytes(32 * shard.BLOCK_BYTES, 2024)
         payload0 = shard.rank_payload(file_bytes, c4_blocks)
     else:
-        payload0 = oracle.xorshift64_bytes(extent, oracle.SEED + rank)
+        payload0 = synthetic_bytes(extent, 2024 + rank)
     bufs = [torch.from_numpy(payload0).to(dev)]
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -226,7 +220,7 @@ def main():
     # correctness gate (outside the timed region): every buffer-0 checksum
     step(0)
     torch.cuda.synchronize()
-    want = reference_checksums(oracle, payload0, pk, nout)
+    want = reference_checksums(payload0, pk, nout)
     got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
     bit_exact = bool(np.array_equal(got0, want))
 
@@ -279,8 +273,8 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3 if world > 1 else None
         if c4_blocks is not None and rank == 0:
-            whole = oracle.uniform_packets(64 * 32)
-            bit_exact = bit_exact and bool(np.array_equal(full, reference_checksums(oracle, file_bytes, whole,
+            whole = uniform_packets(64 * 32)
+            bit_exact = bit_exact and bool(np.array_equal(full, reference_checksums(file_bytes, whole,
                                                                                      64 * 32 * 128)))
 
     total_bytes = nbytes * world * args.steps
@@ -383,14 +377,14 @@ def main():
                 and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
         # the CPU baseline is an N = 1 figure (timed on rank 0's host cores)
-        cpu = None if args.no_cpu or world > 1 else cpu_baseline(oracle, pk, payload0, args.cpu_seconds)
+        cpu = None if args.no_cpu or world > 1 else cpu_baseline(pk, payload0, args.cpu_seconds)
         line = {
             "metric": baseline_metric(),
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "higher_is_better": True, "scaling": "strong" if args.config == "c4" or (args.scaling == "strong" and world > 1) else "weak",
             "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (xorshift64 stream + device random bytes, %d rotating %d MiB buffers per rank)"
+            "data": "synthetic (PCG64 host bytes + device random bytes, %d rotating %d MiB buffers per rank)"
                     % (nbuf, extent >> 20),
             "config": {"workload": workload, "config": args.config, "packets_per_rank": int(pk.size),
                        "packet_bytes": int(pk["len"][0]), "bytes_per_checksum": sorted(set(int(x) for x in pk["bpc"])),

@@ -65,6 +65,15 @@ typedef struct crc32c_packet {
     uint32_t bpc;
 } crc32c_packet;
 
+/* The reference's per-packet loop (hadooprpc.c:733-742) on the host CPU, in
+ * one call: out[i] = crc32c(0, packet + i*bpc, min(bpc, len - i*bpc)) for the
+ * ceil(len / bpc) chunks, htonl'd with CRC32C_BIG_ENDIAN (hadooprpc.c:71-75);
+ * CRC32C_TYPE_CRC32 selects Hadoop's CHECKSUM_CRC32.  Whole chunks run as
+ * three interleaved crc32q chains.  0, or -EINVAL (bpc == 0, unknown flags,
+ * NULL buffers).  This is the per-packet replacement; batches of packets go
+ * to the GPU (sections 3-4). */
+int crc32c_chunks_cpu(const void *packet, size_t len, uint32_t bpc, uint32_t *out, uint32_t flags);
+
 /* Number of checksums of one packet: roundup(len, bpc) (hadooprpc.c:639). */
 uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc);
 

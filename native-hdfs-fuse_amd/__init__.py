@@ -80,6 +80,7 @@ def _bind(L):
         "crc32c_nchunks": (u64, [u64, u32]),
         "crc32c_packetize": (u64, [u64, u64, u32, u32, vp, u64]),
         "crc32c_batch_nchecksums": (u64, [vp, sz]),
+        "crc32c_chunks_cpu": (i32, [vp, sz, u32, vp, u32]),
         "crc32c_device_count": (i32, []),
         "crc32c_ctx_create": (i32, [i32, pp]),
         "crc32c_ctx_destroy": (i32, [vp]),
@@ -306,6 +307,15 @@ class Multi:
             self.close()
         except Exception:
             pass
+
+
+def chunks_cpu(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:
+    """The reference's per-packet loop on one host packet, on the host CPU."""
+    packet = np.ascontiguousarray(packet, dtype=np.uint8)
+    n = nchunks(packet.size, bpc)
+    out = np.zeros(max(n, 1), np.uint32)
+    _check(lib().crc32c_chunks_cpu(_np_ptr(packet), packet.size, bpc, _np_ptr(out), flags), "crc32c_chunks_cpu")
+    return out[:n]
 
 
 def chunks(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:

@@ -15,6 +15,8 @@
 //    chunk is three 168-byte chains + 8 bytes, about half the latency of one
 //    64-step chain (the reference's path for 512 B, crc32c.c:293-299).
 //  * portable slicing-by-8 tables (crc32c.c:78-107's fallback role).
+#include <algorithm>
+#include <cerrno>
 #include <cstring>
 #include <mutex>
 
@@ -89,6 +91,36 @@ __attribute__((target("sse4.2"))) inline uint64_t three_stripes(uint64_t r, cons
     return stripe_shift(SI, stripe_shift(SI, uint32_t(a)) ^ uint32_t(b)) ^ uint32_t(c);
 }
 
+// Software prefetch distance of three_chunks, in groups of three chunks
+// beyond the next one.
+constexpr size_t kPrefetchGroups = 1;
+
+// Three whole chunks of `bpc` bytes (a multiple of 8) at p, p + bpc, p + 2 bpc,
+// each from crc = 0: three independent crc32q chains interleaved, so the
+// instruction's 3-cycle latency is hidden without any merge step (the
+// reference runs one dependent chain per 512-byte chunk, crc32c.c:293-299).
+__attribute__((target("sse4.2"))) void three_chunks(const uint8_t *p, size_t bpc, uint32_t out[3]) {
+    uint64_t a = 0xffffffffu, b = 0xffffffffu, c = 0xffffffffu;
+    const uint8_t *next = p + 3 * bpc + 3 * kPrefetchGroups * bpc;
+    for (size_t i = 0; i < bpc; i += 8) {
+        if ((i & 63) == 0) {  // the hardware prefetchers miss three interleaved streams
+            __builtin_prefetch(next + i);
+            __builtin_prefetch(next + bpc + i);
+            __builtin_prefetch(next + 2 * bpc + i);
+        }
+        uint64_t wa, wb, wc;
+        std::memcpy(&wa, p + i, 8);
+        std::memcpy(&wb, p + bpc + i, 8);
+        std::memcpy(&wc, p + 2 * bpc + i, 8);
+        a = __builtin_ia32_crc32di(a, wa);
+        b = __builtin_ia32_crc32di(b, wb);
+        c = __builtin_ia32_crc32di(c, wc);
+    }
+    out[0] = ~uint32_t(a);
+    out[1] = ~uint32_t(b);
+    out[2] = ~uint32_t(c);
+}
+
 __attribute__((target("sse4.2"))) uint32_t reg_update_hw(uint32_t r32, const uint8_t *p, size_t n) {
     uint64_t r = r32;
     for (; n && (reinterpret_cast<uintptr_t>(p) & 7u); --n) r = __builtin_ia32_crc32qi(uint32_t(r), *p++);
@@ -149,6 +181,29 @@ extern "C" uint32_t hdfs_crc32(uint32_t crc, const void *buf, size_t len) {
     }
     for (; n; --n) r = (r >> 8) ^ g_ieee[0][(r ^ *p++) & 0xffu];
     return ~r;
+}
+
+extern "C" int crc32c_chunks_cpu(const void *packet, size_t len, uint32_t bpc, uint32_t *out, uint32_t flags) {
+    // hadooprpc.c:733-742 on the host: chunk i = crc32c(0, packet + i*bpc,
+    // min(bpc, len - i*bpc)), htonl'd with CRC32C_BIG_ENDIAN (71-75).
+    if (bpc == 0 || (flags & ~uint32_t(CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32))) return -EINVAL;
+    if (len && (!packet || !out)) return -EINVAL;
+    const uint8_t *p = static_cast<const uint8_t *>(packet);
+    const size_t n = (len + bpc - 1) / bpc;
+    size_t i = 0;
+    if (flags & CRC32C_TYPE_CRC32) {
+        for (; i < n; ++i) out[i] = hdfs_crc32(0, p + i * bpc, std::min<size_t>(bpc, len - i * bpc));
+    } else {
+        std::call_once(g_once, init_once);
+#if defined(__x86_64__)
+        if (g_have_sse42 && bpc % 8 == 0)
+            for (; i + 3 <= len / bpc; i += 3) three_chunks(p + i * bpc, bpc, out + i);
+#endif
+        for (; i < n; ++i) out[i] = crc32c(0, p + i * bpc, std::min<size_t>(bpc, len - i * bpc));
+    }
+    if (flags & CRC32C_BIG_ENDIAN)
+        for (size_t k = 0; k < n; ++k) out[k] = __builtin_bswap32(out[k]);
+    return 0;
 }
 
 extern "C" uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc) {

@@ -81,6 +81,35 @@ def test_nchunks_and_packetize(hdfs, orc):
         assert hdfs.packetize(*args) == orc.packetize(*args), args
 
 
+def test_chunks_cpu_matches_reference_loop(hdfs, orc, golden):
+    """crc32c_chunks_cpu (the per-packet loop of hadooprpc.c:733-742 on the
+    host, whole chunks as 3 interleaved crc32q chains): every golden packet
+    vector, random packets of every bpc shape against the oracle, wire
+    order, CHECKSUM_CRC32 against zlib, and argument errors."""
+    import zlib
+
+    for c in golden["packets"]["cases"]:
+        buf = golden_fill(c["kind"], c["len"] + c["skip"], c["seed"])[c["skip"]:]
+        got = hdfs.chunks_cpu(np.ascontiguousarray(buf), c["bpc"])
+        assert ["%08x" % v for v in got] == c["crcs"], (c["bpc"], c["kind"], c["len"])
+    rng = np.random.default_rng(23)
+    data = oracle.xorshift64_bytes(300_000, 23)
+    for _ in range(60):
+        bpc = int(rng.choice([512, 1024, 4096, 8, 24, 100, 1536, 7, 65536]))
+        off, n = int(rng.integers(0, 64)), int(rng.integers(0, 200_000))
+        pkt = np.ascontiguousarray(data[off:off + n])
+        want = orc.chunks(pkt, bpc)
+        assert np.array_equal(hdfs.chunks_cpu(pkt, bpc), want), (bpc, off, n)
+        assert np.array_equal(hdfs.chunks_cpu(pkt, bpc, hdfs.CRC32C_BIG_ENDIAN), want.byteswap())
+        ieee = [zlib.crc32(pkt[i:i + bpc].tobytes()) for i in range(0, n, bpc)]
+        assert hdfs.chunks_cpu(pkt, bpc, hdfs.CRC32C_TYPE_CRC32).tolist() == ieee
+    L = hdfs.lib()
+    out = np.zeros(4, np.uint32)
+    assert L.crc32c_chunks_cpu(data.ctypes.data, 100, 0, out.ctypes.data, 0) == -22
+    assert L.crc32c_chunks_cpu(data.ctypes.data, 100, 512, out.ctypes.data, 0x80) == -22
+    assert L.crc32c_chunks_cpu(None, 0, 512, None, 0) == 0
+
+
 def test_batch_nchecksums(hdfs):
     """crc32c_batch_nchecksums (the checksum array length of a batch): the
     oracle's count on full batches; with empty packets (which own no
@@ -247,3 +276,21 @@ def test_crc32_tables_match_zlib(hdfs, lg):
         import zlib
         assert int(c_small[r]) == zlib.crc32(bytes(r))
     assert img.size > 0
+
+
+def test_workloads_match_oracle_shapes(hdfs):
+    """The bench's synthetic batches (native-hdfs-fuse_amd/workloads.py) have
+    the same packet layout as the oracle's helpers the fixtures were made
+    with."""
+    from hdfs_crc32c_amd import workloads
+
+    for n in (1, 64, 4096):
+        assert np.array_equal(workloads.uniform_packets(n), oracle.uniform_packets(n))
+        assert np.array_equal(workloads.mixed_packets(n), oracle.mixed_packets(n))
+    assert np.array_equal(workloads.uniform_packets(9, pkt_len=65436, stride=65536),
+                          oracle.uniform_packets(9, pkt_len=65436, stride=65536))
+    for name in ("c2", "c3", "c5", "p17"):
+        pk, text = workloads.config_packets(name)
+        assert pk.dtype == hdfs.PACKET_DTYPE and text
+    a, b = workloads.synthetic_bytes(1000, 3), workloads.synthetic_bytes(1000, 3)
+    assert a.dtype == np.uint8 and np.array_equal(a, b)

@@ -26,12 +26,13 @@ def main():
     args = ap.parse_args()
     import torch
 
-    import oracle
-    from bench import config_packets, load_package
+    from bench import load_package
 
     os.environ["HDFS_CRC32C_KVARIANT"] = args.variant
     hdfs = load_package()
-    pk, _ = config_packets("c2", oracle)
+    from hdfs_crc32c_amd.workloads import config_packets, synthetic_bytes
+
+    pk, _ = config_packets("c2")
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)
     dev = torch.device("cuda", 0)
@@ -46,7 +47,7 @@ def main():
         g = torch.Generator(device=dev)
         g.manual_seed(1234)
         if buf0_host:
-            bufs = [torch.from_numpy(oracle.xorshift64_bytes(extent, oracle.SEED)).to(dev)]
+            bufs = [torch.from_numpy(synthetic_bytes(extent, 1)).to(dev)]
         else:
             bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g)]
         for _ in range(3):

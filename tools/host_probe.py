@@ -32,21 +32,22 @@ def main():
     import numpy as np
     import torch
 
-    import oracle
     from bench import load_package
 
     hdfs = load_package()
+    from hdfs_crc32c_amd.workloads import synthetic_bytes, uniform_packets
+
     ctx = hdfs.Context(0)
     dev = torch.device("cuda", 0)
     sizes = [int(x) for x in args.packets.split(",")]
     big = max(sizes) * 65536
     pinned = torch.empty(big, dtype=torch.uint8).pin_memory()
-    pinned.numpy()[:] = np.frombuffer(oracle.xorshift64_bytes(big, 11), np.uint8)
+    pinned.numpy()[:] = synthetic_bytes(big, 11)
     hp = pinned.numpy().copy() if args.pageable else pinned.numpy()
     dst = torch.empty(big, dtype=torch.uint8, device=dev)
     res = {}
     def packets(n):
-        pk = oracle.uniform_packets(n)
+        pk = uniform_packets(n)
         if args.shuffle_blocks and n >= 64:
             perm = np.random.default_rng(n).permutation(n // 64)
             pk = pk.reshape(-1, 64)[perm].reshape(-1).copy()

@@ -30,15 +30,12 @@ def main():
     import numpy as np
     import torch
 
-    import oracle
-    from bench import config_packets, load_package
+    from bench import load_package
 
     hdfs = load_package()
-    if args.config.startswith("p"):  # pN: N uniform 64 KiB packets, 512 B chunks
-        n = int(args.config[1:])
-        pk, workload = oracle.uniform_packets(n), "%d x 64KiB packets, 512B chunks" % n
-    else:
-        pk, workload = config_packets(args.config, oracle)
+    from hdfs_crc32c_amd.workloads import config_packets
+
+    pk, workload = config_packets(args.config)  # c2 / c3 / c5, or pN: N uniform 64 KiB packets
     nbytes = int(pk["len"].astype(np.int64).sum())
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)

@@ -31,11 +31,12 @@ def main():
     import numpy as np
     import torch
 
-    import oracle
-    from bench import config_packets, load_package
+    from bench import load_package
 
     hdfs = load_package()
-    pk, _ = config_packets(args.config, oracle)
+    from hdfs_crc32c_amd.workloads import config_packets
+
+    pk, _ = config_packets(args.config)
     nbytes = int(pk["len"].astype(np.int64).sum())
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)

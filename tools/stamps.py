@@ -17,14 +17,15 @@ def main():
     import numpy as np
     import torch
 
-    import oracle
-    from bench import config_packets, load_package
+    from bench import load_package
 
     cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
     variant = int(sys.argv[2]) if len(sys.argv) > 2 else 5  # 5 = production + stamps, 6 = memory-only + stamps
     wpg = int(sys.argv[3]) if len(sys.argv) > 3 else 12  # waves per workgroup of that variant
     hdfs = load_package()
-    pk, _ = config_packets(cfg, oracle)
+    from hdfs_crc32c_amd.workloads import config_packets
+
+    pk, _ = config_packets(cfg)
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)
     dev = torch.device("cuda", 0)

@@ -24,15 +24,16 @@ def main():
     import numpy as np
     import torch
 
-    import oracle
     from bench import load_package
 
     hdfs = load_package()
-    pk = oracle.uniform_packets(4096)
+    from hdfs_crc32c_amd.workloads import synthetic_bytes, uniform_packets
+
+    pk = uniform_packets(4096)
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)
     dev = torch.device("cuda", 0)
-    host = torch.from_numpy(oracle.xorshift64_bytes(extent, oracle.SEED)).to(dev)
+    host = torch.from_numpy(synthetic_bytes(extent, 1)).to(dev)
     g = torch.Generator(device=dev)
     g.manual_seed(5)
     rnd = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g) for _ in range(4)]
