@@ -207,6 +207,46 @@ def test_host_path_pinned_runs(hdfs, gpu_ctx, orc):
     assert np.array_equal(gpu_ctx.batch_host(payload, pk), want)
 
 
+def test_host_calls_from_threads(hdfs, gpu_ctx, orc):
+    """libfuse calls from many worker threads (fuse.c:1771): host batches on
+    one shared context, per-packet crc32c_chunks on the default context and
+    plan executions on per-thread streams, from 6 threads at once (ctypes
+    drops the GIL), every result exact."""
+    import threading
+
+    torch = _torch()
+    pk = oracle.uniform_packets(80)  # 5 MiB
+    pays = [oracle.xorshift64_bytes(80 * 65536, 300 + k) for k in range(6)]
+    wants = [orc.batch(p, pk, 80 * 128) for p in pays]
+    plan = hdfs.Plan(gpu_ctx, pk)
+    devs = [torch.from_numpy(p).cuda() for p in pays]
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(k):
+        try:
+            s = torch.cuda.Stream()
+            out = torch.zeros(80 * 128, dtype=torch.int32, device="cuda")
+            for rep in range(4):
+                got = gpu_ctx.batch_host(pays[k], pk)
+                assert np.array_equal(got, wants[k]), ("batch_host", k, rep)
+                pkt = pays[k][rep * 65536:(rep + 1) * 65536]
+                assert np.array_equal(hdfs.chunks(pkt, 512), wants[k][rep * 128:(rep + 1) * 128]), ("chunks", k)
+                plan.exec(devs[k].data_ptr(), out.data_ptr(), s.cuda_stream)
+                s.synchronize()
+                assert np.array_equal(out.cpu().numpy().view(np.uint32), wants[k]), ("plan", k, rep)
+        except Exception as e:  # reported on the main thread
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=100)
+    plan.close()
+    assert not errors, errors
+
+
 def test_chunks_default_context(hdfs, orc):
     pkt = oracle.xorshift64_bytes(65536, 99)
     assert np.array_equal(hdfs.chunks(pkt, 512), orc.chunks(pkt, 512))
