@@ -170,7 +170,8 @@ struct Stage {
     size_t payload_cap = 0;
     // Work descriptors: pinned host memory the kernel reads in place (d_desc
     // is its device mapping).  A slice's 64 KiB of descriptors are not worth
-    // a copy of their own: on the copy stream each copy adds ~25 us.
+    // a copy of their own: on the copy stream each copy costs ~25 us (9 us
+    // of transfer plus the ~15 us gap between copy commands).
     uint8_t *h_desc = nullptr, *d_desc = nullptr;
     size_t desc_cap = 0;
     // Checksums: written by the kernel straight into pinned host memory
@@ -197,8 +198,8 @@ struct crc32c_ctx {
     std::mutex mu;
     // Host pipeline: every stage's H2D copies go on one copy stream, so they
     // run back to back at the full link rate while the other stage's kernel
-    // and D2H run on its own stream.  Two copies on two streams would share
-    // the link, finish together and leave it idle while both stages drain.
+    // runs on its own stream.  Two copies on two streams would share the
+    // link, finish together and leave it idle while both stages drain.
     hipStream_t copy_stream = nullptr;
     Stage stage[2];
 };
@@ -276,10 +277,10 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
     return 0;
 }
 
-// Orders the plan's next launch on `stream` after everything it launched
-// before: when the stream changes, an event recorded on the previous stream
-// now (it covers that stream's launches so far) is waited on.  Same stream:
-// nothing to do (stream order).  Caller holds plan->mu.
+// Orders the plan's next verify launch on `stream` after its previous ones:
+// when the stream changes, an event recorded on the previous stream now (it
+// covers that stream's launches so far) is waited on.  Same stream: nothing
+// to do (stream order).  Caller holds plan->mu.
 int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
     if (plan->launched && plan->last_stream != stream) {
         if (!plan->last_done) HIP_TRY(hipEventCreateWithFlags(&plan->last_done, hipEventDisableTiming));
