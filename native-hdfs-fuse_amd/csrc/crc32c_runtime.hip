@@ -166,8 +166,10 @@ struct Stage {
     hipStream_t stream = nullptr;
     hipEvent_t copied = nullptr;  // the slice's H2D payload copy (on the context's copy stream) is done
     hipEvent_t done = nullptr;
-    uint8_t *h_payload = nullptr, *d_payload = nullptr;
+    uint8_t *d_payload = nullptr;
     size_t payload_cap = 0;
+    uint8_t *h_payload = nullptr;  // pinned staging, only for pageable or gathered payloads
+    size_t staging_cap = 0;
     // Work descriptors: pinned host memory the kernel reads in place (d_desc
     // is its device mapping).  A slice's 64 KiB of descriptors are not worth
     // a copy of their own: on the copy stream each copy costs ~25 us (9 us
@@ -315,17 +317,26 @@ int check_packets(const crc32c_packet *pkts, size_t npkts) {
     return 0;
 }
 
-template <class T>
-int grow_pinned_pair(T **h, T **d, size_t *cap, size_t need) {
+// Device buffer of at least `need` bytes.
+int grow_device(uint8_t **d, size_t *cap, size_t need) {
     if (*cap >= need) return 0;
-    if (*h) (void)hipHostFree(*h);
     if (*d) (void)hipFree(*d);
-    *h = nullptr;
     *d = nullptr;
     *cap = 0;
-    size_t c = std::max(need, size_t(4096));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(h), c * sizeof(T), hipHostMallocDefault));
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(d), c * sizeof(T)));
+    const size_t c = std::max(need, size_t(4096));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(d), c));
+    *cap = c;
+    return 0;
+}
+
+// Pinned host buffer of at least `need` bytes.
+int grow_pinned(uint8_t **h, size_t *cap, size_t need) {
+    if (*cap >= need) return 0;
+    if (*h) (void)hipHostFree(*h);
+    *h = nullptr;
+    *cap = 0;
+    const size_t c = std::max(need, size_t(4096));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(h), c, hipHostMallocDefault));
     *cap = c;
     return 0;
 }
@@ -445,7 +456,8 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
             stage_bytes = 0;
             for (const auto &r : runs) stage_bytes += size_t(r.second - (r.first & ~uint64_t(15))) + 16;
         }
-        rc = grow_pinned_pair(&s.h_payload, &s.d_payload, &s.payload_cap, stage_bytes + 16);
+        rc = grow_device(&s.d_payload, &s.payload_cap, stage_bytes + 16);
+        if (!rc && !(pinned && (ranged || by_runs))) rc = grow_pinned(&s.h_payload, &s.staging_cap, stage_bytes + 16);
         if (rc) return rc;
         // 1. The payload copy goes first: it needs no plan, and the copy
         //    stream runs the slices' copies back to back.  (This stage's
