@@ -110,6 +110,26 @@ def test_chunks_cpu_matches_reference_loop(hdfs, orc, golden):
     assert L.crc32c_chunks_cpu(None, 0, 512, None, 0) == 0
 
 
+@pytest.mark.parametrize("name", ["c1_one_packet", "c3_one_block_4MiB", "c5_mixed_bpc_96", "ragged_tail_257"])
+def test_chunks_cpu_golden_batches(hdfs, golden, name):
+    """BASELINE config 1 (one 64 KiB packet, the CPU path) and the other small
+    golden batches through crc32c_chunks_cpu packet by packet: SHA-256 of the
+    checksum array equals the reference build's (tests/golden/batches.json)."""
+    import hashlib
+
+    spec = [b for b in golden["batches"] if b["name"] == name][0]
+    from conftest import golden_batch_packets
+
+    pk = golden_batch_packets(spec)
+    payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+    out = np.zeros(spec["nchecksums"], np.uint32)
+    for p in pk:
+        off, idx, ln, bpc = int(p["payload_off"]), int(p["out_idx"]), int(p["len"]), int(p["bpc"])
+        n = hdfs.nchunks(ln, bpc)
+        out[idx:idx + n] = hdfs.chunks_cpu(np.ascontiguousarray(payload[off:off + ln]), bpc)
+    assert hashlib.sha256(out.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
+
+
 def test_batch_nchecksums(hdfs):
     """crc32c_batch_nchecksums (the checksum array length of a batch): the
     oracle's count on full batches; with empty packets (which own no
