@@ -359,15 +359,12 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
 
 // lin() per piece, then reduce to one lin() per block, combine the blocks of
 // each chunk, store (or compare) the chunk checksums.
-template <int DIAG, bool S4, bool VERIFY>
-__device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
-                                            const uint4 v[8], uint32_t ev, int lane) {
-    const uint32_t nb = t.meta & 0xffu;
-    const uint32_t lg = (t.meta >> 8) & 0xffu;
+// lin() of pieces I0 .. I1-1 of a tile (instruction i's 16 bytes per lane).
+template <int DIAG, bool S4, int I0, int I1>
+__device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8], uint32_t pc[8], int lane) {
     const LaneCols cols = lane_cols(uint32_t(lane & 31));
-    uint32_t pc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = I0; i < I1; ++i) {
         pc[i] = piece<S4, DIAG>(lds, v[i], cols);
         opaque(pc[i]);
         // One piece at a time (nibble tables: 32 independent reads each), or
@@ -376,6 +373,27 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
         // hoisting every piece's LDS reads together (register pressure).
         if (!S4 || (i & 1)) __builtin_amdgcn_sched_barrier(0);
     }
+}
+
+template <int DIAG, bool S4, bool VERIFY>
+__device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            const uint32_t pc[8], uint32_t ev, int lane);
+
+template <int DIAG, bool S4, bool VERIFY>
+__device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            const uint4 v[8], uint32_t ev, int lane) {
+    uint32_t pc[8];
+    tile_pieces<DIAG, S4, 0, 8>(lds, v, pc, lane);
+    reduce_emit<DIAG, S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
+}
+
+// The tile's 8 piece values -> one lin() per block, blocks combined per chunk,
+// chunk checksums stored (or compared).
+template <int DIAG, bool S4, bool VERIFY>
+__device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            const uint32_t pc[8], uint32_t ev, int lane) {
+    const uint32_t nb = t.meta & 0xffu;
+    const uint32_t lg = (t.meta >> 8) & 0xffu;
 
     // Reduce-scatter over lane bits 0, 1, 3 (8 values -> 1), then all-reduce
     // over lane bits 2 and 4.  Afterwards lane l holds lin() of block
@@ -615,6 +633,7 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_wg512x1_nt", 512, 1},                  // A/B: 0 with 8 waves per CU
     {"s4_wg768x1_nt_fixed", 768, 1},            // A/B: 0 on ceil(items / 12) workgroups (concentrated)
     {"s4_nt_shapes", 768, 1},                   // A/B: 0 with 8/4/2/1 waves per workgroup for small batches
+    {"s4_wg512x1_nt_memonly", 512, 1},          // DIAGNOSTIC: memory ceiling of 9 (8 waves, 64 KiB in flight)
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -698,6 +717,7 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 7: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeNoStage); break;
     case 8: HDFS_LAUNCH(768, 3, kS4Nt | kModeDescPf); break;
     case 9: HDFS_LAUNCH(512, 2, kS4Nt); break;
+    case 12: HDFS_LAUNCH(512, 2, kS4Nt | kModeMemDiag); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
