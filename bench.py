@@ -302,6 +302,38 @@ def main():
                   "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
                   "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF)}
 
+    # The box's own streaming-read rate over the same rotating buffers, right
+    # after the timed region (same power state): a plain grid-stride read
+    # with non-temporal loads (stream_probe.hip shape 2, 512 x 256 threads,
+    # the best plain shape of tools/probe_sweep.py), timed like a step.  It
+    # prices the kernel against what this chip actually streams, beside the
+    # 8 TB/s datasheet peak.  Rank 0, N = 1 only.
+    read_probe = None
+    if rank == 0 and world == 1 and nbuf > 1:
+        probe_out = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
+        L = hdfs.lib()
+
+        def probe(i):
+            rc = L.crc32c_debug_stream_probe(bufs[i % nbuf].data_ptr(), extent, probe_out.data_ptr(), 512, 2, sptr)
+            if rc:
+                raise RuntimeError("stream probe rc %d" % rc)
+
+        for i in range(50):
+            probe(i)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        np_ = 500
+        for i in range(np_):
+            probe(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / np_ * 1e3
+        probe_gbs = extent / (us * 1e-6) / 1e9
+        read_probe = {"us_per_pass": round(us, 2), "GB_s": round(probe_gbs, 1),
+                      "kernel_frac_of_probe": round(achieved_gbs / probe_gbs, 4),
+                      "shape": "grid-stride 16 B nt loads, 4 in flight per lane, 512 x 256 threads"}
+
     # Independent batches on two streams (opt-in, rank 0, beside the main
     # line, which stays one stream so that one step = one launch): the next
     # launch's workgroups start on the CUs the previous one has released.
@@ -402,6 +434,7 @@ def main():
             "host_resident_ranks": world if host is not None else None,
             "verify": verify,
             "two_streams": two_streams,
+            "box_read_probe": read_probe,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         }
         print(json.dumps(line), flush=True)
