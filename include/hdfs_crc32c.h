@@ -52,6 +52,11 @@ uint32_t hdfs_crc32(uint32_t crc, const void *buf, size_t len);
 #define CRC32C_TYPE_CRC32 0x2u /* Hadoop CHECKSUM_CRC32 (IEEE 802.3 / zlib polynomial)
                                   instead of CHECKSUM_CRC32C; the reference returns
                                   -ENOSYS for it (hadooprpc.c:629-631) */
+#define CRC32C_DEVICE_ADDRESSES 0x4u /* plan flag: every packet's payload_off is a device
+                                        address, so one plan (one launch) covers packets in
+                                        different device buffers, e.g. many HDFS blocks;
+                                        exec / verify then take dev_payload = NULL.  Not
+                                        valid for the host-resident calls. */
 
 /* One packet of a batch: `len` payload bytes starting `payload_off` bytes into
  * the batch payload buffer, cut into chunks of `bpc` bytes

@@ -27,6 +27,7 @@ INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
 
 CRC32C_BIG_ENDIAN = 0x1
 CRC32C_TYPE_CRC32 = 0x2  # Hadoop CHECKSUM_CRC32 (zlib polynomial) instead of CRC32C
+CRC32C_DEVICE_ADDRESSES = 0x4  # plan flag: payload_off are device addresses; exec/verify take payload 0
 
 PACKET_DTYPE = np.dtype(
     [("payload_off", "<u8"), ("out_idx", "<u8"), ("len", "<u4"), ("bpc", "<u4")], align=True
@@ -211,7 +212,7 @@ class Context:
         return Plan(self, pkts, flags)
 
     def batch_host(self, payload: np.ndarray, pkts, flags: int = 0, out: np.ndarray | None = None) -> np.ndarray:
-        """Host-resident batch: pinned H2D -> kernel -> D2H (crc32c_batch_host)."""
+        """Host-resident batch (crc32c_batch_host): H2D copy -> kernel -> checksums in host memory."""
         pkts = as_packets(pkts)
         payload = np.ascontiguousarray(payload, dtype=np.uint8)
         n = total_checksums(pkts)

@@ -221,6 +221,11 @@ struct crc32c_plan {
     uint32_t ntiles = 0, ngen = 0;
     uint64_t nchecksums = 0, payload_bytes = 0;
     uint32_t flags = 0;
+    // CRC32C_DEVICE_ADDRESSES: the plan's offsets are relative to this device
+    // address (the lowest packet address, rounded down to 16), which the
+    // launches pass as the payload base.
+    uint64_t abs_base = 0;
+    bool absolute = false;
 };
 
 struct crc32c_multi {
@@ -303,7 +308,7 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     return launch(plan->ctx, p, plan->sched, stream);
 }
 
-constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32;
+constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES;
 
 int check_flags(uint32_t flags) {
     if (flags & ~kKnownFlags) return fail(-EINVAL, "unknown flags 0x%x", flags & ~kKnownFlags);
@@ -630,6 +635,17 @@ int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts,
     int rc = check_flags(flags);
     if (!rc) rc = check_packets(pkts, npkts);
     if (rc) return rc;
+    std::vector<crc32c_packet> rebased;
+    uint64_t abs_base = 0;
+    if (flags & CRC32C_DEVICE_ADDRESSES) {  // offsets from the lowest address (16-byte phase kept)
+        abs_base = UINT64_MAX;
+        for (size_t i = 0; i < npkts; ++i)
+            if (pkts[i].len) abs_base = std::min<uint64_t>(abs_base, pkts[i].payload_off & ~uint64_t(15));
+        if (abs_base == UINT64_MAX) abs_base = 0;
+        rebased.assign(pkts, pkts + npkts);
+        for (crc32c_packet &pk : rebased) pk.payload_off = pk.len ? pk.payload_off - abs_base : 0;
+        pkts = rebased.data();
+    }
     HostPlan hp;
     rc = build_plan(pkts, npkts, &hp);
     if (rc) return fail(rc, "invalid packet batch");
@@ -640,7 +656,9 @@ int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts,
     p->ngen = uint32_t(hp.gen.size());
     p->nchecksums = hp.nchecksums;
     p->payload_bytes = hp.payload_bytes;
-    p->flags = flags;
+    p->flags = flags & ~CRC32C_DEVICE_ADDRESSES;
+    p->abs_base = abs_base;
+    p->absolute = (flags & CRC32C_DEVICE_ADDRESSES) != 0;
     DeviceGuard guard(ctx->device);
     if (p->ntiles) {
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p->d_tiles), hp.tiles.size() * sizeof(FastTile)));
@@ -654,9 +672,19 @@ int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts,
     return 0;
 }
 
+// The payload base a launch passes: the caller's buffer, or for a
+// CRC32C_DEVICE_ADDRESSES plan its own base (the caller passes NULL).
+static int plan_payload(const crc32c_plan *plan, const void **dev_payload) {
+    if (!plan->absolute) return 0;
+    if (*dev_payload) return fail(-EINVAL, "a CRC32C_DEVICE_ADDRESSES plan takes dev_payload = NULL");
+    *dev_payload = reinterpret_cast<const void *>(uintptr_t(plan->abs_base));
+    return 0;
+}
+
 int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out, void *stream) {
     if (!plan) return fail(-EINVAL, "plan == NULL");
     if (plan->nchecksums == 0) return 0;
+    if (int rc = plan_payload(plan, &dev_payload)) return rc;
     if (!dev_payload || !dev_out) return fail(-EINVAL, "payload/out == NULL");
     if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
         return fail(-EINVAL, "device payload must be 16-byte aligned");
@@ -677,6 +705,7 @@ int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));
         return 0;
     }
+    if (int rc = plan_payload(plan, &dev_payload)) return rc;
     if (!dev_payload || !dev_expected) return fail(-EINVAL, "payload/expected == NULL");
     if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
         return fail(-EINVAL, "device payload must be 16-byte aligned");
@@ -765,6 +794,7 @@ int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet 
     int rc = check_flags(flags);
     if (!rc) rc = check_packets(pkts, npkts);
     if (rc) return rc;
+    if (flags & CRC32C_DEVICE_ADDRESSES) return fail(-EINVAL, "CRC32C_DEVICE_ADDRESSES is for device-resident plans");
     if (npkts && (!payload || !out)) return fail(-EINVAL, "payload/out == NULL");
     std::lock_guard<std::mutex> lock(ctx->mu);
     rc = batch_host_locked(ctx, static_cast<const uint8_t *>(payload), pkts, npkts, out, flags);

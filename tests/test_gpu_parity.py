@@ -247,6 +247,52 @@ def test_host_calls_from_threads(hdfs, gpu_ctx, orc):
     assert not errors, errors
 
 
+def test_device_address_plan_over_many_buffers(hdfs, gpu_ctx, orc):
+    """CRC32C_DEVICE_ADDRESSES: one plan, one launch over packets living in 12
+    separate device buffers (HDFS blocks allocated one by one), with ragged
+    blocks, one block starting 5 bytes off alignment (general path) and
+    mixed bpc: exact against the oracle per packet, exec and verify; a
+    non-NULL payload and the host-resident calls are refused."""
+    torch = _torch()
+    bufs, rows, want = [], [], []
+    out = 0
+    for k in range(12):
+        n = (4 << 20) - (1000 if k % 3 == 0 else 0)
+        data = oracle.xorshift64_bytes(n + 16, 700 + k)
+        t = torch.from_numpy(data).cuda()
+        bufs.append(t)
+        skew = 5 if k == 4 else 0
+        bpc = (512, 1024, 4096)[k % 3]
+        for o in range(skew, n, 65536):
+            ln = min(65536, n - o)
+            rows.append((t.data_ptr() + o, out, ln, bpc))
+            want.append(orc.chunks(data[o:o + ln], bpc))
+            out += (ln + bpc - 1) // bpc
+    pk = np.array(rows, hdfs.PACKET_DTYPE)
+    want = np.concatenate(want)
+    plan = hdfs.Plan(gpu_ctx, pk, hdfs.CRC32C_DEVICE_ADDRESSES)
+    assert plan.nchecksums == out
+    dev_out = torch.full((out,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    plan.exec(0, dev_out.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert np.array_equal(dev_out.cpu().numpy().view(np.uint32), want)
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    plan.verify(0, exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [0, 0xFFFFFFFF]
+    exp[out // 2] ^= 1
+    plan.verify(0, exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [1, out // 2]
+    with pytest.raises(hdfs.Crc32cError):
+        plan.exec(bufs[0].data_ptr(), dev_out.data_ptr(), stream.cuda_stream)
+    plan.close()
+    with pytest.raises(hdfs.Crc32cError):
+        gpu_ctx.batch_host(np.zeros(16, np.uint8), oracle.uniform_packets(1, pkt_len=16), hdfs.CRC32C_DEVICE_ADDRESSES)
+
+
 def test_chunks_default_context(hdfs, orc):
     pkt = oracle.xorshift64_bytes(65536, 99)
     assert np.array_equal(hdfs.chunks(pkt, 512), orc.chunks(pkt, 512))
