@@ -114,11 +114,12 @@ int crc32c_device_count(void);
  * other: independent batches may run on several streams at once, and two
  * streams let one launch start on the CUs the previous one has released
  * (config 2: 41.2 instead of 43.4 us per batch, tools/overlap_probe.py).
- * Alignment contract: payload_off values that are multiples of 16 with
- * bpc in {512, 1024, 2048, 4096, 8192} take the fast path; anything else is
- * still exact (general path).  The payload buffer must be readable up to the
- * next 16-byte boundary after each packet's last byte (device allocations
- * always are).
+ * Fast path: every full chunk of a packet with bpc in {512, 1024, 2048,
+ * 4096, 8192}, at any alignment (off 16-byte alignment the tile loads are
+ * unaligned: config 2 five bytes off takes 55 instead of 42.5 us); short
+ * tail chunks and other bpc values take the general path (exact, ~4x
+ * slower).  The payload buffer must be readable up to the next 16-byte
+ * boundary after each packet's last byte (device allocations always are).
  * ------------------------------------------------------------------------- */
 typedef struct crc32c_plan crc32c_plan;
 

@@ -686,8 +686,6 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
     if (plan->nchecksums == 0) return 0;
     if (int rc = plan_payload(plan, &dev_payload)) return rc;
     if (!dev_payload || !dev_out) return fail(-EINVAL, "payload/out == NULL");
-    if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
-        return fail(-EINVAL, "device payload must be 16-byte aligned");
     DeviceGuard guard(plan->ctx->device);
     const KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload,
                                  dev_out, plan->flags);
@@ -707,8 +705,6 @@ int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_
     }
     if (int rc = plan_payload(plan, &dev_payload)) return rc;
     if (!dev_payload || !dev_expected) return fail(-EINVAL, "payload/expected == NULL");
-    if (plan->ntiles && (reinterpret_cast<uintptr_t>(dev_payload) & 15u))
-        return fail(-EINVAL, "device payload must be 16-byte aligned");
     if (!variant_verifies(plan->ctx->variant))
         return fail(-EINVAL, "kernel variant %d has no verification mode", plan->ctx->variant);
     KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, nullptr,

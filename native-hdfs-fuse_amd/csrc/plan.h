@@ -5,12 +5,12 @@
 // (hadooprpc.c:639, 733-742) and then regrouped into GPU work items:
 //
 //  * FastTile: up to 16 consecutive 512-byte blocks (8 KiB, one wave-tile)
-//    of FULL chunks of one packet whose bpc is 512 << lg (lg = 0..4) and whose
-//    payload_off is 16-byte aligned.  A tile never straddles a chunk, so a
-//    wave finishes every chunk it starts.
+//    of FULL chunks of one packet whose bpc is 512 << lg (lg = 0..4), at any
+//    alignment.  A tile never straddles a chunk, so a wave finishes every
+//    chunk it starts.
 //  * GenItem: one chunk of any length / alignment (the short tail chunk of a
-//    packet, or every chunk of a packet whose bpc or alignment does not fit the
-//    fast tile), processed by half a wave.
+//    packet, or every chunk of a packet whose bpc does not fit the fast
+//    tile), processed by half a wave.
 #pragma once
 #include <cstdint>
 #include <vector>

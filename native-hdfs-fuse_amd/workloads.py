@@ -51,6 +51,12 @@ def config_packets(name: str):
         return None, "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
     if name == "c5":
         return mixed_packets(4096), "4096 x 64KiB packets, bpc cycling 512/1024/4096 (config 5)"
+    if name == "c2u":  # config 2 with every packet 5 bytes off 16-byte alignment (general path)
+        pk = uniform_packets(4096, stride=PACKET_BYTES + 16)
+        pk["payload_off"] += np.uint64(5)
+        return pk, "4096 x 64KiB packets at 16-byte-misaligned offsets, 512B chunks (general path)"
+    if name == "c2b1536":  # config 2 with bytesPerChecksum 1536 (not a power of two: general path)
+        return uniform_packets(4096, bpc=1536), "4096 x 64KiB packets, 1536B chunks (general path)"
     if name.startswith("p") and name[1:].isdigit():  # pN: N uniform packets
         n = int(name[1:])
         return uniform_packets(n), "%d x 64KiB packets, 512B chunks" % n

@@ -149,6 +149,38 @@ def test_random_batches(hdfs, gpu_ctx, orc):
         assert np.array_equal(got, orc.batch(payload, pk, got.size)), trial
 
 
+@pytest.mark.parametrize("bpc", [512, 1024, 2048, 4096, 8192])
+def test_unaligned_fast_tiles(hdfs, gpu_ctx, orc, bpc):
+    """Full chunks of power-of-two bpc take the fast tiles at any alignment
+    (unaligned dwordx4 buffer loads): 48 packets at every offset mod 16,
+    ragged tails, exec and verify against the oracle."""
+    torch = _torch()
+    n = 48
+    pk = np.zeros(n, hdfs.PACKET_DTYPE)
+    off = out = 0
+    for i in range(n):
+        off += i % 16 + 1  # every phase mod 16
+        ln = 65536 - (0 if i % 5 else 300)
+        pk[i] = (off, out, ln, bpc)
+        off += ln
+        out += (ln + bpc - 1) // bpc
+    tiles, gen = hdfs.debug_plan(pk)
+    assert len(tiles) > 0 and all(int(g["len"]) < bpc for g in gen)  # only short tails go general
+    payload = oracle.xorshift64_bytes(off + 64, 4000 + bpc)
+    want = orc.batch(payload, pk, out)
+    assert np.array_equal(run_dev(hdfs, gpu_ctx, payload, pk), want)
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    exp[out - 1] ^= 1
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [1, out - 1]
+    plan.close()
+
+
 def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
     """crc32c_batch_host over 64 MiB slices on two alternating stages: 3
     slices (~137 MiB, so each stage is reused), from pageable memory (pinned

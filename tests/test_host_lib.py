@@ -173,7 +173,7 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
     seen = np.zeros(n, np.int32)
     for t in tiles:
         nb, lg = int(t["meta"]) & 0xFF, (int(t["meta"]) >> 8) & 0xFF
-        assert 1 <= nb <= 16 and nb % (1 << lg) == 0 and int(t["src"]) % 16 == 0
+        assert 1 <= nb <= 16 and nb % (1 << lg) == 0  # any alignment (unaligned tile loads)
         bpc = 512 << lg
         for c in range(nb >> lg):
             s = int(t["src"]) + c * bpc
