@@ -81,6 +81,8 @@ constexpr int kModeCompDiag = 16;   // DIAGNOSTIC, wrong results: no payload loa
 constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table staging
 constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
 constexpr int kModeDescPf = 128;    // A/B: next tile grabbed at load time, its descriptor prefetched (vector path)
+constexpr int kModeIlp4 = 256;      // A/B: 4 pieces' lookup chains free to interleave
+constexpr int kModeIlp8 = 512;      // A/B: all 8 pieces' lookup chains free to interleave
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -360,13 +362,19 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
 // lin() per piece, then reduce to one lin() per block, combine the blocks of
 // each chunk, store (or compare) the chunk checksums.
 // lin() of pieces I0 .. I1-1 of a tile (instruction i's 16 bytes per lane).
-template <int DIAG, bool S4, int I0, int I1>
+// GROUP > 2 (A/B): GROUP pieces' chains are left free to interleave (no
+// per-piece pin, a scheduling barrier only every GROUP pieces).
+template <int DIAG, bool S4, int I0, int I1, int GROUP = 2>
 __device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8], uint32_t pc[8], int lane) {
     const LaneCols cols = lane_cols(uint32_t(lane & 31));
 #pragma unroll
     for (int i = I0; i < I1; ++i) {
         pc[i] = piece<S4, DIAG>(lds, v[i], cols);
-        opaque(pc[i]);
+        if (GROUP <= 2) opaque(pc[i]);
+        if (GROUP > 2) {
+            if ((i + 1) % GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+            continue;
+        }
         // One piece at a time (nibble tables: 32 independent reads each), or
         // two (S4: a piece is a chain of 4 dependent steps, so two chains
         // interleave to keep 8 reads in flight): keeps the scheduler from
@@ -379,11 +387,11 @@ template <int DIAG, bool S4, bool VERIFY>
 __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             const uint32_t pc[8], uint32_t ev, int lane);
 
-template <int DIAG, bool S4, bool VERIFY>
+template <int DIAG, bool S4, bool VERIFY, int GROUP = 2>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             const uint4 v[8], uint32_t ev, int lane) {
     uint32_t pc[8];
-    tile_pieces<DIAG, S4, 0, 8>(lds, v, pc, lane);
+    tile_pieces<DIAG, S4, 0, 8, GROUP>(lds, v, pc, lane);
     reduce_emit<DIAG, S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
 }
 
@@ -530,6 +538,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
     constexpr bool VERIFY = (MODE & kModeVerify) != 0;
     constexpr bool DESCPF = (MODE & kModeDescPf) != 0;
+    constexpr int GROUP = (MODE & kModeIlp8) ? 8 : (MODE & kModeIlp4) ? 4 : 2;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
@@ -592,7 +601,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         }
     } else {
         while (t < tend) {
-            finish_tile<DIAG, S4, VERIFY>(p, lds, vacc, ft, v, ev, lane);
+            finish_tile<DIAG, S4, VERIFY, GROUP>(p, lds, vacc, ft, v, ev, lane);
             t = pool_grab(pool_ctr, lane);
             if (t >= tend) break;
             ft = tile_at(p, t);
@@ -634,6 +643,9 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_wg768x1_nt_fixed", 768, 1},            // A/B: 0 on ceil(items / 12) workgroups (concentrated)
     {"s4_nt_shapes", 768, 1},                   // A/B: 0 with 8/4/2/1 waves per workgroup for small batches
     {"s4_wg512x1_nt_memonly", 512, 1},          // DIAGNOSTIC: memory ceiling of 9 (8 waves, 64 KiB in flight)
+    {"s4_ilp4_wg512x1_nt", 512, 1},             // A/B: 8 waves, 4 chains free to interleave
+    {"s4_ilp8_wg512x1_nt", 512, 1},             // A/B: 8 waves, 8 chains free to interleave
+    {"s4_ilp4_wg768x1_nt", 768, 1},             // A/B: 12 waves, 4 chains free to interleave
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -718,6 +730,9 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 8: HDFS_LAUNCH(768, 3, kS4Nt | kModeDescPf); break;
     case 9: HDFS_LAUNCH(512, 2, kS4Nt); break;
     case 12: HDFS_LAUNCH(512, 2, kS4Nt | kModeMemDiag); break;
+    case 13: HDFS_LAUNCH(512, 2, kS4Nt | kModeIlp4); break;
+    case 14: HDFS_LAUNCH(512, 2, kS4Nt | kModeIlp8); break;
+    case 15: HDFS_LAUNCH(768, 3, kS4Nt | kModeIlp4); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
