@@ -83,6 +83,8 @@ constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instea
 constexpr int kModeDescPf = 128;    // A/B: next tile grabbed at load time, its descriptor prefetched (vector path)
 constexpr int kModeIlp4 = 256;      // A/B: 4 pieces' lookup chains free to interleave
 constexpr int kModeIlp8 = 512;      // A/B: all 8 pieces' lookup chains free to interleave
+constexpr int kModePrio = 1024;     // A/B: raised wave priority from the end of the lookups to the next tile's loads
+constexpr int kModeEarly = 2048;    // A/B: next tile's loads issued between the lookups and the reduce
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -539,6 +541,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr bool VERIFY = (MODE & kModeVerify) != 0;
     constexpr bool DESCPF = (MODE & kModeDescPf) != 0;
     constexpr int GROUP = (MODE & kModeIlp8) ? 8 : (MODE & kModeIlp4) ? 4 : 2;
+    constexpr bool PRIO = (MODE & kModePrio) != 0;
+    constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
@@ -599,6 +603,30 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             tn = pool_grab(pool_ctr, lane);
             dn = tile_prefetch(p, tn < tend ? tn : 0u);  // unconditional: keeps vmcnt counts exact
         }
+    } else if (EARLY || PRIO) {
+        // A/B: the lookups free v[] before the reduce; EARLY issues the next
+        // tile's loads there, PRIO lets the wave ahead of its SIMD's others
+        // until those loads are out.
+        while (t < tend) {
+            uint32_t pc[8];
+            tile_pieces<DIAG, S4, 0, 8, GROUP>(lds, v, pc, lane);
+            if (PRIO) __builtin_amdgcn_s_setprio(2);
+            const FastTile cur = ft;
+            const uint32_t cev = ev;
+            const uint32_t tn = pool_grab(pool_ctr, lane);
+            if (EARLY && tn < tend) {
+                ft = tile_at(p, tn);
+                load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
+                if (PRIO) __builtin_amdgcn_s_setprio(0);
+            }
+            reduce_emit<DIAG, S4, VERIFY>(p, lds, vacc, cur, pc, cev, lane);
+            t = tn;
+            if (!EARLY && t < tend) {
+                ft = tile_at(p, t);
+                load_tile<AUX, COMPDIAG, VERIFY>(p, ft, lane, v, ev);
+            }
+            if (PRIO) __builtin_amdgcn_s_setprio(0);
+        }
     } else {
         while (t < tend) {
             finish_tile<DIAG, S4, VERIFY, GROUP>(p, lds, vacc, ft, v, ev, lane);
@@ -646,6 +674,9 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_ilp4_wg512x1_nt", 512, 1},             // A/B: 8 waves, 4 chains free to interleave
     {"s4_ilp8_wg512x1_nt", 512, 1},             // A/B: 8 waves, 8 chains free to interleave
     {"s4_ilp4_wg768x1_nt", 768, 1},             // A/B: 12 waves, 4 chains free to interleave
+    {"s4_prio_wg768x1_nt", 768, 1},             // A/B: 0 with raised priority from the lookups' end to the next loads
+    {"s4_early_wg768x1_nt", 768, 1},            // A/B: 0 with the next tile's loads issued before the reduce
+    {"s4_early_prio_wg768x1_nt", 768, 1},       // A/B: 17 + 16
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -733,6 +764,9 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 13: HDFS_LAUNCH(512, 2, kS4Nt | kModeIlp4); break;
     case 14: HDFS_LAUNCH(512, 2, kS4Nt | kModeIlp8); break;
     case 15: HDFS_LAUNCH(768, 3, kS4Nt | kModeIlp4); break;
+    case 16: HDFS_LAUNCH(768, 3, kS4Nt | kModePrio); break;
+    case 17: HDFS_LAUNCH(768, 3, kS4Nt | kModeEarly); break;
+    case 18: HDFS_LAUNCH(768, 3, kS4Nt | kModeEarly | kModePrio); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
