@@ -85,6 +85,8 @@ constexpr int kModeIlp4 = 256;      // A/B: 4 pieces' lookup chains free to inte
 constexpr int kModeIlp8 = 512;      // A/B: all 8 pieces' lookup chains free to interleave
 constexpr int kModePrio = 1024;     // A/B: raised wave priority from the end of the lookups to the next tile's loads
 constexpr int kModeEarly = 2048;    // A/B: next tile's loads issued between the lookups and the reduce
+constexpr int kModeSc0 = 4096;      // A/B: payload loads with the sc0 cache-policy bit as well
+constexpr int kModeSc1 = 8192;      // A/B: payload loads with the sc1 cache-policy bit as well
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -543,7 +545,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr int GROUP = (MODE & kModeIlp8) ? 8 : (MODE & kModeIlp4) ? 4 : 2;
     constexpr bool PRIO = (MODE & kModePrio) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
-    constexpr int AUX = NT ? 2 : 0;
+    constexpr int AUX = (NT ? 2 : 0) | ((MODE & kModeSc0) ? 1 : 0) | ((MODE & kModeSc1) ? 16 : 0);
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
     // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
@@ -677,6 +679,9 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_prio_wg768x1_nt", 768, 1},             // A/B: 0 with raised priority from the lookups' end to the next loads
     {"s4_early_wg768x1_nt", 768, 1},            // A/B: 0 with the next tile's loads issued before the reduce
     {"s4_early_prio_wg768x1_nt", 768, 1},       // A/B: 17 + 16
+    {"s4_nt_sc0", 768, 1},                      // A/B: 0 with payload loads sc0 | nt
+    {"s4_nt_sc1", 768, 1},                      // A/B: 0 with payload loads sc1 | nt
+    {"s4_nt_sc0_sc1", 768, 1},                  // A/B: 0 with payload loads sc0 | sc1 | nt
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -767,6 +772,9 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 16: HDFS_LAUNCH(768, 3, kS4Nt | kModePrio); break;
     case 17: HDFS_LAUNCH(768, 3, kS4Nt | kModeEarly); break;
     case 18: HDFS_LAUNCH(768, 3, kS4Nt | kModeEarly | kModePrio); break;
+    case 19: HDFS_LAUNCH(768, 3, kS4Nt | kModeSc0); break;
+    case 20: HDFS_LAUNCH(768, 3, kS4Nt | kModeSc1); break;
+    case 21: HDFS_LAUNCH(768, 3, kS4Nt | kModeSc0 | kModeSc1); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
