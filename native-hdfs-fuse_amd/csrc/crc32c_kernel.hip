@@ -87,6 +87,7 @@ constexpr int kModePrio = 1024;     // A/B: raised wave priority from the end of
 constexpr int kModeEarly = 2048;    // A/B: next tile's loads issued between the lookups and the reduce
 constexpr int kModeSc0 = 4096;      // A/B: payload loads with the sc0 cache-policy bit as well
 constexpr int kModeSc1 = 8192;      // A/B: payload loads with the sc1 cache-policy bit as well
+constexpr int kModeXcdShift = 14;   // A/B: bits 14-15 = k: odd-XCD workgroups get k/64 less of the tiles
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -565,8 +566,14 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
-    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    // (A/B, XCDK > 0 and an even grid: workgroup b's share is 1 + k/64 for
+    // even b, 1 - k/64 for odd b, i.e. its range starts at b + (k/64)*(b & 1)
+    // shares; blocks go round-robin over the XCDs, so odd b = odd XCD.)
+    constexpr uint32_t XCDK = uint32_t(MODE >> kModeXcdShift) & 3u;
+    const uint32_t xk = (XCDK && !(gridDim.x & 1u)) ? XCDK : 0u;
+    const uint64_t den = 64ull * gridDim.x;
+    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * (64ull * blockIdx.x + xk * (blockIdx.x & 1u))) / den);
+    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (64ull * (blockIdx.x + 1) + xk * ((blockIdx.x + 1) & 1u))) / den);
     if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
     if (threadIdx.x == 0) {
         *pool_ctr = tbeg + kWaves;
@@ -682,6 +689,9 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_nt_sc0", 768, 1},                      // A/B: 0 with payload loads sc0 | nt
     {"s4_nt_sc1", 768, 1},                      // A/B: 0 with payload loads sc1 | nt
     {"s4_nt_sc0_sc1", 768, 1},                  // A/B: 0 with payload loads sc0 | sc1 | nt
+    {"s4_nt_xcd1", 768, 1},                     // A/B: 0 with odd-XCD workgroups given 1/64 fewer tiles
+    {"s4_nt_xcd2", 768, 1},                     // A/B: ... 2/64
+    {"s4_nt_xcd3", 768, 1},                     // A/B: ... 3/64
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -775,6 +785,9 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 19: HDFS_LAUNCH(768, 3, kS4Nt | kModeSc0); break;
     case 20: HDFS_LAUNCH(768, 3, kS4Nt | kModeSc1); break;
     case 21: HDFS_LAUNCH(768, 3, kS4Nt | kModeSc0 | kModeSc1); break;
+    case 22: HDFS_LAUNCH(768, 3, kS4Nt | (1 << kModeXcdShift)); break;
+    case 23: HDFS_LAUNCH(768, 3, kS4Nt | (2 << kModeXcdShift)); break;
+    case 24: HDFS_LAUNCH(768, 3, kS4Nt | (3 << kModeXcdShift)); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
