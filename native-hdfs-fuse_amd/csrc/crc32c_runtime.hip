@@ -584,7 +584,8 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     const int ndev = crc32c_device_count();
     if (ndev <= 0) return fail(-ENODEV, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(-ENODEV, "device %d out of range (%d visible)", device, ndev);
-    std::unique_ptr<crc32c_ctx> c(new crc32c_ctx);
+    // A failure part-way releases what was already allocated.
+    std::unique_ptr<crc32c_ctx, int (*)(crc32c_ctx *)> c(new crc32c_ctx, crc32c_ctx_destroy);
     c->device = device;
     DeviceGuard guard(device);
     hipDeviceProp_t prop;
@@ -650,7 +651,7 @@ int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts,
     rc = build_plan(pkts, npkts, &hp);
     if (rc) return fail(rc, "invalid packet batch");
     if (hp.tiles.size() > UINT32_MAX || hp.gen.size() > UINT32_MAX) return fail(-E2BIG, "batch too large");
-    std::unique_ptr<crc32c_plan> p(new crc32c_plan);
+    std::unique_ptr<crc32c_plan, int (*)(crc32c_plan *)> p(new crc32c_plan, crc32c_plan_destroy);
     p->ctx = ctx;
     p->ntiles = uint32_t(hp.tiles.size());
     p->ngen = uint32_t(hp.gen.size());
