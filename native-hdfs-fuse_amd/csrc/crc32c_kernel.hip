@@ -88,6 +88,7 @@ constexpr int kModeEarly = 2048;    // A/B: next tile's loads issued between the
 constexpr int kModeSc0 = 4096;      // A/B: payload loads with the sc0 cache-policy bit as well
 constexpr int kModeSc1 = 8192;      // A/B: payload loads with the sc1 cache-policy bit as well
 constexpr int kModeXcdShift = 14;   // A/B: bits 14-15 = k: odd-XCD workgroups get k/64 less of the tiles
+constexpr int kModeStageShift = 16; // DIAGNOSTIC, wrong results: bits 16-17 = s: stage only 1/2^s of the image
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -587,7 +588,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     uint4 v[8];
     uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
-    for (uint32_t c = wv; !NOSTAGE && c < kStage / 1024u; c += kWaves)
+    constexpr uint32_t kStageChunks = (kStage / 1024u) >> ((MODE >> kModeStageShift) & 3);
+    for (uint32_t c = wv; !NOSTAGE && c < kStageChunks; c += kWaves)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
             (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
@@ -654,7 +656,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         __syncthreads();
         if (threadIdx.x == 0) verify_finish(p, vacc);
     }
-    if (STAMPS && lane == 0) {
+    if (STAMPS && lane == 0 && p.stamps) {  // (no buffer: a plan exec of a stamped variant)
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
         const uint32_t xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
@@ -692,6 +694,8 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_nt_xcd1", 768, 1},                     // A/B: 0 with odd-XCD workgroups given 1/64 fewer tiles
     {"s4_nt_xcd2", 768, 1},                     // A/B: ... 2/64
     {"s4_nt_xcd3", 768, 1},                     // A/B: ... 3/64
+    {"s4_nt_stamps_halfstage", 768, 1},         // DIAGNOSTIC: 5 staging half the image (wrong results)
+    {"s4_nt_stamps_quarterstage", 768, 1},      // DIAGNOSTIC: 5 staging a quarter of the image (wrong results)
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -788,6 +792,8 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 22: HDFS_LAUNCH(768, 3, kS4Nt | (1 << kModeXcdShift)); break;
     case 23: HDFS_LAUNCH(768, 3, kS4Nt | (2 << kModeXcdShift)); break;
     case 24: HDFS_LAUNCH(768, 3, kS4Nt | (3 << kModeXcdShift)); break;
+    case 25: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps | (1 << kModeStageShift)); break;
+    case 26: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps | (2 << kModeStageShift)); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();
