@@ -39,7 +39,7 @@ void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_
  * crc32c_kernel.hip kVariants): variants 5 and 6 write per-wave timestamps,
  * 4 x u64 per wave: s_memrealtime at start, after table staging, at exit;
  * XCC_ID << 32 | HW_ID, into dev_stamps, which must then hold 4 * (waves
- * launched) entries, as do 25 and 26; variants 3, 4, 6, 7, 12, 25 and 26
+ * launched) entries, as do 25, 26, 28 and 30; variants 3, 4, 6, 7, 12, 25 and 26
  * compute WRONG checksums on purpose (memory-only / compute-only ceilings;
  * 12 = memory-only at 8 waves; 25 / 26 stage only 1/2 / 1/4 of the table
  * image, to time the staging). */

@@ -89,6 +89,8 @@ constexpr int kModeSc0 = 4096;      // A/B: payload loads with the sc0 cache-pol
 constexpr int kModeSc1 = 8192;      // A/B: payload loads with the sc1 cache-policy bit as well
 constexpr int kModeXcdShift = 14;   // A/B: bits 14-15 = k: odd-XCD workgroups get k/64 less of the tiles
 constexpr int kModeStageShift = 16; // DIAGNOSTIC, wrong results: bits 16-17 = s: stage only 1/2^s of the image
+constexpr int kModeCompactDma = 1 << 18;  // A/B: T replica rows staged from the compacted rows (kernel_abi.h)
+constexpr int kModeLdsRep = 1 << 19;      // A/B: T replica rows written by ds_write_b128 from a 4 KiB copy in LDS
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -552,7 +554,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
     // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
     // its mismatch count and first bad index.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
+    constexpr bool LDSREP = S4 && (MODE & kModeLdsRep) != 0;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + (LDSREP ? 1024 + 4096 : 16)];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
     const uint8_t *table = S4 ? p.table_s4 : p.table;
@@ -589,10 +592,37 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs).
     constexpr uint32_t kStageChunks = (kStage / 1024u) >> ((MODE >> kModeStageShift) & 3);
-    for (uint32_t c = wv; !NOSTAGE && c < kStageChunks; c += kWaves)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
-            (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+    constexpr bool CDMA = S4 && (MODE & kModeCompactDma) != 0;
+    constexpr uint32_t kTChunks = uint32_t(hdfs_crc::kS4NibOff) / 1024u;  // T replica region: 128 chunks
+    if (LDSREP) {
+        // The T rows' 1024 values (4 KiB) and the N_q / Z tables by LDS-DMA,
+        // then every 1 KiB chunk of T replicas written from the LDS copy:
+        // lanes 8k..8k+7 fill row 8c + k with one ds_write_b128 each.
+        uint8_t *cv = lds + kStage + 1024;
+        for (uint32_t c = wv; c < 4u; c += kWaves)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(table + hdfs_crc::kS4Compact4Off + c * 1024u +
+                                                                  16u * uint32_t(lane)),
+                (__attribute__((address_space(3))) void *)(cv + c * 1024u), 16, 0, 0);
+        for (uint32_t c = kTChunks + wv; c < kStage / 1024u; c += kWaves)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
+                (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+        __syncthreads();
+        for (uint32_t c = wv; c < kTChunks; c += kWaves) {
+            const uint32_t v = reinterpret_cast<const uint32_t *>(cv)[8u * c + (uint32_t(lane) >> 3)];
+            *reinterpret_cast<uint4 *>(lds + c * 1024u + 16u * uint32_t(lane)) = make_uint4(v, v, v, v);
+        }
+    }
+    for (uint32_t c = wv; !LDSREP && !NOSTAGE && c < kStageChunks; c += kWaves) {
+        // CDMA: a 1 KiB chunk of the T region is 8 replica rows of 128 B;
+        // lanes 8k..8k+7 all read row 8c + k's compacted 16 B.
+        const uint8_t *src = (CDMA && c < uint32_t(hdfs_crc::kS4NibOff) / 1024u)
+                                 ? table + hdfs_crc::kTableAllocS4 + 16u * (8u * c + (uint32_t(lane) >> 3))
+                                 : table + c * 1024u + 16u * uint32_t(lane);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+    }
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
@@ -696,6 +726,10 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_nt_xcd3", 768, 1},                     // A/B: ... 3/64
     {"s4_nt_stamps_halfstage", 768, 1},         // DIAGNOSTIC: 5 staging half the image (wrong results)
     {"s4_nt_stamps_quarterstage", 768, 1},      // DIAGNOSTIC: 5 staging a quarter of the image (wrong results)
+    {"s4_nt_cdma", 768, 1},                     // A/B: 0 with T replica rows staged from compacted rows
+    {"s4_nt_cdma_stamps", 768, 1},              // DIAGNOSTIC: 27 with per-wave timestamps
+    {"s4_nt_ldsrep", 768, 1},                   // A/B: 0 with T replicas written from a 4 KiB LDS copy
+    {"s4_nt_ldsrep_stamps", 768, 1},            // DIAGNOSTIC: 29 with per-wave timestamps
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -794,6 +828,10 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 24: HDFS_LAUNCH(768, 3, kS4Nt | (3 << kModeXcdShift)); break;
     case 25: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps | (1 << kModeStageShift)); break;
     case 26: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps | (2 << kModeStageShift)); break;
+    case 27: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompactDma); break;
+    case 28: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompactDma | kModeStamps); break;
+    case 29: HDFS_LAUNCH(768, 3, kS4Nt | kModeLdsRep); break;
+    case 30: HDFS_LAUNCH(768, 3, kS4Nt | kModeLdsRep | kModeStamps); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();

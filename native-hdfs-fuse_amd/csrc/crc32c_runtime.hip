@@ -602,10 +602,15 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         affine_constants(c->c_lg[ty], c->c_small[ty], poly);
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table[ty]), kTableAlloc));
         HIP_TRY(hipMemcpy(c->d_table[ty], img.data(), kTableAlloc, hipMemcpyHostToDevice));
-        std::vector<uint8_t> img4(kTableAllocS4, 0);
+        std::vector<uint8_t> img4(kTableAllocS4Full, 0);
         build_lds_image_s4(img4.data(), poly);
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4));
-        HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4, hipMemcpyHostToDevice));
+        // compacted T rows (kernel_abi.h): row r's 16 B = its first 4 replicas
+        for (uint32_t r = 0; r < kS4CompactRows; ++r)
+            std::memcpy(img4.data() + kTableAllocS4 + 16u * r, img4.data() + 128u * r, 16);
+        for (uint32_t r = 0; r < kS4CompactRows; ++r)
+            std::memcpy(img4.data() + kS4Compact4Off + 4u * r, img4.data() + 128u * r, 4);
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4Full));
+        HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4Full, hipMemcpyHostToDevice));
     }
     *out = c.release();
     return 0;

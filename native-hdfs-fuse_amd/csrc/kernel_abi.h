@@ -14,6 +14,16 @@ constexpr uint32_t kKernelShiftOff = uint32_t(kLdsShiftOff);
 // 1024-thread workgroup (16 B per thread per round) is in bounds.
 constexpr uint32_t kTableAlloc = ((kKernelLdsBytes + 16384 - 1) / 16384) * 16384;
 constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 16384;
+// After the S4 image (at kTableAllocS4): the T0..T3 rows compacted to 16 B
+// each (4 copies of T_m[b], row r = (m >> 1) * 512 + 2 * b + (m & 1)), so an
+// LDS-DMA instruction whose 8-lane groups all read one row's 16 B fills 8
+// replica rows of 128 B while the L1 returns one 128-byte line.
+constexpr uint32_t kS4CompactRows = 1024;
+constexpr uint32_t kS4CompactBytes = kS4CompactRows * 16;
+// Then the same rows as one u32 each (4 KiB), for replication inside the LDS.
+constexpr uint32_t kS4Compact4Off = kTableAllocS4 + kS4CompactBytes;
+constexpr uint32_t kS4Compact4Bytes = kS4CompactRows * 4;
+constexpr uint32_t kTableAllocS4Full = kS4Compact4Off + kS4Compact4Bytes;
 
 struct KParams {
     const FastTile *tiles;
@@ -68,7 +78,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 27;
+constexpr int kNumVariants = 31;
 // Variants whose verification mode is built (crc32c_plan_verify).
 inline bool variant_verifies(int v) { return v >= 0 && v <= 2; }
 extern const KernelVariant kVariants[kNumVariants];
