@@ -730,6 +730,8 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_nt_cdma_stamps", 768, 1},              // DIAGNOSTIC: 27 with per-wave timestamps
     {"s4_nt_ldsrep", 768, 1},                   // A/B: 0 with T replicas written from a 4 KiB LDS copy
     {"s4_nt_ldsrep_stamps", 768, 1},            // DIAGNOSTIC: 29 with per-wave timestamps
+    {"s4_wg704x1_nt", 704, 1},                  // A/B: 0 with 11 waves per CU
+    {"s4_wg832x1_nt", 832, 1},                  // A/B: 0 with 13 waves per CU
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -832,6 +834,8 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 28: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompactDma | kModeStamps); break;
     case 29: HDFS_LAUNCH(768, 3, kS4Nt | kModeLdsRep); break;
     case 30: HDFS_LAUNCH(768, 3, kS4Nt | kModeLdsRep | kModeStamps); break;
+    case 31: HDFS_LAUNCH(704, 3, kS4Nt); break;
+    case 32: HDFS_LAUNCH(832, 4, kS4Nt); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();

@@ -78,7 +78,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 31;
+constexpr int kNumVariants = 33;
 // Variants whose verification mode is built (crc32c_plan_verify).
 inline bool variant_verifies(int v) { return v >= 0 && v <= 2; }
 extern const KernelVariant kVariants[kNumVariants];
