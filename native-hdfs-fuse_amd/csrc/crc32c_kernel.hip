@@ -91,6 +91,9 @@ constexpr int kModeXcdShift = 14;   // A/B: bits 14-15 = k: odd-XCD workgroups g
 constexpr int kModeStageShift = 16; // DIAGNOSTIC, wrong results: bits 16-17 = s: stage only 1/2^s of the image
 constexpr int kModeCompactDma = 1 << 18;  // A/B: T replica rows staged from the compacted rows (kernel_abi.h)
 constexpr int kModeLdsRep = 1 << 19;      // A/B: T replica rows written by ds_write_b128 from a 4 KiB copy in LDS
+constexpr int kModeTCols16 = 1 << 20;     // A/B: byte-table lookups from 16 of the 32 replica columns
+constexpr int kModeTCols8 = 1 << 21;      // A/B: ... from 8
+constexpr int kModeS4H = 1 << 22;         // A/B: half-column S4 image (64 KiB of T tables, 88 KiB staged)
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -180,10 +183,19 @@ struct LaneCols {
     uint32_t col4;  // (lane & 31) * 4
     uint32_t hi;    // col4 | 65536
     uint32_t nib;   // col4 | kS4NibOff
+    uint32_t toff;  // T1 - T0 (= T3 - T2) in bytes: 128, or 64 in the half-column image
 };
 
 __device__ __forceinline__ LaneCols lane_cols(uint32_t q) {
-    return LaneCols{q << 2, (q << 2) | 65536u, (q << 2) | kS4NibOff};
+    return LaneCols{q << 2, (q << 2) | 65536u, (q << 2) | kS4NibOff, 128u};
+}
+
+// Half-column S4 image (A/B, kModeS4H): T0..T3 share one 256-byte row per
+// byte value, 16 lane columns each (b*256 + m*64 + 4*(q & 15)), 64 KiB in
+// all; the N_q and Z tables stay where the full image has them.
+__device__ __forceinline__ LaneCols lane_cols_h(uint32_t q) {
+    const uint32_t c4 = (q & 15u) << 2;
+    return LaneCols{c4, c4 | 128u, (q << 2) | kS4NibOff, 64u};
 }
 
 // Byte j of v into address bits 8..15 and the column base's bytes 0 and 2
@@ -198,9 +210,9 @@ __device__ __forceinline__ uint32_t byte_addr(uint32_t v, uint32_t base) {
 // ^ T0[v.b3] (each table replicated over the 32 lane columns, so the 32
 // lanes of a half-wave always hit 32 different banks).
 __device__ __forceinline__ uint32_t s4(const uint8_t *lds, const LaneCols &c, uint32_t v, uint32_t next) {
-    const uint32_t a3 = lds_u32(lds, byte_addr<0>(v, c.hi) + 128u);  // T3: upper pair, odd
-    const uint32_t a2 = lds_u32(lds, byte_addr<1>(v, c.hi));         // T2: upper pair, even
-    const uint32_t a1 = lds_u32(lds, byte_addr<2>(v, c.col4) + 128u);  // T1
+    const uint32_t a3 = lds_u32(lds, byte_addr<0>(v, c.hi) + c.toff);  // T3: upper pair, odd
+    const uint32_t a2 = lds_u32(lds, byte_addr<1>(v, c.hi));           // T2: upper pair, even
+    const uint32_t a1 = lds_u32(lds, byte_addr<2>(v, c.col4) + c.toff);  // T1
     const uint32_t a0 = lds_u32(lds, byte_addr<3>(v, c.col4));         // T0
     return xor3(xor3(a3, a2, a1), a0, next);
 }
@@ -372,9 +384,13 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
 // lin() of pieces I0 .. I1-1 of a tile (instruction i's 16 bytes per lane).
 // GROUP > 2 (A/B): GROUP pieces' chains are left free to interleave (no
 // per-piece pin, a scheduling barrier only every GROUP pieces).
-template <int DIAG, bool S4, int I0, int I1, int GROUP = 2>
+template <int DIAG, bool S4, int I0, int I1, int GROUP = 2, uint32_t TCOLS = 31, bool H = false>
 __device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8], uint32_t pc[8], int lane) {
-    const LaneCols cols = lane_cols(uint32_t(lane & 31));
+    LaneCols cols = H ? lane_cols_h(uint32_t(lane & 31)) : lane_cols(uint32_t(lane & 31));
+    if (TCOLS != 31) {  // A/B: byte-table lookups from fewer replica columns (N_q keeps all 32)
+        cols.col4 = (uint32_t(lane) & TCOLS) << 2;
+        cols.hi = cols.col4 | 65536u;
+    }
 #pragma unroll
     for (int i = I0; i < I1; ++i) {
         pc[i] = piece<S4, DIAG>(lds, v[i], cols);
@@ -395,11 +411,11 @@ template <int DIAG, bool S4, bool VERIFY>
 __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             const uint32_t pc[8], uint32_t ev, int lane);
 
-template <int DIAG, bool S4, bool VERIFY, int GROUP = 2>
+template <int DIAG, bool S4, bool VERIFY, int GROUP = 2, uint32_t TCOLS = 31, bool H = false>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             const uint4 v[8], uint32_t ev, int lane) {
     uint32_t pc[8];
-    tile_pieces<DIAG, S4, 0, 8, GROUP>(lds, v, pc, lane);
+    tile_pieces<DIAG, S4, 0, 8, GROUP, TCOLS, H>(lds, v, pc, lane);
     reduce_emit<DIAG, S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
 }
 
@@ -496,7 +512,7 @@ __device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
                       __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
 }
 
-template <bool S4, bool VERIFY>
+template <bool S4, bool VERIFY, bool H = false>
 __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
                                          int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
@@ -521,7 +537,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
             uint32_t w[8];
             load_piece(a0, cbeg, cend, ffend, w);
             load_piece(a0 + 16, cbeg, cend, ffend, w + 4);
-            lin = piece<S4, 0>(lds, funnel(w, uint32_t(a & 15u)), lane_cols(q));
+            lin = piece<S4, 0>(lds, funnel(w, uint32_t(a & 15u)), H ? lane_cols_h(q) : lane_cols(q));
         }
         lin = allreduce32(lin);
         if (m < nbv) acc = zshift<S4>(lds, 1, acc) ^ lin;
@@ -549,6 +565,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     constexpr int GROUP = (MODE & kModeIlp8) ? 8 : (MODE & kModeIlp4) ? 4 : 2;
     constexpr bool PRIO = (MODE & kModePrio) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
+    constexpr uint32_t TCOLS = (MODE & kModeTCols8) ? 7u : (MODE & kModeTCols16) ? 15u : 31u;
+    constexpr bool H = S4 && (MODE & kModeS4H) != 0;
     constexpr int AUX = (NT ? 2 : 0) | ((MODE & kModeSc0) ? 1 : 0) | ((MODE & kModeSc1) ? 16 : 0);
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + (LDSREP ? 1024 + 4096 : 16)];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
-    const uint8_t *table = S4 ? p.table_s4 : p.table;
+    const uint8_t *table = S4 ? (H ? p.table_s4 + hdfs_crc::kS4HOff : p.table_s4) : p.table;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
 
@@ -614,7 +632,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
             *reinterpret_cast<uint4 *>(lds + c * 1024u + 16u * uint32_t(lane)) = make_uint4(v, v, v, v);
         }
     }
-    for (uint32_t c = wv; !LDSREP && !NOSTAGE && c < kStageChunks; c += kWaves) {
+    for (uint32_t c = wv; !LDSREP && !NOSTAGE && c < kStageChunks; c += (H && c + kWaves >= 64u && c + kWaves < 128u) ? kWaves + 64u : kWaves) {
         // CDMA: a 1 KiB chunk of the T region is 8 replica rows of 128 B;
         // lanes 8k..8k+7 all read row 8c + k's compacted 16 B.
         const uint8_t *src = (CDMA && c < uint32_t(hdfs_crc::kS4NibOff) / 1024u)
@@ -670,7 +688,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
         }
     } else {
         while (t < tend) {
-            finish_tile<DIAG, S4, VERIFY, GROUP>(p, lds, vacc, ft, v, ev, lane);
+            finish_tile<DIAG, S4, VERIFY, GROUP, TCOLS, H>(p, lds, vacc, ft, v, ev, lane);
             t = pool_grab(pool_ctr, lane);
             if (t >= tend) break;
             ft = tile_at(p, t);
@@ -681,7 +699,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
     const uint32_t nwaves = gridDim.x * kWaves;
     const uint32_t npairs = (p.ngen + 1u) >> 1;
-    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair<S4, VERIFY>(p, lds, vacc, g, lane);
+    for (uint32_t g = wave; g < npairs; g += nwaves) gen_pair<S4, VERIFY, H>(p, lds, vacc, g, lane);
     if (VERIFY) {
         __syncthreads();
         if (threadIdx.x == 0) verify_finish(p, vacc);
@@ -699,7 +717,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"s4_nt", 768, 1},                          // production: slicing-by-4 chains, 12 waves per CU
+    {"s4h_nt", 768, 1},                         // production: slicing-by-4 chains, half-column image, 12 waves per CU
     {"nibble_wg1024x2_nt", 1024, 2},            // A/B: positional nibble tables, 32 waves per CU
     {"s4_wg1024x1_nt", 1024, 1},                // A/B: 0 with 16 waves per CU (round-1 production)
     {"s4_wg768x1_nt_memonly", 768, 1},          // DIAGNOSTIC: memory ceiling of 0 (no lookups)
@@ -732,6 +750,10 @@ const KernelVariant kVariants[kNumVariants] = {
     {"s4_nt_ldsrep_stamps", 768, 1},            // DIAGNOSTIC: 29 with per-wave timestamps
     {"s4_wg704x1_nt", 704, 1},                  // A/B: 0 with 11 waves per CU
     {"s4_wg832x1_nt", 832, 1},                  // A/B: 0 with 13 waves per CU
+    {"s4_nt_tcols16", 768, 1},                  // A/B: 0 with byte-table lookups from 16 replica columns
+    {"s4_nt_tcols8", 768, 1},                   // A/B: 0 with byte-table lookups from 8 replica columns
+    {"s4h_nt", 768, 1},                         // A/B: 0 with the half-column image (88 KiB staged)
+    {"s4h_nt_stamps", 768, 1},                  // DIAGNOSTIC: 35 with per-wave timestamps
 };
 
 #define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
@@ -785,9 +807,9 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     if (variant == 0) {
         if (p.expect) {
             if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
-            return launch_production<kS4Nt | kModeVerify>(p, items, num_cu, stream);
+            return launch_production<kS4Nt | kModeS4H | kModeVerify>(p, items, num_cu, stream);
         }
-        return launch_production<kS4Nt>(p, items, num_cu, stream);
+        return launch_production<kS4Nt | kModeS4H>(p, items, num_cu, stream);
     }
     if (variant == 11 && !p.expect) return launch_shapes<kS4Nt>(p, items, num_cu, stream);
     const uint64_t waves = uint64_t(kv.threads / 64);
@@ -836,6 +858,10 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     case 30: HDFS_LAUNCH(768, 3, kS4Nt | kModeLdsRep | kModeStamps); break;
     case 31: HDFS_LAUNCH(704, 3, kS4Nt); break;
     case 32: HDFS_LAUNCH(832, 4, kS4Nt); break;
+    case 33: HDFS_LAUNCH(768, 3, kS4Nt | kModeTCols16); break;
+    case 34: HDFS_LAUNCH(768, 3, kS4Nt | kModeTCols8); break;
+    case 35: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H); break;
+    case 36: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H | kModeStamps); break;
     default: HDFS_LAUNCH(768, 3, kS4Nt); break;  // 10
     }
     return hipGetLastError();

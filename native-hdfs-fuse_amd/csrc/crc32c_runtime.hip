@@ -609,6 +609,16 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
             std::memcpy(img4.data() + kTableAllocS4 + 16u * r, img4.data() + 128u * r, 16);
         for (uint32_t r = 0; r < kS4CompactRows; ++r)
             std::memcpy(img4.data() + kS4Compact4Off + 4u * r, img4.data() + 128u * r, 4);
+        {  // half-column image: same N_q / Z, T0..T3 in one row per byte value
+            uint8_t *h = img4.data() + kS4HOff;
+            std::memcpy(h, img4.data(), kTableAllocS4);
+            std::memset(h, 0, kS4NibOff);
+            for (uint32_t b = 0; b < 256; ++b)
+                for (uint32_t m = 0; m < 4; ++m)
+                    for (uint32_t q = 0; q < 16; ++q)
+                        std::memcpy(h + b * 256u + m * 64u + 4u * q,
+                                    img4.data() + (m >> 1) * 65536u + b * 256u + (m & 1u) * 128u, 4);
+        }
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4Full));
         HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4Full, hipMemcpyHostToDevice));
     }

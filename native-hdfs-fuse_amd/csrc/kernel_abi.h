@@ -23,7 +23,10 @@ constexpr uint32_t kS4CompactBytes = kS4CompactRows * 16;
 // Then the same rows as one u32 each (4 KiB), for replication inside the LDS.
 constexpr uint32_t kS4Compact4Off = kTableAllocS4 + kS4CompactBytes;
 constexpr uint32_t kS4Compact4Bytes = kS4CompactRows * 4;
-constexpr uint32_t kTableAllocS4Full = kS4Compact4Off + kS4Compact4Bytes;
+// Then the half-column S4 image (A/B, kModeS4H): the full image with its T
+// region re-laid out as b*256 + m*64 + 4*(q & 15) (the first 64 KiB).
+constexpr uint32_t kS4HOff = kS4Compact4Off + kS4Compact4Bytes;
+constexpr uint32_t kTableAllocS4Full = kS4HOff + kTableAllocS4;
 
 struct KParams {
     const FastTile *tiles;
@@ -78,7 +81,7 @@ struct KernelVariant {
     uint32_t threads;
     uint32_t wg_per_cu;
 };
-constexpr int kNumVariants = 33;
+constexpr int kNumVariants = 37;
 // Variants whose verification mode is built (crc32c_plan_verify).
 inline bool variant_verifies(int v) { return v >= 0 && v <= 2; }
 extern const KernelVariant kVariants[kNumVariants];

@@ -356,7 +356,7 @@ def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     assert np.array_equal(got2[:127], got[1:128])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9, 10, 11, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 27, 29, 31, 32])
+@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9, 10, 11, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 27, 29, 31, 32, 33, 34, 35])
 def test_every_product_kernel_variant(hdfs, golden, orc, variant, monkeypatch):
     """Both table schemes (0 = slicing-by-4 chains, production; 1 = positional
     nibble tables) and the A/B shapes (2 = 16 waves per CU, 8 = descriptor
