@@ -14,14 +14,17 @@
 //    (16 B per lane) = two 512-byte blocks; lane q of each half owns bytes
 //    16q .. 16q+15 of its block in EVERY instruction.  Loads are
 //    non-temporal buffer loads bounded by the tile (partial tiles read zeros).
-//  * Lookups, production (kModeS4): each lane chains its 16-byte piece
-//    d0..d3 through the slicing-by-4 step S (crc32c.c's crc32c_table[0..3],
-//    one 4-byte column per lane so the 32 lanes of a half-wave always hit 32
-//    different banks): u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-
-//    specific operator N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the
-//    piece's contribution to the block end.  20 LDS lookups + 37 VALU per
-//    16 bytes; 152 KiB of LDS, one workgroup per CU, 12 waves (768 threads):
-//    16 waves keep 33 % more bytes in flight per CU and stream 2-3 % slower.
+//  * Lookups, production (kModeS4 | kModeS4H): each lane chains its 16-byte
+//    piece d0..d3 through the slicing-by-4 step S (crc32c.c's
+//    crc32c_table[0..3], replicated over 16 4-byte lane columns, so a
+//    half-wave's lookups are at most 2-way bank conflicts; all 32 columns,
+//    conflict-free, staged 64 KiB more and measured 1.4 % slower):
+//    u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-specific operator
+//    N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the piece's
+//    contribution to the block end.  20 LDS lookups + 37 VALU per 16 bytes;
+//    88 KiB of tables staged into a 152 KiB LDS array, one workgroup per
+//    CU, 12 waves (768 threads): 16 waves keep 33 % more bytes in flight per
+//    CU and stream 2-3 % slower.
 //  * Lookups, A/B variant 1: positional NIBBLE tables, one 128-byte row per
 //    (byte position, nibble value), 2 lookups per byte: 32 lookups + 60 VALU
 //    per 16 bytes, 72 KiB, two workgroups per CU.  The kernel is power-capped
@@ -207,7 +210,8 @@ __device__ __forceinline__ uint32_t byte_addr(uint32_t v, uint32_t base) {
 }
 
 // One slicing-by-4 step: S(v) ^ next, S(v) = T3[v.b0] ^ T2[v.b1] ^ T1[v.b2]
-// ^ T0[v.b3] (each table replicated over the 32 lane columns, so the 32
+// ^ T0[v.b3] (each table replicated over the lane columns of the image: 32,
+// or 16 in the production half-column image; so the 32
 // lanes of a half-wave always hit 32 different banks).
 __device__ __forceinline__ uint32_t s4(const uint8_t *lds, const LaneCols &c, uint32_t v, uint32_t next) {
     const uint32_t a3 = lds_u32(lds, byte_addr<0>(v, c.hi) + c.toff);  // T3: upper pair, odd
