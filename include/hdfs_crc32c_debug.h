@@ -36,10 +36,11 @@ size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags);
 void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_small4);
 
 /* Diagnostic launch of a plan with an explicit kernel variant (see
- * crc32c_kernel.hip kVariants): variants 5 and 6 write per-wave timestamps,
- * 4 x u64 per wave: s_memrealtime at start, after table staging, at exit;
- * XCC_ID << 32 | HW_ID, into dev_stamps, which must then hold 4 * (waves
- * launched) entries, as do 25, 26, 28 and 30; variants 3, 4, 6, 7, 12, 25 and 26
+ * crc32c_kernel.hip kVariants; 0 = production): variants 5, 6, 25, 26, 28,
+ * 30 and 36 (36 = the production image, 5 and 6 the full-column one) write
+ * per-wave timestamps, 4 x u64 per wave: s_memrealtime at start, after
+ * table staging, at exit; XCC_ID << 32 | HW_ID, into dev_stamps, which must
+ * then hold 4 * (waves launched) entries; variants 3, 4, 6, 7, 12, 25 and 26
  * compute WRONG checksums on purpose (memory-only / compute-only ceilings;
  * 12 = memory-only at 8 waves; 25 / 26 stage only 1/2 / 1/4 of the table
  * image, to time the staging). */
