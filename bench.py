@@ -35,9 +35,9 @@ GIB = float(1 << 30)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 KERNEL_NAME = "hdfs_crc32c_plan_kernel"
 # Template instance of the production variant on a full batch (crc32c_kernel.hip,
-# kVariants[0]: 768 threads, 3 waves/SIMD, kModeS4 | kModeNt | kModeS4H); PMC traffic is
+# kVariants[0]: 768 threads, 3 waves/SIMD, kModeS4 | kModeNt); PMC traffic is
 # only reported from a summary of this exact kernel.
-PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<768, 3, 4194307>"
+PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<768, 3, 3>"
 
 
 def load_package():

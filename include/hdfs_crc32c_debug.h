@@ -37,7 +37,7 @@ void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_
 
 /* Diagnostic launch of a plan with an explicit kernel variant (see
  * crc32c_kernel.hip kVariants; 0 = production): variants 5, 6, 25, 26, 28,
- * 30 and 36 (36 = the production image, 5 and 6 the full-column one) write
+ * 30 and 36 (36 = the half-column image, 5 and 6 the production one) write
  * per-wave timestamps, 4 x u64 per wave: s_memrealtime at start, after
  * table staging, at exit; XCC_ID << 32 | HW_ID, into dev_stamps, which must
  * then hold 4 * (waves launched) entries; variants 3, 4, 6, 7, 12, 25 and 26

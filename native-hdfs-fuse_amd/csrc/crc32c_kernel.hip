@@ -14,17 +14,16 @@
 //    (16 B per lane) = two 512-byte blocks; lane q of each half owns bytes
 //    16q .. 16q+15 of its block in EVERY instruction.  Loads are
 //    non-temporal buffer loads bounded by the tile (partial tiles read zeros).
-//  * Lookups, production (kModeS4 | kModeS4H): each lane chains its 16-byte
-//    piece d0..d3 through the slicing-by-4 step S (crc32c.c's
-//    crc32c_table[0..3], replicated over 16 4-byte lane columns, so a
-//    half-wave's lookups are at most 2-way bank conflicts; all 32 columns,
-//    conflict-free, staged 64 KiB more and measured 1.4 % slower):
-//    u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-specific operator
-//    N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the piece's
-//    contribution to the block end.  20 LDS lookups + 37 VALU per 16 bytes;
-//    88 KiB of tables staged into a 152 KiB LDS array, one workgroup per
-//    CU, 12 waves (768 threads): 16 waves keep 33 % more bytes in flight per
-//    CU and stream 2-3 % slower.
+//  * Lookups, production (kModeS4): each lane chains its 16-byte piece
+//    d0..d3 through the slicing-by-4 step S (crc32c.c's crc32c_table[0..3],
+//    one 4-byte column per lane so the 32 lanes of a half-wave always hit 32
+//    different banks): u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-
+//    specific operator N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the
+//    piece's contribution to the block end.  20 LDS lookups + 37 VALU per
+//    16 bytes; 152 KiB of LDS, one workgroup per CU, 12 waves (768 threads):
+//    16 waves keep 33 % more bytes in flight per CU and stream 2-3 % slower.
+//    (The half-column image, kModeS4H, stages 64 KiB less and wins short
+//    bursts, but its 2-way bank conflicts lose 1.7 % sustained.)
 //  * Lookups, A/B variant 1: positional NIBBLE tables, one 128-byte row per
 //    (byte position, nibble value), 2 lookups per byte: 32 lookups + 60 VALU
 //    per 16 bytes, 72 KiB, two workgroups per CU.  The kernel is power-capped
@@ -721,7 +720,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(KParams 
 
 namespace hdfs_crc {
 const KernelVariant kVariants[kNumVariants] = {
-    {"s4h_nt", 768, 1},                         // production: slicing-by-4 chains, half-column image, 12 waves per CU
+    {"s4_nt", 768, 1},                          // production: slicing-by-4 chains, 12 waves per CU
     {"nibble_wg1024x2_nt", 1024, 2},            // A/B: positional nibble tables, 32 waves per CU
     {"s4_wg1024x1_nt", 1024, 1},                // A/B: 0 with 16 waves per CU (round-1 production)
     {"s4_wg768x1_nt_memonly", 768, 1},          // DIAGNOSTIC: memory ceiling of 0 (no lookups)
@@ -811,9 +810,9 @@ hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hi
     if (variant == 0) {
         if (p.expect) {
             if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
-            return launch_production<kS4Nt | kModeS4H | kModeVerify>(p, items, num_cu, stream);
+            return launch_production<kS4Nt | kModeVerify>(p, items, num_cu, stream);
         }
-        return launch_production<kS4Nt | kModeS4H>(p, items, num_cu, stream);
+        return launch_production<kS4Nt>(p, items, num_cu, stream);
     }
     if (variant == 11 && !p.expect) return launch_shapes<kS4Nt>(p, items, num_cu, stream);
     const uint64_t waves = uint64_t(kv.threads / 64);

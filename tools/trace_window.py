@@ -6,7 +6,7 @@ ones.  Writes the window's average / median / min / max (ns) so it can be
 compared with bench.py's own HIP-event average for the same run.
 
     python tools/trace_window.py gpurun_out/prof/run_kernel_trace.csv \
-        --kernel "hdfs_crc32c_plan_kernel<768, 3, 4194307>" [--warmup 500 --steps 2000] [--out f.json]
+        --kernel "hdfs_crc32c_plan_kernel<768, 3, 3>" [--warmup 500 --steps 2000] [--out f.json]
 """
 from __future__ import annotations
 
