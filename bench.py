@@ -311,7 +311,7 @@ def main():
     read_probe = None
     if rank == 0 and world == 1 and nbuf > 1:
         probe_out = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
-        L = hdfs.lib()
+        L = hdfs.debug_lib()  # the read probe lives in the debug library, not the product
 
         def probe(i):
             rc = L.crc32c_debug_stream_probe(bufs[i % nbuf].data_ptr(), extent, probe_out.data_ptr(), 512, 2, sptr)

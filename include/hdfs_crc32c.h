@@ -5,8 +5,12 @@
  * Every entry point is plain C: pointers, sizes and integers, no HIP or torch
  * types in the signatures (a HIP stream is passed as `void *`).  Batch entry
  * points return 0 on success or a negative errno, the reference's convention
- * (src/hadooprpc.c:440-486, 630-636).  They never fall back to a CPU
- * implementation: without a usable GPU they return -ENODEV.
+ * (src/hadooprpc.c:440-486, 630-636).  The GPU entry points never fall back
+ * to a CPU implementation on their own: without a usable GPU they return
+ * -ENODEV.  The two host-memory calls the per-packet loop uses
+ * (crc32c_chunks, crc32c_batch_host) take CRC32C_CPU_FALLBACK to finish on
+ * the host CPU instead (the reference's crc32c() cannot fail), and
+ * crc32c_last_path() says which path ran.
  *
  * Reference interfaces replaced (file:line under the reference tree):
  *   crc32c()             src/crc32c.c:333-343 (declared by hand at src/hadooprpc.c:31)
@@ -14,9 +18,17 @@
  *                        src/hadooprpc.c:639 + 727-748 (roundup, crc32c(0, ...), htonl)
  *   crc32c_packetize()   the packet cutting of hadoop_rpc_send_packets,
  *                        src/hadooprpc.c:827-857
+ *   crc32c_plan_create_buffers()
+ *                        hadoop_rpc_send_packets over a Hadoop_Fuse_Buffer_Pos
+ *                        (src/hadooprpc.c:815-860 packet cutting, 666-725 packet
+ *                        assembly, src/hadooprpc.h:33-45 the buffer types)
  *   crc32c_multi_*()     no reference counterpart: blocks written in parallel
  *                        (src/fuse.c:580-647 writes them one at a time) sharded
- *                        over several GPUs of one node.
+ *                        over several GPUs of one node, RCCL gather.
+ *   crc32c_verify_frames_host()
+ *                        hadoop_rpc_receive_packets (src/hadooprpc.c:497-584)
+ *                        with sendChecksums (the reference asks for none,
+ *                        src/fuse.c:1608-1609)
  */
 #ifndef HDFS_CRC32C_H
 #define HDFS_CRC32C_H
@@ -28,7 +40,7 @@
 extern "C" {
 #endif
 
-#define HDFS_CRC32C_ABI_VERSION 1
+#define HDFS_CRC32C_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------
  * 1. Drop-in scalar checksum (host CPU).
@@ -57,6 +69,17 @@ uint32_t hdfs_crc32(uint32_t crc, const void *buf, size_t len);
                                         different device buffers, e.g. many HDFS blocks;
                                         exec / verify then take dev_payload = NULL.  Not
                                         valid for the host-resident calls. */
+#define CRC32C_CPU_FALLBACK 0x8u /* crc32c_chunks / crc32c_batch_host only: when the GPU
+                                    is unavailable or a HIP call fails, compute on the host
+                                    CPU (crc32c_chunks_cpu) and return 0; crc32c_last_path()
+                                    then reports CRC32C_PATH_CPU */
+
+/* Which path the calling thread's last crc32c_chunks / crc32c_batch_host
+ * call took. */
+#define CRC32C_PATH_NONE 0 /* failed, or nothing to compute */
+#define CRC32C_PATH_GPU 1
+#define CRC32C_PATH_CPU 2  /* CRC32C_CPU_FALLBACK taken */
+int crc32c_last_path(void);
 
 /* One packet of a batch: `len` payload bytes starting `payload_off` bytes into
  * the batch payload buffer, cut into chunks of `bpc` bytes
@@ -144,10 +167,35 @@ uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
  * (no separate reset of dev_result).  A plan's verify launches share its
  * device scratch, so the library keeps them in GPU order, also across
  * streams (a verify launch on another stream than the plan's previous one
- * waits for it).  Kernel variants other than 0 to 2
- * ($HDFS_CRC32C_KVARIANT, A/B only) return -EINVAL. */
+ * waits for it). */
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream);
+
+/* Packet assembly from scatter buffers (hadooprpc.h:33-45, hadooprpc.c:666-725).
+ * The bytes a block write sends are `len` bytes starting `bufferoffset` into
+ * the concatenation of buffers[0 .. n_buffers); a buffer with data == NULL is
+ * `len` zero bytes (Hadoop_Fuse_Buffer).  FUSE writes use up to four:
+ * TRUNCATE, NULLPADDING, THEDATA, TRAILINGDATA (fuse.c:1348-1354), and
+ * ftruncate-extension one NULL buffer (fuse.c:1137-1142). */
+typedef struct crc32c_buffer {
+    const void *data; /* device address, or NULL = zero fill */
+    uint64_t len;
+} crc32c_buffer;
+
+/* Plan of hadoop_rpc_send_packets(from = {buffers, n_buffers, bufferoffset},
+ * len, blockoffset, packetsize, checksum{bpc}) (hadooprpc.c:815-860): the
+ * packets crc32c_packetize(len, blockoffset, packetsize, bpc) lists, each
+ * cut into chunks from its own start (hadooprpc.c:733-742), their checksums
+ * at out indices 0, 1, ... in packet order.  Exec / verify take dev_payload
+ * = NULL (the plan holds the buffer addresses, which must stay valid).
+ * Chunks inside one data buffer are read in place (no assembly copy); a
+ * chunk spanning buffers is read piece by piece; a chunk of zero fill only
+ * is written from a plan-time constant without reading anything, so an
+ * all-NULL write reads no payload at all.  flags: CRC32C_BIG_ENDIAN,
+ * CRC32C_TYPE_CRC32.  -EINVAL when the range exceeds the buffers. */
+int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, uint32_t n_buffers,
+                               uint64_t bufferoffset, uint64_t len, uint64_t blockoffset, uint32_t packetsize,
+                               uint32_t bpc, uint32_t flags, crc32c_plan **out);
 
 /* One-shot device batch: builds a plan, runs it on `stream` and waits for it. */
 int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,
@@ -176,15 +224,57 @@ int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_pa
 int crc32c_chunks(const void *packet, size_t len, uint32_t bpc, uint32_t *out, uint32_t flags);
 
 /* ---------------------------------------------------------------------------
- * 5. Several GPUs of one node, one process.  Packets are sharded in groups of
+ * 5. Several GPUs of one node.  A file's packets are sharded in groups of
  * `group_packets` consecutive packets (64 = one 4 MiB HDFS block of 64 KiB
- * packets) dealt round-robin over the devices; each device checksums its
- * shard and copies its checksums straight into the host `out` array.
+ * packets), group g on rank g % nranks.  Each rank checksums its shard on
+ * its own GPU; RCCL point-to-point transfers over xGMI (one ncclGroupStart /
+ * ncclGroupEnd) gather the u32 checksum arrays into block order on rank 0.
+ * The communicator spans the devices of one process (crc32c_multi_create,
+ * ranks = the devices in the order given) or one device per process
+ * (crc32c_multi_create_rank: every rank calls it at the same time with the
+ * id rank 0 got from crc32c_multi_unique_id and sent to the others).
  * ------------------------------------------------------------------------- */
 typedef struct crc32c_multi crc32c_multi;
 
 int crc32c_multi_create(const int *devices, int ndevices, crc32c_multi **out);
+int crc32c_multi_unique_id(uint8_t id[128]);
+int crc32c_multi_create_rank(int device, int rank, int nranks, const uint8_t id[128], crc32c_multi **out);
 int crc32c_multi_destroy(crc32c_multi *m);
+/* Waits for the library's own per-device streams (used when exec gets none). */
+int crc32c_multi_sync(crc32c_multi *m);
+
+/* Shard layout (host only, no GPU): returns the number of groups G and, per
+ * group g, layout[4g .. 4g+3] = {rank, offset of the group's first byte in
+ * that rank's shard buffer, offset of that byte in the caller's payload,
+ * bytes}; a group's bytes move as one range (its 16-byte phase is kept).
+ * shard_bytes[r] (optional) = bytes of rank r's shard.  A group's checksums
+ * must form one contiguous range of out indices. */
+int64_t crc32c_multi_layout(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                            uint64_t *layout, uint64_t *shard_bytes);
+/* Rank `rank`'s packets with payload offsets into its shard buffer (out
+ * indices unchanged); returns their count (copies at most cap). */
+int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                                   int rank, crc32c_packet *local, size_t cap);
+
+/* Device-resident multi-GPU plan of a file's packets (offsets in the caller's
+ * file layout; every process passes the same list).  Exec: dev_shards[i] =
+ * the shard of the i-th local device (laid out as crc32c_multi_layout says),
+ * root_out = nchecksums device u32s on rank 0's device (rank 0's process
+ * only), streams[i] (or NULL = the library's streams).  Asynchronous: the
+ * checksum launches, then the RCCL gather, on the local devices' streams;
+ * root_out is complete when rank 0's stream is. */
+typedef struct crc32c_multi_plan crc32c_multi_plan;
+int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
+                             uint32_t flags, crc32c_multi_plan **out);
+int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards, uint32_t *root_out,
+                           void *const *streams);
+int crc32c_multi_plan_destroy(crc32c_multi_plan *mp);
+uint64_t crc32c_multi_plan_nchecksums(const crc32c_multi_plan *mp);
+uint64_t crc32c_multi_plan_shard_bytes(const crc32c_multi_plan *mp, int rank);
+
+/* Host-resident: each local device checksums its groups (dealt round-robin
+ * over the local devices) from host memory over its own PCIe link and
+ * copies its checksums straight into the host `out` array. */
 int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_packet *pkts, size_t npkts,
                             uint32_t group_packets, uint32_t *out, uint32_t flags);
 
@@ -215,6 +305,52 @@ size_t crc32c_frame_packets(const crc32c_packet *pkts, size_t npkts, const uint3
  * MD5 over a block's checksums as big-endian bytes (`sums` in host order, or
  * wire order with CRC32C_BIG_ENDIAN). */
 void crc32c_block_md5(const uint32_t *sums, size_t n, uint32_t flags, uint8_t md5[16]);
+
+/* The read side ("next" row 1): the packet stream a DataNode sends for
+ * OP_READ_BLOCK with sendChecksums, per packet PLEN (u32 BE) | HLEN (u16 BE)
+ * | PacketHeaderProto | checksums (u32 BE) | data (hadoop_rpc_receive_packets,
+ * src/hadooprpc.c:497-584; datatransfer.proto:184-191). */
+typedef struct crc32c_frame_info {
+    uint64_t frame_off;      /* offset of the frame's PLEN in the buffer */
+    uint64_t sums_off;       /* offset of its checksums */
+    uint64_t data_off;       /* offset of its data */
+    int64_t offset_in_block; /* PacketHeaderProto.offsetInBlock */
+    int64_t seqno;           /* PacketHeaderProto.seqno */
+    uint32_t data_len;       /* PacketHeaderProto.dataLen */
+    uint32_t nsums;          /* checksums in the frame ((PLEN - 4 - dataLen) / 4) */
+    uint32_t last;           /* PacketHeaderProto.lastPacketInBlock */
+    uint32_t reserved;
+} crc32c_frame_info;
+
+/* Whole frames at the start of `frames` (stops before a partial frame and
+ * after a lastPacketInBlock frame): returns their count (fills at most cap
+ * entries of info), *consumed = their bytes; -EBADMSG for a malformed frame. */
+int64_t crc32c_parse_frames(const void *frames, size_t bytes, crc32c_frame_info *info, size_t cap,
+                            uint64_t *consumed);
+
+typedef struct crc32c_frames_result {
+    uint64_t packets;          /* frames parsed (whole frames) */
+    uint64_t data_bytes;
+    uint64_t checksums;        /* checksums compared */
+    uint64_t mismatches;
+    uint64_t first_bad;        /* index of the first bad checksum in the run, UINT64_MAX if none */
+    int64_t first_bad_offset;  /* offsetInBlock of its chunk, -1 if none */
+    uint64_t consumed;         /* bytes of the whole frames parsed */
+    uint32_t last_packet;      /* a lastPacketInBlock frame was seen */
+    uint32_t reserved;
+} crc32c_frames_result;
+
+/* Verifies a run of received frames on the GPU (host-resident: the frame
+ * buffer is copied once and every chunk is checked against the checksums in
+ * front of it; nothing is de-interleaved by the caller).  chunk_offset =
+ * ReadOpChecksumInfoProto.chunkOffset (datatransfer.proto:218-227): the
+ * first data packet must start there, every packet on a chunk boundary
+ * right after the previous one; the caller skips requested offset -
+ * chunkOffset bytes of the first packet's data, as hadooprpc.c:548-560
+ * does.  flags: CRC32C_TYPE_CRC32 for CHECKSUM_CRC32, CRC32C_CPU_FALLBACK.
+ * 0 (result in *res), -EBADMSG for a malformed or misplaced frame, or -errno. */
+int crc32c_verify_frames_host(crc32c_ctx *ctx, const void *frames, size_t bytes, uint32_t bpc,
+                              uint64_t chunk_offset, uint32_t flags, crc32c_frames_result *res);
 
 /* Last error text of the calling thread (static storage, never NULL). */
 const char *crc32c_last_error(void);

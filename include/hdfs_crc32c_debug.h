@@ -1,8 +1,15 @@
 /*
- * hdfs_crc32c_debug.h -- introspection hooks of libhdfs_crc32c.so used by the
- * CPU test-suite to check the GPU path's host-side inputs without a GPU:
- * the work decomposition and the LDS table image the kernel loads.
- * Not needed by a reference-side integration.
+ * hdfs_crc32c_debug.h -- introspection and diagnostic hooks.
+ *
+ * Section 1 is exported by libhdfs_crc32c.so (host-side only, no launch):
+ * the CPU test-suite checks the GPU path's host-side inputs with it without a
+ * GPU -- the work decomposition and the LDS table image the kernel loads.
+ *
+ * Section 2 is exported only by libhdfs_crc32c_debug.so (built beside the
+ * product library, linked against it): A/B and diagnostic kernel variants
+ * and a plain HBM read probe, for tools/ and the bench's read-rate
+ * reference.  The product library never launches anything but the
+ * production kernel.  Not needed by a reference-side integration.
  */
 #ifndef HDFS_CRC32C_DEBUG_H
 #define HDFS_CRC32C_DEBUG_H
@@ -16,43 +23,54 @@
 extern "C" {
 #endif
 
+/* ---- 1. libhdfs_crc32c.so ---- */
+
 /* Work items a plan would upload: 16-byte FastTile {u64 src, u32 out,
- * u32 meta = nblocks | lg << 8} and 16-byte GenItem {u64 src, u32 out,
- * u32 len}.  Copies at most *_cap items; counts go to *ntiles / *ngen. */
+ * u32 meta} (meta: nblocks | lg << 8, or bit 31 | nch * k | k << 8 |
+ * nch << 13 | pad << 18 for a general tile) and 16-byte GenItem {u64 src,
+ * u32 out, u32 len}.  Copies at most *_cap items; counts go to *ntiles /
+ * *ngen. */
 int crc32c_debug_plan(const crc32c_packet *pkts, size_t npkts, void *tiles, size_t tiles_cap, void *gen,
                       size_t gen_cap, uint64_t *ntiles, uint64_t *ngen);
 
-/* The LDS image the kernel stages (returns its size; fills dst when cap is
- * large enough) and the affine constants crc32c(0, zeros(512 << lg)),
+/* Item counts of a crc32c_plan_create_buffers plan (CRC32C): counts[0..5] =
+ * tiles, gen items, seg items, pieces, constant runs, checksums. */
+int crc32c_debug_write_plan(const crc32c_buffer *buffers, uint32_t n_buffers, uint64_t bufferoffset, uint64_t len,
+                            uint64_t blockoffset, uint32_t packetsize, uint32_t bpc, uint64_t counts[6]);
+
+/* The LDS image the nibble variant stages (returns its size; fills dst when
+ * cap is large enough) and the affine constants crc32c(0, zeros(512 << lg)),
  * lg = 0..4, and crc32c(0, zeros(r)), r = 0..3. */
 size_t crc32c_debug_lds_image(void *dst, size_t cap, uint32_t *c_lg5, uint32_t *c_small4);
 
 /* The slicing-by-4 kernel's LDS image for the checksum type in `flags`
- * (byte tables T0..T3 replicated over
- * the 32 lane columns, the per-column finishing operators N_q, the Z^(512 s)
- * shifts); returns its size and fills dst when cap is large enough. */
+ * (byte tables T0..T3 replicated over the 32 lane columns, the per-column
+ * finishing operators N_q, the Z^(512 s) shifts); returns its size and
+ * fills dst when cap is large enough. */
 size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags);
 /* The affine constants of the checksum type in `flags` (CRC32C_TYPE_CRC32 or not). */
 void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_small4);
 
-/* Diagnostic launch of a plan with an explicit kernel variant (see
- * crc32c_kernel.hip kVariants; 0 = production): variants 5, 6, 25, 26, 28,
- * 30 and 36 (36 = the half-column image, 5 and 6 the production one) write
- * per-wave timestamps, 4 x u64 per wave: s_memrealtime at start, after
- * table staging, at exit; XCC_ID << 32 | HW_ID, into dev_stamps, which must
- * then hold 4 * (waves launched) entries; variants 3, 4, 6, 7, 12, 25 and 26
- * compute WRONG checksums on purpose (memory-only / compute-only ceilings;
- * 12 = memory-only at 8 waves; 25 / 26 stage only 1/2 / 1/4 of the table
- * image, to time the staging). */
+/* ---- 2. libhdfs_crc32c_debug.so only ---- */
+
+/* Launch of a plan with an explicit kernel variant (0 = production; see
+ * debug/crc32c_variants.hip): 5, 6 and 36 write per-wave timestamps, 4 x
+ * u64 per wave (s_memrealtime at start, after table staging, at exit;
+ * XCC_ID << 32 | HW_ID) into dev_stamps, which must then hold 4 * (waves
+ * launched) entries; 3, 4, 6 and 7 compute WRONG checksums on purpose
+ * (memory-only / compute-only ceilings).  -EINVAL for a variant not built. */
 int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
                                    uint64_t *dev_stamps, int variant, void *stream);
+/* Name of a built variant (NULL if none); *exact = 1 when it computes the
+ * right checksums. */
+const char *crc32c_debug_variant_name(int variant, int *exact);
 
-/* DIAGNOSTIC: plain streaming read of `bytes` device bytes; writes one
- * dword per thread to dev_out (at most 2^20 dwords).  Shapes 0-7: grid x 256
- * threads, grid-stride, 16 B per lane, 4 / 8 / 4 nt / 16 / 2 nt / 8 nt /
- * 16 nt / 1 nt loads in flight per lane; shapes 8-15: tile reads like the
- * CRC kernel's (1024 or 512 threads, 8 or 4 KiB per wave, per-workgroup
- * ranges or grid-stride tiles), see stream_probe.hip.  Prices the HBM read
+/* Plain streaming read of `bytes` device bytes; writes one dword per thread
+ * to dev_out (at most 2^20 dwords).  Shapes 0-7: grid x 256 threads,
+ * grid-stride, 16 B per lane, 4 / 8 / 4 nt / 16 / 2 nt / 8 nt / 16 nt / 1 nt
+ * loads in flight per lane; shapes 8-15: tile reads like the CRC kernel's
+ * (1024 or 512 threads, 8 or 4 KiB per wave, per-workgroup ranges or
+ * grid-stride tiles), see debug/stream_probe.hip.  Prices the HBM read
  * roofline this device actually delivers (tools/probe_sweep.py). */
 int crc32c_debug_stream_probe(const void *dev_src, uint64_t bytes, uint32_t *dev_out, uint32_t grid, int shape,
                               void *stream);

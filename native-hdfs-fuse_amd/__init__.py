@@ -23,17 +23,31 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libhdfs_crc32c.so")
+DEBUG_LIB_PATH = os.path.join(HERE, "libhdfs_crc32c_debug.so")  # A/B variants + read probe (tools only)
 INCLUDE_DIR = os.path.join(os.path.dirname(HERE), "include")
 
 CRC32C_BIG_ENDIAN = 0x1
 CRC32C_TYPE_CRC32 = 0x2  # Hadoop CHECKSUM_CRC32 (zlib polynomial) instead of CRC32C
 CRC32C_DEVICE_ADDRESSES = 0x4  # plan flag: payload_off are device addresses; exec/verify take payload 0
+CRC32C_CPU_FALLBACK = 0x8  # crc32c_chunks / crc32c_batch_host: finish on the host CPU if the GPU fails
+PATH_NONE, PATH_GPU, PATH_CPU = 0, 1, 2  # crc32c_last_path()
 
 PACKET_DTYPE = np.dtype(
     [("payload_off", "<u8"), ("out_idx", "<u8"), ("len", "<u4"), ("bpc", "<u4")], align=True
 )
 TILE_DTYPE = np.dtype([("src", "<u8"), ("out", "<u4"), ("meta", "<u4")])
 GEN_DTYPE = np.dtype([("src", "<u8"), ("out", "<u4"), ("len", "<u4")])
+BUFFER_DTYPE = np.dtype([("data", "<u8"), ("len", "<u8")])  # crc32c_buffer (data 0 = zero fill)
+FRAME_DTYPE = np.dtype([("frame_off", "<u8"), ("sums_off", "<u8"), ("data_off", "<u8"), ("offset_in_block", "<i8"),
+                        ("seqno", "<i8"), ("data_len", "<u4"), ("nsums", "<u4"), ("last", "<u4"),
+                        ("reserved", "<u4")])
+
+
+class FramesResult(ctypes.Structure):
+    _fields_ = [("packets", ctypes.c_uint64), ("data_bytes", ctypes.c_uint64), ("checksums", ctypes.c_uint64),
+                ("mismatches", ctypes.c_uint64), ("first_bad", ctypes.c_uint64),
+                ("first_bad_offset", ctypes.c_int64), ("consumed", ctypes.c_uint64),
+                ("last_packet", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class Crc32cError(RuntimeError):
@@ -51,6 +65,7 @@ def build(quiet: bool = True) -> str:
 
 
 _LIB = None
+_DEBUG_LIB = None
 
 
 def lib():
@@ -60,17 +75,45 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise FileNotFoundError(LIB_PATH + " is not built (run build())")
         # One HIP runtime per process: torch ships its own libamdhip64 and
-        # links it by the unversioned name, so it must be loaded first; our
-        # NEEDED libamdhip64.so.7 then binds to the same copy by SONAME.
-        # (Loaded the other way round the process would hold two runtimes and
-        # torch would see no device.)  torch is plumbing only (device memory,
-        # streams, torch.distributed); nothing here computes with it.
+        # librccl and links them by the unversioned names, so it must be
+        # loaded first; our NEEDED libamdhip64.so.7 / librccl.so.1 then bind
+        # to the same copies by SONAME.  (Loaded the other way round the
+        # process would hold two runtimes and torch would see no device.)
+        # torch is plumbing only (device memory, streams, torch.distributed);
+        # nothing here computes with it.
         try:
             import torch  # noqa: F401
         except ImportError:
             pass
         _LIB = _bind(ctypes.CDLL(LIB_PATH))
     return _LIB
+
+
+def debug_lib():
+    """libhdfs_crc32c_debug.so (A/B kernel variants, HBM read probe); it links
+    against the product library, which is loaded first."""
+    global _DEBUG_LIB
+    if _DEBUG_LIB is None:
+        lib()
+        if not os.path.exists(DEBUG_LIB_PATH):
+            raise FileNotFoundError(DEBUG_LIB_PATH + " is not built (run build())")
+        L = ctypes.CDLL(DEBUG_LIB_PATH)
+        vp, i32 = ctypes.c_void_p, ctypes.c_int
+        L.crc32c_debug_plan_exec_variant.restype = i32
+        L.crc32c_debug_plan_exec_variant.argtypes = [vp, vp, vp, vp, i32, vp]
+        L.crc32c_debug_stream_probe.restype = i32
+        L.crc32c_debug_stream_probe.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint32, i32, vp]
+        L.crc32c_debug_variant_name.restype = ctypes.c_char_p
+        L.crc32c_debug_variant_name.argtypes = [i32, ctypes.POINTER(i32)]
+        _DEBUG_LIB = L
+    return _DEBUG_LIB
+
+
+def variant_info(v: int):
+    """(name, exact) of a kernel variant built into the debug library, or None."""
+    ex = ctypes.c_int(0)
+    name = debug_lib().crc32c_debug_variant_name(v, ctypes.byref(ex))
+    return None if name is None else (name.decode(), bool(ex.value))
 
 
 def _bind(L):
@@ -106,8 +149,21 @@ def _bind(L):
         "crc32c_verify_host": (ctypes.c_int64, [vp, vp, vp, sz, vp, u32, vp]),
         "crc32c_debug_affine_constants": (None, [u32, vp, vp]),
         "hdfs_crc32": (u32, [u32, vp, sz]),
-        "crc32c_debug_plan_exec_variant": (i32, [vp, vp, vp, vp, i32, vp]),
-        "crc32c_debug_stream_probe": (i32, [vp, u64, vp, u32, i32, vp]),
+        "crc32c_last_path": (i32, []),
+        "crc32c_plan_create_buffers": (i32, [vp, vp, u32, u64, u64, u64, u32, u32, u32, pp]),
+        "crc32c_debug_write_plan": (i32, [vp, u32, u64, u64, u64, u32, u32, vp]),
+        "crc32c_multi_unique_id": (i32, [vp]),
+        "crc32c_multi_create_rank": (i32, [i32, i32, i32, vp, pp]),
+        "crc32c_multi_sync": (i32, [vp]),
+        "crc32c_multi_layout": (ctypes.c_int64, [vp, sz, u32, i32, vp, vp]),
+        "crc32c_multi_shard_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, vp, sz]),
+        "crc32c_multi_plan_create": (i32, [vp, vp, sz, u32, u32, pp]),
+        "crc32c_multi_plan_exec": (i32, [vp, vp, vp, vp]),
+        "crc32c_multi_plan_destroy": (i32, [vp]),
+        "crc32c_multi_plan_nchecksums": (u64, [vp]),
+        "crc32c_multi_plan_shard_bytes": (u64, [vp, i32]),
+        "crc32c_parse_frames": (ctypes.c_int64, [vp, sz, vp, sz, ctypes.POINTER(u64)]),
+        "crc32c_verify_frames_host": (i32, [vp, vp, sz, u32, u64, u32, ctypes.POINTER(FramesResult)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -211,6 +267,20 @@ class Context:
     def plan(self, pkts, flags: int = 0) -> "Plan":
         return Plan(self, pkts, flags)
 
+    def write_plan(self, buffers, bufferoffset: int, length: int, blockoffset: int = 0, packetsize: int = 65536,
+                   bpc: int = 512, flags: int = 0) -> "Plan":
+        """crc32c_plan_create_buffers: hadoop_rpc_send_packets over a buffer list
+        [(device address or 0 for zero fill, length), ...]; exec with payload 0."""
+        return Plan(self, None, flags, write=(buffers, bufferoffset, length, blockoffset, packetsize, bpc))
+
+    def verify_frames(self, frames: np.ndarray, bpc: int, chunk_offset: int, flags: int = 0) -> FramesResult:
+        """crc32c_verify_frames_host over a buffer of received packet frames."""
+        frames = np.ascontiguousarray(frames, dtype=np.uint8)
+        res = FramesResult()
+        _check(lib().crc32c_verify_frames_host(self.handle, _np_ptr(frames), frames.size, bpc, chunk_offset, flags,
+                                               ctypes.byref(res)), "crc32c_verify_frames_host")
+        return res
+
     def batch_host(self, payload: np.ndarray, pkts, flags: int = 0, out: np.ndarray | None = None) -> np.ndarray:
         """Host-resident batch (crc32c_batch_host): H2D copy -> kernel -> checksums in host memory."""
         pkts = as_packets(pkts)
@@ -243,11 +313,18 @@ class Context:
 class Plan:
     """Device-resident batch plan (crc32c_plan): build once, execute many."""
 
-    def __init__(self, ctx: Context, pkts, flags: int = 0):
-        pkts = as_packets(pkts)
+    def __init__(self, ctx: Context, pkts, flags: int = 0, write=None):
         h = ctypes.c_void_p()
-        _check(lib().crc32c_plan_create(ctx.handle, _np_ptr(pkts), pkts.size, flags, ctypes.byref(h)),
-               "crc32c_plan_create")
+        if write is None:
+            pkts = as_packets(pkts)
+            _check(lib().crc32c_plan_create(ctx.handle, _np_ptr(pkts), pkts.size, flags, ctypes.byref(h)),
+                   "crc32c_plan_create")
+        else:
+            buffers, bufferoffset, length, blockoffset, packetsize, bpc = write
+            bufs = as_buffers(buffers)
+            _check(lib().crc32c_plan_create_buffers(ctx.handle, _np_ptr(bufs), bufs.size, bufferoffset, length,
+                                                    blockoffset, packetsize, bpc, flags, ctypes.byref(h)),
+                   "crc32c_plan_create_buffers")
         self.ctx = ctx  # keeps the context alive
         self.handle = h
         self.nchecksums = int(lib().crc32c_plan_nchecksums(h))
@@ -263,9 +340,10 @@ class Plan:
                                         ctypes.c_void_p(dev_result), ctypes.c_void_p(stream)), "crc32c_plan_verify")
 
     def exec_variant(self, dev_payload: int, dev_out: int, variant: int, dev_stamps: int = 0, stream: int = 0) -> None:
-        """Diagnostic: run an explicit kernel variant (3/6 write per-wave timestamps)."""
-        _check(lib().crc32c_debug_plan_exec_variant(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
-                                                    ctypes.c_void_p(dev_stamps), variant, ctypes.c_void_p(stream)),
+        """Diagnostic (debug library): run an explicit kernel variant (5/6/36 write per-wave timestamps)."""
+        _check(debug_lib().crc32c_debug_plan_exec_variant(self.handle, ctypes.c_void_p(dev_payload),
+                                                          ctypes.c_void_p(dev_out), ctypes.c_void_p(dev_stamps),
+                                                          variant, ctypes.c_void_p(stream)),
                "crc32c_debug_plan_exec_variant")
 
     def close(self) -> None:
@@ -280,14 +358,36 @@ class Plan:
             pass
 
 
-class Multi:
-    """Several GPUs of one node in one process (crc32c_multi)."""
+def multi_unique_id() -> bytes:
+    """crc32c_multi_unique_id: the 128-byte RCCL id rank 0 sends to the other ranks."""
+    buf = (ctypes.c_uint8 * 128)()
+    _check(lib().crc32c_multi_unique_id(buf), "crc32c_multi_unique_id")
+    return bytes(buf)
 
-    def __init__(self, devices):
-        devs = (ctypes.c_int * len(devices))(*devices)
+
+class Multi:
+    """Several GPUs of one node (crc32c_multi): all devices of this process
+    (``Multi([0, 1, ...])``), or one device of a one-process-per-GPU job
+    (``Multi(device=d, rank=r, nranks=n, uid=bytes)``)."""
+
+    def __init__(self, devices=None, device: int = 0, rank: int = 0, nranks: int = 1, uid: bytes | None = None):
         h = ctypes.c_void_p()
-        _check(lib().crc32c_multi_create(devs, len(devices), ctypes.byref(h)), "crc32c_multi_create")
+        if uid is None:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            _check(lib().crc32c_multi_create(devs, len(devices), ctypes.byref(h)), "crc32c_multi_create")
+            self.local_devices = list(devices)
+        else:
+            idb = (ctypes.c_uint8 * 128)(*uid)
+            _check(lib().crc32c_multi_create_rank(device, rank, nranks, idb, ctypes.byref(h)),
+                   "crc32c_multi_create_rank")
+            self.local_devices = [device]
         self.handle = h
+
+    def plan(self, pkts, group_packets: int = 64, flags: int = 0) -> "MultiPlan":
+        return MultiPlan(self, pkts, group_packets, flags)
+
+    def sync(self) -> None:
+        _check(lib().crc32c_multi_sync(self.handle), "crc32c_multi_sync")
 
     def batch_host(self, payload: np.ndarray, pkts, group_packets: int = 64, flags: int = 0) -> np.ndarray:
         pkts = as_packets(pkts)
@@ -308,6 +408,94 @@ class Multi:
             self.close()
         except Exception:
             pass
+
+
+class MultiPlan:
+    """Device-resident multi-GPU plan (crc32c_multi_plan): shards + RCCL gather to rank 0."""
+
+    def __init__(self, multi: Multi, pkts, group_packets: int = 64, flags: int = 0):
+        pkts = as_packets(pkts)
+        h = ctypes.c_void_p()
+        _check(lib().crc32c_multi_plan_create(multi.handle, _np_ptr(pkts), pkts.size, group_packets, flags,
+                                              ctypes.byref(h)), "crc32c_multi_plan_create")
+        self.multi = multi
+        self.handle = h
+        self.nchecksums = int(lib().crc32c_multi_plan_nchecksums(h))
+
+    def shard_bytes(self, rank: int) -> int:
+        return int(lib().crc32c_multi_plan_shard_bytes(self.handle, rank))
+
+    def exec(self, dev_shards, root_out: int, streams=None) -> None:
+        n = len(dev_shards)
+        shards = (ctypes.c_void_p * n)(*[ctypes.c_void_p(x) for x in dev_shards])
+        ss = None if streams is None else (ctypes.c_void_p * n)(*[ctypes.c_void_p(x) for x in streams])
+        _check(lib().crc32c_multi_plan_exec(self.handle, shards, ctypes.c_void_p(root_out), ss),
+               "crc32c_multi_plan_exec")
+
+    def close(self) -> None:
+        if self.handle:
+            lib().crc32c_multi_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def multi_layout(pkts, group_packets: int, nranks: int):
+    """crc32c_multi_layout: (per-group [rank, shard offset, payload offset, bytes] rows, shard bytes per rank)."""
+    pkts = as_packets(pkts)
+    n = int(lib().crc32c_multi_layout(_np_ptr(pkts), pkts.size, group_packets, nranks, None, None))
+    if n < 0:
+        _check(n, "crc32c_multi_layout")
+    lay = np.zeros((max(n, 1), 4), np.uint64)
+    sb = np.zeros(nranks, np.uint64)
+    lib().crc32c_multi_layout(_np_ptr(pkts), pkts.size, group_packets, nranks, _np_ptr(lay), _np_ptr(sb))
+    return lay[:n], sb
+
+
+def multi_shard_packets(pkts, group_packets: int, nranks: int, rank: int) -> np.ndarray:
+    """crc32c_multi_shard_packets: rank's packets, payload offsets into its shard, global out indices."""
+    pkts = as_packets(pkts)
+    n = int(lib().crc32c_multi_shard_packets(_np_ptr(pkts), pkts.size, group_packets, nranks, rank, None, 0))
+    if n < 0:
+        _check(n, "crc32c_multi_shard_packets")
+    out = np.zeros(max(n, 1), PACKET_DTYPE)
+    lib().crc32c_multi_shard_packets(_np_ptr(pkts), pkts.size, group_packets, nranks, rank, _np_ptr(out), n)
+    return out[:n]
+
+
+def parse_frames(frames: np.ndarray):
+    """crc32c_parse_frames: (frame records, bytes consumed)."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    used = ctypes.c_uint64(0)
+    n = int(lib().crc32c_parse_frames(_np_ptr(frames), frames.size, None, 0, ctypes.byref(used)))
+    if n < 0:
+        _check(n, "crc32c_parse_frames")
+    info = np.zeros(max(n, 1), FRAME_DTYPE)
+    lib().crc32c_parse_frames(_np_ptr(frames), frames.size, _np_ptr(info), n, ctypes.byref(used))
+    return info[:n], int(used.value)
+
+
+def last_path() -> int:
+    return int(lib().crc32c_last_path())
+
+
+def as_buffers(buffers) -> np.ndarray:
+    if isinstance(buffers, np.ndarray) and buffers.dtype == BUFFER_DTYPE:
+        return np.ascontiguousarray(buffers)
+    return np.array([(int(d or 0), int(n)) for d, n in buffers], BUFFER_DTYPE)
+
+
+def debug_write_plan(buffers, bufferoffset: int, length: int, blockoffset: int = 0, packetsize: int = 65536,
+                     bpc: int = 512) -> dict:
+    bufs = as_buffers(buffers)
+    c = np.zeros(6, np.uint64)
+    _check(lib().crc32c_debug_write_plan(_np_ptr(bufs), bufs.size, bufferoffset, length, blockoffset, packetsize,
+                                         bpc, _np_ptr(c)), "crc32c_debug_write_plan")
+    return dict(zip(["tiles", "gen", "seg", "pieces", "consts", "nchecksums"], (int(x) for x in c)))
 
 
 def chunks_cpu(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:

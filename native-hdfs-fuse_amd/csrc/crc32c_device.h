@@ -1,0 +1,826 @@
+// crc32c_device.h -- device code of the CDNA4 (gfx950) CRC32C chunk kernel.
+//
+// Included by crc32c_kernel.hip (the production instantiations, in
+// libhdfs_crc32c.so) and by debug/crc32c_variants.hip (A/B and diagnostic
+// instantiations, only in libhdfs_crc32c_debug.so).
+//
+// Computes hadoop_rpc_send_packet's checksum vector (hadooprpc.c:733-742:
+// crc32c(0, chunk) per bytesPerChecksum chunk, crc32c.c semantics) for a
+// whole batch of device-resident packets in one launch.  Integer/bitwise
+// work, HBM-bound; no MFMA.  Design (DESIGN.md has the derivation and the
+// measurements behind each choice):
+//
+//  * CRC32C is affine over GF(2): for a chunk M of n bytes,
+//      crc32c(0, M) = lin(M) ^ crc32c(0, zeros(n)),
+//    and lin(M) is the XOR of one 32-bit contribution per (byte position,
+//    byte value).  So there is no serial dependency inside a chunk.
+//  * Coalesced HBM loads: one wave instruction reads 1 KiB contiguous
+//    (16 B per lane) = two 512-byte blocks; lane q of each half owns bytes
+//    16q .. 16q+15 of its block in EVERY instruction.  Loads are
+//    non-temporal buffer loads bounded by the tile (partial tiles read zeros).
+//  * Lookups, production (kModeS4): each lane chains its 16-byte piece
+//    d0..d3 through the slicing-by-4 step S (crc32c.c's crc32c_table[0..3],
+//    one 4-byte column per lane so the 32 lanes of a half-wave always hit 32
+//    different banks): u = S(S(S(d0) ^ d1) ^ d2) ^ d3, then one column-
+//    specific operator N_q = Z_{16(31-q)} o S (8 nibble lookups) moves the
+//    piece's contribution to the block end.  20 LDS lookups + 37 VALU per
+//    16 bytes; 152 KiB of LDS, one workgroup per CU, 12 waves (768 threads).
+//  * Wave-level reduction: each lane's per-piece value is XOR-reduced over
+//    the 32 lanes of its block with a DPP reduce-scatter, which also packs
+//    the 16 block results of a tile into 16 lanes for one coalesced store.
+//  * bpc = 1024..8192 (power of two): per-block results are shifted by
+//    Z^(512*s) (nibble tables in LDS) and XORed across the blocks of a chunk
+//    with DPP / swizzle steps.
+//  * Any other bpc in [4, 8192] (general tiles): each chunk is right-aligned
+//    into k = ceil(bpc / 512) virtual blocks (leading zeros do not change
+//    lin); the register pre-inversion (crc32c.c:237) is XORed into the
+//    chunk's first 4 bytes, so crc = lin ^ ~0; blocks are shifted by
+//    Z^(512*s) and a chunk's k blocks are XORed by ds_bpermute.
+//  * Work distribution: each workgroup owns an equal range of 8 KiB tiles;
+//    its waves pull tiles from an LDS counter (the SIMD arbiter's age
+//    priority makes static per-wave assignment finish 2x apart).
+//  * Tails / chunks fitting no tile: half a wave per chunk (GenItem), the
+//    chunk right-aligned into zero-prefixed virtual 512-byte blocks,
+//    Horner-combined with Z^512.  Chunks assembled from several buffers
+//    (SegItem) are read piece by piece into the same windows; chunks of
+//    zero fill only (ConstRun) are written from plan-time constants.
+//  * Verification (crc32c_plan_verify): the same kernel compares instead of
+//    storing; the expected values are fetched with the tile and the last
+//    workgroup publishes the launch's result (sharded ticket reduction).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernel_abi.h"
+
+namespace hdfs_crc_dev {
+
+using hdfs_crc::ConstRun;
+using hdfs_crc::FastTile;
+using hdfs_crc::GenItem;
+using hdfs_crc::GenPiece;
+using hdfs_crc::KParams;
+using hdfs_crc::SegItem;
+using hdfs_crc::kGeneralTile;
+using hdfs_crc::kShardWord;
+using hdfs_crc::kTicketShards;
+using hdfs_crc::kTicketWord;
+using hdfs_crc::kVCountWord;
+using hdfs_crc::kVFirstWord;
+
+constexpr uint32_t kLdsBytes = hdfs_crc::kKernelLdsBytes;
+constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
+// Table bytes copied into LDS, rounded up to whole 1 KiB LDS-DMA pieces (the
+// device copy is zero-padded to kTableAlloc >= this).
+constexpr uint32_t kStageBytes = (kLdsBytes + 1023u) / 1024u * 1024u;
+static_assert(kStageBytes <= hdfs_crc::kTableAlloc, "staging reads past the device table");
+// The slicing-by-4 kernel's image (crc_math.h): byte tables, N_q, shifts.
+constexpr uint32_t kS4Bytes = uint32_t(hdfs_crc::kS4Bytes);
+constexpr uint32_t kS4NibOff = uint32_t(hdfs_crc::kS4NibOff);
+constexpr uint32_t kS4ShiftOff = uint32_t(hdfs_crc::kS4ShiftOff);
+constexpr uint32_t kS4StageBytes = (kS4Bytes + 1023u) / 1024u * 1024u;
+static_assert(kS4StageBytes <= hdfs_crc::kTableAllocS4, "staging reads past the device table");
+
+// Kernel modes (template bits).  Production = kModeS4 | kModeNt (+ kModeVerify).
+constexpr int kModeNt = 1;          // payload loads non-temporal (streamed once)
+constexpr int kModeS4 = 2;          // slicing-by-4 chains + per-column finishing operator (S4 image)
+constexpr int kModeStamps = 4;      // DIAGNOSTIC: per-wave timestamps
+constexpr int kModeMemDiag = 8;     // DIAGNOSTIC, wrong results: no lookups (memory ceiling)
+constexpr int kModeCompDiag = 16;   // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
+constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table staging
+constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
+constexpr int kModeS4H = 128;       // A/B: half-column S4 image (64 KiB of T tables, 88 KiB staged)
+constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
+                                    // their code: the power-of-two tile loop stays as compact as round 1's)
+
+// Work descriptors are read-only for the whole launch: reading them through
+// the constant address space lets every (wave-uniform) descriptor fetch be a
+// scalar s_load instead of a vector load that would join the payload loads
+// on the vector-memory counter.
+typedef const __attribute__((address_space(4))) FastTile *ConstTiles;
+typedef const __attribute__((address_space(4))) ConstRun *ConstRuns;
+
+__device__ __forceinline__ FastTile tile_at(const KParams &p, uint32_t i) {
+    const ConstTiles t = (ConstTiles)(p.tiles) + i;
+    FastTile r;
+    r.src = t->src;
+    r.out = t->out;
+    r.meta = t->meta;
+    return r;
+}
+
+// gfx950 has no v_xor3_b32 but has v_bitop3_b32 (any 3-input bitwise
+// function by truth table); 0x96 is a ^ b ^ c.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// Opaque to the optimiser: stops InstCombine from re-associating the XOR
+// trees of different pieces into one tree over every LDS read of the tile
+// (which keeps all 256 reads live and spills).
+__device__ __forceinline__ void opaque(uint32_t &x) { asm volatile("" : "+v"(x)); }
+
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *lds, uint32_t off) {
+    return *reinterpret_cast<const uint32_t *>(lds + off);
+}
+
+// lin() contribution of one lane's 16-byte piece at column col (= lane & 31),
+// positional nibble tables (A/B variant 1).  Byte k of the piece: low nibble
+// row at k*4096 + n*256, high nibble row at 128 + k*256 + n*4096; the lane's
+// column is col*4.  DIAG 1 (diagnostic builds only, wrong results): the
+// lookups are skipped.
+template <int DIAG>
+__device__ __forceinline__ uint32_t piece_lin(const uint8_t *lds, uint4 d, uint32_t col4) {
+    uint32_t acc = 0;
+    const uint32_t dw[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const uint32_t x = dw[w];
+        if (DIAG == 1) {
+            acc ^= x;
+            continue;
+        }
+        const uint32_t xs[4] = {x << 8, x, x >> 8, x >> 16};
+        uint32_t r[8];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t k = 4 * w + t;
+            r[2 * t] = lds_u32(lds, ((xs[t] & 0x0F00u) | col4) + k * 4096u);
+            r[2 * t + 1] = lds_u32(lds, ((xs[t] & 0xF000u) | col4) + 128u + k * 256u);
+        }
+        acc = xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], acc));
+    }
+    return acc;
+}
+
+// (a & mask) | c as ONE v_and_or_b32: left to itself the compiler proves the
+// operands disjoint, turns the OR into an add and splits it in two.
+__device__ __forceinline__ uint32_t and_or(uint32_t a, uint32_t mask, uint32_t c) {
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(mask), "v"(c));
+    return r;
+}
+
+// Per-lane LDS address constants: the lane's column offset, and the same
+// with the base of the S4 image's upper byte-table pair / N_q section.
+struct LaneCols {
+    uint32_t col4;  // (lane & 31) * 4
+    uint32_t hi;    // col4 | 65536
+    uint32_t nib;   // col4 | kS4NibOff
+    uint32_t toff;  // T1 - T0 (= T3 - T2) in bytes: 128, or 64 in the half-column image
+};
+
+template <bool H>
+__device__ __forceinline__ LaneCols lane_cols(uint32_t q) {
+    if (H) {  // half-column S4 image (A/B, kModeS4H): T0..T3 share one 256-byte row per byte value
+        const uint32_t c4 = (q & 15u) << 2;
+        return LaneCols{c4, c4 | 128u, (q << 2) | kS4NibOff, 64u};
+    }
+    return LaneCols{q << 2, (q << 2) | 65536u, (q << 2) | kS4NibOff, 128u};
+}
+
+// Byte j of v into address bits 8..15 and the column base's bytes 0 and 2
+// into bits 0..7 and 16..23 (v_perm_b32: selectors 0-3 = bytes of the
+// second operand, 4-7 = bytes of the first, 0x0C = zero).
+template <int J>
+__device__ __forceinline__ uint32_t byte_addr(uint32_t v, uint32_t base) {
+    return __builtin_amdgcn_perm(v, base, 0x0C020000u | uint32_t(4 + J) << 8);
+}
+
+// One slicing-by-4 step: S(v) ^ next, S(v) = T3[v.b0] ^ T2[v.b1] ^ T1[v.b2]
+// ^ T0[v.b3] (each table replicated over the lane columns of the image, so
+// the 32 lanes of a half-wave always hit 32 different banks).
+__device__ __forceinline__ uint32_t s4(const uint8_t *lds, const LaneCols &c, uint32_t v, uint32_t next) {
+    const uint32_t a3 = lds_u32(lds, byte_addr<0>(v, c.hi) + c.toff);    // T3: upper pair, odd
+    const uint32_t a2 = lds_u32(lds, byte_addr<1>(v, c.hi));             // T2: upper pair, even
+    const uint32_t a1 = lds_u32(lds, byte_addr<2>(v, c.col4) + c.toff);  // T1
+    const uint32_t a0 = lds_u32(lds, byte_addr<3>(v, c.col4));           // T0
+    return xor3(xor3(a3, a2, a1), a0, next);
+}
+
+// lin() of the lane's 16-byte piece with the S4 image: u = S(S(S(d0) ^ d1)
+// ^ d2) ^ d3 is the register after the piece; N_q(u) = Z_{16(31-q)}(S(u))
+// moves it to the block end (8 nibble lookups in the lane's column).
+template <int DIAG>
+__device__ __forceinline__ uint32_t piece_lin_s4(const uint8_t *lds, uint4 d, const LaneCols &c) {
+    if (DIAG == 1) return d.x ^ d.y ^ d.z ^ d.w;
+    const uint32_t u = s4(lds, c, s4(lds, c, s4(lds, c, d.x, d.y), d.z), d.w);
+    const uint32_t xs[8] = {u << 8, u << 4, u, u >> 4, u >> 8, u >> 12, u >> 16, u >> 20};
+    uint32_t r[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) r[t] = lds_u32(lds, and_or(xs[t], 0x0F00u, c.nib) + (t >> 1) * 4096u + (t & 1) * 128u);
+    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
+template <bool S4, int DIAG>
+__device__ __forceinline__ uint32_t piece(const uint8_t *lds, uint4 d, const LaneCols &c) {
+    if (S4) return piece_lin_s4<DIAG>(lds, d, c);
+    return piece_lin<DIAG>(lds, d, c.col4);
+}
+
+// Z^(512*s)(x), s in 1..15, from 8 nibble tables (16 entries each).
+template <bool S4 = false>
+__device__ __forceinline__ uint32_t zshift(const uint8_t *lds, uint32_t s, uint32_t x) {
+    const uint32_t base = (S4 ? kS4ShiftOff : kShiftOff) + (s - 1u) * 512u;
+    uint32_t r = 0;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) r ^= lds_u32(lds, base + t * 64u + ((x >> (4 * t)) & 15u) * 4u);
+    return r;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1;   // quad_perm(1,0,3,2): lane ^ 1
+constexpr int kDppXor2 = 0x4E;   // quad_perm(2,3,0,1): lane ^ 2
+constexpr int kDppXor8 = 0x128;  // row_ror:8 inside a 16-lane row: lane ^ 8
+
+template <int XORMASK>
+__device__ __forceinline__ uint32_t swz_xor(uint32_t v) {
+    // ds_swizzle bit mode inside 32-lane groups: and 0x1F, or 0, xor XORMASK.
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x1F | (XORMASK << 10)));
+}
+
+__device__ __forceinline__ uint32_t allreduce32(uint32_t x) {
+    x ^= dpp<kDppXor1>(x);
+    x ^= dpp<kDppXor2>(x);
+    x ^= swz_xor<4>(x);
+    x ^= dpp<kDppXor8>(x);
+    x ^= swz_xor<16>(x);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
+    return (flags & 1u) ? __builtin_bswap32(crc) : crc;  // htonl on the wire, hadooprpc.c:71-75
+}
+
+// A mismatch (VERIFY): bump the workgroup's LDS count and lower its LDS
+// first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish).
+__device__ __forceinline__ void mismatch(uint32_t *vacc, uint32_t idx) {
+    atomicAdd(vacc, 1u);
+    atomicMin(vacc + 1, idx);
+}
+
+// Checksum `idx` of the batch: stored, or (VERIFY) compared with `expect`.
+template <bool VERIFY>
+__device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t expect) {
+    const uint32_t v = out_order(crc, p.flags);
+    if (VERIFY) {
+        if (v != expect) mismatch(vacc, idx);
+    } else {
+        p.out[idx] = v;
+    }
+}
+
+// ---- launch-wide verification state (kernel_abi.h slots) -----------------
+// Start of a verification launch, one thread of workgroup 0: restore the
+// OTHER slot of the pair (used by the previous launch, which has completed)
+// for the next launch.
+__device__ __forceinline__ void reset_next_slot(const KParams &p) {
+    uint32_t *s = p.sched_next;
+    atomicExch(s + kTicketWord, 0u);
+    atomicExch(s + kVCountWord, 0u);
+    atomicExch(s + kVFirstWord, 0xffffffffu);
+#pragma unroll
+    for (uint32_t i = 0; i < kTicketShards; ++i) atomicExch(s + kShardWord + 32 * i, 0u);
+}
+
+// Waits until every vector-memory operation of the wave has completed; for a
+// returning device-scope atomic that means it has been performed.
+__device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// End of a verification launch, thread 0 of every workgroup: fold the
+// workgroup's count / first-bad index into the slot, take a ticket, and let
+// the last workgroup publish the totals to p.result[0..1] (no host-side reset
+// of the result is needed).  Every word of the slot is only ever touched by
+// device-scope atomics, which are performed in one place, so ordering needs
+// only completion waits, no cache fences (a __threadfence() is an L2
+// writeback + invalidate, ~3.5 us each on the launch's critical tail).
+__device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
+    uint32_t *s = p.sched;
+    const uint32_t cnt = vacc[0], first = vacc[1];
+    if (cnt) {
+        uint32_t a = atomicAdd(s + kVCountWord, cnt);
+        uint32_t b = atomicMin(s + kVFirstWord, first);
+        asm volatile("" : "+v"(a), "+v"(b));  // returning forms: the wait below covers them
+        wait_vmem();
+    }
+    // shard ticket, then (last of the shard) the global ticket
+    const uint32_t shard = blockIdx.x % kTicketShards;
+    const uint32_t shards = min(gridDim.x, kTicketShards);
+    const uint32_t in_shard = (gridDim.x - shard + kTicketShards - 1u) / kTicketShards;
+    if (atomicAdd(s + kShardWord + 32u * shard, 1u) != in_shard - 1u) return;
+    if (atomicAdd(s + kTicketWord, 1u) == shards - 1u) {
+        // every other workgroup's adds completed before its tickets
+        p.result[0] = atomicAdd(s + kVCountWord, 0u);
+        p.result[1] = atomicAdd(s + kVFirstWord, 0u);
+    }
+}
+
+// ---- tiles: one wave, 16 blocks ------------------------------------------
+// Block of the tile whose lin() lane `lane` holds after block_lin's
+// reduce-scatter, and whether the lane emits that block's chunk checksum.
+__device__ __forceinline__ uint32_t rep_block(int lane) {
+    return 2u * (((lane & 8) ? 1u : 0u) + ((lane & 2) ? 2u : 0u) + ((lane & 1) ? 4u : 0u)) + (uint32_t(lane) >> 5);
+}
+// Inverse: a lane (lane bits 2 and 4 clear) that holds block b's lin().
+__device__ __forceinline__ uint32_t block_lane(uint32_t b) {
+    const uint32_t i = b >> 1;
+    return ((i >> 2) & 1u) | (((i >> 1) & 1u) << 1) | ((i & 1u) << 3) | ((b & 1u) << 5);
+}
+__device__ __forceinline__ bool rep_lane(int lane, uint32_t blk, uint32_t nb, uint32_t lg) {
+    return ((lane & 0x14) == 0) && ((blk & ((1u << lg) - 1u)) == 0) && blk < nb;
+}
+
+// Loads of one power-of-two tile: instruction i reads 1 KiB contiguous
+// (blocks 2i, 2i+1) through a buffer descriptor whose range is the tile's
+// nb * 512 valid bytes.  Lanes of blocks a partial tile does not have fall
+// outside the range and read zeros without touching memory (lin() of zeros
+// is 0, so they need no mask), every lane uses the same one-VGPR offset plus
+// an immediate, and the instruction stream has no divergent branch.
+// AUX 2 = non-temporal.  VERIFY: the expected checksum the lane compares is
+// fetched with the tile.
+template <int AUX, bool COMPDIAG, bool VERIFY>
+__device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
+    if (COMPDIAG) {  // synthetic data, no memory traffic
+        const uint32_t x = uint32_t(t.src) * 2654435761u + uint32_t(lane) * 40503u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = make_uint4(x ^ i, x + i, x * 3u + i, x ^ (i << 16));
+        return;
+    }
+    const uint32_t nb = t.meta & 0xffu;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src), 0, int(nb * 512u), 0x00020000);
+    const uint32_t voff = 16u * uint32_t(lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
+        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+    if (VERIFY) {  // default policy: the next tile's lanes read the rest of the line
+        const uint32_t lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
+        if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];
+    }
+    // Keep the loads ahead of whatever compute follows.
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// General tile geometry (plan.h general_meta).
+struct GShape {
+    uint32_t k, nch, pad, bpc;
+};
+__device__ __forceinline__ GShape gshape(uint32_t meta) {
+    GShape g;
+    g.k = (meta >> 8) & 31u;
+    g.nch = (meta >> 13) & 31u;
+    g.pad = (meta >> 18) & 511u;
+    g.bpc = g.k * 512u - g.pad;
+    return g;
+}
+
+// Virtual block b -> (chunk, block in chunk) for b = 2i + h, stepped by 2.
+__device__ __forceinline__ void gstep(uint32_t &c, uint32_t &j, uint32_t k) {
+    j += 2u;
+    if (j >= k) {
+        j -= k;
+        ++c;
+    }
+    if (j >= k) {
+        j -= k;
+        ++c;
+    }
+}
+
+// Loads of one general tile: lane q of block b = 2i + h (chunk c = b / k,
+// block j = b % k of it) reads chunk bytes 512 j + 16 q - pad .. +15 through
+// a descriptor over [src - 16, src + nch * bpc) (from src when pad == 0).
+// Lanes wholly inside a chunk's zero prefix, or past the last chunk, read
+// zeros without touching memory; the straddling lane's bytes before the
+// chunk are masked in gtile_prepare.
+template <int AUX, bool COMPDIAG, bool VERIFY>
+__device__ __forceinline__ void load_gtile(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
+    if (COMPDIAG) {
+        load_tile<AUX, true, false>(p, t, lane, v, ev);
+        return;
+    }
+    const GShape g = gshape(t.meta);
+    const uint32_t shift = g.pad ? 16u : 0u;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(p.payload + t.src - shift), 0, int(shift + g.nch * g.bpc), 0x00020000);
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
+    uint32_t c = g.k == 1 ? h : 0u, j = g.k == 1 ? 0u : h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const bool skip = c >= g.nch || (j == 0 && 16u * q + 16u <= g.pad);
+        const uint32_t voff = skip ? 0x80000000u : shift + c * g.bpc + j * 512u + 16u * q - g.pad;
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, AUX);
+        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
+        gstep(c, j, g.k);
+    }
+    if (VERIFY && uint32_t(lane) < g.nch) ev = p.expect[t.out + uint32_t(lane)];
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// Bytes of a dword with index < n (n clamped to 0..4).
+__device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
+    return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
+}
+
+// Chunk bytes before position 0 of the lane's dwords -> 0, chunk bytes 0..3
+// ^= 0xff (the register pre-inversion of crc32c.c:237 moved into the data).
+// m = position in the lane's 16 bytes where the chunk starts (may be < 0).
+__device__ __forceinline__ uint4 chunk_start_mask(uint4 d, int m) {
+    uint32_t w[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int dm = m - 4 * k;
+        const uint32_t lo = bytes_mask(dm);
+        const uint32_t ff = bytes_mask(dm + 4) & ~lo;
+        w[k] = (w[k] & ~lo) ^ ff;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// General tile, after its loads: apply the chunk-start masks.
+__device__ __forceinline__ void gtile_prepare(FastTile t, int lane, uint4 v[8]) {
+    const GShape g = gshape(t.meta);
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
+    uint32_t c = 0, j = g.k == 1 ? 0u : h;
+    if (g.pad) {
+        // The chunk starts at position pad - 512 j - 16 q of lane q's piece
+        // of block j; its 4 pre-inverted bytes reach block 1's lane 0 when
+        // pad > 508.
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (j == 0 || (j == 1 && q == 0)) v[i] = chunk_start_mask(v[i], int(g.pad) - int(512u * j + 16u * q));
+            gstep(c, j, g.k);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (j == 0 && q == 0) v[i].x ^= 0xffffffffu;
+            gstep(c, j, g.k);
+        }
+    }
+}
+
+// lin() of pieces I0 .. I1-1 of a tile (instruction i's 16 bytes per lane).
+template <int DIAG, bool S4, bool H>
+__device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8], uint32_t pc[8], int lane) {
+    const LaneCols cols = lane_cols<H>(uint32_t(lane & 31));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        pc[i] = piece<S4, DIAG>(lds, v[i], cols);
+        opaque(pc[i]);
+        // One piece at a time (nibble tables: 32 independent reads each), or
+        // two (S4: a piece is a chain of 4 dependent steps, so two chains
+        // interleave to keep 8 reads in flight): keeps the scheduler from
+        // hoisting every piece's LDS reads together (register pressure).
+        if (!S4 || (i & 1)) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// The tile's 8 piece values -> one lin() per block: reduce-scatter over lane
+// bits 0, 1, 3 (8 values -> 1), then all-reduce over lane bits 2 and 4.
+// Afterwards lane l holds lin() of block rep_block(l) = 2*i + h with
+// i = b3 + 2*b1 + 4*b0 (b = bits of l).
+__device__ __forceinline__ uint32_t block_lin(const uint32_t pc[8], int lane) {
+    const bool b0 = lane & 1, b1 = lane & 2, b3 = lane & 8;
+    uint32_t u[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t keep = b0 ? pc[k + 4] : pc[k];
+        const uint32_t send = b0 ? pc[k] : pc[k + 4];
+        u[k] = keep ^ dpp<kDppXor1>(send);
+    }
+    uint32_t w2[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const uint32_t keep = b1 ? u[j + 2] : u[j];
+        const uint32_t send = b1 ? u[j] : u[j + 2];
+        w2[j] = keep ^ dpp<kDppXor2>(send);
+    }
+    uint32_t x;
+    {
+        const uint32_t keep = b3 ? w2[1] : w2[0];
+        const uint32_t send = b3 ? w2[0] : w2[1];
+        x = keep ^ dpp<kDppXor8>(send);
+    }
+    x ^= swz_xor<4>(x);
+    x ^= swz_xor<16>(x);
+    return x;
+}
+
+// Power-of-two tile: blocks combined per chunk, chunk checksums stored (or compared).
+template <bool S4, bool VERIFY>
+__device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            const uint32_t pc[8], uint32_t ev, int lane) {
+    const uint32_t nb = t.meta & 0xffu;
+    const uint32_t lg = (t.meta >> 8) & 0xffu;
+    uint32_t x = block_lin(pc, lane);
+    const uint32_t blk = rep_block(lane);
+    if (lg) {  // chunks of 2^lg blocks: shift each block to the chunk end, XOR them
+        const uint32_t nbc = 1u << lg;
+        const uint32_t s = nbc - 1u - (blk & (nbc - 1u));
+        if (s) x = zshift<S4>(lds, s, x);
+        x ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), 32));  // block bit 0 = lane bit 5
+        if (lg >= 2) x ^= dpp<kDppXor8>(x);                               // block bit 1 = lane bit 3
+        if (lg >= 3) x ^= dpp<kDppXor2>(x);                               // block bit 2 = lane bit 1
+        if (lg >= 4) x ^= dpp<kDppXor1>(x);                               // block bit 3 = lane bit 0
+    }
+    const uint32_t crc = x ^ p.c_lg[lg];
+    if (rep_lane(lane, blk, nb, lg)) emit<VERIFY>(p, vacc, t.out + (blk >> lg), crc, ev);
+}
+
+// General tile: block b (chunk b / k, block j = b % k of it) shifted by
+// Z^(512 (k - 1 - j)), then lane c < nch XORs its chunk's k blocks from the
+// lanes holding them; the data carried the pre-inversion, so crc = lin ^ ~0.
+template <bool S4, bool VERIFY>
+__device__ __forceinline__ void reduce_emit_general(const KParams &p, const uint8_t *lds, uint32_t *vacc,
+                                                    FastTile t, const uint32_t pc[8], uint32_t ev, int lane) {
+    const GShape g = gshape(t.meta);
+    uint32_t x = block_lin(pc, lane);
+    const uint32_t blk = rep_block(lane);
+    // blk / k for blk < 16, k <= 16: (blk + 1/2) / k is never within 1/32 of an integer
+    const uint32_t quo = uint32_t((float(blk) + 0.5f) * __builtin_amdgcn_rcpf(float(g.k)));
+    const uint32_t s = g.k - 1u - (blk - quo * g.k);
+    if (s) x = zshift<S4>(lds, s, x);
+    uint32_t acc = 0;
+    const uint32_t b0 = uint32_t(lane) * g.k;
+    for (uint32_t u = 0; u < g.k; ++u) {
+        const uint32_t b = min(b0 + u, 15u);
+        acc ^= uint32_t(__builtin_amdgcn_ds_bpermute(int(block_lane(b) << 2), int(x)));
+    }
+    if (uint32_t(lane) < g.nch) emit<VERIFY>(p, vacc, t.out + uint32_t(lane), acc ^ 0xffffffffu, ev);
+}
+
+template <int DIAG, bool S4, bool VERIFY, bool H, bool GENERAL>
+__device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            uint4 v[8], uint32_t ev, int lane) {
+    uint32_t pc[8];
+    if (GENERAL && (t.meta & kGeneralTile)) {
+        gtile_prepare(t, lane, v);
+        tile_pieces<DIAG, S4, H>(lds, v, pc, lane);
+        reduce_emit_general<S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
+    } else {
+        tile_pieces<DIAG, S4, H>(lds, v, pc, lane);
+        reduce_emit<S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
+    }
+}
+
+template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL>
+__device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
+    if (GENERAL && (t.meta & kGeneralTile))
+        load_gtile<AUX, COMPDIAG, VERIFY>(p, t, lane, v, ev);
+    else
+        load_tile<AUX, COMPDIAG, VERIFY>(p, t, lane, v, ev);
+}
+
+// One tile index from the workgroup's LDS counter (one ds_add_rtn per wave).
+__device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
+    uint32_t t = 0;
+    if (lane == 0) t = atomicAdd(pool_ctr, 1u);
+    return __builtin_amdgcn_readfirstlane(t);
+}
+
+// ---- general path: half a wave per chunk of any length / alignment -------
+// Loads the aligned 16 bytes at a0 when they touch [cbeg, cend), zeroes the
+// bytes outside it and XORs 0xff into the bytes inside [cbeg, ffend)
+// (the register pre-inversion of crc32c.c:237 moved into the data).
+__device__ __forceinline__ void load_piece(uintptr_t a0, uintptr_t cbeg, uintptr_t cend, uintptr_t ffend,
+                                           uint32_t w[4]) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (a0 < cend && a0 + 16 > cbeg) v = *reinterpret_cast<const uint4 *>(a0);
+    const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uintptr_t d = a0 + 4u * j;
+        const uint32_t lo = bytes_mask(int64_t(cbeg - d));
+        const uint32_t keep = bytes_mask(int64_t(cend - d)) & ~lo;
+        const uint32_t ff = bytes_mask(int64_t(ffend - d)) & ~lo;
+        w[j] = (dv[j] & keep) ^ ff;
+    }
+}
+
+// Bytes sh .. sh+15 of the 32 bytes w[0..7]: a two-stage dword select (by 2,
+// then by 1) and v_alignbyte.  Written out as values so the compiler cannot
+// turn it into an indexed scratch access.
+__device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
+    const bool by2 = (sh & 8u) != 0, by1 = (sh & 4u) != 0;
+    const uint32_t bi = sh & 3u;
+    const uint32_t t0 = by2 ? w[2] : w[0], t1 = by2 ? w[3] : w[1], t2 = by2 ? w[4] : w[2];
+    const uint32_t t3 = by2 ? w[5] : w[3], t4 = by2 ? w[6] : w[4], t5 = by2 ? w[7] : w[5];
+    const uint32_t s0 = by1 ? t1 : t0, s1 = by1 ? t2 : t1, s2 = by1 ? t3 : t2;
+    const uint32_t s3 = by1 ? t4 : t3, s4 = by1 ? t5 : t4;
+    return make_uint4(__builtin_amdgcn_alignbyte(s1, s0, bi), __builtin_amdgcn_alignbyte(s2, s1, bi),
+                      __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
+}
+
+template <bool S4, bool VERIFY, bool H>
+__device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
+                                         int lane) {
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
+    const uint32_t idx = 2u * pair + h;
+    const bool valid = idx < p.ngen;
+    GenItem g{0, 0, 0};
+    if (valid) g = p.gen[idx];
+    const uint32_t r = g.len;
+    const uint32_t nbv = (r + 511u) >> 9;  // virtual 512-byte blocks
+    const uint32_t nmax = max(__builtin_amdgcn_readlane(nbv, 0), __builtin_amdgcn_readlane(nbv, 32));
+    const int64_t pad = int64_t(nbv) * 512 - int64_t(r);
+    const uintptr_t cbeg = reinterpret_cast<uintptr_t>(p.payload) + g.src;
+    const uintptr_t cend = cbeg + r;
+    const uintptr_t ffend = r >= 4 ? cbeg + 4 : cbeg;
+    const LaneCols cols = lane_cols<H>(q);
+    uint32_t acc = 0;
+    for (uint32_t m = 0; m < nmax; ++m) {
+        uint32_t lin = 0;
+        if (m < nbv) {
+            const int64_t o = int64_t(m) * 512 + int64_t(16 * q) - pad;  // may be negative (zero prefix)
+            const uintptr_t a = cbeg + uintptr_t(o);
+            const uintptr_t a0 = a & ~uintptr_t(15);
+            uint32_t w[8];
+            load_piece(a0, cbeg, cend, ffend, w);
+            load_piece(a0 + 16, cbeg, cend, ffend, w + 4);
+            lin = piece<S4, 0>(lds, funnel(w, uint32_t(a & 15u)), cols);
+        }
+        lin = allreduce32(lin);
+        if (m < nbv) acc = zshift<S4>(lds, 1, acc) ^ lin;
+    }
+    if (valid && q == 0) {
+        const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
+        emit<VERIFY>(p, vacc, g.out, crc, VERIFY ? p.expect[g.out] : 0u);
+    }
+}
+
+// A chunk assembled from several buffers (SegItem): like gen_pair, but each
+// lane's 16-byte window (chunk positions o .. o+15) is filled from every data
+// piece it overlaps; positions no piece covers are zero fill.
+template <bool S4, bool VERIFY, bool H>
+__device__ __forceinline__ void seg_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
+                                         int lane) {
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
+    const uint32_t idx = 2u * pair + h;
+    const bool valid = idx < p.nseg;
+    SegItem s{0, 0, 0, 0};
+    if (valid) s = p.seg[idx];
+    const uint32_t r = s.len;
+    const uint32_t nbv = (r + 511u) >> 9;
+    const uint32_t nmax = max(__builtin_amdgcn_readlane(nbv, 0), __builtin_amdgcn_readlane(nbv, 32));
+    const int64_t pad = int64_t(nbv) * 512 - int64_t(r);
+    const uintptr_t base = reinterpret_cast<uintptr_t>(p.payload);
+    const LaneCols cols = lane_cols<H>(q);
+    uint32_t acc = 0;
+    for (uint32_t m = 0; m < nmax; ++m) {
+        uint32_t lin = 0;
+        if (m < nbv) {
+            const int64_t o = int64_t(m) * 512 + int64_t(16 * q) - pad;  // chunk position of the window
+            uint4 d = make_uint4(0, 0, 0, 0);
+            for (uint32_t u = 0; u < s.npieces; ++u) {
+                const GenPiece g = p.pieces[s.first + u];
+                if (o >= int64_t(g.start) + g.len || o + 16 <= int64_t(g.start)) continue;
+                const uintptr_t cbeg = base + g.src, cend = cbeg + g.len;
+                const uintptr_t a = cbeg + uintptr_t(o - int64_t(g.start));
+                const uintptr_t a0 = a & ~uintptr_t(15);
+                uint32_t w[8];
+                load_piece(a0, cbeg, cend, cbeg, w);
+                load_piece(a0 + 16, cbeg, cend, cbeg, w + 4);
+                const uint4 f = funnel(w, uint32_t(a & 15u));
+                d = make_uint4(d.x | f.x, d.y | f.y, d.z | f.z, d.w | f.w);
+            }
+            if (r >= 4) d = chunk_start_mask(d, int(-o));  // (o + 16 > 0 here: nothing before the chunk is loaded)
+            lin = piece<S4, 0>(lds, d, cols);
+        }
+        lin = allreduce32(lin);
+        if (m < nbv) acc = zshift<S4>(lds, 1, acc) ^ lin;
+    }
+    if (valid && q == 0) {
+        const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
+        emit<VERIFY>(p, vacc, s.out, crc, VERIFY ? p.expect[s.out] : 0u);
+    }
+}
+
+// Checksums known at plan time (chunks of zero fill only): stored (or compared).
+template <bool VERIFY>
+__device__ __forceinline__ void const_run(const KParams &p, uint32_t *vacc, uint32_t i, int lane) {
+    const ConstRuns c = (ConstRuns)(p.consts) + i;
+    const uint32_t out = c->out, count = c->count, value = c->value;
+    for (uint32_t k = uint32_t(lane); k < count; k += 64u)
+        emit<VERIFY>(p, vacc, out + k, value, VERIFY ? p.expect[out + k] : 0u);
+}
+
+}  // namespace hdfs_crc_dev
+
+// THREADS per workgroup, WPS = waves per SIMD the launch bound asks for
+// (= workgroups per CU x THREADS / 256; it caps VGPRs at 512 / WPS).
+template <int THREADS, int WPS, int MODE>
+__global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc::KParams p) {
+    using namespace hdfs_crc_dev;
+    constexpr bool NT = (MODE & kModeNt) != 0;
+    constexpr bool S4 = (MODE & kModeS4) != 0;
+    constexpr bool STAMPS = (MODE & kModeStamps) != 0;
+    constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
+    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : 0;
+    constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
+    constexpr bool VERIFY = (MODE & kModeVerify) != 0;
+    constexpr bool H = S4 && (MODE & kModeS4H) != 0;
+    constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
+    constexpr int AUX = NT ? 2 : 0;
+    constexpr uint32_t kWaves = THREADS / 64;
+    constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
+    // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
+    // its mismatch count and first bad index.
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
+    uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
+    uint32_t *vacc = pool_ctr + 1;
+    const uint8_t *table = S4 ? (H ? p.table_s4 + hdfs_crc::kS4HOff : p.table_s4) : p.table;
+    const int lane = int(threadIdx.x & 63u);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
+
+    // Diagnostic build only (STAMPS): per-wave s_memrealtime stamps at start,
+    // after table staging and at exit, plus HW_ID / XCC_ID, written to a
+    // buffer nothing else reads.  Production variants contain no stamp.
+    uint64_t t_start = 0, t_staged = 0;
+    if (STAMPS) t_start = __builtin_amdgcn_s_memrealtime();
+
+    // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
+    // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
+    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
+    if (threadIdx.x == 0) {
+        *pool_ctr = tbeg + kWaves;
+        if (VERIFY) {
+            vacc[0] = 0;
+            vacc[1] = 0xffffffffu;
+        }
+    }
+    uint32_t t = tbeg + wv;
+    FastTile ft{0, 0, 0};
+    uint4 v[8];
+    uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
+    // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs); a
+    // launch of constant runs only needs none.
+    const bool tables = (p.ntiles | p.ngen | p.nseg) != 0;
+    constexpr uint32_t kStageChunks = kStage / 1024u;
+    if (!NOSTAGE && tables) {
+        for (uint32_t c = wv; c < kStageChunks; c += (H && c + kWaves >= 64u && c + kWaves < 128u) ? kWaves + 64u : kWaves) {
+            // (half-column image: its T region is the first 64 KiB; chunks 64-127 are unused)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
+                (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
+
+    if (t < tend) {
+        ft = tile_at(p, t);
+        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+    }
+    while (t < tend) {
+        finish_tile<DIAG, S4, VERIFY, H, GENERAL>(p, lds, vacc, ft, v, ev, lane);
+        t = pool_grab(pool_ctr, lane);
+        if (t >= tend) break;
+        ft = tile_at(p, t);
+        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+    }
+
+    // Gen pairs, seg pairs and constant runs, dealt over every wave of the grid.
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
+    const uint32_t nwaves = gridDim.x * kWaves;
+    const uint32_t ngp = (p.ngen + 1u) >> 1, nsp = (p.nseg + 1u) >> 1;
+    const uint32_t nitems = ngp + nsp + p.nconst;
+    for (uint32_t g = wave; g < nitems; g += nwaves) {
+        if (g < ngp)
+            gen_pair<S4, VERIFY, H>(p, lds, vacc, g, lane);
+        else if (g < ngp + nsp)
+            seg_pair<S4, VERIFY, H>(p, lds, vacc, g - ngp, lane);
+        else
+            const_run<VERIFY>(p, vacc, g - ngp - nsp, lane);
+    }
+    if (VERIFY) {
+        __syncthreads();
+        if (threadIdx.x == 0) verify_finish(p, vacc);
+    }
+    if (STAMPS && lane == 0 && p.stamps) {  // (no buffer: a plan exec of a stamped variant)
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        const uint32_t xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+        p.stamps[4 * wave + 0] = t_start;
+        p.stamps[4 * wave + 1] = t_staged;
+        p.stamps[4 * wave + 2] = t_end;
+        p.stamps[4 * wave + 3] = (uint64_t(xcc_id) << 32) | hw_id;
+    }
+}
+
+namespace hdfs_crc {
+// Grid of a launch: one workgroup per CU, or one per work item when there
+// are fewer items than CUs (a small batch leaves most waves without a tile;
+// they still share the table staging, which is what bounds a small launch).
+inline uint32_t production_grid(const KParams &p, uint32_t num_cu) {
+    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
+    return uint32_t(items < num_cu ? (items ? items : 1) : num_cu);
+}
+}  // namespace hdfs_crc

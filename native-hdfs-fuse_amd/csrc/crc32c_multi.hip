@@ -1,0 +1,368 @@
+// crc32c_multi.hip -- several GPUs of one node (include/hdfs_crc32c.h
+// section 5): a file's packets dealt round-robin over the GPUs in groups of
+// consecutive packets (one HDFS block each: fuse.c:580-647 writes a file
+// block by block, hadoop_rpc_send_packets cuts each block into packets,
+// hadooprpc.c:815-860), every GPU checksumming its shard device-resident,
+// and one RCCL group of point-to-point transfers over xGMI gathering the
+// u32 checksum arrays straight into block order on rank 0's device.  The
+// checksums are the path's only exchange; no payload byte crosses GPUs.
+//
+// Two ways to build the communicator: one process driving every device
+// (crc32c_multi_create, ncclCommInitAll) or one process per device
+// (crc32c_multi_create_rank, ncclCommInitRank with an id from
+// crc32c_multi_unique_id passed between the processes by the caller).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hdfs_crc32c.h"
+#include "plan.h"
+#include "runtime_internal.h"
+
+using namespace hdfs_crc;
+
+#define NCCL_TRY(expr)                                                                                  \
+    do {                                                                                                \
+        ncclResult_t r_ = (expr);                                                                       \
+        if (r_ != ncclSuccess)                                                                          \
+            return fail(-EIO, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__);     \
+    } while (0)
+
+struct crc32c_multi {
+    std::vector<crc32c_ctx *> ctxs;  // local devices
+    std::vector<int> ranks;          // communicator rank of each local device
+    int nranks = 0;
+    std::vector<ncclComm_t> comms;   // per local device (single-process: created on first exec)
+    std::vector<hipStream_t> streams;  // per local device, used when the caller passes none
+    std::mutex mu;
+};
+
+namespace {
+
+// One group of consecutive packets (an HDFS block) and where it lives.
+struct Group {
+    uint64_t lo = 0, hi = 0;  // payload range of its non-empty packets in the caller's layout
+    uint64_t omin = 0, n = 0;  // its checksums: global out indices [omin, omin + n)
+    int rank = 0;
+    uint64_t shard_off = 0;  // where byte lo sits in its rank's shard (same 16-byte phase)
+    uint64_t local_out = 0;  // index of its first checksum in its rank's local array
+};
+
+// Groups of `gp` packets, group g on rank g % nranks; each rank's shard is
+// its groups' byte ranges back to back (16-byte phase kept), its local
+// checksum array their checksum ranges back to back.
+int build_layout(const crc32c_packet *pkts, size_t npkts, uint32_t gp, int nranks, std::vector<Group> *groups,
+                 std::vector<uint64_t> *shard_bytes, std::vector<uint64_t> *local_nout) {
+    if (nranks <= 0 || gp == 0 || (npkts && !pkts)) return fail(-EINVAL, "bad layout arguments");
+    groups->assign((npkts + gp - 1) / gp, Group());
+    shard_bytes->assign(size_t(nranks), 0);
+    local_nout->assign(size_t(nranks), 0);
+    for (size_t g = 0; g < groups->size(); ++g) {
+        Group &G = (*groups)[g];
+        uint64_t lo = UINT64_MAX, hi = 0, n = 0;
+        std::vector<std::pair<uint64_t, uint64_t>> outs;  // (out_idx, checksums) of its packets
+        for (size_t i = g * gp; i < std::min<size_t>(npkts, (g + 1) * gp); ++i) {
+            const crc32c_packet &p = pkts[i];
+            if (p.bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
+            if (!p.len) continue;
+            const uint64_t c = crc32c_nchunks(p.len, p.bpc);
+            lo = std::min(lo, p.payload_off);
+            hi = std::max(hi, p.payload_off + p.len);
+            outs.emplace_back(p.out_idx, c);
+            n += c;
+        }
+        G.rank = int(g % size_t(nranks));
+        if (lo == UINT64_MAX) continue;  // only empty packets
+        // its packets' checksum ranges must tile one contiguous range
+        std::sort(outs.begin(), outs.end());
+        for (size_t k = 1; k < outs.size(); ++k)
+            if (outs[k].first != outs[k - 1].first + outs[k - 1].second)
+                return fail(-EINVAL, "group %zu: its checksums are not one contiguous range", g);
+        const uint64_t omin = outs.front().first;
+        G.lo = lo;
+        G.hi = hi;
+        G.omin = omin;
+        G.n = n;
+        uint64_t &cur = (*shard_bytes)[size_t(G.rank)];
+        G.shard_off = ((cur + 15) & ~uint64_t(15)) + (lo & 15);
+        cur = G.shard_off + (hi - lo);
+        G.local_out = (*local_nout)[size_t(G.rank)];
+        (*local_nout)[size_t(G.rank)] += n;
+    }
+    return 0;
+}
+
+// Rank r's packets: payload offsets in its shard; out indices in its local
+// array (local = true) or the global ones.
+void shard_packets(const crc32c_packet *pkts, size_t npkts, uint32_t gp, const std::vector<Group> &groups, int rank,
+                   bool local, std::vector<crc32c_packet> *out) {
+    out->clear();
+    for (size_t g = 0; g < groups.size(); ++g) {
+        const Group &G = groups[g];
+        if (G.rank != rank) continue;
+        for (size_t i = g * gp; i < std::min<size_t>(npkts, (g + 1) * gp); ++i) {
+            crc32c_packet p = pkts[i];
+            if (!p.len) continue;
+            p.payload_off = G.shard_off + (p.payload_off - G.lo);
+            if (local) p.out_idx = G.local_out + (p.out_idx - G.omin);
+            out->push_back(p);
+        }
+    }
+}
+
+int ensure_comms(crc32c_multi *m) {
+    if (!m->comms.empty()) return 0;
+    std::vector<int> devs;
+    for (crc32c_ctx *c : m->ctxs) devs.push_back(c->device);
+    std::vector<ncclComm_t> comms(devs.size());
+    NCCL_TRY(ncclCommInitAll(comms.data(), int(devs.size()), devs.data()));
+    m->comms = comms;
+    return 0;
+}
+
+hipStream_t local_stream(crc32c_multi *m, size_t i, void *const *streams) {
+    if (streams && streams[i]) return static_cast<hipStream_t>(streams[i]);
+    return m->streams[i];
+}
+
+}  // namespace
+
+struct crc32c_multi_plan {
+    crc32c_multi *m = nullptr;
+    std::vector<Group> groups;
+    std::vector<uint64_t> shard_bytes;  // per rank
+    std::vector<crc32c_plan *> plans;    // per local device
+    std::vector<uint32_t *> d_local;     // per local device: its local checksum array
+    uint64_t nchecksums = 0;
+};
+
+extern "C" {
+
+int crc32c_multi_create(const int *devices, int ndevices, crc32c_multi **out) {
+    if (!out || ndevices <= 0) return fail(-EINVAL, "bad arguments");
+    *out = nullptr;
+    std::unique_ptr<crc32c_multi, int (*)(crc32c_multi *)> m(new crc32c_multi, crc32c_multi_destroy);
+    m->nranks = ndevices;
+    for (int i = 0; i < ndevices; ++i) {
+        crc32c_ctx *c = nullptr;
+        if (int rc = crc32c_ctx_create(devices ? devices[i] : i, &c)) return rc;
+        m->ctxs.push_back(c);
+        m->ranks.push_back(i);
+        hipStream_t s = nullptr;
+        DeviceGuard guard(c->device);
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        m->streams.push_back(s);
+    }
+    *out = m.release();
+    return 0;
+}
+
+int crc32c_multi_unique_id(uint8_t id[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+    if (!id) return fail(-EINVAL, "id == NULL");
+    ncclUniqueId u;
+    NCCL_TRY(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof u);
+    return 0;
+}
+
+int crc32c_multi_create_rank(int device, int rank, int nranks, const uint8_t id[128], crc32c_multi **out) {
+    if (!out || !id || nranks <= 0 || rank < 0 || rank >= nranks) return fail(-EINVAL, "bad arguments");
+    *out = nullptr;
+    std::unique_ptr<crc32c_multi, int (*)(crc32c_multi *)> m(new crc32c_multi, crc32c_multi_destroy);
+    m->nranks = nranks;
+    crc32c_ctx *c = nullptr;
+    if (int rc = crc32c_ctx_create(device, &c)) return rc;
+    m->ctxs.push_back(c);
+    m->ranks.push_back(rank);
+    DeviceGuard guard(device);
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    m->streams.push_back(s);
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclComm_t comm = nullptr;
+    NCCL_TRY(ncclCommInitRank(&comm, nranks, u, rank));
+    m->comms.push_back(comm);
+    *out = m.release();
+    return 0;
+}
+
+int crc32c_multi_destroy(crc32c_multi *m) {
+    if (!m) return 0;
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        DeviceGuard guard(m->ctxs[i]->device);
+        if (i < m->streams.size() && m->streams[i]) {
+            (void)hipStreamSynchronize(m->streams[i]);
+            (void)hipStreamDestroy(m->streams[i]);
+        }
+        if (i < m->comms.size() && m->comms[i]) (void)ncclCommDestroy(m->comms[i]);
+    }
+    for (crc32c_ctx *c : m->ctxs) crc32c_ctx_destroy(c);
+    delete m;
+    return 0;
+}
+
+int crc32c_multi_sync(crc32c_multi *m) {
+    if (!m) return fail(-EINVAL, "multi == NULL");
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        DeviceGuard guard(m->ctxs[i]->device);
+        HIP_TRY(hipStreamSynchronize(m->streams[i]));
+    }
+    return 0;
+}
+
+int64_t crc32c_multi_layout(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                            uint64_t *layout, uint64_t *shard_bytes) {
+    std::vector<Group> groups;
+    std::vector<uint64_t> sb, ln;
+    if (int rc = build_layout(pkts, npkts, group_packets, nranks, &groups, &sb, &ln)) return rc;
+    for (size_t g = 0; layout && g < groups.size(); ++g) {
+        layout[4 * g] = uint64_t(groups[g].rank);
+        layout[4 * g + 1] = groups[g].shard_off;
+        layout[4 * g + 2] = groups[g].lo;
+        layout[4 * g + 3] = groups[g].hi - groups[g].lo;
+    }
+    if (shard_bytes) std::copy(sb.begin(), sb.end(), shard_bytes);
+    return int64_t(groups.size());
+}
+
+int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                                   int rank, crc32c_packet *local, size_t cap) {
+    std::vector<Group> groups;
+    std::vector<uint64_t> sb, ln;
+    if (int rc = build_layout(pkts, npkts, group_packets, nranks, &groups, &sb, &ln)) return rc;
+    if (rank < 0 || rank >= nranks) return fail(-EINVAL, "rank %d out of range", rank);
+    std::vector<crc32c_packet> v;
+    shard_packets(pkts, npkts, group_packets, groups, rank, false, &v);
+    if (local) std::copy(v.begin(), v.begin() + std::min(cap, v.size()), local);
+    return int64_t(v.size());
+}
+
+int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
+                             uint32_t flags, crc32c_multi_plan **out) {
+    if (!m || !out) return fail(-EINVAL, "multi/out == NULL");
+    *out = nullptr;
+    if (flags & (CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK))
+        return fail(-EINVAL, "flags 0x%x not valid for a multi-GPU plan", flags);
+    if (group_packets == 0) group_packets = 64;
+    std::unique_ptr<crc32c_multi_plan, int (*)(crc32c_multi_plan *)> mp(new crc32c_multi_plan,
+                                                                        crc32c_multi_plan_destroy);
+    mp->m = m;
+    std::vector<uint64_t> local_nout;
+    if (int rc = build_layout(pkts, npkts, group_packets, m->nranks, &mp->groups, &mp->shard_bytes, &local_nout))
+        return rc;
+    for (const Group &G : mp->groups) mp->nchecksums = std::max(mp->nchecksums, G.omin + G.n);
+    std::vector<crc32c_packet> local;
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        const int r = m->ranks[i];
+        shard_packets(pkts, npkts, group_packets, mp->groups, r, true, &local);
+        crc32c_plan *p = nullptr;
+        if (int rc = crc32c_plan_create(m->ctxs[i], local.data(), local.size(), flags, &p)) return rc;
+        mp->plans.push_back(p);
+        uint32_t *d = nullptr;
+        if (local_nout[size_t(r)]) {
+            DeviceGuard guard(m->ctxs[i]->device);
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), local_nout[size_t(r)] * sizeof(uint32_t)));
+        }
+        mp->d_local.push_back(d);
+    }
+    *out = mp.release();
+    return 0;
+}
+
+uint64_t crc32c_multi_plan_nchecksums(const crc32c_multi_plan *mp) { return mp ? mp->nchecksums : 0; }
+
+uint64_t crc32c_multi_plan_shard_bytes(const crc32c_multi_plan *mp, int rank) {
+    if (!mp || rank < 0 || size_t(rank) >= mp->shard_bytes.size()) return 0;
+    return mp->shard_bytes[size_t(rank)];
+}
+
+int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards, uint32_t *root_out,
+                           void *const *streams) {
+    if (!mp) return fail(-EINVAL, "plan == NULL");
+    crc32c_multi *m = mp->m;
+    std::lock_guard<std::mutex> lock(m->mu);
+    bool root = false;
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        if (m->ranks[i] == 0) root = true;
+        if (mp->d_local[i] && (!dev_shards || !dev_shards[i]))
+            return fail(-EINVAL, "local device %zu: shard payload == NULL", i);
+    }
+    if (root && mp->nchecksums && !root_out) return fail(-EINVAL, "root_out == NULL on rank 0");
+    if (int rc = ensure_comms(m)) return rc;
+    // 1. every local device checksums its shard into its local array
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        if (!mp->d_local[i]) continue;
+        if (int rc = crc32c_plan_exec(mp->plans[i], dev_shards[i], mp->d_local[i], local_stream(m, i, streams)))
+            return rc;
+    }
+    // 2. one group of point-to-point transfers: every group's checksum range
+    //    from its rank's local array into its place on rank 0
+    NCCL_TRY(ncclGroupStart());
+    ncclResult_t r = ncclSuccess;
+    for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
+        const hipStream_t s = local_stream(m, i, streams);
+        for (const Group &G : mp->groups) {
+            if (!G.n) continue;
+            if (G.rank == m->ranks[i])
+                r = ncclSend(mp->d_local[i] + G.local_out, G.n, ncclUint32, 0, m->comms[i], s);
+            if (r == ncclSuccess && m->ranks[i] == 0)
+                r = ncclRecv(root_out + G.omin, G.n, ncclUint32, G.rank, m->comms[i], s);
+            if (r != ncclSuccess) break;
+        }
+    }
+    const ncclResult_t e = ncclGroupEnd();
+    NCCL_TRY(r);
+    NCCL_TRY(e);
+    return 0;
+}
+
+int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
+    if (!mp) return 0;
+    for (size_t i = 0; i < mp->plans.size(); ++i) {
+        crc32c_plan_destroy(mp->plans[i]);
+        if (i < mp->d_local.size() && mp->d_local[i]) {
+            DeviceGuard guard(mp->m->ctxs[i]->device);
+            (void)hipFree(mp->d_local[i]);
+        }
+    }
+    delete mp;
+    return 0;
+}
+
+int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_packet *pkts, size_t npkts,
+                            uint32_t group_packets, uint32_t *out, uint32_t flags) {
+    if (!m || m->ctxs.empty()) return fail(-EINVAL, "multi == NULL");
+    for (size_t i = 0; i < npkts; ++i)
+        if (!pkts || pkts[i].bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
+    if (group_packets == 0) group_packets = 64;
+    const size_t g = m->ctxs.size();
+    // Groups of consecutive packets (an HDFS block's worth) dealt round-robin
+    // over the local devices, each over its own PCIe link.
+    std::vector<std::vector<crc32c_packet>> shard(g);
+    for (size_t i = 0; i < npkts; ++i) shard[(i / group_packets) % g].push_back(pkts[i]);
+    std::vector<int> rcs(g, 0);
+    std::vector<std::string> errs(g);
+    std::vector<std::thread> th;
+    for (size_t d = 0; d < g; ++d)
+        th.emplace_back([&, d] {
+            rcs[d] = crc32c_batch_host(m->ctxs[d], payload, shard[d].data(), shard[d].size(), out,
+                                       flags & ~CRC32C_CPU_FALLBACK);
+            if (rcs[d]) errs[d] = crc32c_last_error();
+        });
+    for (auto &t : th) t.join();
+    for (size_t d = 0; d < g; ++d)
+        if (rcs[d]) return fail(rcs[d], "device %d: %s", m->ctxs[d]->device, errs[d].c_str());
+    return 0;
+}
+
+}  // extern "C"

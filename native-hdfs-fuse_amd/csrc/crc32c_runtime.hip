@@ -1,7 +1,9 @@
 // crc32c_runtime.hip -- host side of the C ABI (include/hdfs_crc32c.h):
-// device contexts, batch plans, the host-resident staging pipeline and the
-// one-process multi-GPU driver.  Every GPU entry point returns 0 or -errno
-// and never substitutes a CPU computation: no GPU => -ENODEV.
+// device contexts, batch plans (packet batches and Hadoop_Fuse_Buffer write
+// plans) and the host-resident staging pipeline.  The multi-GPU driver is in
+// crc32c_multi.hip.  Every GPU entry point returns 0 or -errno; only the
+// per-packet host calls given CRC32C_CPU_FALLBACK substitute the CPU path
+// (crc32c_chunks_cpu), and they report it (crc32c_last_path).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,12 +23,14 @@
 #include "hdfs_crc32c.h"
 #include "kernel_abi.h"
 #include "plan.h"
+#include "runtime_internal.h"
 
-using namespace hdfs_crc;
+namespace hdfs_crc {
 
 namespace {
-
 thread_local char g_err[512] = "";
+thread_local int g_last_path = CRC32C_PATH_NONE;
+}  // namespace
 
 int fail(int code, const char *fmt, ...) {
     va_list ap;
@@ -36,25 +40,11 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
-#define HIP_TRY(expr)                                                                                   \
-    do {                                                                                                \
-        hipError_t e_ = (expr);                                                                         \
-        if (e_ != hipSuccess) return fail(-EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
-                                          __LINE__);                                                    \
-    } while (0)
+}  // namespace hdfs_crc
 
-// Restores the caller's current device (torch and other libraries keep their own).
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-    }
-};
+using namespace hdfs_crc;
+
+namespace {
 
 constexpr size_t kSliceBytes = 64ull << 20;  // host pipeline slice (whole packets), default
 // Scattered packets from pinned memory are copied run by run when the runs
@@ -155,107 +145,81 @@ void copy_range_pipelined(uint8_t *dst, const uint8_t *src, size_t n, size_t pie
     for (auto &x : th) x.join();
 }
 
-// The two device scheduler slots (kernel_abi.h) of one launch sequence that
-// the GPU runs in order: a plan, or a host-pipeline stage.
-struct SchedSlots {
-    uint32_t *d = nullptr;  // 2 * kSlotWords u32
-    int cur = 0;
-};
-
-struct Stage {
-    hipStream_t stream = nullptr;
-    hipEvent_t copied = nullptr;  // the slice's H2D payload copy (on the context's copy stream) is done
-    hipEvent_t done = nullptr;
-    uint8_t *d_payload = nullptr;
-    size_t payload_cap = 0;
-    uint8_t *h_payload = nullptr;  // pinned staging, only for pageable or gathered payloads
-    size_t staging_cap = 0;
-    // Work descriptors: pinned host memory the kernel reads in place (d_desc
-    // is its device mapping).  A slice's 64 KiB of descriptors are not worth
-    // a copy of their own: on the copy stream each copy costs ~25 us (9 us
-    // of transfer plus the ~15 us gap between copy commands).
-    uint8_t *h_desc = nullptr, *d_desc = nullptr;
-    size_t desc_cap = 0;
-    // Checksums: written by the kernel straight into pinned host memory
-    // (d_out is h_out's mapping), which saves a D2H copy on the tail.
-    uint32_t *h_out = nullptr, *d_out = nullptr;
-    size_t out_cap = 0;
-    bool pending = false;
-    // packets of the slice in flight: (global out_idx, local out index, count)
-    std::vector<uint64_t> scatter;
-    SchedSlots sched;  // this stage's launches are serialised on its stream
-};
-
 }  // namespace
 
-struct crc32c_ctx {
-    int device = 0;
-    int num_cu = 0;
-    int variant = 0;  // kernel variant, $HDFS_CRC32C_KVARIANT (A/B measurement only)
-    // per checksum type (0 = CRC32C, 1 = CRC32 / CRC32C_TYPE_CRC32)
-    uint8_t *d_table[2] = {nullptr, nullptr};
-    uint8_t *d_table_s4[2] = {nullptr, nullptr};
-    uint32_t c_lg[2][5];
-    uint32_t c_small[2][4];
-    std::mutex mu;
-    // Host pipeline: every stage's H2D copies go on one copy stream, so they
-    // run back to back at the full link rate while the other stage's kernel
-    // runs on its own stream.  Two copies on two streams would share the
-    // link, finish together and leave it idle while both stages drain.
-    hipStream_t copy_stream = nullptr;
-    Stage stage[2];
-};
+namespace hdfs_crc {
 
-struct crc32c_plan {
-    crc32c_ctx *ctx = nullptr;
-    // Verify launches of a plan share its scheduler slots, so they are kept
-    // in GPU order: one on another stream than the previous one first waits
-    // for it (last_done).  Exec launches are not ordered.
-    std::mutex mu;
-    SchedSlots sched;
-    hipStream_t last_stream = nullptr;
-    hipEvent_t last_done = nullptr;
-    bool launched = false;
-    FastTile *d_tiles = nullptr;
-    GenItem *d_gen = nullptr;
-    uint32_t ntiles = 0, ngen = 0;
-    uint64_t nchecksums = 0, payload_bytes = 0;
-    uint32_t flags = 0;
-    // CRC32C_DEVICE_ADDRESSES: the plan's offsets are relative to this device
-    // address (the lowest packet address, rounded down to 16), which the
-    // launches pass as the payload base.
-    uint64_t abs_base = 0;
-    bool absolute = false;
-};
-
-struct crc32c_multi {
-    std::vector<crc32c_ctx *> ctxs;
-};
-
-namespace {
-
-KParams params_for(const crc32c_ctx *ctx, const void *tiles, uint32_t ntiles, const void *gen, uint32_t ngen,
-                   const void *payload, uint32_t *out, uint32_t flags) {
+static KParams base_params(const crc32c_ctx *ctx, const void *payload, uint32_t *out, uint32_t flags) {
     KParams p;
-    p.tiles = static_cast<const FastTile *>(tiles);
-    p.gen = static_cast<const GenItem *>(gen);
+    std::memset(&p, 0, sizeof p);
     p.payload = static_cast<const uint8_t *>(payload);
     p.out = out;
     const int ty = (flags & CRC32C_TYPE_CRC32) ? 1 : 0;
     p.table = ctx->d_table[ty];
     p.table_s4 = ctx->d_table_s4[ty];
-    p.ntiles = ntiles;
-    p.ngen = ngen;
     p.flags = flags;
     std::memcpy(p.c_lg, ctx->c_lg[ty], sizeof p.c_lg);
     std::memcpy(p.c_small, ctx->c_small[ty], sizeof p.c_small);
-    p.stamps = nullptr;
-    p.expect = nullptr;
-    p.result = nullptr;
-    p.sched = nullptr;
-    p.sched_next = nullptr;
     return p;
 }
+
+static bool has_general(const HostPlan &hp) {
+    for (const FastTile &t : hp.tiles)
+        if (t.meta & kGeneralTile) return true;
+    return false;
+}
+
+KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out) {
+    KParams p = base_params(plan->ctx, payload, out, plan->flags);
+    const DevicePlan &dp = plan->dp;
+    p.tiles = reinterpret_cast<const FastTile *>(dp.d + dp.tiles_off);
+    p.gen = reinterpret_cast<const GenItem *>(dp.d + dp.gen_off);
+    p.seg = reinterpret_cast<const SegItem *>(dp.d + dp.seg_off);
+    p.pieces = reinterpret_cast<const GenPiece *>(dp.d + dp.pieces_off);
+    p.consts = reinterpret_cast<const ConstRun *>(dp.d + dp.consts_off);
+    p.ntiles = dp.ntiles;
+    p.ngen = dp.ngen;
+    p.nseg = dp.nseg;
+    p.nconst = dp.nconst;
+    p.general = dp.general ? 1u : 0u;
+    return p;
+}
+
+int upload_plan(const HostPlan &hp, DevicePlan *dp) {
+    if (hp.tiles.size() > UINT32_MAX || hp.gen.size() > UINT32_MAX || hp.seg.size() > UINT32_MAX ||
+        hp.consts.size() > UINT32_MAX)
+        return fail(-E2BIG, "batch too large");
+    dp->ntiles = uint32_t(hp.tiles.size());
+    dp->ngen = uint32_t(hp.gen.size());
+    dp->nseg = uint32_t(hp.seg.size());
+    dp->nconst = uint32_t(hp.consts.size());
+    dp->general = has_general(hp);
+    dp->tiles_off = 0;
+    dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
+    dp->seg_off = dp->gen_off + hp.gen.size() * sizeof(GenItem);
+    dp->pieces_off = dp->seg_off + hp.seg.size() * sizeof(SegItem);
+    dp->consts_off = dp->pieces_off + hp.pieces.size() * sizeof(GenPiece);
+    const size_t bytes = dp->consts_off + hp.consts.size() * sizeof(ConstRun);
+    if (!bytes) return 0;
+    std::vector<uint8_t> img(bytes);
+    std::memcpy(img.data() + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
+    std::memcpy(img.data() + dp->gen_off, hp.gen.data(), hp.gen.size() * sizeof(GenItem));
+    std::memcpy(img.data() + dp->seg_off, hp.seg.data(), hp.seg.size() * sizeof(SegItem));
+    std::memcpy(img.data() + dp->pieces_off, hp.pieces.data(), hp.pieces.size() * sizeof(GenPiece));
+    std::memcpy(img.data() + dp->consts_off, hp.consts.data(), hp.consts.size() * sizeof(ConstRun));
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dp->d), bytes));
+    HIP_TRY(hipMemcpy(dp->d, img.data(), bytes, hipMemcpyHostToDevice));
+    return 0;
+}
+
+void free_device_plan(DevicePlan *dp) {
+    if (dp->d) (void)hipFree(dp->d);
+    *dp = DevicePlan();
+}
+
+}  // namespace hdfs_crc
+
+namespace {
 
 int alloc_slots(SchedSlots &s) {
     if (s.d) return 0;
@@ -270,7 +234,7 @@ int alloc_slots(SchedSlots &s) {
 // reset the other one, and the pair flips; the caller keeps launches on
 // `slots` in GPU order.
 int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream) {
-    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2;
+    const uint64_t items = uint64_t(p.ntiles) + p.ngen + p.nseg + p.nconst;
     if (!items) return 0;
     const bool sched = p.expect != nullptr;
     if (sched) {
@@ -279,7 +243,7 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
         p.sched = slots.d + slots.cur * kSlotWords;
         p.sched_next = slots.d + (slots.cur ^ 1) * kSlotWords;
     }
-    HIP_TRY(launch_plan_kernel(p, ctx->variant, uint32_t(ctx->num_cu), stream));
+    HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream));
     if (sched) slots.cur ^= 1;
     return 0;
 }
@@ -308,7 +272,7 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     return launch(plan->ctx, p, plan->sched, stream);
 }
 
-constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES;
+constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK;
 
 int check_flags(uint32_t flags) {
     if (flags & ~kKnownFlags) return fail(-EINVAL, "unknown flags 0x%x", flags & ~kKnownFlags);
@@ -543,8 +507,12 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         std::memcpy(s.h_desc + plan.tiles.size() * 16, plan.gen.data(), plan.gen.size() * 16);
         // 3. Kernel and checksums on the stage's stream, after the copy.
         HIP_TRY(hipStreamWaitEvent(s.stream, s.copied, 0));
-        const KParams p = params_for(ctx, s.d_desc, uint32_t(plan.tiles.size()), s.d_desc + plan.tiles.size() * 16,
-                                     uint32_t(plan.gen.size()), s.d_payload, s.d_out, flags);
+        KParams p = base_params(ctx, s.d_payload, s.d_out, flags);
+        p.tiles = reinterpret_cast<const FastTile *>(s.d_desc);
+        p.gen = reinterpret_cast<const GenItem *>(s.d_desc + plan.tiles.size() * 16);
+        p.ntiles = uint32_t(plan.tiles.size());
+        p.ngen = uint32_t(plan.gen.size());
+        p.general = has_general(plan) ? 1u : 0u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));
@@ -563,11 +531,61 @@ std::once_flag g_default_once;
 crc32c_ctx *g_default_ctx = nullptr;
 int g_default_rc = 0;
 
+// Host-resident batch with the context lock held and the stages reset on failure.
+int batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts, uint32_t *out,
+               uint32_t flags) {
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    int rc = batch_host_locked(ctx, static_cast<const uint8_t *>(payload), pkts, npkts, out, flags);
+    if (rc) {
+        if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
+        for (Stage &s : ctx->stage) {
+            s.pending = false;
+            s.scatter.clear();
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+        }
+    }
+    return rc;
+}
+
+// CRC32C_CPU_FALLBACK: the host CPU path over the same packets (the
+// product's crc32c_chunks_cpu, never the test oracle).
+int batch_cpu(const void *payload, const crc32c_packet *pkts, size_t npkts, uint32_t *out, uint32_t flags) {
+    const uint32_t f = flags & (CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32);
+    for (size_t i = 0; i < npkts; ++i) {
+        if (!pkts[i].len) continue;
+        const int rc = crc32c_chunks_cpu(static_cast<const uint8_t *>(payload) + pkts[i].payload_off, pkts[i].len,
+                                         pkts[i].bpc, out + pkts[i].out_idx, f);
+        if (rc) return rc;
+    }
+    g_last_path = CRC32C_PATH_CPU;
+    return 0;
+}
+
 }  // namespace
+
+namespace hdfs_crc {
+
+int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute, uint64_t abs_base,
+              crc32c_plan **out) {
+    std::unique_ptr<crc32c_plan, int (*)(crc32c_plan *)> p(new crc32c_plan, crc32c_plan_destroy);
+    p->ctx = ctx;
+    p->nchecksums = hp.nchecksums;
+    p->payload_bytes = hp.payload_bytes;
+    p->flags = flags & (CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32);
+    p->abs_base = abs_base;
+    p->absolute = absolute;
+    DeviceGuard guard(ctx->device);
+    if (int rc = upload_plan(hp, &p->dp)) return rc;
+    *out = p.release();
+    return 0;
+}
+
+}  // namespace hdfs_crc
 
 extern "C" {
 
 const char *crc32c_last_error(void) { return g_err; }
+int crc32c_last_path(void) { return g_last_path; }
 
 int crc32c_device_count(void) {
     int n = 0;
@@ -593,8 +611,6 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
-    if (const char *kv = std::getenv("HDFS_CRC32C_KVARIANT")) c->variant = std::atoi(kv);
-    if (c->variant < 0 || c->variant >= kNumVariants) c->variant = 0;
     for (int ty = 0; ty < 2; ++ty) {
         const uint32_t poly = ty ? kPolyIeee : kPoly;
         std::vector<uint8_t> img(kTableAlloc, 0);
@@ -604,12 +620,7 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         HIP_TRY(hipMemcpy(c->d_table[ty], img.data(), kTableAlloc, hipMemcpyHostToDevice));
         std::vector<uint8_t> img4(kTableAllocS4Full, 0);
         build_lds_image_s4(img4.data(), poly);
-        // compacted T rows (kernel_abi.h): row r's 16 B = its first 4 replicas
-        for (uint32_t r = 0; r < kS4CompactRows; ++r)
-            std::memcpy(img4.data() + kTableAllocS4 + 16u * r, img4.data() + 128u * r, 16);
-        for (uint32_t r = 0; r < kS4CompactRows; ++r)
-            std::memcpy(img4.data() + kS4Compact4Off + 4u * r, img4.data() + 128u * r, 4);
-        {  // half-column image: same N_q / Z, T0..T3 in one row per byte value
+        {  // half-column image (A/B, debug library): same N_q / Z, T0..T3 in one row per byte value
             uint8_t *h = img4.data() + kS4HOff;
             std::memcpy(h, img4.data(), kTableAllocS4);
             std::memset(h, 0, kS4NibOff);
@@ -651,61 +662,50 @@ int crc32c_plan_create(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts,
     int rc = check_flags(flags);
     if (!rc) rc = check_packets(pkts, npkts);
     if (rc) return rc;
-    std::vector<crc32c_packet> rebased;
-    uint64_t abs_base = 0;
-    if (flags & CRC32C_DEVICE_ADDRESSES) {  // offsets from the lowest address (16-byte phase kept)
-        abs_base = UINT64_MAX;
-        for (size_t i = 0; i < npkts; ++i)
-            if (pkts[i].len) abs_base = std::min<uint64_t>(abs_base, pkts[i].payload_off & ~uint64_t(15));
-        if (abs_base == UINT64_MAX) abs_base = 0;
-        rebased.assign(pkts, pkts + npkts);
-        for (crc32c_packet &pk : rebased) pk.payload_off = pk.len ? pk.payload_off - abs_base : 0;
-        pkts = rebased.data();
-    }
+    const bool absolute = (flags & CRC32C_DEVICE_ADDRESSES) != 0;
     HostPlan hp;
-    rc = build_plan(pkts, npkts, &hp);
+    rc = build_plan(pkts, npkts, &hp, absolute);
     if (rc) return fail(rc, "invalid packet batch");
-    if (hp.tiles.size() > UINT32_MAX || hp.gen.size() > UINT32_MAX) return fail(-E2BIG, "batch too large");
-    std::unique_ptr<crc32c_plan, int (*)(crc32c_plan *)> p(new crc32c_plan, crc32c_plan_destroy);
-    p->ctx = ctx;
-    p->ntiles = uint32_t(hp.tiles.size());
-    p->ngen = uint32_t(hp.gen.size());
-    p->nchecksums = hp.nchecksums;
-    p->payload_bytes = hp.payload_bytes;
-    p->flags = flags & ~CRC32C_DEVICE_ADDRESSES;
-    p->abs_base = abs_base;
-    p->absolute = (flags & CRC32C_DEVICE_ADDRESSES) != 0;
-    DeviceGuard guard(ctx->device);
-    if (p->ntiles) {
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p->d_tiles), hp.tiles.size() * sizeof(FastTile)));
-        HIP_TRY(hipMemcpy(p->d_tiles, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile), hipMemcpyHostToDevice));
-    }
-    if (p->ngen) {
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p->d_gen), hp.gen.size() * sizeof(GenItem)));
-        HIP_TRY(hipMemcpy(p->d_gen, hp.gen.data(), hp.gen.size() * sizeof(GenItem), hipMemcpyHostToDevice));
-    }
-    *out = p.release();
+    uint64_t base = 0;
+    if (absolute) rebase_plan(&hp, &base);  // offsets from the lowest address (16-byte phase kept)
+    return make_plan(ctx, hp, flags, absolute, base, out);
+}
+
+int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, uint32_t n_buffers,
+                               uint64_t bufferoffset, uint64_t len, uint64_t blockoffset, uint32_t packetsize,
+                               uint32_t bpc, uint32_t flags, crc32c_plan **out) {
+    if (!ctx || !out) return fail(-EINVAL, "ctx/out == NULL");
+    *out = nullptr;
+    if (int rc = check_flags(flags)) return rc;
+    HostPlan hp;
+    const uint32_t poly = (flags & CRC32C_TYPE_CRC32) ? kPolyIeee : kPoly;
+    int rc = build_write_plan(buffers, n_buffers, bufferoffset, len, blockoffset, packetsize, bpc, poly, &hp);
+    if (rc) return fail(rc, "invalid buffer list / write range");
+    uint64_t base = 0;
+    rebase_plan(&hp, &base);
+    return make_plan(ctx, hp, flags, true, base, out);
+}
+
+// The payload base a launch passes: the caller's buffer, or for an absolute
+// plan its own base (the caller passes NULL).
+static int plan_payload(const crc32c_plan *plan, const void **dev_payload) {
+    if (!plan->absolute) return 0;
+    if (*dev_payload) return fail(-EINVAL, "a device-address plan takes dev_payload = NULL");
+    *dev_payload = reinterpret_cast<const void *>(uintptr_t(plan->abs_base));
     return 0;
 }
 
-// The payload base a launch passes: the caller's buffer, or for a
-// CRC32C_DEVICE_ADDRESSES plan its own base (the caller passes NULL).
-static int plan_payload(const crc32c_plan *plan, const void **dev_payload) {
-    if (!plan->absolute) return 0;
-    if (*dev_payload) return fail(-EINVAL, "a CRC32C_DEVICE_ADDRESSES plan takes dev_payload = NULL");
-    *dev_payload = reinterpret_cast<const void *>(uintptr_t(plan->abs_base));
-    return 0;
+static bool plan_reads_payload(const crc32c_plan *plan) {
+    return plan->dp.ntiles || plan->dp.ngen || plan->dp.nseg;
 }
 
 int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out, void *stream) {
     if (!plan) return fail(-EINVAL, "plan == NULL");
     if (plan->nchecksums == 0) return 0;
     if (int rc = plan_payload(plan, &dev_payload)) return rc;
-    if (!dev_payload || !dev_out) return fail(-EINVAL, "payload/out == NULL");
+    if ((!dev_payload && plan_reads_payload(plan)) || !dev_out) return fail(-EINVAL, "payload/out == NULL");
     DeviceGuard guard(plan->ctx->device);
-    const KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload,
-                                 dev_out, plan->flags);
-    return launch_plan(plan, p, static_cast<hipStream_t>(stream));
+    return launch_plan(plan, plan_params(plan, dev_payload, dev_out), static_cast<hipStream_t>(stream));
 }
 
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
@@ -714,17 +714,16 @@ int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_
     if (!dev_result) return fail(-EINVAL, "result == NULL");
     DeviceGuard guard(plan->ctx->device);
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (uint64_t(plan->ntiles) + plan->ngen == 0) {  // nothing to compare: no launch, set the result directly
+    const DevicePlan &dp = plan->dp;
+    if (uint64_t(dp.ntiles) + dp.ngen + dp.nseg + dp.nconst == 0) {  // nothing to compare: set the result directly
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result), 0, 1, s));
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));
         return 0;
     }
     if (int rc = plan_payload(plan, &dev_payload)) return rc;
-    if (!dev_payload || !dev_expected) return fail(-EINVAL, "payload/expected == NULL");
-    if (!variant_verifies(plan->ctx->variant))
-        return fail(-EINVAL, "kernel variant %d has no verification mode", plan->ctx->variant);
-    KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, nullptr,
-                           plan->flags);
+    if ((!dev_payload && plan_reads_payload(plan)) || !dev_expected)
+        return fail(-EINVAL, "payload/expected == NULL");
+    KParams p = plan_params(plan, dev_payload, nullptr);
     p.expect = dev_expected;
     p.result = dev_result;
     return launch_plan(plan, p, s);
@@ -756,25 +755,11 @@ int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_pa
     return bad;
 }
 
-int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
-                                   uint64_t *dev_stamps, int variant, void *stream) {
-    if (!plan) return fail(-EINVAL, "plan == NULL");
-    if (plan->nchecksums == 0) return 0;
-    DeviceGuard guard(plan->ctx->device);
-    KParams p = params_for(plan->ctx, plan->d_tiles, plan->ntiles, plan->d_gen, plan->ngen, dev_payload, dev_out,
-                           plan->flags);
-    p.stamps = dev_stamps;
-    if (variant < 0 || variant >= kNumVariants) return fail(-EINVAL, "no kernel variant %d", variant);
-    HIP_TRY(launch_plan_kernel(p, variant, uint32_t(plan->ctx->num_cu), static_cast<hipStream_t>(stream)));
-    return 0;
-}
-
 int crc32c_plan_destroy(crc32c_plan *plan) {
     if (!plan) return 0;
     {
         DeviceGuard guard(plan->ctx->device);
-        if (plan->d_tiles) (void)hipFree(plan->d_tiles);
-        if (plan->d_gen) (void)hipFree(plan->d_gen);
+        free_device_plan(&plan->dp);
         if (plan->sched.d) (void)hipFree(plan->sched.d);
         if (plan->last_done) (void)hipEventDestroy(plan->last_done);
     }
@@ -802,88 +787,41 @@ int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, 
 
 int crc32c_batch_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
                       uint32_t *out, uint32_t flags) {
-    if (!ctx) return fail(-EINVAL, "ctx == NULL");
+    g_last_path = CRC32C_PATH_NONE;
     int rc = check_flags(flags);
     if (!rc) rc = check_packets(pkts, npkts);
     if (rc) return rc;
     if (flags & CRC32C_DEVICE_ADDRESSES) return fail(-EINVAL, "CRC32C_DEVICE_ADDRESSES is for device-resident plans");
     if (npkts && (!payload || !out)) return fail(-EINVAL, "payload/out == NULL");
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    rc = batch_host_locked(ctx, static_cast<const uint8_t *>(payload), pkts, npkts, out, flags);
-    if (rc) {
-        if (ctx->copy_stream) (void)hipStreamSynchronize(ctx->copy_stream);
-        for (Stage &s : ctx->stage) {
-            s.pending = false;
-            s.scatter.clear();
-            if (s.stream) (void)hipStreamSynchronize(s.stream);
-        }
+    rc = ctx ? batch_host(ctx, payload, pkts, npkts, out, flags) : fail(-ENODEV, "ctx == NULL");
+    if (!rc) {
+        g_last_path = CRC32C_PATH_GPU;
+        return 0;
     }
-    return rc;
+    if (!(flags & CRC32C_CPU_FALLBACK) || rc == -EINVAL) return rc;
+    return batch_cpu(payload, pkts, npkts, out, flags);
 }
 
 int crc32c_chunks(const void *packet, size_t len, uint32_t bpc, uint32_t *out, uint32_t flags) {
+    g_last_path = CRC32C_PATH_NONE;
     if (bpc == 0) return fail(-EINVAL, "bytesPerChecksum == 0");
+    if (int rc = check_flags(flags)) return rc;
     if (len == 0) return 0;
     if (len > UINT32_MAX) return fail(-EINVAL, "packet too large");
     std::call_once(g_default_once, [] {
         const char *env = std::getenv("HDFS_CRC32C_DEVICE");
         g_default_rc = crc32c_ctx_create(env ? std::atoi(env) : 0, &g_default_ctx);
     });
-    if (g_default_rc) return fail(g_default_rc, "default GPU context unavailable");
     crc32c_packet p;
     p.payload_off = 0;
     p.out_idx = 0;
     p.len = uint32_t(len);
     p.bpc = bpc;
-    return crc32c_batch_host(g_default_ctx, packet, &p, 1, out, flags);
-}
-
-int crc32c_multi_create(const int *devices, int ndevices, crc32c_multi **out) {
-    if (!out || ndevices <= 0) return fail(-EINVAL, "bad arguments");
-    *out = nullptr;
-    std::unique_ptr<crc32c_multi> m(new crc32c_multi);
-    for (int i = 0; i < ndevices; ++i) {
-        crc32c_ctx *c = nullptr;
-        const int rc = crc32c_ctx_create(devices ? devices[i] : i, &c);
-        if (rc) {
-            for (crc32c_ctx *x : m->ctxs) crc32c_ctx_destroy(x);
-            return rc;
-        }
-        m->ctxs.push_back(c);
+    if (g_default_rc) {
+        const int rc = fail(g_default_rc, "default GPU context unavailable");
+        return (flags & CRC32C_CPU_FALLBACK) ? batch_cpu(packet, &p, 1, out, flags) : rc;
     }
-    *out = m.release();
-    return 0;
-}
-
-int crc32c_multi_destroy(crc32c_multi *m) {
-    if (!m) return 0;
-    for (crc32c_ctx *c : m->ctxs) crc32c_ctx_destroy(c);
-    delete m;
-    return 0;
-}
-
-int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_packet *pkts, size_t npkts,
-                            uint32_t group_packets, uint32_t *out, uint32_t flags) {
-    if (!m || m->ctxs.empty()) return fail(-EINVAL, "multi == NULL");
-    int rc = check_packets(pkts, npkts);
-    if (rc) return rc;
-    if (group_packets == 0) group_packets = 64;
-    const size_t g = m->ctxs.size();
-    // Groups of consecutive packets (an HDFS block's worth) dealt round-robin.
-    std::vector<std::vector<crc32c_packet>> shard(g);
-    for (size_t i = 0; i < npkts; ++i) shard[(i / group_packets) % g].push_back(pkts[i]);
-    std::vector<int> rcs(g, 0);
-    std::vector<std::string> errs(g);
-    std::vector<std::thread> th;
-    for (size_t d = 0; d < g; ++d)
-        th.emplace_back([&, d] {
-            rcs[d] = crc32c_batch_host(m->ctxs[d], payload, shard[d].data(), shard[d].size(), out, flags);
-            if (rcs[d]) errs[d] = crc32c_last_error();
-        });
-    for (auto &t : th) t.join();
-    for (size_t d = 0; d < g; ++d)
-        if (rcs[d]) return fail(rcs[d], "device %d: %s", m->ctxs[d]->device, errs[d].c_str());
-    return 0;
+    return crc32c_batch_host(g_default_ctx, packet, &p, 1, out, flags);
 }
 
 }  // extern "C"

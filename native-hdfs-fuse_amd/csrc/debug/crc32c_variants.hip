@@ -1,0 +1,99 @@
+// crc32c_variants.hip -- A/B and DIAGNOSTIC instantiations of the CRC32C
+// kernel (device code: ../crc32c_device.h).  Built only into
+// libhdfs_crc32c_debug.so, which links against libhdfs_crc32c.so and adds
+// crc32c_debug_plan_exec_variant; the product library launches nothing but
+// the production kernel, whatever the environment says.
+//
+// Variant numbers are those of DESIGN.md (round 1 measured 37; the ones
+// still built are listed below, the others were within noise of variant 0
+// and were removed).
+#include "../crc32c_device.h"
+#include "../runtime_internal.h"
+#include "hdfs_crc32c_debug.h"
+
+namespace {
+
+using namespace hdfs_crc_dev;
+constexpr int kS4Nt = kModeS4 | kModeNt | kModeGeneral;  // A/B variants always carry the general-tile code
+
+struct Variant {
+    int id;
+    const char *name;
+    uint32_t threads, wg_per_cu;
+    bool exact;  // computes the right checksums
+};
+
+constexpr Variant kVariants[] = {
+    {0, "s4_nt", 768, 1, true},                            // production (launched through the product library)
+    {1, "nibble_wg1024x2_nt", 1024, 2, true},              // positional nibble tables, 32 waves per CU
+    {2, "s4_wg1024x1_nt", 1024, 1, true},                  // 0 with 16 waves per CU
+    {3, "s4_wg768x1_nt_memonly", 768, 1, false},           // memory ceiling of 0 (no lookups)
+    {4, "s4_wg768x1_nt_compute_only", 768, 1, false},      // compute ceiling of 0 (no payload loads)
+    {5, "s4_wg768x1_nt_stamps", 768, 1, true},             // 0 with per-wave timestamps
+    {6, "s4_wg768x1_nt_memonly_stamps", 768, 1, false},    // 3 with per-wave timestamps
+    {7, "s4_wg768x1_nt_memonly_nostage", 768, 1, false},   // 3 without the table staging
+    {9, "s4_wg512x1_nt", 512, 1, true},                    // 0 with 8 waves per CU
+    {35, "s4h_nt", 768, 1, true},                          // half-column image (88 KiB staged)
+    {36, "s4h_nt_stamps", 768, 1, true},                   // 35 with per-wave timestamps
+};
+
+const Variant *find(int v) {
+    for (const Variant &x : kVariants)
+        if (x.id == v) return &x;
+    return nullptr;
+}
+
+#define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
+
+hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
+    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
+    const uint64_t waves = v.threads / 64;
+    uint64_t grid = (items + waves - 1) / waves;
+    const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
+    if (grid > cap) grid = cap;
+    if (grid == 0) grid = 1;
+    const dim3 g{uint32_t(grid), 1, 1}, b{v.threads, 1, 1};
+    switch (v.id) {
+    case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
+    case 2: HDFS_LAUNCH(1024, 4, kS4Nt); break;
+    case 3: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag); break;
+    case 4: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompDiag); break;
+    case 5: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps); break;
+    case 6: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeStamps); break;
+    case 7: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeNoStage); break;
+    case 9: HDFS_LAUNCH(512, 2, kS4Nt); break;
+    case 35: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H); break;
+    case 36: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H | kModeStamps); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#undef HDFS_LAUNCH
+
+}  // namespace
+
+extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
+                                              uint64_t *dev_stamps, int variant, void *stream) {
+    using namespace hdfs_crc;
+    if (!plan) return fail(-EINVAL, "plan == NULL");
+    const Variant *v = find(variant);
+    if (!v) return fail(-EINVAL, "kernel variant %d is not built", variant);
+    if (plan->nchecksums == 0) return 0;
+    if (plan->absolute) {
+        if (dev_payload) return fail(-EINVAL, "a device-address plan takes dev_payload = NULL");
+        dev_payload = reinterpret_cast<const void *>(uintptr_t(plan->abs_base));
+    }
+    DeviceGuard guard(plan->ctx->device);
+    KParams p = plan_params(plan, dev_payload, dev_out);
+    p.stamps = dev_stamps;
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
+                         : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));
+    return 0;
+}
+
+extern "C" const char *crc32c_debug_variant_name(int variant, int *exact) {
+    const Variant *v = find(variant);
+    if (exact) *exact = v ? int(v->exact) : 0;
+    return v ? v->name : nullptr;
+}

@@ -14,33 +14,31 @@ constexpr uint32_t kKernelShiftOff = uint32_t(kLdsShiftOff);
 // 1024-thread workgroup (16 B per thread per round) is in bounds.
 constexpr uint32_t kTableAlloc = ((kKernelLdsBytes + 16384 - 1) / 16384) * 16384;
 constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 16384;
-// After the S4 image (at kTableAllocS4): the T0..T3 rows compacted to 16 B
-// each (4 copies of T_m[b], row r = (m >> 1) * 512 + 2 * b + (m & 1)), so an
-// LDS-DMA instruction whose 8-lane groups all read one row's 16 B fills 8
-// replica rows of 128 B while the L1 returns one 128-byte line.
-constexpr uint32_t kS4CompactRows = 1024;
-constexpr uint32_t kS4CompactBytes = kS4CompactRows * 16;
-// Then the same rows as one u32 each (4 KiB), for replication inside the LDS.
-constexpr uint32_t kS4Compact4Off = kTableAllocS4 + kS4CompactBytes;
-constexpr uint32_t kS4Compact4Bytes = kS4CompactRows * 4;
-// Then the half-column S4 image (A/B, kModeS4H): the full image with its T
-// region re-laid out as b*256 + m*64 + 4*(q & 15) (the first 64 KiB).
-constexpr uint32_t kS4HOff = kS4Compact4Off + kS4Compact4Bytes;
+// After the S4 image (at kTableAllocS4): the half-column S4 image (A/B only,
+// debug library): the full image with its T region re-laid out as
+// b*256 + m*64 + 4*(q & 15) (the first 64 KiB).
+constexpr uint32_t kS4HOff = kTableAllocS4;
 constexpr uint32_t kTableAllocS4Full = kS4HOff + kTableAllocS4;
 
 struct KParams {
-    const FastTile *tiles;
+    const FastTile *tiles;  // power-of-two and general tiles
     const GenItem *gen;
+    const SegItem *seg;
+    const GenPiece *pieces;  // SegItem pieces
+    const ConstRun *consts;
     const uint8_t *payload;
     uint32_t *out;
-    const uint8_t *table;  // kLdsBytes, staged into LDS by every workgroup
-    const uint8_t *table_s4;  // kS4Bytes: the slicing-by-4 variants' image
+    const uint8_t *table;     // kLdsBytes: the nibble image (A/B variant 1)
+    const uint8_t *table_s4;  // kS4Bytes: the slicing-by-4 image (production)
     uint32_t ntiles;
     uint32_t ngen;
+    uint32_t nseg;
+    uint32_t nconst;
+    uint32_t general;  // nonzero when tiles[] holds general tiles (selects the kernel that has their code)
     uint32_t flags;
     uint32_t c_lg[5];
     uint32_t c_small[4];
-    uint64_t *stamps;  // diagnostic variant only: 4 x u64 per wave
+    uint64_t *stamps;  // diagnostic variants only: 4 x u64 per wave
     // Verification (crc32c_plan_verify): compare with expect[] instead of
     // storing to out[]; the last workgroup writes result[0] = mismatches,
     // result[1] = min bad index.
@@ -74,21 +72,8 @@ inline void init_sched_slots(uint32_t *w) {
     w[kSlotWords + kVFirstWord] = 0xffffffffu;
 }
 
-// Kernel variants; 0 is the production kernel, the others stay built for
-// A/B measurement and diagnostics (tools/kbench.py, tools/stamps.py).
-struct KernelVariant {
-    const char *name;
-    uint32_t threads;
-    uint32_t wg_per_cu;
-};
-constexpr int kNumVariants = 37;
-// Variants whose verification mode is built (crc32c_plan_verify).
-inline bool variant_verifies(int v) { return v >= 0 && v <= 2; }
-extern const KernelVariant kVariants[kNumVariants];
-
-// Persistent grid: min(work items / waves per workgroup, wg_per_cu * CUs) of the
-// variant; variant 0 runs one 12-wave workgroup per CU, min(items, CUs) of
-// them, and variant 11 picks its waves per workgroup by batch size.
-hipError_t launch_plan_kernel(const KParams &p, int variant, uint32_t num_cu, hipStream_t stream);
+// The production kernel (crc32c_kernel.hip): one 12-wave workgroup per CU,
+// min(work items, CUs) of them; p.expect selects the verification mode.
+hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream);
 
 }  // namespace hdfs_crc

@@ -2,6 +2,7 @@
 #include "plan.h"
 #include "hdfs_crc32c.h"
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 
@@ -16,54 +17,211 @@ static int fast_lg(uint32_t bpc) {
     return -1;
 }
 
-int build_plan(const crc32c_packet *pkts, size_t npkts, HostPlan *plan) {
-    plan->tiles.clear();
-    plan->gen.clear();
-    plan->nchecksums = plan->payload_bytes = plan->payload_extent = 0;
-    for (size_t i = 0; i < npkts; ++i) {
-        const crc32c_packet &p = pkts[i];
-        if (p.bpc == 0) return -EINVAL;
-        if (p.len == 0) continue;  // last-packet marker: no checksums (hadooprpc.c:644, 666)
-        const uint64_t n = (uint64_t(p.len) + p.bpc - 1) / p.bpc;  // hadooprpc.c:639
-        if (p.out_idx + n > (1ull << 32)) return -EINVAL;
-        if (p.out_idx + n > plan->nchecksums) plan->nchecksums = p.out_idx + n;
-        plan->payload_bytes += p.len;
-        if (p.payload_off + p.len > plan->payload_extent) plan->payload_extent = p.payload_off + p.len;
+void HostPlan::clear() {
+    tiles.clear();
+    gen.clear();
+    seg.clear();
+    pieces.clear();
+    consts.clear();
+    nchecksums = payload_bytes = 0;
+}
 
-        const uint64_t nfull = p.len / p.bpc;
-        const uint32_t tail = p.len % p.bpc;
-        const int lg = fast_lg(p.bpc);
+uint64_t HostPlan::items() const {
+    return uint64_t(tiles.size()) + (gen.size() + 1) / 2 + (seg.size() + 1) / 2 + consts.size();
+}
+
+static void push_gen(HostPlan *plan, uint64_t src, uint64_t out, uint32_t len) {
+    GenItem g;
+    g.src = src;
+    g.out = uint32_t(out);
+    g.len = len;
+    plan->gen.push_back(g);
+}
+
+int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
+    if (p.bpc == 0) return -EINVAL;
+    if (p.len == 0) return 0;  // last-packet marker: no checksums (hadooprpc.c:644, 666)
+    const uint64_t n = (uint64_t(p.len) + p.bpc - 1) / p.bpc;  // hadooprpc.c:639
+    if (p.out_idx + n > (1ull << 32)) return -EINVAL;
+    if (p.out_idx + n > plan->nchecksums) plan->nchecksums = p.out_idx + n;
+    plan->payload_bytes += p.len;
+
+    const uint64_t nfull = p.len / p.bpc;
+    const uint32_t tail = p.len % p.bpc;
+    const int lg = fast_lg(p.bpc);
+    if (lg >= 0) {
         // Any alignment: a tile off 16-byte alignment is read with unaligned
-        // dwordx4 buffer loads (config 2 five bytes off: 55 instead of 42.5
-        // us; through the general path it took 220 us).
-        if (lg >= 0) {
-            const uint64_t blocks = nfull << lg;  // 512-byte blocks of full chunks
-            for (uint64_t b = 0; b < blocks; b += kTileBlocks) {
-                const uint64_t nb = blocks - b < kTileBlocks ? blocks - b : kTileBlocks;
-                FastTile t;
-                t.src = p.payload_off + b * kBlockBytes;
-                t.out = uint32_t(p.out_idx + (b >> lg));
-                t.meta = uint32_t(nb) | (uint32_t(lg) << 8);
-                plan->tiles.push_back(t);
-            }
-        } else {
-            for (uint64_t c = 0; c < nfull; ++c) {
-                GenItem g;
-                g.src = p.payload_off + c * p.bpc;
-                g.out = uint32_t(p.out_idx + c);
-                g.len = p.bpc;
-                plan->gen.push_back(g);
-            }
+        // dwordx4 buffer loads (config 2 five bytes off: 55 instead of 42.5 us).
+        const uint64_t blocks = nfull << lg;  // 512-byte blocks of full chunks
+        for (uint64_t b = 0; b < blocks; b += kTileBlocks) {
+            const uint64_t nb = blocks - b < kTileBlocks ? blocks - b : kTileBlocks;
+            FastTile t;
+            t.src = p.payload_off + b * kBlockBytes;
+            t.out = uint32_t(p.out_idx + (b >> lg));
+            t.meta = uint32_t(nb) | (uint32_t(lg) << 8);
+            plan->tiles.push_back(t);
         }
-        if (tail) {
-            GenItem g;
-            g.src = p.payload_off + nfull * p.bpc;
-            g.out = uint32_t(p.out_idx + nfull);
-            g.len = tail;
-            plan->gen.push_back(g);
+    } else if (p.bpc >= 4 && p.bpc <= kMaxTileBpc) {
+        // General tiles: 16 / k chunks of k virtual blocks each.  A padded
+        // tile's first loads start up to 15 bytes before its first chunk
+        // (masked to zero): allowed when those bytes are in the same
+        // allocation (offset >= 16) or, for device addresses, the same page.
+        const uint32_t k = (p.bpc + kBlockBytes - 1) / kBlockBytes;
+        const uint32_t pad = k * kBlockBytes - p.bpc;
+        const uint64_t per = kTileBlocks / k;
+        for (uint64_t c = 0; c < nfull;) {
+            const uint64_t src = p.payload_off + c * p.bpc;
+            if (pad && !(absolute ? (src & 4095u) >= 16 : src >= 16)) {
+                push_gen(plan, src, p.out_idx + c, p.bpc);
+                ++c;
+                continue;
+            }
+            const uint64_t nch = std::min(per, nfull - c);
+            FastTile t;
+            t.src = src;
+            t.out = uint32_t(p.out_idx + c);
+            t.meta = general_meta(uint32_t(nch), k, pad);
+            plan->tiles.push_back(t);
+            c += nch;
         }
+    } else {
+        for (uint64_t c = 0; c < nfull; ++c) push_gen(plan, p.payload_off + c * p.bpc, p.out_idx + c, p.bpc);
+    }
+    if (tail) push_gen(plan, p.payload_off + nfull * p.bpc, p.out_idx + nfull, tail);
+    return 0;
+}
+
+int build_plan(const crc32c_packet *pkts, size_t npkts, HostPlan *plan, bool absolute) {
+    plan->clear();
+    for (size_t i = 0; i < npkts; ++i) {
+        const int rc = append_packet(pkts[i], plan, absolute);
+        if (rc) return rc;
     }
     return 0;
+}
+
+namespace {
+
+// crc(0, zeros(n)) for the polynomial: the register ~0 moved over n zero
+// bytes, post-inverted (crc32c.c:84, 106 conditioning).
+struct ZeroCrc {
+    uint32_t poly;
+    uint32_t last_len = 0, last = 0;
+    uint32_t operator()(uint32_t n) {
+        if (n != last_len || !last_len) {
+            last = op_zeros(n, poly).apply(0xffffffffu) ^ 0xffffffffu;
+            last_len = n;
+        }
+        return last;
+    }
+};
+
+void push_const(HostPlan *plan, uint64_t out, uint32_t value) {
+    if (!plan->consts.empty()) {
+        ConstRun &r = plan->consts.back();
+        if (r.value == value && uint64_t(r.out) + r.count == out && r.count < kConstRunMax) {
+            ++r.count;
+            return;
+        }
+    }
+    plan->consts.push_back(ConstRun{uint32_t(out), 1u, value, 0u});
+}
+
+}  // namespace
+
+int build_write_plan(const crc32c_buffer *buffers, uint32_t n_buffers, uint64_t bufferoffset, uint64_t len,
+                     uint64_t blockoffset, uint32_t packetsize, uint32_t bpc, uint32_t poly, HostPlan *plan) {
+    plan->clear();
+    if (bpc == 0 || packetsize == 0 || (n_buffers && !buffers)) return -EINVAL;
+    std::vector<uint64_t> start(size_t(n_buffers) + 1, 0);  // stream offset of each buffer
+    for (uint32_t i = 0; i < n_buffers; ++i) {
+        if (buffers[i].len > UINT64_MAX - start[i]) return -EINVAL;
+        start[i + 1] = start[i] + buffers[i].len;
+    }
+    if (bufferoffset > start[n_buffers] || len > start[n_buffers] - bufferoffset) return -EINVAL;
+
+    ZeroCrc zero{poly};
+    uint64_t out = 0, sent = 0;
+    uint32_t bi = 0;  // buffer holding the current chunk's first byte
+    crc32c_packet run{};  // consecutive chunks of one packet inside one data buffer
+    bool in_run = false;
+    uint32_t run_buf = 0;
+    auto flush = [&]() -> int {
+        if (!in_run) return 0;
+        in_run = false;
+        return append_packet(run, plan, true);
+    };
+    // Packet cutting of hadoop_rpc_send_packets (hadooprpc.c:827-857), as crc32c_packetize.
+    for (;;) {
+        uint64_t plen = len - sent < packetsize ? len - sent : packetsize;
+        const uint64_t past = (blockoffset + sent) % bpc;
+        if (plen > 0 && past != 0) plen = std::min<uint64_t>(bpc - past, len - sent);
+        if (plen == 0) break;
+        if (plen > UINT32_MAX) return -E2BIG;
+        const uint64_t pos = bufferoffset + sent;  // stream offset of the packet
+        const uint64_t nch = (plen + bpc - 1) / bpc;
+        if (out + nch > (1ull << 32)) return -E2BIG;
+        for (uint64_t c = 0; c < nch; ++c) {
+            const uint64_t a = pos + c * bpc;
+            const uint32_t clen = uint32_t(std::min<uint64_t>(bpc, plen - c * bpc));
+            const uint64_t b = a + clen;
+            while (bi + 1 < n_buffers && start[bi + 1] <= a) ++bi;
+            // (zero-length buffers are skipped by the loop above)
+            if (b <= start[bi + 1]) {  // inside one buffer
+                if (buffers[bi].data) {
+                    const uint64_t addr = uint64_t(uintptr_t(buffers[bi].data)) + (a - start[bi]);
+                    if (in_run && run_buf == bi && c > 0 && run.payload_off + run.len == addr) {
+                        run.len += clen;
+                    } else {
+                        if (int rc = flush()) return rc;
+                        run = crc32c_packet{addr, out + c, clen, bpc};
+                        run_buf = bi;
+                        in_run = true;
+                    }
+                } else {
+                    if (int rc = flush()) return rc;
+                    push_const(plan, out + c, zero(clen));
+                }
+                continue;
+            }
+            // spans buffers: one SegItem with a piece per data buffer
+            if (int rc = flush()) return rc;
+            SegItem s{uint32_t(plan->pieces.size()), 0u, uint32_t(out + c), clen};
+            for (uint32_t j = bi; j < n_buffers && start[j] < b; ++j) {
+                const uint64_t lo = std::max(a, start[j]), hi = std::min(b, start[j + 1]);
+                if (hi <= lo || !buffers[j].data) continue;
+                GenPiece pc;
+                pc.src = uint64_t(uintptr_t(buffers[j].data)) + (lo - start[j]);
+                pc.start = uint32_t(lo - a);
+                pc.len = uint32_t(hi - lo);
+                plan->pieces.push_back(pc);
+                ++s.npieces;
+            }
+            if (s.npieces == 0)
+                push_const(plan, out + c, zero(clen));
+            else
+                plan->seg.push_back(s);
+        }
+        if (int rc = flush()) return rc;
+        out += nch;
+        sent += plen;
+    }
+    // append_packet counted the runs; the totals cover every chunk.
+    plan->nchecksums = out;
+    plan->payload_bytes = len;
+    return 0;
+}
+
+void rebase_plan(HostPlan *plan, uint64_t *base) {
+    uint64_t lo = UINT64_MAX;
+    for (const FastTile &t : plan->tiles) lo = std::min(lo, t.src);
+    for (const GenItem &g : plan->gen) lo = std::min(lo, g.src);
+    for (const GenPiece &p : plan->pieces) lo = std::min(lo, p.src);
+    lo = lo == UINT64_MAX ? 0 : lo & ~uint64_t(15);
+    for (FastTile &t : plan->tiles) t.src -= lo;
+    for (GenItem &g : plan->gen) g.src -= lo;
+    for (GenPiece &p : plan->pieces) p.src -= lo;
+    *base = lo;
 }
 
 }  // namespace hdfs_crc
@@ -81,6 +239,24 @@ extern "C" int crc32c_debug_plan(const crc32c_packet *pkts, size_t npkts, void *
     if (gen && gen_cap)
         std::memcpy(gen, plan.gen.data(),
                     sizeof(hdfs_crc::GenItem) * (plan.gen.size() < gen_cap ? plan.gen.size() : gen_cap));
+    return 0;
+}
+
+extern "C" int crc32c_debug_write_plan(const crc32c_buffer *buffers, uint32_t n_buffers, uint64_t bufferoffset,
+                                       uint64_t len, uint64_t blockoffset, uint32_t packetsize, uint32_t bpc,
+                                       uint64_t counts[6]) {
+    hdfs_crc::HostPlan plan;
+    const int rc = hdfs_crc::build_write_plan(buffers, n_buffers, bufferoffset, len, blockoffset, packetsize, bpc,
+                                              hdfs_crc::kPoly, &plan);
+    if (rc) return rc;
+    if (counts) {
+        counts[0] = plan.tiles.size();
+        counts[1] = plan.gen.size();
+        counts[2] = plan.seg.size();
+        counts[3] = plan.pieces.size();
+        counts[4] = plan.consts.size();
+        counts[5] = plan.nchecksums;
+    }
     return 0;
 }
 

@@ -1,0 +1,129 @@
+// runtime_internal.h -- the host runtime's object layouts, shared by the
+// product library's runtime files and by the debug library (which links
+// against libhdfs_crc32c.so).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <mutex>
+#include <vector>
+
+#include "hdfs_crc32c.h"
+#include "kernel_abi.h"
+#include "plan.h"
+
+namespace hdfs_crc {
+
+// Thread-local error text (crc32c_last_error) and its setter.
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#define HIP_TRY(expr)                                                                                          \
+    do {                                                                                                       \
+        hipError_t e_ = (expr);                                                                                \
+        if (e_ != hipSuccess)                                                                                  \
+            return ::hdfs_crc::fail(-EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+    } while (0)
+
+// Restores the caller's current device (torch and other libraries keep their own).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// The two device scheduler slots (kernel_abi.h) of one launch sequence that
+// the GPU runs in order: a plan, or a host-pipeline stage.
+struct SchedSlots {
+    uint32_t *d = nullptr;  // 2 * kSlotWords u32
+    int cur = 0;
+};
+
+struct Stage {
+    hipStream_t stream = nullptr;
+    hipEvent_t copied = nullptr;  // the slice's H2D payload copy (on the context's copy stream) is done
+    hipEvent_t done = nullptr;
+    uint8_t *d_payload = nullptr;
+    size_t payload_cap = 0;
+    uint8_t *h_payload = nullptr;  // pinned staging, only for pageable or gathered payloads
+    size_t staging_cap = 0;
+    // Work descriptors: pinned host memory the kernel reads in place (d_desc
+    // is its device mapping).  A slice's 64 KiB of descriptors are not worth
+    // a copy of their own: on the copy stream each copy costs ~25 us (9 us
+    // of transfer plus the ~15 us gap between copy commands).
+    uint8_t *h_desc = nullptr, *d_desc = nullptr;
+    size_t desc_cap = 0;
+    // Checksums: written by the kernel straight into pinned host memory
+    // (d_out is h_out's mapping), which saves a D2H copy on the tail.
+    uint32_t *h_out = nullptr, *d_out = nullptr;
+    size_t out_cap = 0;
+    bool pending = false;
+    // packets of the slice in flight: (global out_idx, local out index, count)
+    std::vector<uint64_t> scatter;
+    SchedSlots sched;  // this stage's launches are serialised on its stream
+};
+
+// Device copy of a HostPlan's work items, one allocation.
+struct DevicePlan {
+    uint8_t *d = nullptr;
+    uint32_t ntiles = 0, ngen = 0, nseg = 0, nconst = 0;
+    bool general = false;  // some tile is a general tile
+    size_t tiles_off = 0, gen_off = 0, seg_off = 0, pieces_off = 0, consts_off = 0;
+};
+
+}  // namespace hdfs_crc
+
+struct crc32c_ctx {
+    int device = 0;
+    int num_cu = 0;
+    // per checksum type (0 = CRC32C, 1 = CRC32 / CRC32C_TYPE_CRC32)
+    uint8_t *d_table[2] = {nullptr, nullptr};
+    uint8_t *d_table_s4[2] = {nullptr, nullptr};
+    uint32_t c_lg[2][5];
+    uint32_t c_small[2][4];
+    std::mutex mu;
+    // Host pipeline: every stage's H2D copies go on one copy stream, so they
+    // run back to back at the full link rate while the other stage's kernel
+    // runs on its own stream.  Two copies on two streams would share the
+    // link, finish together and leave it idle while both stages drain.
+    hipStream_t copy_stream = nullptr;
+    hdfs_crc::Stage stage[2];
+};
+
+struct crc32c_plan {
+    crc32c_ctx *ctx = nullptr;
+    // Verify launches of a plan share its scheduler slots, so they are kept
+    // in GPU order: one on another stream than the previous one first waits
+    // for it (last_done).  Exec launches are not ordered.
+    std::mutex mu;
+    hdfs_crc::SchedSlots sched;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t last_done = nullptr;
+    bool launched = false;
+    hdfs_crc::DevicePlan dp;
+    uint64_t nchecksums = 0, payload_bytes = 0;
+    uint32_t flags = 0;
+    // Absolute plans (CRC32C_DEVICE_ADDRESSES, crc32c_plan_create_buffers):
+    // offsets are relative to this device address (the lowest address read,
+    // rounded down to 16), which the launches pass as the payload base.
+    uint64_t abs_base = 0;
+    bool absolute = false;
+};
+
+namespace hdfs_crc {
+
+// Kernel parameters of a plan's launch on (payload, out); checks nothing.
+KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out);
+// Uploads a HostPlan's items to the context's device (into *dp).
+int upload_plan(const HostPlan &hp, DevicePlan *dp);
+void free_device_plan(DevicePlan *dp);
+// Creates a plan object from a built HostPlan (absolute: rebased, base given).
+int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute, uint64_t abs_base,
+              crc32c_plan **out);
+
+}  // namespace hdfs_crc

@@ -1,17 +1,14 @@
-"""Multi-GPU layout of the CRC32C path.
+"""Python mirror of the multi-GPU layout and gather.
 
-Every chunk's checksum depends only on its own bytes (crc32c(0, chunk),
-src/hadooprpc.c:740), and packets / blocks are independent
-(src/hadooprpc.c:815-860, src/fuse.c:580-647), so a file shards by whole
-blocks with no data-path exchange: block b of the file goes to rank
-b mod world (round-robin, as BASELINE config 4 states), each rank checksums
-its blocks from its own HBM, and the only collective is one gather of the
-u32 checksum arrays to rank 0 (RCCL over xGMI on the GPU box; gloo in the
-CPU tests).  One process per GPU.
-
-Functions here are pure host logic plus one torch.distributed call, so the
-same code runs under ``gloo`` on CPU tensors and ``nccl`` (= RCCL) on GPU
-tensors.
+The product path is the C ABI's crc32c_multi_plan_* (csrc/crc32c_multi.hip):
+a file's packets dealt round-robin over the ranks in groups of consecutive
+packets (one HDFS block each, src/fuse.c:580-647 / src/hadooprpc.c:815-860),
+every rank checksumming its shard from its own HBM, and one group of RCCL
+point-to-point transfers landing every group's u32 checksum range in file
+order on rank 0 -- the path's only exchange.  This module uses the SAME
+layout code (crc32c_multi_layout / crc32c_multi_shard_packets, host-only C)
+and the same per-group send / receive pattern over torch.distributed, so the
+CPU tests can run the N > 1 path under gloo.
 """
 from __future__ import annotations
 
@@ -21,54 +18,87 @@ BLOCK_BYTES = 4 << 20      # dfs.block.size in BASELINE config 3/4
 PACKET_BYTES = 64 << 10    # packetsize, src/hadooprpc.c:830
 
 
+def _pkg():
+    import sys
+
+    return sys.modules["hdfs_crc32c_amd"]
+
+
 def rank_blocks(nblocks: int, world: int, rank: int) -> list[int]:
-    """Global block indices owned by `rank` (round-robin)."""
+    """Global block (group) indices owned by `rank` (round-robin)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError("bad rank %d of world %d" % (rank, world))
     return list(range(rank, nblocks, world))
 
 
-def max_blocks_per_rank(nblocks: int, world: int) -> int:
-    return (nblocks + world - 1) // world
+def layout(pkts, group_packets: int, world: int):
+    """(per-group [rank, shard offset, payload offset, bytes], shard bytes per rank) -- crc32c_multi_layout."""
+    return _pkg().multi_layout(pkts, group_packets, world)
 
 
-def rank_payload(file_bytes: np.ndarray, blocks: list[int], block_bytes: int = BLOCK_BYTES) -> np.ndarray:
-    """The rank's device buffer: its blocks back to back (block j of the
-    rank at offset j * block_bytes)."""
-    out = np.empty(len(blocks) * block_bytes, dtype=np.uint8)
-    for j, b in enumerate(blocks):
-        out[j * block_bytes:(j + 1) * block_bytes] = file_bytes[b * block_bytes:(b + 1) * block_bytes]
+def rank_payload(file_bytes: np.ndarray, lay: np.ndarray, shard_bytes: np.ndarray, rank: int) -> np.ndarray:
+    """Rank's shard buffer, laid out as crc32c_multi_layout says (+16 bytes slack)."""
+    out = np.zeros(int(shard_bytes[rank]) + 16, np.uint8)
+    for r, soff, poff, n in lay.astype(np.int64):
+        if r == rank:
+            out[soff:soff + n] = file_bytes[poff:poff + n]
     return out
 
 
-def assemble(gathered: list[np.ndarray], nblocks: int, per_block: int) -> np.ndarray:
-    """Rank 0: the file's checksum array in block order from every rank's
-    (padded) array; rank r's j-th block is global block r + j * world."""
-    world = len(gathered)
-    out = np.empty(nblocks * per_block, dtype=np.uint32)
-    for r, arr in enumerate(gathered):
-        a = np.asarray(arr).view(np.uint32)
-        for j, b in enumerate(range(r, nblocks, world)):
-            out[b * per_block:(b + 1) * per_block] = a[j * per_block:(j + 1) * per_block]
+def rank_packets(pkts, group_packets: int, world: int, rank: int) -> np.ndarray:
+    """Rank's packets: payload offsets into its shard, out indices global -- crc32c_multi_shard_packets."""
+    return _pkg().multi_shard_packets(pkts, group_packets, world, rank)
+
+
+def group_ranges(pkts, group_packets: int) -> list[tuple[int, int]]:
+    """Each group's checksum range (first global out index, count)."""
+    pkts = np.asarray(pkts)
+    out = []
+    for g in range(0, pkts.size, group_packets):
+        p = pkts[g:g + group_packets]
+        p = p[p["len"] > 0]
+        if not p.size:
+            out.append((0, 0))
+            continue
+        n = (p["len"].astype(np.int64) + p["bpc"] - 1) // p["bpc"]
+        out.append((int(p["out_idx"].min()), int(n.sum())))
     return out
 
 
-def gather_checksums(local, nblocks: int, per_block: int, world: int, rank: int):
-    """Gather every rank's checksum array (a torch int32 tensor holding
-    len(rank_blocks) * per_block values, on the rank's device for nccl or on
-    the CPU for gloo) to rank 0.  Returns the file's checksums in block
-    order (np.uint32) on rank 0, None elsewhere."""
+def gather_checksums(local, pkts, group_packets: int, world: int, rank: int):
+    """Every group's checksum range from its rank's array (a torch int32
+    tensor indexed by GLOBAL out index, on the rank's device for nccl or on
+    the CPU for gloo) into place on rank 0, one send / receive per group, as
+    crc32c_multi_plan_exec does with RCCL.  Returns the file's checksums
+    (np.uint32) on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
 
-    cap = max_blocks_per_rank(nblocks, world) * per_block
-    send = torch.zeros(cap, dtype=torch.int32, device=local.device)
-    n = min(int(local.numel()), cap)
-    send[:n] = local.reshape(-1)[:n]
-    if world == 1:
-        return assemble([send.cpu().numpy()], nblocks, per_block)
-    bufs = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
-    dist.gather(send, bufs, dst=0)
+    ranges = group_ranges(pkts, group_packets)
+    total = max((o + n for o, n in ranges), default=0)
+    full = torch.zeros(max(total, 1), dtype=torch.int32, device=local.device) if rank == 0 else None
+    ops = []
+    for g, (o, n) in enumerate(ranges):
+        owner = g % world
+        if not n:
+            continue
+        if owner == rank and rank == 0:
+            full[o:o + n] = local[o:o + n]
+        elif owner == rank:
+            ops.append(dist.P2POp(dist.isend, local[o:o + n].contiguous(), 0))
+        elif rank == 0:
+            buf = torch.empty(n, dtype=torch.int32, device=local.device)
+            ops.append((dist.P2POp(dist.irecv, buf, owner), o, buf))
+    if world > 1:
+        p2p = [op if isinstance(op, dist.P2POp) else op[0] for op in ops]
+        if p2p:
+            for req in dist.batch_isend_irecv(p2p):
+                req.wait()
+        if rank == 0:
+            for op in ops:
+                if not isinstance(op, dist.P2POp):
+                    _, o, buf = op
+                    full[o:o + buf.numel()] = buf
     if rank != 0:
         return None
-    return assemble([b.cpu().numpy() for b in bufs], nblocks, per_block)
+    return full[:total].cpu().numpy().view(np.uint32)

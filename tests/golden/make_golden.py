@@ -128,6 +128,10 @@ def main() -> None:
         ("c2_4096_packets", oracle.uniform_packets(4096)),
         ("c5_mixed_bpc_4096", oracle.mixed_packets(4096)),
         ("ragged_tail_257", oracle.uniform_packets(257, pkt_len=65436, bpc=512, stride=65536)),
+        # config 4: a 128 MiB file = 32 blocks x 64 packets, checksums in file order
+        ("c4_file_128MiB", oracle.uniform_packets(2048)),
+        # config 2 with bytesPerChecksum 1536 (general tiles + 1024-byte tails)
+        ("c2_bpc1536", oracle.uniform_packets(4096, bpc=1536)),
     ]
     for name, pk in specs:
         nbytes = int((pk["payload_off"] + pk["len"]).max())
@@ -139,6 +143,7 @@ def main() -> None:
             "packets": {"count": int(pk.size), "len": [int(x) for x in np.unique(pk["len"])],
                         "bpc_cycle": [int(x) for x in pk["bpc"][:3]],
                         "layout": "mixed_packets" if name.startswith("c5") else "uniform_packets",
+                        "bpc": int(pk["bpc"][0]),
                         "stride": int(pk["payload_off"][1]) if pk.size > 1 else 0},
             "sha256_le": hashlib.sha256(exp.astype("<u4").tobytes()).hexdigest(),
             "head": [hx(int(v)) for v in exp[:8]], "tail": [hx(int(v)) for v in exp[-8:]],

@@ -1,5 +1,6 @@
 // Host-code sanitizer run (TEST INFRASTRUCTURE): the host-only sources of
-// libhdfs_crc32c.so (crc_math.cpp, cpu_crc32c.cpp, plan.cpp, framing.cpp)
+// libhdfs_crc32c.so (crc_math.cpp, cpu_crc32c.cpp, plan.cpp, framing.cpp,
+// frames.cpp)
 // built with -fsanitize=address,undefined and driven over randomized inputs
 // whose buffers are heap blocks of exactly the size the ABI promises to touch,
 // so a read or write one byte past them aborts.  Results are compared with the
@@ -9,6 +10,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -26,6 +28,13 @@ int crc32c_debug_plan(const crc32c_packet *pkts, size_t npkts, void *tiles, size
                       size_t gen_cap, uint64_t *ntiles, uint64_t *ngen);
 size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags);
 size_t crc32c_debug_lds_image(void *dst, size_t cap, uint32_t *c_lg, uint32_t *c_small);
+
+// frames.cpp verifies through the GPU runtime, which is not part of this
+// host-only build: only its parser is exercised here.
+int64_t crc32c_verify_host(crc32c_ctx *, const void *, const crc32c_packet *, size_t, const uint32_t *, uint32_t,
+                           uint64_t *) {
+    return -19;
+}
 }
 
 namespace {
@@ -149,10 +158,22 @@ void plans_and_framing(std::mt19937_64 &rng) {
         const uint64_t nsums = crc32c_batch_nchecksums(pk.data(), pk.size());
         std::vector<int> seen(nsums, 0);
         for (uint64_t i = 0; i < nt; ++i) {
-            const uint32_t nb = tiles[i].meta & 0xffu, lg = (tiles[i].meta >> 8) & 0xffu;
-            CHECK(nb >= 1 && nb <= 16 && lg <= 4 && (nb % (1u << lg)) == 0, "tile meta %x", tiles[i].meta);
-            CHECK(tiles[i].src + 512ull * nb <= extent, "tile past the payload");
-            for (uint32_t c = 0; c < (nb >> lg); ++c)
+            const uint32_t meta = tiles[i].meta;
+            uint32_t nch, bpc;
+            if (meta & hdfs_crc::kGeneralTile) {
+                const uint32_t k = (meta >> 8) & 31u, pad = (meta >> 18) & 511u;
+                nch = (meta >> 13) & 31u;
+                bpc = k * 512u - pad;
+                CHECK(nch >= 1 && nch * k <= 16 && (meta & 0xffu) == nch * k && bpc >= 4, "general tile meta %x", meta);
+                CHECK(pad == 0 || tiles[i].src >= 16, "padded tile too close to the payload start");
+            } else {
+                const uint32_t nb = meta & 0xffu, lg = (meta >> 8) & 0xffu;
+                CHECK(nb >= 1 && nb <= 16 && lg <= 4 && (nb % (1u << lg)) == 0, "tile meta %x", meta);
+                nch = nb >> lg;
+                bpc = 512u << lg;
+            }
+            CHECK(tiles[i].src + uint64_t(bpc) * nch <= extent, "tile past the payload");
+            for (uint32_t c = 0; c < nch; ++c)
                 if (tiles[i].out + c < nsums) seen[tiles[i].out + c]++;
         }
         for (uint64_t i = 0; i < ng; ++i) {
@@ -196,6 +217,148 @@ void plans_and_framing(std::mt19937_64 &rng) {
     }
 }
 
+// crc(0, chunk) of one HostPlan item evaluated on the CPU from its
+// descriptor alone (addresses absolute: host pointers of the test).
+uint32_t crc_at(uint64_t addr, uint32_t len) {
+    return oracle_crc32c_bytewise(0, reinterpret_cast<const void *>(uintptr_t(addr)), len);
+}
+
+// Packet assembly (build_write_plan) over random buffer lists of exactly
+// sized heap blocks (NULL = zero fill): every item is evaluated from its
+// descriptor and compared with the oracle over the assembled stream, cut
+// into packets and chunks as hadooprpc.c:815-860 / 733-742 do.
+void write_plans(std::mt19937_64 &rng) {
+    for (int it = 0; it < 300; ++it) {
+        const uint32_t nb = 1 + uint32_t(rng() % 5);
+        std::vector<crc32c_buffer> bufs(nb);
+        std::vector<uint8_t *> owned;
+        std::vector<uint8_t> stream;
+        for (auto &b : bufs) {
+            b.len = (rng() % 4 == 0) ? rng() % 50 : rng() % 90000;
+            if (rng() % 3 == 0) {
+                b.data = nullptr;
+                stream.insert(stream.end(), size_t(b.len), 0);
+            } else {
+                uint8_t *p = exact_bytes(rng, size_t(b.len));
+                owned.push_back(p);
+                b.data = p;
+                stream.insert(stream.end(), p, p + b.len);
+            }
+        }
+        const uint64_t total = stream.size();
+        const uint64_t boff = total ? rng() % (total + 1) : 0;
+        const uint64_t len = total - boff ? rng() % (total - boff + 1) : 0;
+        const uint32_t bpcs[] = {512, 1024, 4096, 100, 1536, 3};
+        const uint32_t bpc = bpcs[rng() % 6];
+        const uint64_t blockoffset = rng() % 3 ? 0 : rng() % 100000;
+        const uint32_t psize = rng() % 2 ? 65536u : bpc * uint32_t(1 + rng() % 8);
+        hdfs_crc::HostPlan hp;
+        CHECK(hdfs_crc::build_write_plan(bufs.data(), nb, boff, len, blockoffset, psize, bpc, hdfs_crc::kPoly, &hp) == 0,
+              "write plan rc");
+        // expected: the assembled bytes, packetized and chunked
+        std::vector<uint32_t> want;
+        const uint64_t np = crc32c_packetize(len, blockoffset, psize, bpc, nullptr, 0);
+        std::vector<uint64_t> lens(np);
+        crc32c_packetize(len, blockoffset, psize, bpc, lens.data(), np);
+        uint64_t pos = boff;
+        for (uint64_t pl : lens) {
+            for (uint64_t c = 0; c * bpc < pl; ++c) {
+                const uint32_t cl = uint32_t(std::min<uint64_t>(bpc, pl - c * bpc));
+                want.push_back(oracle_crc32c_bytewise(0, stream.data() + pos + c * bpc, cl));
+            }
+            pos += pl;
+        }
+        CHECK(hp.nchecksums == want.size(), "write plan checksums %llu vs %zu", (unsigned long long)hp.nchecksums,
+              want.size());
+        std::vector<uint32_t> got(want.size(), 0xdeadbeefu);
+        std::vector<int> seen(want.size(), 0);
+        auto put = [&](uint64_t i, uint32_t v) {
+            if (i < got.size()) {
+                got[i] = v;
+                seen[i]++;
+            }
+        };
+        for (const auto &t : hp.tiles) {
+            uint32_t nch, tb;
+            if (t.meta & hdfs_crc::kGeneralTile) {
+                nch = (t.meta >> 13) & 31u;
+                tb = ((t.meta >> 8) & 31u) * 512u - ((t.meta >> 18) & 511u);
+                CHECK(((t.meta >> 18) & 511u) == 0 || (t.src & 4095u) >= 16, "padded tile page rule");
+            } else {
+                nch = (t.meta & 0xffu) >> ((t.meta >> 8) & 0xffu);
+                tb = 512u << ((t.meta >> 8) & 0xffu);
+            }
+            for (uint32_t c = 0; c < nch; ++c) put(t.out + c, crc_at(t.src + uint64_t(c) * tb, tb));
+        }
+        for (const auto &g : hp.gen) put(g.out, crc_at(g.src, g.len));
+        for (const auto &sg : hp.seg) {
+            std::vector<uint8_t> chunk(sg.len, 0);
+            for (uint32_t u = 0; u < sg.npieces; ++u) {
+                const auto &pc = hp.pieces[sg.first + u];
+                CHECK(pc.start + uint64_t(pc.len) <= sg.len && pc.len >= 1, "piece range");
+                std::memcpy(chunk.data() + pc.start, reinterpret_cast<const void *>(uintptr_t(pc.src)), pc.len);
+            }
+            put(sg.out, oracle_crc32c_bytewise(0, chunk.data(), sg.len));
+        }
+        for (const auto &cr : hp.consts)
+            for (uint32_t k = 0; k < cr.count; ++k) put(cr.out + k, cr.value);
+        for (size_t i = 0; i < want.size(); ++i) {
+            CHECK(seen[i] == 1, "write chunk %zu covered %d times", i, seen[i]);
+            CHECK(got[i] == want[i], "write chunk %zu: %08x vs %08x", i, got[i], want[i]);
+        }
+        for (uint8_t *p : owned) std::free(p);
+    }
+}
+
+// Received frames (frames.cpp): frames built by crc32c_frame_packets with
+// the data behind each prefix parse back to the same fields, into an
+// exactly sized buffer; a truncated buffer yields only its whole frames.
+void frames_parse(std::mt19937_64 &rng) {
+    for (int it = 0; it < 200; ++it) {
+        const size_t np = 1 + rng() % 20;
+        std::vector<crc32c_packet> pk(np);
+        uint64_t off = 0, out = 0;
+        for (size_t i = 0; i < np; ++i) {
+            pk[i].payload_off = off;
+            pk[i].len = i + 1 == np ? 0 : uint32_t(rng() % 70000);
+            pk[i].bpc = 512;
+            pk[i].out_idx = out;
+            out += crc32c_nchunks(pk[i].len, 512);
+            off += pk[i].len;
+        }
+        std::vector<uint32_t> sums(out ? out : 1, 0x12345678u);
+        const size_t need = crc32c_frame_packets(pk.data(), np, sums.data(), 0, 4096, 0, 4, nullptr, 0, nullptr);
+        std::vector<uint8_t> prefix(need);
+        std::vector<uint64_t> po(np + 1);
+        crc32c_frame_packets(pk.data(), np, sums.data(), 0, 4096, 0, 4, prefix.data(), need, po.data());
+        const size_t total = need + off;
+        uint8_t *buf = static_cast<uint8_t *>(std::malloc(total));
+        size_t w = 0;
+        for (size_t i = 0; i < np; ++i) {
+            std::memcpy(buf + w, prefix.data() + po[i], po[i + 1] - po[i]);
+            w += po[i + 1] - po[i];
+            std::memset(buf + w, int(i), pk[i].len);
+            w += pk[i].len;
+        }
+        std::vector<crc32c_frame_info> info(np);
+        uint64_t used = 0;
+        CHECK(crc32c_parse_frames(buf, total, info.data(), np, &used) == int64_t(np) && used == total, "parse all");
+        for (size_t i = 0; i < np; ++i) {
+            CHECK(info[i].data_len == pk[i].len && info[i].offset_in_block == int64_t(4096 + pk[i].payload_off) &&
+                      info[i].seqno == int64_t(i) && info[i].last == (i + 1 == np) &&
+                      info[i].nsums == crc32c_nchunks(pk[i].len, 512),
+                  "frame %zu fields", i);
+        }
+        const size_t cut = rng() % total;
+        uint8_t *part = static_cast<uint8_t *>(std::malloc(cut ? cut : 1));
+        std::memcpy(part, buf, cut);
+        const int64_t k = crc32c_parse_frames(part, cut, info.data(), np, &used);
+        CHECK(k >= 0 && k < int64_t(np) && used <= cut, "partial parse");
+        std::free(part);
+        std::free(buf);
+    }
+}
+
 void table_images() {
     const size_t n4 = crc32c_debug_lds_image_s4(nullptr, 0, 0);
     for (uint32_t flags : {0u, uint32_t(CRC32C_TYPE_CRC32)}) {
@@ -217,6 +380,8 @@ int main() {
     scalar_and_chunks(rng);
     packetize(rng);
     plans_and_framing(rng);
+    write_plans(rng);
+    frames_parse(rng);
     table_images();
     if (g_fail) {
         std::fprintf(stderr, "%d failures\n", g_fail);

@@ -41,7 +41,7 @@ def run_dev(hdfs, ctx, payload: np.ndarray, pk: np.ndarray, flags: int = 0, offs
 
 
 @pytest.mark.parametrize("name", ["c1_one_packet", "c3_one_block_4MiB", "c5_mixed_bpc_96", "ragged_tail_257",
-                                  "c2_4096_packets", "c5_mixed_bpc_4096"])
+                                  "c2_4096_packets", "c5_mixed_bpc_4096", "c4_file_128MiB", "c2_bpc1536"])
 def test_golden_batches_device_resident(hdfs, gpu_ctx, golden, name):
     spec = [b for b in golden["batches"] if b["name"] == name][0]
     pk = golden_batch_packets(spec)
@@ -356,118 +356,170 @@ def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     assert np.array_equal(got2[:127], got[1:128])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 8, 9, 10, 11, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 27, 29, 31, 32, 33, 34, 35])
-def test_every_product_kernel_variant(hdfs, golden, orc, variant, monkeypatch):
-    """Both table schemes (0 = slicing-by-4 chains, production; 1 = positional
-    nibble tables) and the A/B shapes (2 = 16 waves per CU, 8 = descriptor
-    prefetch, 9 = 8 waves, 10 = concentrated grid, 11 = small-batch shapes of
-    8 / 4 / 2 / 1 waves per workgroup) are bit-exact: golden
-    config-2 digest, mixed bpc and a ragged batch through the general path."""
-    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
+@pytest.mark.parametrize("name", ["c1_one_packet", "c3_one_block_4MiB", "c5_mixed_bpc_96", "ragged_tail_257",
+                                  "c2_4096_packets", "c5_mixed_bpc_4096", "c4_file_128MiB", "c2_bpc1536"])
+def test_golden_batches_verify_clean(hdfs, gpu_ctx, golden, name):
+    """crc32c_plan_verify of every golden batch against its own digest-checked
+    checksums: no mismatch; one flipped expected value: exactly that one."""
+    torch = _torch()
+    spec = [b for b in golden["batches"] if b["name"] == name][0]
+    pk = golden_batch_packets(spec)
+    payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+    got = run_dev(hdfs, gpu_ctx, payload, pk)
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(got.view(np.int32).copy()).cuda()
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [0, 0xFFFFFFFF]
+    k = got.size * 2 // 3
+    exp[k] ^= 0x40
+    plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [1, k]
+    plan.close()
+
+
+def test_kernel_variant_env_has_no_effect(hdfs, golden, monkeypatch):
+    """The product library never switches kernels: with the round-1 A/B
+    selector set to a wrong-result diagnostic variant, a fresh context still
+    computes the golden config-2 digest and verifies clean."""
+    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", "3")
     ctx = hdfs.Context(0)
     try:
-        for name in ("c2_4096_packets", "c5_mixed_bpc_96", "ragged_tail_257"):
-            spec = [b for b in golden["batches"] if b["name"] == name][0]
-            pk = golden_batch_packets(spec)
-            payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
-            got = run_dev(hdfs, ctx, payload, pk)
-            assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"], name
+        spec = [b for b in golden["batches"] if b["name"] == "c2_4096_packets"][0]
+        pk = golden_batch_packets(spec)
+        payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+        got = run_dev(hdfs, ctx, payload, pk)
+        assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 5, 9, 35, 36])
+def test_debug_library_variants_exact(hdfs, golden, orc, variant):
+    """The A/B kernels of libhdfs_crc32c_debug.so that compute checksums (1 =
+    positional nibble tables, 2 = 16 waves per CU, 5 / 36 = stamped, 9 = 8
+    waves, 35 = half-column image) are bit-exact through
+    crc32c_debug_plan_exec_variant: golden config-2 / mixed / ragged digests,
+    a random ragged batch with general tiles, and CHECKSUM_CRC32."""
+    torch = _torch()
+    name, exact = hdfs.variant_info(variant)
+    assert exact and name
+    ctx = hdfs.Context(0)
+    stream = torch.cuda.current_stream()
+
+    def run(payload, pk, flags=0):
+        dev = torch.from_numpy(payload).cuda()
+        n = hdfs.total_checksums(pk)
+        out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        plan = hdfs.Plan(ctx, pk, flags)
+        stamps = torch.zeros(4 * 256 * 16, dtype=torch.int64, device="cuda")
+        plan.exec_variant(dev.data_ptr(), out.data_ptr(), variant, stamps.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        plan.close()
+        return out.cpu().numpy().view(np.uint32)[:n]
+
+    try:
+        for nm in ("c2_4096_packets", "c5_mixed_bpc_96", "ragged_tail_257", "c2_bpc1536"):
+            spec = [b for b in golden["batches"] if b["name"] == nm][0]
+            got = run(oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"]), golden_batch_packets(spec))
+            assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"], nm
         rng = np.random.default_rng(variant)
         pk = oracle.mixed_packets(24)
+        pk["bpc"][::4] = 1000
         pk["len"] = rng.integers(0, 65537, pk.size).astype(np.uint32)
         pk["payload_off"] = np.arange(pk.size, dtype=np.uint64) * np.uint64(65536 + 48) + np.uint64(16)
         per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
         pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
         payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 99 + variant)
-        got = run_dev(hdfs, ctx, payload, pk)
-        assert np.array_equal(got, orc.batch(payload, pk, hdfs.total_checksums(pk)))
+        assert np.array_equal(run(payload, pk), orc.batch(payload, pk, hdfs.total_checksums(pk)))
+        T = hdfs.CRC32C_TYPE_CRC32
+        assert np.array_equal(run(payload, pk, T), oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk)))
     finally:
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1])
-def test_crc32_type_matches_zlib(hdfs, variant, monkeypatch):
+def test_crc32_type_matches_zlib(hdfs, gpu_ctx):
     """CHECKSUM_CRC32 (CRC32C_TYPE_CRC32): same kernel, zlib-polynomial tables;
     per-chunk results equal zlib.crc32 (the reference returns -ENOSYS here,
-    hadooprpc.c:629-631).  Fast tiles, mixed bpc, ragged tails, unaligned
-    packets, big-endian output, host path."""
-    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
-    ctx = hdfs.Context(0)
-    try:
-        T = hdfs.CRC32C_TYPE_CRC32
-        pk = oracle.uniform_packets(64)
-        payload = oracle.xorshift64_bytes(64 * 65536, 77)
-        want = oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk))
-        assert np.array_equal(run_dev(hdfs, ctx, payload, pk, T), want)
-        be = run_dev(hdfs, ctx, payload, pk, T | hdfs.CRC32C_BIG_ENDIAN)
-        assert np.array_equal(be, want.byteswap())
-        rng = np.random.default_rng(40 + variant)
-        pk = oracle.mixed_packets(30)
-        pk["len"] = rng.integers(0, 65537, pk.size).astype(np.uint32)
-        pk["payload_off"] = np.arange(pk.size, dtype=np.uint64) * np.uint64(65536 + 40) + np.uint64(3)
-        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
-        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
-        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 81 + variant)
-        want = oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk))
-        assert np.array_equal(run_dev(hdfs, ctx, payload, pk, T), want)
-        assert np.array_equal(ctx.batch_host(payload, pk, T), want)
-    finally:
-        ctx.close()
+    hadooprpc.c:629-631).  Fast tiles, general tiles, mixed bpc, ragged
+    tails, unaligned packets, big-endian output, host path."""
+    ctx = gpu_ctx
+    T = hdfs.CRC32C_TYPE_CRC32
+    pk = oracle.uniform_packets(64)
+    payload = oracle.xorshift64_bytes(64 * 65536, 77)
+    want = oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk))
+    assert np.array_equal(run_dev(hdfs, ctx, payload, pk, T), want)
+    be = run_dev(hdfs, ctx, payload, pk, T | hdfs.CRC32C_BIG_ENDIAN)
+    assert np.array_equal(be, want.byteswap())
+    rng = np.random.default_rng(40)
+    pk = oracle.mixed_packets(30)
+    pk["bpc"][1::5] = 1536
+    pk["bpc"][2::5] = 700
+    pk["len"] = rng.integers(0, 65537, pk.size).astype(np.uint32)
+    pk["payload_off"] = np.arange(pk.size, dtype=np.uint64) * np.uint64(65536 + 40) + np.uint64(3)
+    per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 81)
+    want = oracle.zlib_batch(payload, pk, hdfs.total_checksums(pk))
+    assert np.array_equal(run_dev(hdfs, ctx, payload, pk, T), want)
+    assert np.array_equal(ctx.batch_host(payload, pk, T), want)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
-def test_verify_reports_mismatches(hdfs, orc, variant, monkeypatch):
+@pytest.mark.parametrize("bpcs", [(512, 1024, 4096), (100, 1000, 1536)])
+def test_verify_reports_mismatches(hdfs, gpu_ctx, orc, bpcs):
     """Read-side verification (crc32c_plan_verify / crc32c_verify_host): no
     mismatch on intact data; a corrupted payload byte or expected checksum is
     counted and the lowest bad index reported; wire-order expectations with
-    CRC32C_BIG_ENDIAN; fast tiles and general-path chunks."""
+    CRC32C_BIG_ENDIAN; power-of-two tiles, general tiles and general-path
+    chunks."""
     torch = _torch()
-    monkeypatch.setenv("HDFS_CRC32C_KVARIANT", str(variant))
-    ctx = hdfs.Context(0)
-    try:
-        rng = np.random.default_rng(60 + variant)
-        pk = oracle.mixed_packets(40)
-        pk["len"] = rng.integers(1, 65537, pk.size).astype(np.uint32)
-        pk["len"][:20] = 65536  # fast tiles
-        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
-        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
-        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 5 + variant)
-        n = hdfs.total_checksums(pk)
-        stream = torch.cuda.current_stream()
-        for flags in (0, hdfs.CRC32C_BIG_ENDIAN):
-            want = orc.batch(payload, pk, n, big_endian=bool(flags))
-            plan = hdfs.Plan(ctx, pk, flags)
-            dev = torch.from_numpy(payload).cuda()
-            exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
-            res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    ctx = gpu_ctx
+    rng = np.random.default_rng(60 + bpcs[0])
+    pk = oracle.mixed_packets(40, bpcs=bpcs)
+    pk["len"] = rng.integers(1, 65537, pk.size).astype(np.uint32)
+    pk["len"][:20] = 65536  # whole tiles
+    per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 5 + bpcs[0])
+    n = hdfs.total_checksums(pk)
+    stream = torch.cuda.current_stream()
+    for flags in (0, hdfs.CRC32C_BIG_ENDIAN):
+        want = orc.batch(payload, pk, n, big_endian=bool(flags))
+        plan = hdfs.Plan(ctx, pk, flags)
+        dev = torch.from_numpy(payload).cuda()
+        exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+        res = torch.zeros(2, dtype=torch.int32, device="cuda")
 
-            def verify():
-                plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
-                stream.synchronize()
-                r = res.cpu().numpy().view(np.uint32)
-                return int(r[0]), int(r[1])
+        def verify():
+            plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+            stream.synchronize()
+            r = res.cpu().numpy().view(np.uint32)
+            return int(r[0]), int(r[1])
 
-            assert verify() == (0, 0xFFFFFFFF)
-            # corrupt one payload byte inside packet 25 (a general-path packet) -> its chunk
-            p25 = pk[25]
-            off = int(p25["len"]) // 2
-            dev[int(p25["payload_off"]) + off] ^= 0x01
-            bad_idx = int(p25["out_idx"]) + off // int(p25["bpc"])
-            assert verify() == (1, bad_idx)
-            dev[int(p25["payload_off"]) + off] ^= 0x01
-            # corrupt expected checksums 7 (fast tile) and bad_idx
-            exp[7] ^= 0x100
-            exp[bad_idx] ^= 0x1
-            assert verify() == (2, 7)
-            plan.close()
-            # host path
-            cnt, first = ctx.verify_host(payload, pk, want, flags)
-            assert (cnt, first) == (0, None)
-            w2 = want.copy()
-            w2[[3, n - 1]] ^= 1
-            assert ctx.verify_host(payload, pk, w2, flags) == (2, 3)
-    finally:
-        ctx.close()
+        assert verify() == (0, 0xFFFFFFFF)
+        # corrupt one payload byte inside packet 25 -> its chunk
+        p25 = pk[25]
+        off = int(p25["len"]) // 2
+        dev[int(p25["payload_off"]) + off] ^= 0x01
+        bad_idx = int(p25["out_idx"]) + off // int(p25["bpc"])
+        assert verify() == (1, bad_idx)
+        dev[int(p25["payload_off"]) + off] ^= 0x01
+        # corrupt expected checksums 7 (a whole tile) and bad_idx
+        exp[7] ^= 0x100
+        exp[bad_idx] ^= 0x1
+        assert verify() == (2, 7)
+        plan.close()
+        # host path
+        cnt, first = ctx.verify_host(payload, pk, want, flags)
+        assert (cnt, first) == (0, None)
+        w2 = want.copy()
+        w2[[3, n - 1]] ^= 1
+        assert ctx.verify_host(payload, pk, w2, flags) == (2, 3)
 
 
 @pytest.mark.parametrize("npkts", [1, 3, 75, 138, 263, 388])

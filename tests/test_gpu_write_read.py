@@ -1,0 +1,364 @@
+"""GPU parity of round 2's paths: general tiles (any bytesPerChecksum), packet
+assembly from Hadoop_Fuse_Buffer lists with NULL = zero fill
+(crc32c_plan_create_buffers), received-frame verification
+(crc32c_verify_frames_host), and the multi-GPU plan with its RCCL gather
+(crc32c_multi_plan_*).  Everything runs through the C ABI; the oracle is the
+checker."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden_batch_packets
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch
+
+
+def _expected_write(orc, stream: np.ndarray, bufferoffset, length, blockoffset, packetsize, bpc, big_endian=False):
+    """hadoop_rpc_send_packets' checksums over the assembled stream (oracle):
+    packets as crc32c_packetize cuts them, chunks from each packet's start."""
+    out, pos, sent = [], bufferoffset, 0
+    while True:
+        plen = min(length - sent, packetsize)
+        past = (blockoffset + sent) % bpc
+        if plen > 0 and past:
+            plen = min(bpc - past, length - sent)
+        if plen == 0:
+            break
+        out.append(orc.chunks(stream[pos:pos + plen], bpc, big_endian))
+        pos += plen
+        sent += plen
+    return np.concatenate(out) if out else np.zeros(0, np.uint32)
+
+
+def _run_plan(plan, n, stream, payload=0):
+    torch = _torch()
+    out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    plan.exec(payload, out.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    return out.cpu().numpy().view(np.uint32)[:n]
+
+
+def _verify(plan, expected: np.ndarray, stream, payload=0):
+    torch = _torch()
+    exp = torch.from_numpy(expected.view(np.int32).copy()).cuda()
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    plan.verify(payload, exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    return res.cpu().numpy().view(np.uint32).tolist()
+
+
+# ---- general tiles -----------------------------------------------------------
+@pytest.mark.parametrize("bpc", [4, 7, 100, 511, 513, 1000, 1536, 2560, 3072, 4000, 6144, 7680, 8191])
+def test_general_tiles_any_bpc(hdfs, gpu_ctx, orc, bpc):
+    """Packets of bpc outside 512 * 2^k take general tiles (16 // k chunks of k
+    virtual blocks): at offset 0 (padded tiles fall back to the general path
+    only for the first chunk), at every phase mod 16, with ragged tails; exec
+    and verify against the oracle."""
+    torch = _torch()
+    rows, off, out = [], 0, 0
+    for i in range(20):
+        ln = 65536 - (0 if i % 3 else 777)
+        rows.append((off, out, ln, bpc))
+        out += (ln + bpc - 1) // bpc
+        off += ln + (i % 16) + 1
+    pk = np.array(rows, hdfs.PACKET_DTYPE)
+    tiles, gen = hdfs.debug_plan(pk)
+    assert np.any(tiles["meta"] & 0x80000000)
+    payload = oracle.xorshift64_bytes(off + 64, 3000 + bpc)
+    payload[:bpc * 2] = 0  # a zero chunk
+    want = orc.batch(payload, pk, out)
+    dev = torch.from_numpy(payload).cuda()
+    stream = torch.cuda.current_stream()
+    plan = hdfs.Plan(gpu_ctx, pk)
+    assert np.array_equal(_run_plan(plan, out, stream, dev.data_ptr()), want)
+    assert _verify(plan, want, stream, dev.data_ptr()) == [0, 0xFFFFFFFF]
+    bad = want.copy()
+    bad[[out // 3, out - 2]] ^= 0x800
+    assert _verify(plan, bad, stream, dev.data_ptr()) == [2, out // 3]
+    plan.close()
+
+
+def test_general_tiles_device_addresses_near_page_start(hdfs, gpu_ctx, orc):
+    """CRC32C_DEVICE_ADDRESSES plans with padded general tiles: packets
+    starting 0..20 bytes into a fresh allocation (padded tiles load up to 15
+    bytes before a chunk, allowed only inside the same 4 KiB page)."""
+    torch = _torch()
+    bufs, rows, want, out = [], [], [], 0
+    for k in range(21):
+        data = oracle.xorshift64_bytes(40000 + 64, 50 + k)
+        t = torch.from_numpy(data).cuda()
+        bufs.append(t)
+        bpc = (100, 1000, 1536, 700)[k % 4]
+        ln = 40000 - k
+        rows.append((t.data_ptr() + k, out, ln, bpc))
+        want.append(orc.chunks(data[k:k + ln], bpc))
+        out += (ln + bpc - 1) // bpc
+    pk = np.array(rows, hdfs.PACKET_DTYPE)
+    plan = hdfs.Plan(gpu_ctx, pk, hdfs.CRC32C_DEVICE_ADDRESSES)
+    stream = torch.cuda.current_stream()
+    assert np.array_equal(_run_plan(plan, out, stream), np.concatenate(want))
+    plan.close()
+
+
+# ---- packet assembly from buffer lists (hadooprpc.c:666-725) -----------------
+def _fuse_write_buffers(torch, rng, lens, null_mask, seed):
+    """Device buffers of the given lengths (None where NULL), and the host
+    stream they assemble to."""
+    bufs, devs, parts = [], [], []
+    for i, (n, is_null) in enumerate(zip(lens, null_mask)):
+        if is_null:
+            bufs.append((0, n))
+            parts.append(np.zeros(n, np.uint8))
+        else:
+            d = oracle.xorshift64_bytes(n + 32, seed + i)
+            skew = int(rng.integers(0, 16))
+            t = torch.from_numpy(d).cuda()
+            devs.append(t)
+            bufs.append((t.data_ptr() + skew, n))
+            parts.append(d[skew:skew + n])
+    return bufs, devs, np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+
+
+@pytest.mark.parametrize("shape", ["truncate_pad_data_trailing", "data_only", "pad_then_data", "tiny_pieces",
+                                   "unaligned_block_offset", "bpc_1536", "crc32_big_endian"])
+def test_write_plan_four_buffers(hdfs, gpu_ctx, orc, shape):
+    """The buffer shapes of hadoop_fuse_write (fuse.c:1348-1354): TRUNCATE
+    (old data), NULLPADDING (zeros), THEDATA (the write), TRAILINGDATA (old
+    data after it), cut into packets by hadoop_rpc_send_packets
+    (hadooprpc.c:815-860) from a block offset; bit-exact against the oracle
+    over the assembled stream, exec and verify."""
+    torch = _torch()
+    rng = np.random.default_rng(sum(shape.encode()))
+    bpc, flags, blockoffset, bufferoffset = 512, 0, 0, 0
+    if shape == "truncate_pad_data_trailing":
+        lens, nulls = [10000, 300000, 1 << 20, 77777], [False, True, False, False]
+    elif shape == "data_only":
+        lens, nulls = [4 << 20], [False]
+    elif shape == "pad_then_data":
+        lens, nulls = [12345, 100000], [True, False]
+    elif shape == "tiny_pieces":
+        lens, nulls = [3, 1, 700, 5, 2000, 1, 9], [False, True, False, True, False, False, True]
+    elif shape == "unaligned_block_offset":
+        lens, nulls = [5000, 20000, 200000, 3000], [False, True, False, False]
+        blockoffset, bufferoffset = 1000 + 37, 333
+    elif shape == "bpc_1536":
+        lens, nulls = [10000, 4096, 300000, 6000], [False, True, False, False]
+        bpc, blockoffset = 1536, 1536 * 3
+    else:
+        lens, nulls = [10000, 300000, 1 << 20, 77777], [False, True, False, False]
+        flags = hdfs.CRC32C_TYPE_CRC32 | hdfs.CRC32C_BIG_ENDIAN
+    bufs, devs, stream_bytes = _fuse_write_buffers(torch, rng, lens, nulls, 900)
+    length = stream_bytes.size - bufferoffset - 11
+    plan = gpu_ctx.write_plan(bufs, bufferoffset, length, blockoffset, 65536, bpc, flags)
+    if flags & hdfs.CRC32C_TYPE_CRC32:
+        want, pos, sent = [], bufferoffset, 0
+        for plen in hdfs.packetize(length, blockoffset, 65536, bpc):
+            if plen:
+                want.append(oracle.zlib_chunks(stream_bytes[pos:pos + plen], bpc).byteswap())
+            pos += plen
+        want = np.concatenate(want)
+    else:
+        want = _expected_write(orc, stream_bytes, bufferoffset, length, blockoffset, 65536, bpc)
+    assert plan.nchecksums == want.size
+    s = torch.cuda.current_stream()
+    got = _run_plan(plan, want.size, s)
+    assert np.array_equal(got, want)
+    assert _verify(plan, want, s) == [0, 0xFFFFFFFF]
+    bad = want.copy()
+    bad[want.size // 2] ^= 1
+    assert _verify(plan, bad, s) == [1, want.size // 2]
+    plan.close()
+
+
+def test_write_plan_ftruncate_extend_reads_nothing(hdfs, gpu_ctx, orc):
+    """ftruncate growing a file by a whole 4 MiB block is a write of NULL
+    buffers (fuse.c:1137-1142): every checksum is a plan-time constant
+    (crc32c of 512 zero bytes = 30fcedc0), written without reading payload;
+    a ragged extension ends with the short zero chunk's constant."""
+    torch = _torch()
+    s = torch.cuda.current_stream()
+    n4 = 4 << 20
+    counts = hdfs.debug_write_plan([(0, n4)], 0, n4)
+    assert counts["tiles"] == counts["gen"] == counts["seg"] == 0
+    plan = gpu_ctx.write_plan([(0, n4)], 0, n4)
+    got = _run_plan(plan, 8192, s)
+    assert np.all(got == 0x30FCEDC0)
+    assert _verify(plan, got, s) == [0, 0xFFFFFFFF]
+    plan.close()
+    plan = gpu_ctx.write_plan([(0, 1000001)], 0, 1000001, blockoffset=4096)
+    want = _expected_write(orc, np.zeros(1000001, np.uint8), 0, 1000001, 4096, 65536, 512)
+    assert np.array_equal(_run_plan(plan, want.size, s), want)
+    plan.close()
+
+
+def test_write_plan_random_buffer_lists(hdfs, gpu_ctx, orc):
+    """Random buffer lists (1-6 buffers, NULL or data, lengths 0..200000,
+    any skew), random bufferoffset / len / blockoffset / bpc / packetsize."""
+    torch = _torch()
+    rng = np.random.default_rng(77)
+    s = torch.cuda.current_stream()
+    for trial in range(12):
+        nb = int(rng.integers(1, 7))
+        lens = [int(x) for x in rng.integers(0, 200000, nb)]
+        nulls = [bool(x) for x in rng.random(nb) < 0.3]
+        bufs, devs, sb = _fuse_write_buffers(torch, rng, lens, nulls, 2000 + 10 * trial)
+        total = sb.size
+        bo = int(rng.integers(0, total // 3 + 1))
+        length = int(rng.integers(0, total - bo + 1))
+        bpc = int(rng.choice([512, 1024, 4096, 100, 1536]))
+        blockoffset = int(rng.integers(0, 3)) * int(rng.integers(0, 1 << 20))
+        psize = int(rng.choice([65536, bpc * 7]))
+        want = _expected_write(orc, sb, bo, length, blockoffset, psize, bpc)
+        plan = gpu_ctx.write_plan(bufs, bo, length, blockoffset, psize, bpc)
+        assert plan.nchecksums == want.size, trial
+        if want.size:
+            assert np.array_equal(_run_plan(plan, want.size, s), want), trial
+        plan.close()
+
+
+# ---- received frames (hadooprpc.c:497-584) --------------------------------
+def _frames(hdfs, orc, payload, pk, bpc, chunk_offset):
+    """A DataNode's packet stream for pk (contiguous from chunk_offset):
+    prefixes from crc32c_frame_packets, data behind each."""
+    sums = orc.batch(payload, pk, oracle.total_checksums(pk))
+    pre, offs = hdfs.frame_packets(pk, sums, 0, block_offset=chunk_offset)
+    parts = []
+    for i in range(pk.size):
+        parts.append(np.frombuffer(pre[int(offs[i]):int(offs[i + 1])], np.uint8))
+        o = int(pk["payload_off"][i])
+        parts.append(payload[o:o + int(pk["len"][i])])
+    return np.concatenate(parts)
+
+
+@pytest.mark.parametrize("bpc", [512, 4096, 1536])
+def test_verify_received_frames(hdfs, gpu_ctx, orc, bpc):
+    """A read of 3 MiB + a ragged tail from chunkOffset 8 * bpc: the frame
+    run (PLEN|HLEN|header|checksums|data per packet, final empty packet) is
+    verified on the GPU without de-interleaving; a flipped data byte and a
+    flipped checksum byte are found at the right chunk and offsetInBlock; a
+    truncated buffer verifies its whole frames only; a misplaced frame is
+    refused."""
+    n = 48
+    pk = oracle.uniform_packets(n, pkt_len=65536 - 65536 % bpc, bpc=bpc)
+    pk["len"][-1] = 12345
+    pk = np.concatenate([pk, np.zeros(1, pk.dtype)])
+    pk["payload_off"][-1] = pk["payload_off"][-2] + pk["len"][-2]
+    payload = oracle.xorshift64_bytes(int(pk["payload_off"][-1]) + 16, 4242 + bpc)
+    chunk_offset = 8 * bpc
+    fr = _frames(hdfs, orc, payload, pk, bpc, chunk_offset)
+    info, used = hdfs.parse_frames(fr)
+    assert info.size == n + 1 and used == fr.size and int(info["last"][-1]) == 1
+    r = gpu_ctx.verify_frames(fr, bpc, chunk_offset)
+    assert (r.packets, r.data_bytes, r.mismatches, r.first_bad, r.last_packet) == (
+        n + 1, int(pk["len"].sum()), 0, 2**64 - 1, 1)
+    assert r.checksums == oracle.total_checksums(pk)
+    # a flipped data byte in packet 20, chunk 5
+    bad = fr.copy()
+    at = int(info["data_off"][20]) + 5 * bpc + 17
+    bad[at] ^= 0x10
+    r = gpu_ctx.verify_frames(bad, bpc, chunk_offset)
+    k = int(oracle.total_checksums(pk[:20])) + 5
+    assert (r.mismatches, r.first_bad, r.first_bad_offset) == (1, k, chunk_offset + int(pk["payload_off"][20]) + 5 * bpc)
+    # a flipped checksum byte of packet 3's first chunk
+    bad = fr.copy()
+    bad[int(info["sums_off"][3]) + 2] ^= 1
+    r = gpu_ctx.verify_frames(bad, bpc, chunk_offset)
+    assert (r.mismatches, r.first_bad) == (1, int(oracle.total_checksums(pk[:3])))
+    # the first 10.5 frames arrived
+    cut = int(info["frame_off"][10]) + 1000
+    r = gpu_ctx.verify_frames(fr[:cut], bpc, chunk_offset)
+    assert (r.packets, r.consumed, r.mismatches, r.last_packet) == (10, int(info["frame_off"][10]), 0, 0)
+    # the DataNode must start at chunkOffset
+    with pytest.raises(hdfs.Crc32cError):
+        gpu_ctx.verify_frames(fr, bpc, chunk_offset + bpc)
+
+
+# ---- several GPUs: device-resident plan + RCCL gather (config 4) ------------
+def test_multi_plan_config4_rccl_gather(hdfs, golden, orc):
+    """Config 4 through crc32c_multi_plan_*: a 128 MiB file as 32 x 4 MiB
+    blocks dealt round-robin over the communicator's ranks (here every
+    visible device, one process; the box has one), each rank checksumming
+    its shard device-resident, the u32 arrays gathered into file order on
+    rank 0 by RCCL send/recv: the golden c4 digest from the reference."""
+    torch = _torch()
+    spec = [b for b in golden["batches"] if b["name"] == "c4_file_128MiB"][0]
+    pk = golden_batch_packets(spec)
+    payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+    ndev = torch.cuda.device_count()
+    m = hdfs.Multi(list(range(ndev)))
+    mp = m.plan(pk, 64)
+    assert mp.nchecksums == spec["nchecksums"]
+    layout, shard_bytes = hdfs.multi_layout(pk, 64, ndev)
+    assert layout.shape == (32, 4) and list(layout[:, 0]) == [g % ndev for g in range(32)]
+    shards = []
+    for r in range(ndev):
+        host = np.zeros(int(shard_bytes[r]) + 16, np.uint8)
+        for g in range(32):
+            rank, soff, poff, nbytes = (int(x) for x in layout[g])
+            if rank == r:
+                host[soff:soff + nbytes] = payload[poff:poff + nbytes]
+        shards.append(torch.from_numpy(host).to("cuda:%d" % r))
+    out = torch.zeros(mp.nchecksums, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    mp.exec([t.data_ptr() for t in shards], out.data_ptr())
+    m.sync()
+    got = out.cpu().numpy().view(np.uint32)
+    assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
+    # again, on the caller's streams, after clearing the output
+    out.zero_()
+    streams = [torch.cuda.Stream(device="cuda:%d" % r) for r in range(ndev)]
+    torch.cuda.synchronize()
+    mp.exec([t.data_ptr() for t in shards], out.data_ptr(), [s.cuda_stream for s in streams])
+    for s in streams:
+        s.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), got)
+    mp.close()
+    m.close()
+
+
+def test_multi_rank_mode_single_rank(hdfs, orc):
+    """One-process-per-GPU communicator (ncclCommInitRank with an id from
+    crc32c_multi_unique_id), nranks = 1: mixed-bpc blocks of ragged packets
+    with empty last packets, gathered into place on rank 0."""
+    torch = _torch()
+    uid = hdfs.multi_unique_id()
+    assert len(uid) == 128
+    m = hdfs.Multi(device=0, rank=0, nranks=1, uid=uid)
+    pk = oracle.mixed_packets(130)
+    pk["len"][63::64] = 0  # each block ends with the empty last packet
+    pk["len"][5] = 1000
+    per = (pk["len"].astype(np.int64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 16, 31)
+    mp = m.plan(pk, 64)
+    layout, sb = hdfs.multi_layout(pk, 64, 1)
+    host = np.zeros(int(sb[0]) + 16, np.uint8)
+    for rank, soff, poff, nbytes in layout.astype(np.int64):
+        host[soff:soff + nbytes] = payload[poff:poff + nbytes]
+    shard = torch.from_numpy(host).cuda()
+    out = torch.full((mp.nchecksums,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    mp.exec([shard.data_ptr()], out.data_ptr())
+    m.sync()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, mp.nchecksums))
+    mp.close()
+    m.close()
+
+
+def test_last_path_gpu(hdfs, orc):
+    """crc32c_chunks reports the GPU path when it ran there (CRC32C_CPU_FALLBACK
+    set or not)."""
+    pkt = oracle.xorshift64_bytes(65536, 98)
+    assert np.array_equal(hdfs.chunks(pkt, 512, hdfs.CRC32C_CPU_FALLBACK), orc.chunks(pkt, 512))
+    assert hdfs.last_path() == hdfs.PATH_GPU

@@ -16,10 +16,19 @@ from conftest import ROOT, golden_fill
 from kernel_model import KernelModel, KernelModelS4
 
 
-def _declared_functions():
+def _declared_functions(debug_only: bool = False):
+    """crc32c* functions the headers declare: the product library's, or
+    (debug_only) section 2 of hdfs_crc32c_debug.h, which only
+    libhdfs_crc32c_debug.so exports."""
     names = set()
     for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
-        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        text = open(h).read()
+        if h.endswith("_debug.h"):
+            head, _, tail = text.partition("/* ---- 2. libhdfs_crc32c_debug.so only ---- */")
+            text = tail if debug_only else head
+        elif debug_only:
+            continue
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         for m in re.finditer(r"^[A-Za-z_][\w \*]*?\b(crc32c\w*)\s*\(", text, flags=re.M):
             names.add(m.group(1))
     return names
@@ -31,6 +40,31 @@ def test_exports_every_declared_symbol(hdfs):
     lib = hdfs.lib()
     for n in sorted(names):
         assert hasattr(lib, n), n
+    dbg = _declared_functions(debug_only=True)
+    assert dbg == {"crc32c_debug_plan_exec_variant", "crc32c_debug_variant_name", "crc32c_debug_stream_probe"}
+    dlib = hdfs.debug_lib()
+    for n in sorted(dbg):
+        assert hasattr(dlib, n), n
+
+
+def test_product_library_has_no_variant_switch(hdfs):
+    """The public path launches only the production kernel: the product .so
+    exports no variant entry point or read probe, never reads a kernel-variant
+    environment variable, and holds exactly the four production kernels
+    (exec, verify; with and without general-tile code); the A/B kernels live in the debug library."""
+    import ctypes
+
+    lib = ctypes.CDLL(hdfs.LIB_PATH)
+    for n in _declared_functions(debug_only=True):
+        assert not hasattr(lib, n), n
+    blob = open(hdfs.LIB_PATH, "rb").read()
+    assert b"KVARIANT" not in blob
+    kernels = set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", blob))
+    # modes: 3 = S4 | NT, + 64 verify, + 256 general-tile code
+    assert kernels == {b"_Z23hdfs_crc32c_plan_kernelILi768ELi3ELi%dEEvN8hdfs_crc7KParamsE" % m
+                       for m in (3, 67, 259, 323)}, kernels
+    dblob = open(hdfs.DEBUG_LIB_PATH, "rb").read()
+    assert len(set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", dblob))) >= 9
 
 
 def test_scalar_dropin_known_answers(hdfs, golden):
@@ -172,10 +206,18 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
     got = np.full(n, 0xDEADBEEF, np.uint32)
     seen = np.zeros(n, np.int32)
     for t in tiles:
-        nb, lg = int(t["meta"]) & 0xFF, (int(t["meta"]) >> 8) & 0xFF
-        assert 1 <= nb <= 16 and nb % (1 << lg) == 0  # any alignment (unaligned tile loads)
-        bpc = 512 << lg
-        for c in range(nb >> lg):
+        meta = int(t["meta"])
+        if meta & 0x80000000:  # general tile: nch chunks of any bpc in [4, 8192], k virtual blocks each
+            k, nch, pad = (meta >> 8) & 31, (meta >> 13) & 31, (meta >> 18) & 511
+            bpc = k * 512 - pad
+            assert meta & 0xFF == nch * k <= 16 and nch >= 1 and 4 <= bpc <= 8192 and pad < 512
+            assert bpc & (bpc - 1) or bpc < 512  # powers of two >= 512 take the power-of-two tiles
+            assert pad == 0 or int(t["src"]) >= 16  # padded loads start up to 15 bytes early
+        else:
+            nb, lg = meta & 0xFF, (meta >> 8) & 0xFF
+            assert 1 <= nb <= 16 and nb % (1 << lg) == 0  # any alignment (unaligned tile loads)
+            bpc, nch = 512 << lg, nb >> lg
+        for c in range(nch):
             s = int(t["src"]) + c * bpc
             got[int(t["out"]) + c] = orc.crc32c(payload[s:s + bpc])
             seen[int(t["out"]) + c] += 1
@@ -228,6 +270,57 @@ def test_kernel_model_general_chunks(orc, model):
         assert model.general_chunk(np.zeros(n, np.uint8)) == orc.crc32c(np.zeros(n, np.uint8))
 
 
+@pytest.mark.parametrize("bpc", [4, 5, 100, 511, 513, 1000, 1536, 2560, 4000, 7680, 8191])
+def test_kernel_model_general_tiles(hdfs, orc, bpc):
+    """General tiles: each chunk right-aligned into k = ceil(bpc / 512)
+    virtual blocks, 0xff folded into its first 4 bytes, block b shifted by
+    Z^(512 (k - 1 - b)) from the S4 image's shift section, XORed, ^ ~0."""
+    m4 = KernelModelS4(hdfs.debug_lds_image_s4())
+    img, c_lg, c_small = hdfs.debug_lds_image()
+    zm = KernelModel(img, c_lg, c_small)
+    k = (bpc + 511) // 512
+    pad = k * 512 - bpc
+    data = oracle.xorshift64_bytes(bpc * 5, bpc)
+    data[:bpc] = 0
+    got = []
+    for c in range(5):
+        v = np.zeros(k * 512, np.uint8)
+        v[pad:] = data[c * bpc:(c + 1) * bpc]
+        v[pad:pad + 4] ^= 0xFF
+        lins = m4.block_lin(v.reshape(k, 512))
+        x = 0
+        for j in range(k):
+            s = k - 1 - j
+            x ^= zm.zshift(s, int(lins[j])) if s else int(lins[j])
+        got.append(x ^ 0xFFFFFFFF)
+    assert np.array_equal(np.array(got, np.uint32), orc.chunks(data, bpc))
+
+
+def test_write_plan_decomposition(hdfs):
+    """crc32c_plan_create_buffers' work items (hadooprpc.c:666-725 packet
+    assembly): an all-NULL 4 MiB ftruncate extension is constant runs only (no
+    payload read); the four FUSE write buffers give tiles inside each data
+    buffer, seg items only for chunks spanning a buffer boundary, and
+    constants for chunks of zero fill."""
+    MB4 = 4 << 20
+    c = hdfs.debug_write_plan([(0, MB4)], 0, MB4)
+    assert c == {"tiles": 0, "gen": 0, "seg": 0, "pieces": 0, "consts": 8, "nchecksums": 8192}
+    base = 1 << 40  # device addresses are opaque to the plan builder
+    # TRUNCATE 1000 B of old data, NULLPADDING 3000, THEDATA 70000, TRAILINGDATA 5000
+    bufs = [(base, 1000), (0, 3000), (base + (1 << 20), 70000), (base + (2 << 20), 5000)]
+    c = hdfs.debug_write_plan(bufs, 0, 79000, blockoffset=0)
+    n = sum((ln + 511) // 512 for ln in hdfs.packetize(79000, 0, 65536, 512))
+    assert c["nchecksums"] == n == (65536 // 512) + (79000 - 65536 + 511) // 512
+    # chunk 1 (1000 / 3000 boundary) and the chunks at 4000 and 74000 span buffers
+    assert c["seg"] == 3 and c["pieces"] == 4
+    assert c["consts"] == 1  # chunks 2..6: zero fill only (bytes 1024 .. 3583)
+    # an unaligned block offset: the first packet finishes one chunk (hadooprpc.c:832-840)
+    c = hdfs.debug_write_plan(bufs, 100, 5000, blockoffset=700)
+    assert c["nchecksums"] == sum((ln + 511) // 512 for ln in hdfs.packetize(5000, 700, 65536, 512))
+    with pytest.raises(hdfs.Crc32cError):
+        hdfs.debug_write_plan(bufs, 0, 79001)  # beyond the buffers
+
+
 def test_gpu_entry_points_fail_loudly_without_gpu(hdfs):
     if hdfs.device_count() > 0:
         pytest.skip("a GPU is visible")
@@ -236,6 +329,24 @@ def test_gpu_entry_points_fail_loudly_without_gpu(hdfs):
     assert ei.value.rc == -19  # -ENODEV: no CPU substitute behind the GPU API
     with pytest.raises(hdfs.Crc32cError):
         hdfs.chunks(np.zeros(1024, np.uint8), 512)
+    assert hdfs.last_path() == hdfs.PATH_NONE
+
+
+def test_cpu_fallback_is_opt_in_and_observable(hdfs, orc):
+    """SURVEY.md section 5's failure contract, as an explicit flag: without a
+    GPU, crc32c_chunks / crc32c_batch_host given CRC32C_CPU_FALLBACK finish
+    on the product's host path (crc32c_chunks_cpu) and crc32c_last_path()
+    says so; without the flag they fail (-ENODEV)."""
+    if hdfs.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    pkt = oracle.xorshift64_bytes(70000, 12)
+    F = hdfs.CRC32C_CPU_FALLBACK
+    assert np.array_equal(hdfs.chunks(pkt, 512, F), orc.chunks(pkt, 512))
+    assert hdfs.last_path() == hdfs.PATH_CPU
+    assert np.array_equal(hdfs.chunks(pkt, 1000, F | hdfs.CRC32C_BIG_ENDIAN), orc.chunks(pkt, 1000, True))
+    with pytest.raises(hdfs.Crc32cError):
+        hdfs.chunks(pkt, 512)
+    assert hdfs.last_path() == hdfs.PATH_NONE
 
 
 def test_s4_image_matches_nibble_image(hdfs, model):

@@ -28,8 +28,8 @@ def main():
 
     from bench import load_package
 
-    os.environ["HDFS_CRC32C_KVARIANT"] = args.variant
-    hdfs = load_package()
+    hdfs = load_package()  # (production kernel; --variant is kept for old command lines, 0 only)
+    assert args.variant == "0", "kernel variants are launched through the debug library (tools/kbench.py)"
     from hdfs_crc32c_amd.workloads import config_packets, synthetic_bytes
 
     pk, _ = config_packets("c2")

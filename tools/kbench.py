@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--nbuf", type=int, default=4)
     ap.add_argument("--variants", default="0,1,2,3,4,5")
-    ap.add_argument("--verify", action="store_true", help="also time crc32c_plan_verify of variants 0-2 as 'verify_<v>'")
+    ap.add_argument("--verify", action="store_true", help="also time crc32c_plan_verify (production) as 'verify_0'")
     args = ap.parse_args()
 
     import numpy as np
@@ -45,12 +45,26 @@ def main():
     bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g) for _ in range(args.nbuf)]
     outs = [torch.zeros(nout, dtype=torch.int32, device=dev) for _ in range(args.nbuf)]
     variants = args.variants.split(",")
-    plans = {}
-    for v in variants:
-        os.environ["HDFS_CRC32C_KVARIANT"] = v
-        ctx = hdfs.Context(0)
-        plans[v] = (ctx, ctx.plan(pk))
+    # One plan; variant 0 through the product entry point (crc32c_plan_exec),
+    # the others through the debug library's crc32c_debug_plan_exec_variant.
+    ctx = hdfs.Context(0)
+    the_plan = ctx.plan(pk)
     stream = torch.cuda.current_stream()
+
+    class _Runner:
+        def __init__(self, v):
+            self.v = int(v)
+
+        def exec(self, src, dst, s):
+            if self.v == 0:
+                the_plan.exec(src, dst, s)
+            else:
+                the_plan.exec_variant(src, dst, self.v, 0, s)
+
+        def verify(self, *a):
+            the_plan.verify(*a)
+
+    plans = {v: (ctx, _Runner(v)) for v in variants}
     ref = None
     for v in variants:
         plans[v][1].exec(bufs[0].data_ptr(), outs[0].data_ptr(), stream.cuda_stream)
@@ -61,7 +75,7 @@ def main():
         if not np.array_equal(got, ref):
             print("note: variant %s checksums differ (diagnostic variant?)" % v, file=sys.stderr)
     times = {v: [] for v in variants}
-    vvars = [v for v in variants if int(v) in (0, 1, 2)] if args.verify else []  # variants with a compare mode
+    vvars = [v for v in variants if int(v) == 0] if args.verify else []  # the production compare mode
     if vvars:
         exps = [torch.zeros_like(o) for o in outs]
         for i in range(args.nbuf):  # expected checksums of every buffer (diagnostic variants overwrite outs)
@@ -113,7 +127,7 @@ def main():
     res = {"torch_copy": {"us": round(copy_us, 2), "GBps_rw": round(2 * extent / (copy_us * 1e-6) / 1e9, 1)}}
     # reference: plain streaming reads (stream_probe.hip), several shapes
     probe_out = torch.zeros(256 * 256 * 16, dtype=torch.int32, device=dev)
-    L = hdfs.lib()
+    L = hdfs.debug_lib()
     for shape in (0, 2):
         for grid in (512, 1024):
             tt = []

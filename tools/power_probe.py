@@ -57,11 +57,17 @@ def main():
     s = torch.cuda.current_stream()
     res = {}
     for v in args.variants.split(","):
-        os.environ["HDFS_CRC32C_KVARIANT"] = v
         ctx = hdfs.Context(0)
         plan = ctx.plan(pk)
+
+        def launch(i, v=int(v)):  # variant 0: the product entry; others: the debug library
+            if v == 0:
+                plan.exec(bufs[i % 4].data_ptr(), outs[i % 4].data_ptr(), s.cuda_stream)
+            else:
+                plan.exec_variant(bufs[i % 4].data_ptr(), outs[i % 4].data_ptr(), v, 0, s.cuda_stream)
+
         for i in range(20):
-            plan.exec(bufs[i % 4].data_ptr(), outs[i % 4].data_ptr(), s.cuda_stream)
+            launch(i)
         torch.cuda.synchronize()
         time.sleep(1.0)  # let clocks / power settle back
         e0 = torch.cuda.Event(enable_timing=True)
@@ -69,7 +75,7 @@ def main():
         t_begin = time.time()
         e0.record(s)
         for i in range(args.launches):
-            plan.exec(bufs[i % 4].data_ptr(), outs[i % 4].data_ptr(), s.cuda_stream)
+            launch(i)
         e1.record(s)
         samples = [] if args.external_smi else [smi() for _ in range(2)]
         torch.cuda.synchronize()

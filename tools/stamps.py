@@ -31,7 +31,7 @@ def main():
     dev = torch.device("cuda", 0)
     bufs = [torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev) for _ in range(4)]
     out = torch.zeros(nout, dtype=torch.int32, device=dev)
-    os.environ["HDFS_CRC32C_KVARIANT"] = "0"
+    # (the plan is the production one; stamped variants run through the debug library)
     ctx = hdfs.Context(0)
     plan = ctx.plan(pk)
     stamps = torch.zeros(4 * 256 * 2 * 16, dtype=torch.int64, device=dev)
