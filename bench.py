@@ -89,29 +89,50 @@ def latest_pmc(profile_dir: str):
         return None
 
 
-def cpu_baseline(pk, payload_np: np.ndarray, seconds: float):
-    """The reference's own crc32c.c (oracle/_ref, kind "reference") or the
-    clean-room oracle (kind "port"), per chunk as hadooprpc.c:739-742, on
-    the host cores of this box: bounded sample = the same batch, repeated
-    until `seconds` of wall time per thread count."""
+def host_sockets() -> int:
+    try:
+        with open("/proc/cpuinfo") as f:
+            ids = {l.split(":", 1)[1].strip() for l in f if l.startswith("physical id")}
+        return max(1, len(ids))
+    except Exception:
+        return 1
+
+
+def cpu_baseline(pk, payload_np: np.ndarray, seconds: float, nbuf: int = 4):
+    """The reference's own crc32c.c (oracle/_ref, kind "reference") per chunk
+    as hadooprpc.c:739-742, on this box's host cores, at full width
+    (os.cpu_count() threads), one socket's worth and 1
+    thread: each thread owns a contiguous packet slice, the batch is copied
+    into `nbuf` distinct first-touched buffers (more than the host L3, as the
+    GPU side rotates its buffers) and the passes rotate over them, so the
+    rate is a DRAM-streaming one.  Bounded sample: about `seconds` of wall
+    time per thread count.  Falls back to the clean-room oracle ("port",
+    single-buffer timing) when the reference build is absent."""
     import oracle as oracle_mod
 
-    try:
-        impl = oracle_mod.Reference()
-        kind = "reference"
-    except Exception:
-        impl = oracle_mod.Oracle()
-        kind = "port"
     nout = oracle_mod.total_checksums(pk)
     out = np.zeros(nout, np.uint32)
     nbytes = int(pk["len"].astype(np.int64).sum())
-    threads = max(1, min(16, os.cpu_count() or 1))
+    ncpu = os.cpu_count() or 1
+    sockets = host_sockets()
+    counts = sorted({1, max(1, ncpu // sockets), ncpu})
     res = {}
-    for t in sorted({1, threads}):
-        dt = impl.batch_mt_seconds(payload_np, pk, out, t, 1)
-        reps = max(1, int(seconds / max(dt, 1e-6)))
-        dt = impl.batch_mt_seconds(payload_np, pk, out, t, reps)
-        res[t] = nbytes * reps / dt / GIB
+    try:
+        impl = oracle_mod.Reference()
+        kind = "reference"
+        for t in counts:
+            reps = max(nbuf, 2 * t)
+            dt = impl.batch_rot_seconds(payload_np, pk, out, t, nbuf, reps)
+            reps = max(nbuf, int(reps * seconds / max(dt, 1e-6)))
+            dt = impl.batch_rot_seconds(payload_np, pk, out, t, nbuf, reps)
+            res[t] = nbytes * reps / dt / GIB
+    except (FileNotFoundError, OSError):
+        impl = oracle_mod.Oracle()
+        kind = "port"
+        for t in counts:
+            dt = impl.batch_mt_seconds(payload_np, pk, out, t, 1)
+            reps = max(1, int(seconds / max(dt, 1e-6)))
+            res[t] = nbytes * reps / impl.batch_mt_seconds(payload_np, pk, out, t, reps) / GIB
     cpu_model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -119,10 +140,13 @@ def cpu_baseline(pk, payload_np: np.ndarray, seconds: float):
     except Exception:
         pass
     return {
-        "value": round(res[threads], 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-        "sample": "%s: the config batch (%d packets, %.0f MiB) per pass, %.0fs per thread count; reference "
-                  "crc32c.c built -O2 (its Makefile builds -O0)" % (kind, pk.size, nbytes / 2**20, seconds),
-        "one_core_gib_s": round(res[1], 3), "host_cpus": os.cpu_count(), "cpu_model": cpu_model,
+        "value": round(res[ncpu], 3), "unit": "GiB/s", "cores": ncpu, "kind": kind,
+        "sample": "%s: the config batch (%d packets, %.0f MiB) in %d distinct first-touched host copies rotated "
+                  "per pass (DRAM-streaming), ~%.0fs per thread count; reference crc32c.c built -O2 (its Makefile "
+                  "builds -O0)" % (kind, pk.size, nbytes / 2**20, nbuf if kind == "reference" else 1, seconds),
+        "per_threads_gib_s": {str(t): round(v, 3) for t, v in res.items()},
+        "one_core_gib_s": round(res[1], 3), "one_socket_gib_s": round(res[max(1, ncpu // sockets)], 3),
+        "host_cpus": ncpu, "sockets": sockets, "cpu_model": cpu_model,
     }
 
 
@@ -134,9 +158,9 @@ def main():
     # the 1.4 kW package cap).  2500 launches take ~0.1 s.
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "c2b1536", "c2u"])
     ap.add_argument("--nbuf", type=int, default=4, help="rotating payload buffers (defeat the 256 MiB L3)")
-    ap.add_argument("--cpu-seconds", type=float, default=5.0)
+    ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
@@ -172,13 +196,25 @@ def main():
     from hdfs_crc32c_amd import shard
     from hdfs_crc32c_amd.workloads import config_packets, synthetic_bytes, uniform_packets
 
-    c4_blocks = None
-    if args.config == "c4":
-        # 128 MiB file = 32 x 4 MiB blocks, block b on rank b mod world
-        c4_blocks = shard.rank_blocks(32, world, rank)
-        pk = uniform_packets(64 * len(c4_blocks))
-        workload = "128MiB file as 32 x 4MiB blocks round-robin over ranks (config 4)"
-        nbuf = 1
+    c4 = args.config == "c4"
+    if c4:
+        # 128 MiB file = 32 x 4 MiB blocks, block b on rank b mod world, through
+        # the C ABI's multi-GPU plan: every rank checksums its shard and one
+        # RCCL send/recv group lands the checksums in file order on rank 0.
+        # One step = shard checksums + the gather (the whole config-4 job).
+        file_pk = uniform_packets(64 * 32)
+        file_bytes = synthetic_bytes(32 * shard.BLOCK_BYTES, 2024)
+        if world == 1:
+            multi = hdfs.Multi([local_rank])
+        else:
+            obj = [hdfs.multi_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            multi = hdfs.Multi(device=local_rank, rank=rank, nranks=world, uid=obj[0])
+        mplan = multi.plan(file_pk, 64)
+        lay, shard_sizes = shard.layout(file_pk, 64, world)
+        pk = shard.rank_packets(file_pk, 64, world, rank)
+        workload = "128MiB file as 32 x 4MiB blocks round-robin over %d ranks, RCCL gather to rank 0 (config 4)" % world
+        nbuf = args.nbuf
     else:
         pk, workload = config_packets(args.config)
         if args.scaling == "strong" and world > 1:
@@ -194,14 +230,17 @@ def main():
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)
 
-    ctx = hdfs.Context(local_rank)
-    plan = ctx.plan(pk)
+    ctx = plan = None
+    if not c4:
+        ctx = hdfs.Context(local_rank)
+        plan = ctx.plan(pk)
     dev = torch.device("cuda", local_rank)
     # buffer 0: PCG64 host bytes (checked against the CPU
     # path below); the rest: device-generated random bytes.
-    if c4_blocks is not None:
-        file_bytes = synthetic_bytes(32 * shard.BLOCK_BYTES, 2024)
-        payload0 = shard.rank_payload(file_bytes, c4_blocks)
+    if c4:
+        payload0 = shard.rank_payload(file_bytes, lay, shard_sizes, rank)
+        extent = payload0.size
+        root_out = torch.zeros(max(mplan.nchecksums, 1), dtype=torch.int32, device=dev)
     else:
         payload0 = synthetic_bytes(extent, 2024 + rank)
     bufs = [torch.from_numpy(payload0).to(dev)]
@@ -215,14 +254,22 @@ def main():
 
     def step(i):
         b = i % nbuf
-        plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sptr)
+        if c4:
+            mplan.exec([bufs[b].data_ptr()], root_out.data_ptr() if rank == 0 else 0, [sptr])
+        else:
+            plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sptr)
 
     # correctness gate (outside the timed region): every buffer-0 checksum
+    # (config 4: the whole file's, gathered on rank 0)
     step(0)
     torch.cuda.synchronize()
-    want = reference_checksums(payload0, pk, nout)
-    got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
-    bit_exact = bool(np.array_equal(got0, want))
+    if c4:
+        want = reference_checksums(file_bytes, file_pk, mplan.nchecksums) if rank == 0 else None
+        bit_exact = rank != 0 or bool(np.array_equal(root_out.cpu().numpy().view(np.uint32), want))
+    else:
+        want = reference_checksums(payload0, pk, nout)
+        got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
+        bit_exact = bool(np.array_equal(got0, want))
 
     for i in range(args.warmup):
         step(i)
@@ -253,31 +300,21 @@ def main():
         ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         bit_exact = bool(ok.item())
-    # RCCL gather of every rank's checksum array to rank 0 (the path's only
-    # exchange; timed on its own, outside the kernel's timed region).  For
-    # config 4 rank 0 reassembles the file's checksums in block order and
-    # checks them against the reference over the whole 128 MiB file.
+    # Configs 2/5 (weak scaling, independent batches): RCCL gather of every
+    # rank's checksum array to rank 0 after the timed region, timed on its
+    # own.  (Config 4's gather is inside every step.)
     gather_ms = None
-    if world > 1 or c4_blocks is not None:
+    if world > 1 and not c4:
         torch.cuda.synchronize()
         g0 = time.perf_counter()
-        if c4_blocks is not None:
-            per_block = 64 * 128
-            full = shard.gather_checksums(outs[0][:nout].to(cdev), 32, per_block, world, rank)
-        else:
-            send = outs[0].to(cdev)
-            gathered = [torch.empty_like(send) for _ in range(world)] if rank == 0 and world > 1 else None
-            if world > 1:
-                dist.gather(send, gathered, dst=0)
-            full = None
+        send = outs[0].to(cdev)
+        gathered = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+        dist.gather(send, gathered, dst=0)
         torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3 if world > 1 else None
-        if c4_blocks is not None and rank == 0:
-            whole = uniform_packets(64 * 32)
-            bit_exact = bit_exact and bool(np.array_equal(full, reference_checksums(file_bytes, whole,
-                                                                                     64 * 32 * 128)))
+        gather_ms = (time.perf_counter() - g0) * 1e3
 
-    total_bytes = nbytes * world * args.steps
+    # config 4: every rank's shard is part of one 128 MiB file
+    total_bytes = (32 * shard.BLOCK_BYTES if c4 else nbytes * world) * args.steps
     value = total_bytes / elapsed / GIB
     achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
 
@@ -285,7 +322,7 @@ def main():
     # against their checksums (outs[b] now holds buffer b's), timed the same
     # way (rank 0, reported beside the main line).
     verify = None
-    if rank == 0:
+    if rank == 0 and plan is not None:
         res = torch.zeros(2, dtype=torch.int32, device=dev)
         for i in range(50):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
@@ -309,7 +346,7 @@ def main():
     # prices the kernel against what this chip actually streams, beside the
     # 8 TB/s datasheet peak.  Rank 0, N = 1 only.
     read_probe = None
-    if rank == 0 and world == 1 and nbuf > 1:
+    if rank == 0 and world == 1 and nbuf > 1 and not c4:
         probe_out = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
         L = hdfs.debug_lib()  # the read probe lives in the debug library, not the product
 
@@ -338,7 +375,7 @@ def main():
     # line, which stays one stream so that one step = one launch): the next
     # launch's workgroups start on the CUs the previous one has released.
     two_streams = None
-    if args.two_streams and rank == 0 and world == 1 and nbuf > 1:
+    if args.two_streams and rank == 0 and world == 1 and nbuf > 1 and not c4:
         ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
 
         def two(n):
@@ -409,7 +446,8 @@ def main():
                 and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
         # the CPU baseline is an N = 1 figure (timed on rank 0's host cores)
-        cpu = None if args.no_cpu or world > 1 else cpu_baseline(pk, payload0, args.cpu_seconds)
+        cpu = None if args.no_cpu or world > 1 else (
+            cpu_baseline(file_pk, file_bytes, args.cpu_seconds) if c4 else cpu_baseline(pk, payload0, args.cpu_seconds))
         line = {
             "metric": baseline_metric(),
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -421,8 +459,10 @@ def main():
             "config": {"workload": workload, "config": args.config, "packets_per_rank": int(pk.size),
                        "packet_bytes": int(pk["len"][0]), "bytes_per_checksum": sorted(set(int(x) for x in pk["bpc"])),
                        "payload_bytes_per_rank": nbytes, "checksums_per_rank": nout,
-                       "parallelism": "dp%d (independent shards, %s gather of checksums after timing)"
-                                      % (world, "RCCL" if backend == "nccl" else backend + " rehearsal")},
+                       "parallelism": ("dp%d (block shards, crc32c_multi_plan: RCCL send/recv gather of the "
+                                       "checksums to rank 0 inside every step)" % world) if c4 else
+                                      ("dp%d (independent shards, %s gather of checksums after timing)"
+                                       % (world, "RCCL" if backend == "nccl" else backend + " rehearsal"))},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "kernel": KERNEL_NAME, "kernel_avg_us": round(kernel_ms * 1e3, 2),
@@ -438,8 +478,12 @@ def main():
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         }
         print(json.dumps(line), flush=True)
-    plan.close()
-    ctx.close()
+    if c4:
+        mplan.close()
+        multi.close()
+    else:
+        plan.close()
+        ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

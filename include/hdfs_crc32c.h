@@ -261,8 +261,14 @@ int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint
  * the shard of the i-th local device (laid out as crc32c_multi_layout says),
  * root_out = nchecksums device u32s on rank 0's device (rank 0's process
  * only), streams[i] (or NULL = the library's streams).  Asynchronous: the
- * checksum launches, then the RCCL gather, on the local devices' streams;
- * root_out is complete when rank 0's stream is. */
+ * checksum launches, then the RCCL gather (every other rank's array in one
+ * ncclSend; rank 0 computes its own groups in place and scatters the
+ * received ones into file order), on the local devices' streams; root_out
+ * is complete when rank 0's stream is.  flags: CRC32C_BIG_ENDIAN,
+ * CRC32C_TYPE_CRC32, CRC32C_MULTI_SELF_SEND. */
+#define CRC32C_MULTI_SELF_SEND 0x10u /* crc32c_multi_plan_create: rank 0's own checksums also travel
+                                       through RCCL (a send to itself) instead of being written in
+                                       place -- exercises the transport on a one-GPU communicator */
 typedef struct crc32c_multi_plan crc32c_multi_plan;
 int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
                              uint32_t flags, crc32c_multi_plan **out);

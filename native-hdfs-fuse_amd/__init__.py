@@ -30,6 +30,7 @@ CRC32C_BIG_ENDIAN = 0x1
 CRC32C_TYPE_CRC32 = 0x2  # Hadoop CHECKSUM_CRC32 (zlib polynomial) instead of CRC32C
 CRC32C_DEVICE_ADDRESSES = 0x4  # plan flag: payload_off are device addresses; exec/verify take payload 0
 CRC32C_CPU_FALLBACK = 0x8  # crc32c_chunks / crc32c_batch_host: finish on the host CPU if the GPU fails
+CRC32C_MULTI_SELF_SEND = 0x10  # multi plan: rank 0's own checksums also go through RCCL (one-GPU transport test)
 PATH_NONE, PATH_GPU, PATH_CPU = 0, 1, 2  # crc32c_last_path()
 
 PACKET_DTYPE = np.dtype(

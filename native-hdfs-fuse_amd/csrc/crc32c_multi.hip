@@ -4,8 +4,15 @@
 // block by block, hadoop_rpc_send_packets cuts each block into packets,
 // hadooprpc.c:815-860), every GPU checksumming its shard device-resident,
 // and one RCCL group of point-to-point transfers over xGMI gathering the
-// u32 checksum arrays straight into block order on rank 0's device.  The
-// checksums are the path's only exchange; no payload byte crosses GPUs.
+// u32 checksum arrays into block order on rank 0's device.  The checksums
+// are the path's only exchange; no payload byte crosses GPUs.
+//
+// Rank 0 checksums its own groups straight into their final places; every
+// other rank checksums its groups into one local array and sends it with ONE
+// ncclSend; rank 0 receives each peer's array into a staging slot and one
+// copy kernel scatters the groups into file order.  (So a one-GPU
+// communicator needs no transfer; CRC32C_MULTI_SELF_SEND routes rank 0's
+// own array through RCCL as well, to exercise the transport on one GPU.)
 //
 // Two ways to build the communicator: one process driving every device
 // (crc32c_multi_create, ncclCommInitAll) or one process per device
@@ -139,10 +146,30 @@ struct crc32c_multi_plan {
     crc32c_multi *m = nullptr;
     std::vector<Group> groups;
     std::vector<uint64_t> shard_bytes;  // per rank
+    std::vector<uint64_t> local_nout;   // per rank: checksums of its shard
     std::vector<crc32c_plan *> plans;    // per local device
-    std::vector<uint32_t *> d_local;     // per local device: its local checksum array
+    std::vector<uint32_t *> d_local;     // per local device: its local array (none for rank 0 in place)
     uint64_t nchecksums = 0;
+    bool self_send = false;
+    // rank 0's process: the peers' arrays land in d_staging (staging_off[r]
+    // for rank r), then scatter_groups() moves every group into place.
+    uint32_t *d_staging = nullptr;
+    std::vector<uint64_t> staging_off;
+    uint4 *d_scatter = nullptr;  // {src index in staging, dst index in root_out, count, 0}
+    uint32_t nscatter = 0;
+    int root_local = -1;  // local device index of rank 0 (-1: not in this process)
 };
+
+namespace {
+
+// One workgroup per received group: its checksums from the staging area to
+// their place in rank 0's output (u32 copies, coalesced).
+__global__ __launch_bounds__(256) void scatter_groups(const uint32_t *staging, const uint4 *items, uint32_t *out) {
+    const uint4 it = items[blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < it.z; k += blockDim.x) out[it.y + k] = staging[it.x + k];
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -257,23 +284,48 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
     std::unique_ptr<crc32c_multi_plan, int (*)(crc32c_multi_plan *)> mp(new crc32c_multi_plan,
                                                                         crc32c_multi_plan_destroy);
     mp->m = m;
-    std::vector<uint64_t> local_nout;
-    if (int rc = build_layout(pkts, npkts, group_packets, m->nranks, &mp->groups, &mp->shard_bytes, &local_nout))
+    mp->self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
+    flags &= ~CRC32C_MULTI_SELF_SEND;
+    if (int rc = build_layout(pkts, npkts, group_packets, m->nranks, &mp->groups, &mp->shard_bytes, &mp->local_nout))
         return rc;
     for (const Group &G : mp->groups) mp->nchecksums = std::max(mp->nchecksums, G.omin + G.n);
     std::vector<crc32c_packet> local;
     for (size_t i = 0; i < m->ctxs.size(); ++i) {
         const int r = m->ranks[i];
-        shard_packets(pkts, npkts, group_packets, mp->groups, r, true, &local);
+        // rank 0 in place: its packets keep their global out indices
+        const bool in_place = r == 0 && !mp->self_send;
+        if (r == 0) mp->root_local = int(i);
+        shard_packets(pkts, npkts, group_packets, mp->groups, r, !in_place, &local);
         crc32c_plan *p = nullptr;
         if (int rc = crc32c_plan_create(m->ctxs[i], local.data(), local.size(), flags, &p)) return rc;
         mp->plans.push_back(p);
         uint32_t *d = nullptr;
-        if (local_nout[size_t(r)]) {
+        if (!in_place && mp->local_nout[size_t(r)]) {
             DeviceGuard guard(m->ctxs[i]->device);
-            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), local_nout[size_t(r)] * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), mp->local_nout[size_t(r)] * sizeof(uint32_t)));
         }
         mp->d_local.push_back(d);
+    }
+    if (mp->root_local >= 0) {  // staging slots and scatter list for the arrays rank 0 receives
+        mp->staging_off.assign(size_t(m->nranks), 0);
+        uint64_t total = 0;
+        for (int r = 0; r < m->nranks; ++r) {
+            mp->staging_off[size_t(r)] = total;
+            if (r != 0 || mp->self_send) total += mp->local_nout[size_t(r)];
+        }
+        std::vector<uint4> items;
+        for (const Group &G : mp->groups)
+            if (G.n && (G.rank != 0 || mp->self_send))
+                items.push_back(make_uint4(uint32_t(mp->staging_off[size_t(G.rank)] + G.local_out), uint32_t(G.omin),
+                                           uint32_t(G.n), 0u));
+        if (total > UINT32_MAX || mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
+        DeviceGuard guard(m->ctxs[size_t(mp->root_local)]->device);
+        if (total) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_staging), total * sizeof(uint32_t)));
+        if (!items.empty()) {
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_scatter), items.size() * sizeof(uint4)));
+            HIP_TRY(hipMemcpy(mp->d_scatter, items.data(), items.size() * sizeof(uint4), hipMemcpyHostToDevice));
+        }
+        mp->nscatter = uint32_t(items.size());
     }
     *out = mp.release();
     return 0;
@@ -291,38 +343,47 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
     if (!mp) return fail(-EINVAL, "plan == NULL");
     crc32c_multi *m = mp->m;
     std::lock_guard<std::mutex> lock(m->mu);
-    bool root = false;
-    for (size_t i = 0; i < m->ctxs.size(); ++i) {
-        if (m->ranks[i] == 0) root = true;
-        if (mp->d_local[i] && (!dev_shards || !dev_shards[i]))
+    for (size_t i = 0; i < m->ctxs.size(); ++i)
+        if (mp->local_nout[size_t(m->ranks[i])] && (!dev_shards || !dev_shards[i]))
             return fail(-EINVAL, "local device %zu: shard payload == NULL", i);
-    }
-    if (root && mp->nchecksums && !root_out) return fail(-EINVAL, "root_out == NULL on rank 0");
-    if (int rc = ensure_comms(m)) return rc;
-    // 1. every local device checksums its shard into its local array
+    if (mp->root_local >= 0 && mp->nchecksums && !root_out) return fail(-EINVAL, "root_out == NULL on rank 0");
+    // 1. every local device checksums its shard: rank 0 into place, the
+    //    others into their local arrays
     for (size_t i = 0; i < m->ctxs.size(); ++i) {
-        if (!mp->d_local[i]) continue;
-        if (int rc = crc32c_plan_exec(mp->plans[i], dev_shards[i], mp->d_local[i], local_stream(m, i, streams)))
-            return rc;
+        if (!mp->local_nout[size_t(m->ranks[i])]) continue;
+        uint32_t *dst = mp->d_local[i] ? mp->d_local[i] : root_out;
+        if (int rc = crc32c_plan_exec(mp->plans[i], dev_shards[i], dst, local_stream(m, i, streams))) return rc;
     }
-    // 2. one group of point-to-point transfers: every group's checksum range
-    //    from its rank's local array into its place on rank 0
+    // 2. one group of point-to-point transfers: each sending rank's whole
+    //    local array to rank 0's staging slot for it
+    bool any = false;
+    for (int r = 0; r < m->nranks; ++r)
+        if ((r != 0 || mp->self_send) && mp->local_nout[size_t(r)]) any = true;
+    if (!any) return 0;
+    if (int rc = ensure_comms(m)) return rc;
     NCCL_TRY(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
     for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
         const hipStream_t s = local_stream(m, i, streams);
-        for (const Group &G : mp->groups) {
-            if (!G.n) continue;
-            if (G.rank == m->ranks[i])
-                r = ncclSend(mp->d_local[i] + G.local_out, G.n, ncclUint32, 0, m->comms[i], s);
-            if (r == ncclSuccess && m->ranks[i] == 0)
-                r = ncclRecv(root_out + G.omin, G.n, ncclUint32, G.rank, m->comms[i], s);
-            if (r != ncclSuccess) break;
-        }
+        const int me = m->ranks[i];
+        if (mp->d_local[i]) r = ncclSend(mp->d_local[i], mp->local_nout[size_t(me)], ncclUint32, 0, m->comms[i], s);
+        if (me != 0) continue;
+        for (int peer = 0; peer < m->nranks && r == ncclSuccess; ++peer)
+            if ((peer != 0 || mp->self_send) && mp->local_nout[size_t(peer)])
+                r = ncclRecv(mp->d_staging + mp->staging_off[size_t(peer)], mp->local_nout[size_t(peer)], ncclUint32,
+                             peer, m->comms[i], s);
     }
     const ncclResult_t e = ncclGroupEnd();
     NCCL_TRY(r);
     NCCL_TRY(e);
+    // 3. rank 0: the received groups into file order
+    if (mp->root_local >= 0 && mp->nscatter) {
+        const size_t i = size_t(mp->root_local);
+        DeviceGuard guard(m->ctxs[i]->device);
+        hipLaunchKernelGGL(scatter_groups, dim3(mp->nscatter), dim3(256), 0, local_stream(m, i, streams),
+                           mp->d_staging, mp->d_scatter, root_out);
+        HIP_TRY(hipGetLastError());
+    }
     return 0;
 }
 
@@ -334,6 +395,11 @@ int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
             DeviceGuard guard(mp->m->ctxs[i]->device);
             (void)hipFree(mp->d_local[i]);
         }
+    }
+    if (mp->root_local >= 0) {
+        DeviceGuard guard(mp->m->ctxs[size_t(mp->root_local)]->device);
+        if (mp->d_staging) (void)hipFree(mp->d_staging);
+        if (mp->d_scatter) (void)hipFree(mp->d_scatter);
     }
     delete mp;
     return 0;

@@ -174,6 +174,8 @@ class Reference:
         lib.ref_batch.argtypes = [vp, vp, u64, vp]
         lib.ref_batch_mt.restype = ctypes.c_double
         lib.ref_batch_mt.argtypes = [vp, vp, u64, vp, ctypes.c_int, ctypes.c_int]
+        lib.ref_batch_mt_rot.restype = ctypes.c_double
+        lib.ref_batch_mt_rot.argtypes = [vp, u64, vp, u64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         self.lib = lib
 
     @staticmethod
@@ -194,6 +196,15 @@ class Reference:
 
     def batch_mt_seconds(self, payload, pkts, out, nthreads: int, reps: int) -> float:
         return float(self.lib.ref_batch_mt(_ptr(payload), _ptr(pkts), pkts.size, _ptr(out), nthreads, reps))
+
+    def batch_rot_seconds(self, payload, pkts, out, nthreads: int, nbuf: int, reps: int) -> float:
+        """Full-width timing: nbuf distinct first-touched copies rotated over reps
+        (ref_harness.c ref_batch_mt_rot); wall seconds of the reps."""
+        t = float(self.lib.ref_batch_mt_rot(_ptr(payload), payload.size, _ptr(pkts), pkts.size, _ptr(out), nthreads,
+                                            nbuf, reps))
+        if t < 0:
+            raise MemoryError("ref_batch_mt_rot: allocation failed")
+        return t
 
 
 def py_crc32c(data: bytes, crc: int = 0) -> int:

@@ -11,6 +11,7 @@
 #include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <time.h>
 
 /* The reference exports exactly this symbol (src/crc32c.c:333) and its only
@@ -93,5 +94,101 @@ double ref_batch_mt(const void *payload, const ref_packet *pkts, uint64_t npkts,
             pthread_join(th[t], NULL);
     }
     clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---- cpu_baseline at full host width, streaming from DRAM ----------------
+ * nbuf distinct copies of the batch (first-touched by the threads that read
+ * them, so each NUMA node streams its own memory), nthreads persistent
+ * threads each owning a contiguous packet slice, rep r reading copy r % nbuf:
+ * consecutive reps cannot be served from the L3.  Timed from the moment
+ * every thread is ready to the last thread's finish.  Returns wall seconds,
+ * or a negative value when memory could not be allocated. */
+typedef struct {
+    const uint8_t *src;
+    uint8_t **bufs;
+    int nbuf, reps;
+    const ref_packet *pkts;
+    uint64_t lo, hi;
+    uint32_t *out;
+    pthread_barrier_t *ready, *go;
+} ref_rot_job;
+
+static void *ref_rot_worker(void *arg)
+{
+    ref_rot_job *j = (ref_rot_job *)arg;
+    if (j->hi > j->lo) {
+        uint64_t b0 = j->pkts[j->lo].payload_off, b1 = b0;
+        for (uint64_t i = j->lo; i < j->hi; i++) {
+            if (j->pkts[i].payload_off < b0)
+                b0 = j->pkts[i].payload_off;
+            if (j->pkts[i].payload_off + j->pkts[i].len > b1)
+                b1 = j->pkts[i].payload_off + j->pkts[i].len;
+        }
+        for (int b = 0; b < j->nbuf; b++)
+            for (uint64_t o = b0; o < b1; o++)
+                j->bufs[b][o] = j->src[o];
+    }
+    pthread_barrier_wait(j->ready);
+    pthread_barrier_wait(j->go);
+    for (int r = 0; r < j->reps; r++) {
+        const uint8_t *p = j->bufs[r % j->nbuf];
+        for (uint64_t i = j->lo; i < j->hi; i++)
+            ref_packet_chunks(p + j->pkts[i].payload_off, j->pkts[i].len, j->pkts[i].bpc, j->out + j->pkts[i].out_idx);
+    }
+    return NULL;
+}
+
+double ref_batch_mt_rot(const void *payload, uint64_t bytes, const ref_packet *pkts, uint64_t npkts, uint32_t *out,
+                        int nthreads, int nbuf, int reps)
+{
+    enum { MAXT = 1024, MAXB = 16 };
+    static pthread_t th[MAXT];
+    static ref_rot_job jobs[MAXT];
+    uint8_t *bufs[MAXB];
+    pthread_barrier_t ready, go;
+    struct timespec t0, t1;
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > MAXT)
+        nthreads = MAXT;
+    if (nbuf < 1)
+        nbuf = 1;
+    if (nbuf > MAXB)
+        nbuf = MAXB;
+    for (int b = 0; b < nbuf; b++) {
+        bufs[b] = (uint8_t *)malloc(bytes ? bytes : 1);
+        if (!bufs[b]) {
+            for (int k = 0; k < b; k++)
+                free(bufs[k]);
+            return -1.0;
+        }
+    }
+    (void)crc32c(0, "", 0);
+    pthread_barrier_init(&ready, NULL, (unsigned)nthreads + 1);
+    pthread_barrier_init(&go, NULL, (unsigned)nthreads + 1);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].src = (const uint8_t *)payload;
+        jobs[t].bufs = bufs;
+        jobs[t].nbuf = nbuf;
+        jobs[t].reps = reps;
+        jobs[t].pkts = pkts;
+        jobs[t].lo = npkts * (uint64_t)t / (uint64_t)nthreads;
+        jobs[t].hi = npkts * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        jobs[t].out = out;
+        jobs[t].ready = &ready;
+        jobs[t].go = &go;
+        pthread_create(&th[t], NULL, ref_rot_worker, &jobs[t]);
+    }
+    pthread_barrier_wait(&ready);
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    pthread_barrier_wait(&go);
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    pthread_barrier_destroy(&ready);
+    pthread_barrier_destroy(&go);
+    for (int b = 0; b < nbuf; b++)
+        free(bufs[b]);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }

@@ -285,19 +285,22 @@ def test_verify_received_frames(hdfs, gpu_ctx, orc, bpc):
 
 
 # ---- several GPUs: device-resident plan + RCCL gather (config 4) ------------
-def test_multi_plan_config4_rccl_gather(hdfs, golden, orc):
+@pytest.mark.parametrize("self_send", [False, True])
+def test_multi_plan_config4_rccl_gather(hdfs, golden, orc, self_send):
     """Config 4 through crc32c_multi_plan_*: a 128 MiB file as 32 x 4 MiB
     blocks dealt round-robin over the communicator's ranks (here every
     visible device, one process; the box has one), each rank checksumming
     its shard device-resident, the u32 arrays gathered into file order on
-    rank 0 by RCCL send/recv: the golden c4 digest from the reference."""
+    rank 0 by RCCL send/recv + the scatter kernel: the golden c4 digest from
+    the reference.  With CRC32C_MULTI_SELF_SEND rank 0's own array travels
+    through RCCL too (a send to itself), so the transport runs on one GPU."""
     torch = _torch()
     spec = [b for b in golden["batches"] if b["name"] == "c4_file_128MiB"][0]
     pk = golden_batch_packets(spec)
     payload = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
     ndev = torch.cuda.device_count()
     m = hdfs.Multi(list(range(ndev)))
-    mp = m.plan(pk, 64)
+    mp = m.plan(pk, 64, hdfs.CRC32C_MULTI_SELF_SEND if self_send else 0)
     assert mp.nchecksums == spec["nchecksums"]
     layout, shard_bytes = hdfs.multi_layout(pk, 64, ndev)
     assert layout.shape == (32, 4) and list(layout[:, 0]) == [g % ndev for g in range(32)]
@@ -336,12 +339,13 @@ def test_multi_rank_mode_single_rank(hdfs, orc):
     assert len(uid) == 128
     m = hdfs.Multi(device=0, rank=0, nranks=1, uid=uid)
     pk = oracle.mixed_packets(130)
+    pk["bpc"][7::9] = 1536  # general tiles too
     pk["len"][63::64] = 0  # each block ends with the empty last packet
     pk["len"][5] = 1000
     per = (pk["len"].astype(np.int64) + pk["bpc"] - 1) // pk["bpc"]
     pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
     payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 16, 31)
-    mp = m.plan(pk, 64)
+    mp = m.plan(pk, 64, hdfs.CRC32C_MULTI_SELF_SEND | hdfs.CRC32C_BIG_ENDIAN)
     layout, sb = hdfs.multi_layout(pk, 64, 1)
     host = np.zeros(int(sb[0]) + 16, np.uint8)
     for rank, soff, poff, nbytes in layout.astype(np.int64):
@@ -351,7 +355,7 @@ def test_multi_rank_mode_single_rank(hdfs, orc):
     torch.cuda.synchronize()
     mp.exec([shard.data_ptr()], out.data_ptr())
     m.sync()
-    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, mp.nchecksums))
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, mp.nchecksums, big_endian=True))
     mp.close()
     m.close()
 

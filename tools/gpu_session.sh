@@ -26,11 +26,12 @@ for s in $STEPS; do
     bench5) run bench5 600 python bench.py --config c5 --no-cpu ;;
     bench3) run bench3 600 python bench.py --config c3 --no-cpu --no-host ;;
     bench4) run bench4 600 python bench.py --config c4 --no-cpu --no-host ;;
+    cfgs) for c in ${CFGS:-c3 c2b1536 c4 c5}; do run bench_$c 600 python bench.py --config $c --no-cpu --no-host ${CFG_ARGS:-}; done ;;
     pmc) run pmc 1100 bash tools/pmc_session.sh ;;
-    stamps) for v in ${SV:-5 6}; do run stamps_v$v 300 python tools/stamps.py c2 $v ${SW:-12}; done ;;
+    stamps) for v in ${SV:-5 6}; do run stamps_${SCFG:-c2}_v$v 300 python tools/stamps.py ${SCFG:-c2} $v ${SW:-12}; done ;;
     tprobe) run tprobe 300 python tools/timing_probe.py ;;
     sweep) run sweep 300 python tools/probe_sweep.py ;;
-    kbench) run kbench ${KB_TIMEOUT:-600} python tools/kbench.py --config c2 --variants ${KV:-0,1,2,3,4,5} ${KB_ARGS:-} ;;
+    kbench) run kbench_${KCFG:-c2} ${KB_TIMEOUT:-600} python tools/kbench.py --config ${KCFG:-c2} --variants ${KV:-0,1,2,3,4,5} ${KB_ARGS:-} ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 --variants ${KV:-0,1} ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
             python3 bench.py --no-cpu --no-host ;;
