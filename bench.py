@@ -89,6 +89,33 @@ def latest_pmc(profile_dir: str):
         return None
 
 
+def cpu_quota():
+    """(CPUs this process may run on, CPU bandwidth quota in CPUs or None):
+    sched_getaffinity and the cgroup v2 cpu.max / v1 cfs quota -- a container
+    can show every host CPU to os.cpu_count() and still cap the time they get."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = round(int(q) / int(per), 2)
+    except Exception:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = round(q / per, 2)
+        except Exception:
+            pass
+    return affinity, quota
+
+
 def host_sockets() -> int:
     try:
         with open("/proc/cpuinfo") as f:
@@ -147,6 +174,7 @@ def cpu_baseline(pk, payload_np: np.ndarray, seconds: float, nbuf: int = 4):
         "per_threads_gib_s": {str(t): round(v, 3) for t, v in res.items()},
         "one_core_gib_s": round(res[1], 3), "one_socket_gib_s": round(res[max(1, ncpu // sockets)], 3),
         "host_cpus": ncpu, "sockets": sockets, "cpu_model": cpu_model,
+        "cpu_affinity": cpu_quota()[0], "cgroup_cpu_quota": cpu_quota()[1],
     }
 
 

@@ -260,7 +260,9 @@ int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint
  * file layout; every process passes the same list).  Exec: dev_shards[i] =
  * the shard of the i-th local device (laid out as crc32c_multi_layout says),
  * root_out = nchecksums device u32s on rank 0's device (rank 0's process
- * only), streams[i] (or NULL = the library's streams).  Asynchronous: the
+ * only), streams[i] = the local device i's stream (NULL entry = its default
+ * stream; streams == NULL = the library's own streams, see
+ * crc32c_multi_sync).  Asynchronous: the
  * checksum launches, then the RCCL gather (every other rank's array in one
  * ncclSend; rank 0 computes its own groups in place and scatters the
  * received ones into file order), on the local devices' streams; root_out

@@ -65,7 +65,6 @@ using hdfs_crc::kGeneralTile;
 using hdfs_crc::kShardWord;
 using hdfs_crc::kTicketShards;
 using hdfs_crc::kTicketWord;
-using hdfs_crc::kVCountWord;
 using hdfs_crc::kVFirstWord;
 
 constexpr uint32_t kLdsBytes = hdfs_crc::kKernelLdsBytes;
@@ -90,6 +89,7 @@ constexpr int kModeCompDiag = 16;   // DIAGNOSTIC, wrong results: no payload loa
 constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table staging
 constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
 constexpr int kModeS4H = 128;       // A/B: half-column S4 image (64 KiB of T tables, 88 KiB staged)
+constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
 
@@ -170,12 +170,22 @@ struct LaneCols {
     uint32_t toff;  // T1 - T0 (= T3 - T2) in bytes: 128, or 64 in the half-column image
 };
 
-template <bool H>
+// S4 image layouts (template parameter IMG): the full image (32 replica
+// columns of T0..T3), the half-column image (A/B), and the compact image
+// (T0..T3 once each, for small batches: crc_math.h kS4C*).
+constexpr int kImgFull = 0, kImgHalf = 1, kImgCompact = 2;
+constexpr uint32_t kS4CNibOff = uint32_t(hdfs_crc::kS4CNibOff);
+constexpr uint32_t kS4CShiftOff = uint32_t(hdfs_crc::kS4CShiftOff);
+constexpr uint32_t kS4CStageBytes = (uint32_t(hdfs_crc::kS4CBytes) + 1023u) / 1024u * 1024u;
+
+template <int IMG>
 __device__ __forceinline__ LaneCols lane_cols(uint32_t q) {
-    if (H) {  // half-column S4 image (A/B, kModeS4H): T0..T3 share one 256-byte row per byte value
+    if (IMG == kImgHalf) {  // half-column S4 image (A/B, kModeS4H): T0..T3 share one 256-byte row per byte value
         const uint32_t c4 = (q & 15u) << 2;
         return LaneCols{c4, c4 | 128u, (q << 2) | kS4NibOff, 64u};
     }
+    if (IMG == kImgCompact)  // T_m[b] at m * 1024 + 4 b: col4 = T0 base, hi = T2 base
+        return LaneCols{0u, 2048u, (q << 2) | kS4CNibOff, 1024u};
     return LaneCols{q << 2, (q << 2) | 65536u, (q << 2) | kS4NibOff, 128u};
 }
 
@@ -190,7 +200,15 @@ __device__ __forceinline__ uint32_t byte_addr(uint32_t v, uint32_t base) {
 // One slicing-by-4 step: S(v) ^ next, S(v) = T3[v.b0] ^ T2[v.b1] ^ T1[v.b2]
 // ^ T0[v.b3] (each table replicated over the lane columns of the image, so
 // the 32 lanes of a half-wave always hit 32 different banks).
+template <int IMG>
 __device__ __forceinline__ uint32_t s4(const uint8_t *lds, const LaneCols &c, uint32_t v, uint32_t next) {
+    if (IMG == kImgCompact) {  // byte j of v -> bits 2..9 (v_bfe + v_lshl_add), one copy of each table
+        const uint32_t a3 = lds_u32(lds, (__builtin_amdgcn_ubfe(v, 0, 8) << 2) + c.hi + c.toff);
+        const uint32_t a2 = lds_u32(lds, (__builtin_amdgcn_ubfe(v, 8, 8) << 2) + c.hi);
+        const uint32_t a1 = lds_u32(lds, (__builtin_amdgcn_ubfe(v, 16, 8) << 2) + c.toff);
+        const uint32_t a0 = lds_u32(lds, (v >> 24) << 2);
+        return xor3(xor3(a3, a2, a1), a0, next);
+    }
     const uint32_t a3 = lds_u32(lds, byte_addr<0>(v, c.hi) + c.toff);    // T3: upper pair, odd
     const uint32_t a2 = lds_u32(lds, byte_addr<1>(v, c.hi));             // T2: upper pair, even
     const uint32_t a1 = lds_u32(lds, byte_addr<2>(v, c.col4) + c.toff);  // T1
@@ -201,10 +219,10 @@ __device__ __forceinline__ uint32_t s4(const uint8_t *lds, const LaneCols &c, ui
 // lin() of the lane's 16-byte piece with the S4 image: u = S(S(S(d0) ^ d1)
 // ^ d2) ^ d3 is the register after the piece; N_q(u) = Z_{16(31-q)}(S(u))
 // moves it to the block end (8 nibble lookups in the lane's column).
-template <int DIAG>
+template <int DIAG, int IMG>
 __device__ __forceinline__ uint32_t piece_lin_s4(const uint8_t *lds, uint4 d, const LaneCols &c) {
     if (DIAG == 1) return d.x ^ d.y ^ d.z ^ d.w;
-    const uint32_t u = s4(lds, c, s4(lds, c, s4(lds, c, d.x, d.y), d.z), d.w);
+    const uint32_t u = s4<IMG>(lds, c, s4<IMG>(lds, c, s4<IMG>(lds, c, d.x, d.y), d.z), d.w);
     const uint32_t xs[8] = {u << 8, u << 4, u, u >> 4, u >> 8, u >> 12, u >> 16, u >> 20};
     uint32_t r[8];
 #pragma unroll
@@ -212,16 +230,16 @@ __device__ __forceinline__ uint32_t piece_lin_s4(const uint8_t *lds, uint4 d, co
     return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
-template <bool S4, int DIAG>
+template <bool S4, int DIAG, int IMG>
 __device__ __forceinline__ uint32_t piece(const uint8_t *lds, uint4 d, const LaneCols &c) {
-    if (S4) return piece_lin_s4<DIAG>(lds, d, c);
+    if (S4) return piece_lin_s4<DIAG, IMG>(lds, d, c);
     return piece_lin<DIAG>(lds, d, c.col4);
 }
 
 // Z^(512*s)(x), s in 1..15, from 8 nibble tables (16 entries each).
-template <bool S4 = false>
+template <bool S4, int IMG>
 __device__ __forceinline__ uint32_t zshift(const uint8_t *lds, uint32_t s, uint32_t x) {
-    const uint32_t base = (S4 ? kS4ShiftOff : kShiftOff) + (s - 1u) * 512u;
+    const uint32_t base = (!S4 ? kShiftOff : IMG == kImgCompact ? kS4CShiftOff : kS4ShiftOff) + (s - 1u) * 512u;
     uint32_t r = 0;
 #pragma unroll
     for (int t = 0; t < 8; ++t) r ^= lds_u32(lds, base + t * 64u + ((x >> (4 * t)) & 15u) * 4u);
@@ -279,43 +297,54 @@ __device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t 
 // for the next launch.
 __device__ __forceinline__ void reset_next_slot(const KParams &p) {
     uint32_t *s = p.sched_next;
-    atomicExch(s + kTicketWord, 0u);
-    atomicExch(s + kVCountWord, 0u);
+    atomicExch(reinterpret_cast<unsigned long long *>(s + kTicketWord), 0ull);
     atomicExch(s + kVFirstWord, 0xffffffffu);
 #pragma unroll
-    for (uint32_t i = 0; i < kTicketShards; ++i) atomicExch(s + kShardWord + 32 * i, 0u);
+    for (uint32_t i = 0; i < kTicketShards; ++i)
+        atomicExch(reinterpret_cast<unsigned long long *>(s + kShardWord + 32 * i), 0ull);
 }
 
 // Waits until every vector-memory operation of the wave has completed; for a
 // returning device-scope atomic that means it has been performed.
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// End of a verification launch, thread 0 of every workgroup: fold the
-// workgroup's count / first-bad index into the slot, take a ticket, and let
-// the last workgroup publish the totals to p.result[0..1] (no host-side reset
-// of the result is needed).  Every word of the slot is only ever touched by
-// device-scope atomics, which are performed in one place, so ordering needs
-// only completion waits, no cache fences (a __threadfence() is an L2
-// writeback + invalidate, ~3.5 us each on the launch's critical tail).
+// A ticket word: tickets taken in bits 40-63, mismatches counted in 0-39.
+constexpr unsigned long long kTicket = 1ull << 40;
+constexpr unsigned long long kCountMask = kTicket - 1;
+
+// End of a verification launch, thread 0 of every workgroup: take a ticket
+// in its shard that also adds the workgroup's mismatch count (one 64-bit
+// atomic); the last of a shard adds the shard's total to the global ticket
+// word the same way, and the last of those publishes the totals to
+// p.result[0..1] (no host-side reset of the result is needed).  The first-bad
+// index is lowered (and completed) before the ticket, and only read back when
+// something mismatched, so a clean launch's critical tail is two atomics.
+// Every word of the slot is only ever touched by device-scope atomics, which
+// are performed in one place, so ordering needs only completion waits, no
+// cache fences (a __threadfence() is an L2 writeback + invalidate, ~3.5 us
+// on the launch's critical tail).
 __device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
     uint32_t *s = p.sched;
     const uint32_t cnt = vacc[0], first = vacc[1];
     if (cnt) {
-        uint32_t a = atomicAdd(s + kVCountWord, cnt);
         uint32_t b = atomicMin(s + kVFirstWord, first);
-        asm volatile("" : "+v"(a), "+v"(b));  // returning forms: the wait below covers them
+        asm volatile("" : "+v"(b));  // returning form: the wait below covers it
         wait_vmem();
     }
-    // shard ticket, then (last of the shard) the global ticket
     const uint32_t shard = blockIdx.x % kTicketShards;
     const uint32_t shards = min(gridDim.x, kTicketShards);
     const uint32_t in_shard = (gridDim.x - shard + kTicketShards - 1u) / kTicketShards;
-    if (atomicAdd(s + kShardWord + 32u * shard, 1u) != in_shard - 1u) return;
-    if (atomicAdd(s + kTicketWord, 1u) == shards - 1u) {
-        // every other workgroup's adds completed before its tickets
-        p.result[0] = atomicAdd(s + kVCountWord, 0u);
-        p.result[1] = atomicAdd(s + kVFirstWord, 0u);
-    }
+    const unsigned long long o =
+        atomicAdd(reinterpret_cast<unsigned long long *>(s + kShardWord + 32u * shard), kTicket | cnt);
+    if ((o >> 40) != in_shard - 1u) return;
+    const unsigned long long shard_total = (o & kCountMask) + cnt;
+    const unsigned long long g =
+        atomicAdd(reinterpret_cast<unsigned long long *>(s + kTicketWord), kTicket | shard_total);
+    if ((g >> 40) != shards - 1u) return;
+    // every other workgroup's first-bad update completed before its ticket
+    const unsigned long long total = (g & kCountMask) + shard_total;
+    p.result[0] = uint32_t(total);
+    p.result[1] = total ? atomicAdd(s + kVFirstWord, 0u) : 0xffffffffu;
 }
 
 // ---- tiles: one wave, 16 blocks ------------------------------------------
@@ -479,12 +508,12 @@ __device__ __forceinline__ void gtile_prepare(FastTile t, int lane, uint4 v[8]) 
 }
 
 // lin() of pieces I0 .. I1-1 of a tile (instruction i's 16 bytes per lane).
-template <int DIAG, bool S4, bool H>
+template <int DIAG, bool S4, int IMG>
 __device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8], uint32_t pc[8], int lane) {
-    const LaneCols cols = lane_cols<H>(uint32_t(lane & 31));
+    const LaneCols cols = lane_cols<IMG>(uint32_t(lane & 31));
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        pc[i] = piece<S4, DIAG>(lds, v[i], cols);
+        pc[i] = piece<S4, DIAG, IMG>(lds, v[i], cols);
         opaque(pc[i]);
         // One piece at a time (nibble tables: 32 independent reads each), or
         // two (S4: a piece is a chain of 4 dependent steps, so two chains
@@ -526,7 +555,7 @@ __device__ __forceinline__ uint32_t block_lin(const uint32_t pc[8], int lane) {
 }
 
 // Power-of-two tile: blocks combined per chunk, chunk checksums stored (or compared).
-template <bool S4, bool VERIFY>
+template <bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             const uint32_t pc[8], uint32_t ev, int lane) {
     const uint32_t nb = t.meta & 0xffu;
@@ -536,7 +565,7 @@ __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds
     if (lg) {  // chunks of 2^lg blocks: shift each block to the chunk end, XOR them
         const uint32_t nbc = 1u << lg;
         const uint32_t s = nbc - 1u - (blk & (nbc - 1u));
-        if (s) x = zshift<S4>(lds, s, x);
+        if (s) x = zshift<S4, IMG>(lds, s, x);
         x ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), 32));  // block bit 0 = lane bit 5
         if (lg >= 2) x ^= dpp<kDppXor8>(x);                               // block bit 1 = lane bit 3
         if (lg >= 3) x ^= dpp<kDppXor2>(x);                               // block bit 2 = lane bit 1
@@ -549,7 +578,7 @@ __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds
 // General tile: block b (chunk b / k, block j = b % k of it) shifted by
 // Z^(512 (k - 1 - j)), then lane c < nch XORs its chunk's k blocks from the
 // lanes holding them; the data carried the pre-inversion, so crc = lin ^ ~0.
-template <bool S4, bool VERIFY>
+template <bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void reduce_emit_general(const KParams &p, const uint8_t *lds, uint32_t *vacc,
                                                     FastTile t, const uint32_t pc[8], uint32_t ev, int lane) {
     const GShape g = gshape(t.meta);
@@ -558,7 +587,7 @@ __device__ __forceinline__ void reduce_emit_general(const KParams &p, const uint
     // blk / k for blk < 16, k <= 16: (blk + 1/2) / k is never within 1/32 of an integer
     const uint32_t quo = uint32_t((float(blk) + 0.5f) * __builtin_amdgcn_rcpf(float(g.k)));
     const uint32_t s = g.k - 1u - (blk - quo * g.k);
-    if (s) x = zshift<S4>(lds, s, x);
+    if (s) x = zshift<S4, IMG>(lds, s, x);
     uint32_t acc = 0;
     const uint32_t b0 = uint32_t(lane) * g.k;
     for (uint32_t u = 0; u < g.k; ++u) {
@@ -568,17 +597,17 @@ __device__ __forceinline__ void reduce_emit_general(const KParams &p, const uint
     if (uint32_t(lane) < g.nch) emit<VERIFY>(p, vacc, t.out + uint32_t(lane), acc ^ 0xffffffffu, ev);
 }
 
-template <int DIAG, bool S4, bool VERIFY, bool H, bool GENERAL>
+template <int DIAG, bool S4, bool VERIFY, int IMG, bool GENERAL>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             uint4 v[8], uint32_t ev, int lane) {
     uint32_t pc[8];
     if (GENERAL && (t.meta & kGeneralTile)) {
         gtile_prepare(t, lane, v);
-        tile_pieces<DIAG, S4, H>(lds, v, pc, lane);
-        reduce_emit_general<S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane);
+        reduce_emit_general<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
     } else {
-        tile_pieces<DIAG, S4, H>(lds, v, pc, lane);
-        reduce_emit<S4, VERIFY>(p, lds, vacc, t, pc, ev, lane);
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane);
+        reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
     }
 }
 
@@ -630,7 +659,7 @@ __device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
                       __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
 }
 
-template <bool S4, bool VERIFY, bool H>
+template <bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
                                          int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
@@ -645,7 +674,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
     const uintptr_t cbeg = reinterpret_cast<uintptr_t>(p.payload) + g.src;
     const uintptr_t cend = cbeg + r;
     const uintptr_t ffend = r >= 4 ? cbeg + 4 : cbeg;
-    const LaneCols cols = lane_cols<H>(q);
+    const LaneCols cols = lane_cols<IMG>(q);
     uint32_t acc = 0;
     for (uint32_t m = 0; m < nmax; ++m) {
         uint32_t lin = 0;
@@ -656,10 +685,10 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
             uint32_t w[8];
             load_piece(a0, cbeg, cend, ffend, w);
             load_piece(a0 + 16, cbeg, cend, ffend, w + 4);
-            lin = piece<S4, 0>(lds, funnel(w, uint32_t(a & 15u)), cols);
+            lin = piece<S4, 0, IMG>(lds, funnel(w, uint32_t(a & 15u)), cols);
         }
         lin = allreduce32(lin);
-        if (m < nbv) acc = zshift<S4>(lds, 1, acc) ^ lin;
+        if (m < nbv) acc = zshift<S4, IMG>(lds, 1, acc) ^ lin;
     }
     if (valid && q == 0) {
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
@@ -670,7 +699,7 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
 // A chunk assembled from several buffers (SegItem): like gen_pair, but each
 // lane's 16-byte window (chunk positions o .. o+15) is filled from every data
 // piece it overlaps; positions no piece covers are zero fill.
-template <bool S4, bool VERIFY, bool H>
+template <bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void seg_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
                                          int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
@@ -683,7 +712,7 @@ __device__ __forceinline__ void seg_pair(const KParams &p, const uint8_t *lds, u
     const uint32_t nmax = max(__builtin_amdgcn_readlane(nbv, 0), __builtin_amdgcn_readlane(nbv, 32));
     const int64_t pad = int64_t(nbv) * 512 - int64_t(r);
     const uintptr_t base = reinterpret_cast<uintptr_t>(p.payload);
-    const LaneCols cols = lane_cols<H>(q);
+    const LaneCols cols = lane_cols<IMG>(q);
     uint32_t acc = 0;
     for (uint32_t m = 0; m < nmax; ++m) {
         uint32_t lin = 0;
@@ -703,10 +732,10 @@ __device__ __forceinline__ void seg_pair(const KParams &p, const uint8_t *lds, u
                 d = make_uint4(d.x | f.x, d.y | f.y, d.z | f.z, d.w | f.w);
             }
             if (r >= 4) d = chunk_start_mask(d, int(-o));  // (o + 16 > 0 here: nothing before the chunk is loaded)
-            lin = piece<S4, 0>(lds, d, cols);
+            lin = piece<S4, 0, IMG>(lds, d, cols);
         }
         lin = allreduce32(lin);
-        if (m < nbv) acc = zshift<S4>(lds, 1, acc) ^ lin;
+        if (m < nbv) acc = zshift<S4, IMG>(lds, 1, acc) ^ lin;
     }
     if (valid && q == 0) {
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
@@ -738,16 +767,18 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
     constexpr bool VERIFY = (MODE & kModeVerify) != 0;
     constexpr bool H = S4 && (MODE & kModeS4H) != 0;
+    constexpr bool C = S4 && (MODE & kModeS4C) != 0;
+    constexpr int IMG = H ? kImgHalf : C ? kImgCompact : kImgFull;
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
-    constexpr uint32_t kStage = S4 ? kS4StageBytes : kStageBytes;
+    constexpr uint32_t kStage = !S4 ? kStageBytes : C ? kS4CStageBytes : kS4StageBytes;
     // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
     // its mismatch count and first bad index.
     __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
-    const uint8_t *table = S4 ? (H ? p.table_s4 + hdfs_crc::kS4HOff : p.table_s4) : p.table;
+    const uint8_t *table = !S4 ? p.table : H ? p.table_s4 + hdfs_crc::kS4HOff : C ? p.table_s4 + hdfs_crc::kS4COff : p.table_s4;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
 
@@ -779,8 +810,20 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     // launch of constant runs only needs none.
     const bool tables = (p.ntiles | p.ngen | p.nseg) != 0;
     constexpr uint32_t kStageChunks = kStage / 1024u;
-    if (!NOSTAGE && tables) {
-        for (uint32_t c = wv; c < kStageChunks; c += (H && c + kWaves >= 64u && c + kWaves < 128u) ? kWaves + 64u : kWaves) {
+    if (!NOSTAGE && tables && !H) {
+        // Every workgroup copies the same 152 chunks: start each one at a
+        // different chunk (the 32 CUs of an XCD would otherwise walk the same
+        // L2 lines, hence the same L2 channel, in lock step).
+        const uint32_t rot = (blockIdx.x * 37u) % kStageChunks;
+        for (uint32_t i = wv; i < kStageChunks; i += kWaves) {
+            const uint32_t c = i + rot < kStageChunks ? i + rot : i + rot - kStageChunks;
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
+                (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+        }
+    }
+    if (!NOSTAGE && tables && H) {
+        for (uint32_t c = wv; c < kStageChunks; c += (c + kWaves >= 64u && c + kWaves < 128u) ? kWaves + 64u : kWaves) {
             // (half-column image: its T region is the first 64 KiB; chunks 64-127 are unused)
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
@@ -795,7 +838,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
     }
     while (t < tend) {
-        finish_tile<DIAG, S4, VERIFY, H, GENERAL>(p, lds, vacc, ft, v, ev, lane);
+        finish_tile<DIAG, S4, VERIFY, IMG, GENERAL>(p, lds, vacc, ft, v, ev, lane);
         t = pool_grab(pool_ctr, lane);
         if (t >= tend) break;
         ft = tile_at(p, t);
@@ -809,9 +852,9 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     const uint32_t nitems = ngp + nsp + p.nconst;
     for (uint32_t g = wave; g < nitems; g += nwaves) {
         if (g < ngp)
-            gen_pair<S4, VERIFY, H>(p, lds, vacc, g, lane);
+            gen_pair<S4, VERIFY, IMG>(p, lds, vacc, g, lane);
         else if (g < ngp + nsp)
-            seg_pair<S4, VERIFY, H>(p, lds, vacc, g - ngp, lane);
+            seg_pair<S4, VERIFY, IMG>(p, lds, vacc, g - ngp, lane);
         else
             const_run<VERIFY>(p, vacc, g - ngp - nsp, lane);
     }

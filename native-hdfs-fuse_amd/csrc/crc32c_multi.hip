@@ -135,8 +135,10 @@ int ensure_comms(crc32c_multi *m) {
     return 0;
 }
 
+// The caller's stream of local device i (NULL = that device's default
+// stream), or the library's own when the caller passes no stream array.
 hipStream_t local_stream(crc32c_multi *m, size_t i, void *const *streams) {
-    if (streams && streams[i]) return static_cast<hipStream_t>(streams[i]);
+    if (streams) return static_cast<hipStream_t>(streams[i]);
     return m->streams[i];
 }
 

@@ -132,6 +132,14 @@ void build_lds_image_s4(uint8_t *dst, uint32_t poly) {
     std::memcpy(dst + kS4ShiftOff, nib.data() + kLdsShiftOff, kMaxShift * 512);
 }
 
+void compact_s4_image(const uint8_t *full, uint8_t *dst) {
+    std::memset(dst, 0, kS4CBytes);
+    for (uint32_t m = 0; m < 4; ++m)
+        for (uint32_t b = 0; b < 256; ++b)  // column 0 of T_m
+            std::memcpy(dst + m * 1024u + 4u * b, full + (m >> 1) * 65536u + b * 256u + (m & 1u) * 128u, 4);
+    std::memcpy(dst + kS4CNibOff, full + kS4NibOff, kS4Bytes - kS4NibOff);
+}
+
 void affine_constants(uint32_t c_lg[5], uint32_t c_small[4], uint32_t poly) {
     // crc(0, zeros(n)) = Z^n(0xffffffff) ^ 0xffffffff (crc32c.c:237, 312).
     for (int lg = 0; lg < 5; ++lg) c_lg[lg] = op_zeros(512ull << lg, poly).apply(0xffffffffu) ^ 0xffffffffu;

@@ -70,6 +70,15 @@ constexpr size_t kS4NibOff = 131072;
 constexpr size_t kS4ShiftOff = 147456;
 constexpr size_t kS4Bytes = kS4ShiftOff + kMaxShift * 512;
 
+// The compact S4 image (small batches): T0..T3 once each (T_m[b] at
+// m * 1024 + 4 b), then the N_q section and the Z^(512 s) section laid out as
+// in the full image.
+constexpr size_t kS4CNibOff = 4096;
+constexpr size_t kS4CShiftOff = kS4CNibOff + (kS4ShiftOff - kS4NibOff);
+constexpr size_t kS4CBytes = kS4CShiftOff + kMaxShift * 512;
+// Fills `dst` (kS4CBytes) from a full S4 image.
+void compact_s4_image(const uint8_t *full, uint8_t *dst);
+
 // Fills `dst` (kS4Bytes) with the slicing-by-4 LDS image.
 void build_lds_image_s4(uint8_t *dst, uint32_t poly = kPoly);
 // S(u): the register after feeding the 4 bytes of u (little-endian) into register 0.

@@ -21,6 +21,7 @@ struct Variant {
     const char *name;
     uint32_t threads, wg_per_cu;
     bool exact;  // computes the right checksums
+    bool prod_grid = false;  // the production grid: min(items, CUs) workgroups
 };
 
 constexpr Variant kVariants[] = {
@@ -35,6 +36,10 @@ constexpr Variant kVariants[] = {
     {9, "s4_wg512x1_nt", 512, 1, true},                    // 0 with 8 waves per CU
     {35, "s4h_nt", 768, 1, true},                          // half-column image (88 KiB staged)
     {36, "s4h_nt_stamps", 768, 1, true},                   // 35 with per-wave timestamps
+    {40, "s4_nt_memonly_nostage_prodgrid", 768, 1, false, true},  // 7 on the production grid (launch floor)
+    {41, "s4c_nt_prodgrid", 768, 1, true, true},           // compact image (28 KiB staged), production grid
+    {42, "s4c_nt_stamps_prodgrid", 768, 1, true, true},    // 41 with per-wave timestamps
+    {43, "s4_nt_stamps_prodgrid", 768, 1, true, true},     // 0 with per-wave timestamps, production grid
 };
 
 const Variant *find(int v) {
@@ -48,7 +53,7 @@ const Variant *find(int v) {
 hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
-    uint64_t grid = (items + waves - 1) / waves;
+    uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu) : (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
@@ -64,6 +69,10 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 9: HDFS_LAUNCH(512, 2, kS4Nt); break;
     case 35: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H); break;
     case 36: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H | kModeStamps); break;
+    case 40: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeNoStage); break;
+    case 41: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C); break;
+    case 42: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeStamps); break;
+    case 43: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

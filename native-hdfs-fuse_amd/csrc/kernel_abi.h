@@ -18,7 +18,11 @@ constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 
 // debug library): the full image with its T region re-laid out as
 // b*256 + m*64 + 4*(q & 15) (the first 64 KiB).
 constexpr uint32_t kS4HOff = kTableAllocS4;
-constexpr uint32_t kTableAllocS4Full = kS4HOff + kTableAllocS4;
+// Then the compact S4 image (crc_math.h kS4C*), padded to whole 1 KiB
+// staging pieces.
+constexpr uint32_t kS4COff = kS4HOff + kTableAllocS4;
+constexpr uint32_t kTableAllocS4C = ((uint32_t(kS4CBytes) + 16384 - 1) / 16384) * 16384;
+constexpr uint32_t kTableAllocS4Full = kS4COff + kTableAllocS4C;
 
 struct KParams {
     const FastTile *tiles;  // power-of-two and general tiles
@@ -54,15 +58,16 @@ struct KParams {
 // own 128-B line: the grid-wide merge of the workgroups' mismatch counts.
 // Launches of one plan (or one host-pipeline stage) alternate between two
 // slots and run in GPU order, so a launch resets the slot its predecessor
-// used: {ticket, vcount, vfirst, shard tickets} = {0, 0, ~0, 0} at launch
-// start.  Workgroup b first takes a ticket in shard b % kTicketShards; the
-// last of a shard takes one of the global ticket (one counter per 32
-// workgroups instead of one for all 256: every add to one word serialises).
+// used: {global ticket, first bad, shard tickets} = {0, ~0, 0} at launch
+// start.  Ticket words are 64-bit: tickets taken (bits 40-63) and the
+// mismatches they carried (bits 0-39).  Workgroup b first takes a ticket in
+// shard b % kTicketShards; the last of a shard takes one of the global
+// ticket (one counter per 32 workgroups instead of one for all 256: every
+// add to one word serialises).
 constexpr uint32_t kTicketShards = 8;
-constexpr uint32_t kTicketWord = 0;
-constexpr uint32_t kVCountWord = 32;
-constexpr uint32_t kVFirstWord = 64;
-constexpr uint32_t kShardWord = 96;  // + 32 * shard
+constexpr uint32_t kTicketWord = 0;   // u64
+constexpr uint32_t kVFirstWord = 64;  // u32
+constexpr uint32_t kShardWord = 96;   // u64, + 32 * shard
 constexpr uint32_t kSlotWords = kShardWord + 32 * kTicketShards;
 
 // Fills two slots' initial state (2 * kSlotWords words).
