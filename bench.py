@@ -432,7 +432,7 @@ def main():
     # checksums in host memory), every rank at once on its own GPU and PCIe
     # link; the node-level rate is all ranks' bytes / the slowest rank's time.
     # Beside it, the link's ceiling: a plain pinned H2D copy of the same bytes.
-    host = h2d = None
+    host = h2d = host_multi = None
     if not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
         hp = pinned.numpy()
@@ -466,13 +466,29 @@ def main():
         torch.cuda.synchronize()
         h2d = round(world * pinned.numel() * reps / slowest(time.perf_counter() - h0) / GIB, 2)
         del dst
+        # The N-link lever: crc32c_multi_batch_host deals the batch's 4 MiB
+        # blocks over every GPU this process sees, each over its own PCIe link
+        # (one process; N = 1 on a one-GPU box).
+        if world == 1:
+            ndev = torch.cuda.device_count()
+            m = hdfs.Multi(list(range(ndev)))
+            mout = m.batch_host(hp, pk, group_packets=64)
+            exact_multi = bool(np.array_equal(mout[:nout], want))
+            h0 = time.perf_counter()
+            for _ in range(reps):
+                m.batch_host(hp, pk, group_packets=64)
+            host_multi = {"gib_s": round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2), "devices": ndev,
+                          "bit_exact": exact_multi, "entry": "crc32c_multi_batch_host"}
+            bit_exact = bit_exact and exact_multi
+            m.close()
 
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"))
-        traffic = None
+        traffic = traffic_commit = None
         if (pmc and pmc.get("config") == args.config
                 and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
+            traffic_commit = pmc.get("commit")
         # the CPU baseline is an N = 1 figure (timed on rank 0's host cores)
         cpu = None if args.no_cpu or world > 1 else (
             cpu_baseline(file_pk, file_bytes, args.cpu_seconds) if c4 else cpu_baseline(pk, payload0, args.cpu_seconds))
@@ -493,6 +509,9 @@ def main():
                                        % (world, "RCCL" if backend == "nccl" else backend + " rehearsal"))},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "traffic_source": None if traffic is None else
+                         "rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE per launch, profiles/ summary at commit %s"
+                         % traffic_commit,
                          "kernel": KERNEL_NAME, "kernel_avg_us": round(kernel_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": nbytes},
             "cpu_baseline": cpu,
@@ -500,6 +519,7 @@ def main():
             "host_resident_gib_s": host,
             "host_h2d_copy_gib_s": h2d,
             "host_resident_ranks": world if host is not None else None,
+            "host_resident_multi": host_multi,
             "verify": verify,
             "two_streams": two_streams,
             "box_read_probe": read_probe,

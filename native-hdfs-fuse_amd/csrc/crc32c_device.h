@@ -90,6 +90,7 @@ constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table stagin
 constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
 constexpr int kModeS4H = 128;       // A/B: half-column S4 image (64 KiB of T tables, 88 KiB staged)
 constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
+constexpr int kModeEarly = 1024;    // the first tile's loads are issued before the table staging
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
 
@@ -770,6 +771,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool C = S4 && (MODE & kModeS4C) != 0;
     constexpr int IMG = H ? kImgHalf : C ? kImgCompact : kImgFull;
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
+    constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = !S4 ? kStageBytes : C ? kS4CStageBytes : kS4StageBytes;
@@ -804,8 +806,14 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     FastTile ft{0, 0, 0};
     uint4 v[8];
     uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
-    // (Issuing the first tile's loads before the staging was measured slower:
-    // 3072 waves x 8 KiB in flight queue the staging DMA behind them.)
+    // EARLY: the first tile's loads go out before the staging (their latency
+    // overlaps it).  Measured slower for large batches -- 3072 waves x 8 KiB
+    // in flight queue the 152 KiB staging DMA behind them -- so only the
+    // small-batch kernel (compact image, 28 KiB) does it.
+    if (EARLY && t < tend) {
+        ft = tile_at(p, t);
+        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+    }
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs); a
     // launch of constant runs only needs none.
     const bool tables = (p.ntiles | p.ngen | p.nseg) != 0;
@@ -833,7 +841,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
-    if (t < tend) {
+    if (!EARLY && t < tend) {
         ft = tile_at(p, t);
         load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
     }

@@ -1,29 +1,49 @@
 // crc32c_kernel.hip -- the production instantiations of the CDNA4 (gfx950)
 // CRC32C chunk kernel (device code and design notes: crc32c_device.h).
 //
-// Exactly four kernels ship in libhdfs_crc32c.so: the slicing-by-4 kernel
-// with non-temporal payload loads, 12 waves (768 threads) per workgroup and
-// one workgroup per CU, storing checksums (crc32c_plan_exec) or comparing
-// them (crc32c_plan_verify), each with or without the general-tile code (a
-// batch without bpc outside 512 * 2^k runs the kernel that lacks it).  A/B and diagnostic variants are built only
-// into libhdfs_crc32c_debug.so (debug/crc32c_variants.hip).
+// libhdfs_crc32c.so ships the slicing-by-4 kernel with non-temporal payload
+// loads, 12 waves (768 threads) per workgroup and one workgroup per CU, in
+// three builds, each storing checksums (crc32c_plan_exec) or comparing them
+// (crc32c_plan_verify):
+//   * full image, power-of-two tiles only: the bulk path (config 2);
+//   * full image with the general-tile code (bpc outside 512 * 2^k);
+//   * compact image (28 KiB staged instead of 152 KiB, with the general-tile
+//     code): batches of at most kSmallBatchItems work items, where the table
+//     staging is most of a launch (one 4 MiB block: 5.8 -> 5.2 us).
+// A/B and diagnostic variants are built only into libhdfs_crc32c_debug.so
+// (debug/crc32c_variants.hip).
 #include "crc32c_device.h"
 
 namespace hdfs_crc {
 
+namespace {
+// Work items per CU up to which the compact image wins: its T lookups are
+// not conflict-free (one copy of each table instead of 32 lane columns), so
+// once every CU has several tiles the full image's faster lookups pay back
+// its staging (small batches).
+constexpr uint64_t kSmallBatchItemsPerCu = 8;
+}  // namespace
+
 hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream) {
     using namespace hdfs_crc_dev;
     constexpr int kProd = kModeS4 | kModeNt;
-    const dim3 g{production_grid(p, num_cu), 1, 1}, b{768, 1, 1};
     constexpr int kGen = kModeGeneral;
+    constexpr int kSmall = kModeS4C | kModeGeneral;
+    const dim3 g{production_grid(p, num_cu), 1, 1}, b{768, 1, 1};
+    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
+    const bool small = items <= kSmallBatchItemsPerCu * num_cu;
     if (p.expect) {
         if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
-        if (p.general)
+        if (small)
+            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>), g, b, 0, stream, p);
+        else if (p.general)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeVerify>), g, b, 0, stream, p);
         else
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeVerify>), g, b, 0, stream, p);
     } else {
-        if (p.general)
+        if (small)
+            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>), g, b, 0, stream, p);
+        else if (p.general)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen>), g, b, 0, stream, p);
         else
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd>), g, b, 0, stream, p);

@@ -40,6 +40,13 @@ constexpr Variant kVariants[] = {
     {41, "s4c_nt_prodgrid", 768, 1, true, true},           // compact image (28 KiB staged), production grid
     {42, "s4c_nt_stamps_prodgrid", 768, 1, true, true},    // 41 with per-wave timestamps
     {43, "s4_nt_stamps_prodgrid", 768, 1, true, true},     // 0 with per-wave timestamps, production grid
+    // small batches: compact image, one tile per wave, smaller workgroups
+    {44, "s4c_wg256_nt", 256, 4, true},                    // 4 waves per workgroup
+    {45, "s4c_wg128_nt", 128, 8, true},                    // 2 waves per workgroup
+    {46, "s4c_wg256_nt_early", 256, 4, true},              // 44, first tile's loads before the staging
+    {47, "s4c_wg128_nt_early", 128, 8, true},              // 45, first tile's loads before the staging
+    {48, "s4c_nt_early_prodgrid", 768, 1, true, true},     // 41, first tile's loads before the staging
+    {49, "s4_nt_general_prodgrid", 768, 1, true, true},    // the full-image production build, any batch size
 };
 
 const Variant *find(int v) {
@@ -73,6 +80,12 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 41: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C); break;
     case 42: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeStamps); break;
     case 43: HDFS_LAUNCH(768, 3, kS4Nt | kModeStamps); break;
+    case 44: HDFS_LAUNCH(256, 4, kS4Nt | kModeS4C); break;
+    case 45: HDFS_LAUNCH(128, 4, kS4Nt | kModeS4C); break;
+    case 46: HDFS_LAUNCH(256, 4, kS4Nt | kModeS4C | kModeEarly); break;
+    case 47: HDFS_LAUNCH(128, 4, kS4Nt | kModeS4C | kModeEarly); break;
+    case 48: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeEarly); break;
+    case 49: HDFS_LAUNCH(768, 3, kS4Nt); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -50,8 +50,14 @@ def main():
     args = ap.parse_args()
     c, dur, meta = load(args.pmc_dir)
     med_ns = dur[len(dur) // 2] if dur else None
+    import subprocess
+    try:  # the commit the profiled library was built from (collect right after committing)
+        commit = subprocess.run(["git", "describe", "--always", "--dirty"], capture_output=True, text=True,
+                                cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout.strip()
+    except Exception:
+        commit = None
     res = {"kernel": KERNEL, "config": args.config, "counters_avg_per_dispatch": c, "dispatch_meta": meta,
-           "profiled_duration_ns_median": med_ns}
+           "profiled_duration_ns_median": med_ns, "commit": commit}
     if "FETCH_SIZE" in c:
         fetch = c["FETCH_SIZE"] * 1024 * 2  # KiB; gfx950 under-count of wide streams corrected x2
         write = c.get("WRITE_SIZE", 0.0) * 1024
