@@ -91,6 +91,7 @@ constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instea
 constexpr int kModeS4H = 128;       // A/B: half-column S4 image (64 KiB of T tables, 88 KiB staged)
 constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
 constexpr int kModeEarly = 1024;    // the first tile's loads are issued before the table staging
+constexpr int kModeItemsFirst = 2048;  // gen / seg / const items before the tiles instead of after
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
 
@@ -772,6 +773,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr int IMG = H ? kImgHalf : C ? kImgCompact : kImgFull;
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
+    constexpr bool ITEMSFIRST = !EARLY && (MODE & kModeItemsFirst) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = !S4 ? kStageBytes : C ? kS4CStageBytes : kS4StageBytes;
@@ -841,6 +843,26 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
+    // Gen pairs, seg pairs and constant runs, dealt over every wave of the
+    // grid: after the tiles, or (ITEMSFIRST) before them, so that their
+    // latency-bound loads overlap the other waves' tile streaming instead of
+    // the launch's tail.
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
+    const uint32_t nwaves = gridDim.x * kWaves;
+    auto items = [&]() {
+        const uint32_t ngp = (p.ngen + 1u) >> 1, nsp = (p.nseg + 1u) >> 1;
+        const uint32_t nitems = ngp + nsp + p.nconst;
+        for (uint32_t g = wave; g < nitems; g += nwaves) {
+            if (g < ngp)
+                gen_pair<S4, VERIFY, IMG>(p, lds, vacc, g, lane);
+            else if (g < ngp + nsp)
+                seg_pair<S4, VERIFY, IMG>(p, lds, vacc, g - ngp, lane);
+            else
+                const_run<VERIFY>(p, vacc, g - ngp - nsp, lane);
+        }
+    };
+    if (ITEMSFIRST) items();
+
     if (!EARLY && t < tend) {
         ft = tile_at(p, t);
         load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
@@ -852,20 +874,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         ft = tile_at(p, t);
         load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
     }
-
-    // Gen pairs, seg pairs and constant runs, dealt over every wave of the grid.
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
-    const uint32_t nwaves = gridDim.x * kWaves;
-    const uint32_t ngp = (p.ngen + 1u) >> 1, nsp = (p.nseg + 1u) >> 1;
-    const uint32_t nitems = ngp + nsp + p.nconst;
-    for (uint32_t g = wave; g < nitems; g += nwaves) {
-        if (g < ngp)
-            gen_pair<S4, VERIFY, IMG>(p, lds, vacc, g, lane);
-        else if (g < ngp + nsp)
-            seg_pair<S4, VERIFY, IMG>(p, lds, vacc, g - ngp, lane);
-        else
-            const_run<VERIFY>(p, vacc, g - ngp - nsp, lane);
-    }
+    if (!ITEMSFIRST) items();
     if (VERIFY) {
         __syncthreads();
         if (threadIdx.x == 0) verify_finish(p, vacc);

@@ -47,6 +47,7 @@ constexpr Variant kVariants[] = {
     {47, "s4c_wg128_nt_early", 128, 8, true},              // 45, first tile's loads before the staging
     {48, "s4c_nt_early_prodgrid", 768, 1, true, true},     // 41, first tile's loads before the staging
     {49, "s4_nt_general_prodgrid", 768, 1, true, true},    // the full-image production build, any batch size
+    {50, "s4_nt_itemsfirst_prodgrid", 768, 1, true, true},  // 49 with gen / seg / const items before the tiles
 };
 
 const Variant *find(int v) {
@@ -86,6 +87,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 47: HDFS_LAUNCH(128, 4, kS4Nt | kModeS4C | kModeEarly); break;
     case 48: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeEarly); break;
     case 49: HDFS_LAUNCH(768, 3, kS4Nt); break;
+    case 50: HDFS_LAUNCH(768, 3, kS4Nt | kModeItemsFirst); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
