@@ -397,72 +397,115 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// General tile geometry (plan.h general_meta).
+// General tile geometry (plan.h general_meta): nch full chunks of bpc bytes
+// (k virtual blocks, pad leading zeros each), then optionally a tail chunk
+// of tl bytes (kt blocks, padt leading zeros) starting right after them.
 struct GShape {
-    uint32_t k, nch, pad, bpc;
+    uint32_t k, nch, pad, bpc, tl, kt, padt;
+    uint64_t src;  // payload offset of the first chunk
 };
-__device__ __forceinline__ GShape gshape(uint32_t meta) {
+__device__ __forceinline__ GShape gshape(FastTile t) {
     GShape g;
-    g.k = (meta >> 8) & 31u;
-    g.nch = (meta >> 13) & 31u;
-    g.pad = (meta >> 18) & 511u;
+    g.k = (t.meta >> 8) & 31u;
+    g.nch = (t.meta >> 13) & 31u;
+    g.pad = (t.meta >> 18) & 511u;
     g.bpc = g.k * 512u - g.pad;
+    g.tl = uint32_t(t.src >> 48);
+    g.kt = (g.tl + 511u) >> 9;
+    g.padt = g.kt * 512u - g.tl;
+    g.src = t.src & hdfs_crc::kSrcMask;
     return g;
 }
 
-// Virtual block b -> (chunk, block in chunk) for b = 2i + h, stepped by 2.
-__device__ __forceinline__ void gstep(uint32_t &c, uint32_t &j, uint32_t k) {
-    j += 2u;
-    if (j >= k) {
-        j -= k;
-        ++c;
+// Per-k patterns of whole chunks of k blocks over the 16 block slots:
+// start bit b = (b % k == 0), nibble b of dist = k - 1 - b % k (the block's
+// distance from its chunk's end, the Z^512 power it is shifted by).
+struct GPatterns {
+    uint64_t dist[17];
+    uint32_t start[17];
+    constexpr GPatterns() : dist(), start() {
+        for (int k = 1; k <= 16; ++k)
+            for (int b = 0; b < 16; ++b) {
+                dist[k] |= uint64_t(k - 1 - b % k) << (4 * b);
+                if (b % k == 0) start[k] |= 1u << b;
+            }
     }
-    if (j >= k) {
-        j -= k;
-        ++c;
-    }
+};
+__constant__ const GPatterns kGPat{};
+
+// Wave-uniform block facts of one general tile (from its descriptor, on the
+// scalar unit; lanes only select their block's bit or nibble): the tile
+// replaces per-lane (chunk, block) tracking with these.
+struct GBlocks {
+    uint32_t start;  // bit b: block b is its chunk's first (tail chunk included)
+    uint32_t sfull;  // the same for the full chunks only
+    uint32_t nfb;    // blocks of the full chunks (nch * k); the tail's follow
+    uint32_t nb;     // blocks in the tile (nfb + kt)
+    uint64_t dist;   // nibble b: blocks from b to its chunk's end
+};
+__device__ __forceinline__ GBlocks gblocks(const GShape &g) {
+    GBlocks r;
+    r.nfb = g.nch * g.k;
+    r.nb = r.nfb + g.kt;
+    r.sfull = kGPat.start[g.k] & ((1u << r.nfb) - 1u);
+    r.start = r.sfull | (g.kt ? 1u << r.nfb : 0u);
+    const uint64_t full = r.nfb >= 16 ? ~0ull : (1ull << (4 * r.nfb)) - 1ull;
+    r.dist = kGPat.dist[g.k] & full;
+    if (g.kt) r.dist |= (kGPat.dist[g.kt] & ((1ull << (4 * g.kt)) - 1ull)) << (4 * r.nfb);
+    return r;
 }
 
-// Loads of one general tile: lane q of block b = 2i + h (chunk c = b / k,
-// block j = b % k of it) reads chunk bytes 512 j + 16 q - pad .. +15 through
-// a descriptor over [src - 16, src + nch * bpc) (from src when pad == 0).
-// Lanes wholly inside a chunk's zero prefix, or past the last chunk, read
-// zeros without touching memory; the straddling lane's bytes before the
-// chunk are masked in gtile_prepare.
+// Loads of one general tile: lane q of block b = 2i + h reads bytes
+// 512 b + 16 q - D(b) .. +15 of the tile, D(b) = pad x (full chunks started
+// at or before b) + (padt in the tail chunk): the virtual blocks of chunk c
+// start pad_c bytes before c's data.  The descriptor covers [src - 16,
+// src + nch * bpc + tl) (from src when no chunk is padded: then the blocks
+// are contiguous and load exactly like a power-of-two tile).  Lanes wholly
+// inside a chunk's zero prefix, or past the last chunk, read zeros without
+// touching memory; the straddling lane's bytes before the chunk are masked
+// in gtile_pieces.
 template <int AUX, bool COMPDIAG, bool VERIFY>
 __device__ __forceinline__ void load_gtile(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
     if (COMPDIAG) {
         load_tile<AUX, true, false>(p, t, lane, v, ev);
         return;
     }
-    const GShape g = gshape(t.meta);
-    if (g.pad == 0) {  // bpc = 512 k: the tile's nch * k blocks are contiguous, loaded as a power-of-two tile's
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t *>(p.payload + t.src), 0, int(g.nch * g.bpc), 0x00020000);
+    const GShape g = gshape(t);
+    const uint32_t nout = g.nch + (g.kt ? 1u : 0u);
+    const uint32_t bytes = g.nch * g.bpc + g.tl;
+    if (g.pad == 0 && g.padt == 0) {
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + g.src), 0, int(bytes), 0x00020000);
         const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
             v[i] = make_uint4(r[0], r[1], r[2], r[3]);
         }
-        if (VERIFY && uint32_t(lane) < g.nch) ev = p.expect[t.out + uint32_t(lane)];
+        if (VERIFY && uint32_t(lane) < nout) ev = p.expect[t.out + uint32_t(lane)];
         __builtin_amdgcn_sched_barrier(0);
         return;
     }
+    const GBlocks gb = gblocks(g);
     const uint32_t shift = 16u;
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(p.payload + t.src - shift), 0, int(shift + g.nch * g.bpc), 0x00020000);
+        const_cast<uint8_t *>(p.payload + g.src - shift), 0, int(shift + bytes), 0x00020000);
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    uint32_t c = g.k == 1 ? h : 0u, j = g.k == 1 ? 0u : h;
+    const uint32_t upto = 2u << h;          // (upto << 2i) - 1: blocks 0 .. b
+    const uint32_t sth = gb.start >> h;     // bit 2i: block b starts a chunk
+    const uint32_t qs = 16u * q + 16u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const bool skip = c >= g.nch || (j == 0 && 16u * q + 16u <= g.pad);
-        const uint32_t voff = skip ? 0x80000000u : shift + c * g.bpc + j * 512u + 16u * q - g.pad;
+        const uint32_t b = 2u * i + h;
+        const bool tail = b >= gb.nfb;
+        const uint32_t pc = tail ? g.padt : g.pad;
+        const uint32_t d = g.pad * __builtin_popcount(gb.sfull & ((upto << (2 * i)) - 1u)) + (tail ? g.padt : 0u);
+        const bool skip = b >= gb.nb || (((sth >> (2 * i)) & 1u) && qs <= pc);
+        const uint32_t voff = skip ? 0x80000000u : shift + 1024u * i + 16u * uint32_t(lane) - d;
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
-        gstep(c, j, g.k);
     }
-    if (VERIFY && uint32_t(lane) < g.nch) ev = p.expect[t.out + uint32_t(lane)];
+    if (VERIFY && uint32_t(lane) < nout) ev = p.expect[t.out + uint32_t(lane)];
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -486,35 +529,15 @@ __device__ __forceinline__ uint4 chunk_start_mask(uint4 d, int m) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// General tile, after its loads: apply the chunk-start masks.
-__device__ __forceinline__ void gtile_prepare(FastTile t, int lane, uint4 v[8]) {
-    const GShape g = gshape(t.meta);
-    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    uint32_t c = 0, j = g.k == 1 ? 0u : h;
-    if (g.pad) {
-        // The chunk starts at position pad - 512 j - 16 q of lane q's piece
-        // of block j; its 4 pre-inverted bytes reach block 1's lane 0 when
-        // pad > 508.
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (j == 0 || (j == 1 && q == 0)) v[i] = chunk_start_mask(v[i], int(g.pad) - int(512u * j + 16u * q));
-            gstep(c, j, g.k);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (j == 0 && q == 0) v[i].x ^= 0xffffffffu;
-            gstep(c, j, g.k);
-        }
-    }
-}
-
-// lin() of pieces I0 .. I1-1 of a tile (instruction i's 16 bytes per lane).
-template <int DIAG, bool S4, int IMG>
-__device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8], uint32_t pc[8], int lane) {
+// lin() of a tile's 8 pieces (instruction i's 16 bytes per lane), each
+// piece first passed through prep(i, piece) (general tiles: the chunk-start
+// masks), so that piece i's lookups start as soon as its own load is back.
+template <int DIAG, bool S4, int IMG, typename Prep>
+__device__ __forceinline__ void tile_pieces(const uint8_t *lds, uint4 v[8], uint32_t pc[8], int lane, Prep prep) {
     const LaneCols cols = lane_cols<IMG>(uint32_t(lane & 31));
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
+        prep(i, v[i]);
         pc[i] = piece<S4, DIAG, IMG>(lds, v[i], cols);
         opaque(pc[i]);
         // One piece at a time (nibble tables: 32 independent reads each), or
@@ -522,6 +545,38 @@ __device__ __forceinline__ void tile_pieces(const uint8_t *lds, const uint4 v[8]
         // interleave to keep 8 reads in flight): keeps the scheduler from
         // hoisting every piece's LDS reads together (register pressure).
         if (!S4 || (i & 1)) __builtin_amdgcn_sched_barrier(0);
+    }
+}
+struct NoPrep {
+    __device__ __forceinline__ void operator()(int, uint4 &) const {}
+};
+
+// General tile pieces with the chunk-start masks (bytes before a chunk
+// zeroed, its first 4 bytes ^ 0xff).  The chunk starts at position
+// pad_c - 16 q of lane q's piece of the chunk's first block; its 4
+// pre-inverted bytes reach the second block's lane 0 when pad_c > 508.
+// Unpadded tiles (bpc = 512 k) only XOR ~0 into lane 0 of each chunk's
+// first block; the two forms are separate loops so that neither waits for
+// all 8 loads before its first lookup.
+template <int DIAG, bool S4, int IMG>
+__device__ __forceinline__ void gtile_pieces(const uint8_t *lds, FastTile t, uint4 v[8], uint32_t pc[8], int lane) {
+    const GShape g = gshape(t);
+    const GBlocks gb = gblocks(g);
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
+    if (g.pad || g.padt) {
+        const uint32_t sth = gb.start >> h;
+        const uint32_t s2h = (gb.start << 1) >> h;  // bit 2i: block b is its chunk's second (or past the tile)
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
+            const uint32_t b = 2u * i + h;
+            const int pcl = int(b >= gb.nfb ? g.padt : g.pad);
+            const bool first = (sth >> (2 * i)) & 1u, second = (s2h >> (2 * i)) & 1u;
+            const int m = first ? pcl - int(16u * q) : pcl - 512 - int(16u * q);
+            if ((first || (second && q == 0)) && m > -4 && m < 16) x = chunk_start_mask(x, m);
+        });
+    } else {
+        const uint32_t sth = q == 0 ? gb.start >> h : 0u;
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane,
+                                   [&](int i, uint4 &x) { x.x ^= uint32_t(-int32_t((sth >> (2 * i)) & 1u)); });
     }
 }
 
@@ -577,26 +632,32 @@ __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds
     if (rep_lane(lane, blk, nb, lg)) emit<VERIFY>(p, vacc, t.out + (blk >> lg), crc, ev);
 }
 
-// General tile: block b (chunk b / k, block j = b % k of it) shifted by
-// Z^(512 (k - 1 - j)), then lane c < nch XORs its chunk's k blocks from the
-// lanes holding them; the data carried the pre-inversion, so crc = lin ^ ~0.
+// General tile: block b (chunk c, block j of it) shifted by
+// Z^(512 (kc - 1 - j)), kc the chunk's blocks, then lane c XORs its chunk's
+// blocks from the lanes holding them; the data carried the pre-inversion, so
+// crc = lin ^ ~0.
 template <bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void reduce_emit_general(const KParams &p, const uint8_t *lds, uint32_t *vacc,
                                                     FastTile t, const uint32_t pc[8], uint32_t ev, int lane) {
-    const GShape g = gshape(t.meta);
+    const GShape g = gshape(t);
+    const GBlocks gb = gblocks(g);
+    const uint32_t nfb = gb.nfb;
     uint32_t x = block_lin(pc, lane);
     const uint32_t blk = rep_block(lane);
-    // blk / k for blk < 16, k <= 16: (blk + 1/2) / k is never within 1/32 of an integer
-    const uint32_t quo = uint32_t((float(blk) + 0.5f) * __builtin_amdgcn_rcpf(float(g.k)));
-    const uint32_t s = g.k - 1u - (blk - quo * g.k);
+    const uint32_t half = blk < 8u ? uint32_t(gb.dist) : uint32_t(gb.dist >> 32);
+    const uint32_t s = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
     if (s) x = zshift<S4, IMG>(lds, s, x);
+    const uint32_t c = uint32_t(lane);
+    const uint32_t b0 = c < g.nch ? c * g.k : nfb;        // the chunk's first block
+    const uint32_t nb = c < g.nch ? g.k : g.kt;           // its blocks (lanes past the tail: garbage, not stored)
+    const uint32_t umax = max(g.k, g.kt);
     uint32_t acc = 0;
-    const uint32_t b0 = uint32_t(lane) * g.k;
-    for (uint32_t u = 0; u < g.k; ++u) {
+    for (uint32_t u = 0; u < umax; ++u) {
         const uint32_t b = min(b0 + u, 15u);
-        acc ^= uint32_t(__builtin_amdgcn_ds_bpermute(int(block_lane(b) << 2), int(x)));
+        const uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(block_lane(b) << 2), int(x)));
+        if (u < nb) acc ^= y;
     }
-    if (uint32_t(lane) < g.nch) emit<VERIFY>(p, vacc, t.out + uint32_t(lane), acc ^ 0xffffffffu, ev);
+    if (c < g.nch + (g.kt ? 1u : 0u)) emit<VERIFY>(p, vacc, t.out + c, acc ^ 0xffffffffu, ev);
 }
 
 template <int DIAG, bool S4, bool VERIFY, int IMG, bool GENERAL>
@@ -604,11 +665,10 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
                                             uint4 v[8], uint32_t ev, int lane) {
     uint32_t pc[8];
     if (GENERAL && (t.meta & kGeneralTile)) {
-        gtile_prepare(t, lane, v);
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane);
+        gtile_pieces<DIAG, S4, IMG>(lds, t, v, pc, lane);
         reduce_emit_general<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
     } else {
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane);
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
         reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
     }
 }

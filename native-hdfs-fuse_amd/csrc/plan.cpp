@@ -49,6 +49,7 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
     const uint64_t nfull = p.len / p.bpc;
     const uint32_t tail = p.len % p.bpc;
     const int lg = fast_lg(p.bpc);
+    bool tail_done = false;
     if (lg >= 0) {
         // Any alignment: a tile off 16-byte alignment is read with unaligned
         // dwordx4 buffer loads (config 2 five bytes off: 55 instead of 42.5 us).
@@ -81,13 +82,22 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             t.src = src;
             t.out = uint32_t(p.out_idx + c);
             t.meta = general_meta(uint32_t(nch), k, pad);
+            // The packet's tail chunk rides in its last tile when it fits:
+            // it starts right after the tile's full chunks, so its loads
+            // never reach before the packet.
+            const uint32_t kt = (tail + kBlockBytes - 1) / kBlockBytes;
+            if (c + nch == nfull && tail >= 4 && nch * k + kt <= kTileBlocks) {
+                t.src |= uint64_t(tail) << 48;
+                t.meta = general_meta(uint32_t(nch), k, pad, kt);
+                tail_done = true;
+            }
             plan->tiles.push_back(t);
             c += nch;
         }
     } else {
         for (uint64_t c = 0; c < nfull; ++c) push_gen(plan, p.payload_off + c * p.bpc, p.out_idx + c, p.bpc);
     }
-    if (tail) push_gen(plan, p.payload_off + nfull * p.bpc, p.out_idx + nfull, tail);
+    if (tail && !tail_done) push_gen(plan, p.payload_off + nfull * p.bpc, p.out_idx + nfull, tail);
     return 0;
 }
 
@@ -214,7 +224,7 @@ int build_write_plan(const crc32c_buffer *buffers, uint32_t n_buffers, uint64_t 
 
 void rebase_plan(HostPlan *plan, uint64_t *base) {
     uint64_t lo = UINT64_MAX;
-    for (const FastTile &t : plan->tiles) lo = std::min(lo, t.src);
+    for (const FastTile &t : plan->tiles) lo = std::min(lo, t.src & kSrcMask);  // (bits 48-63: a tail length)
     for (const GenItem &g : plan->gen) lo = std::min(lo, g.src);
     for (const GenPiece &p : plan->pieces) lo = std::min(lo, p.src);
     lo = lo == UINT64_MAX ? 0 : lo & ~uint64_t(15);

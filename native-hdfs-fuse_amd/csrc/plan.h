@@ -12,7 +12,9 @@
 //    packet with any other bpc in [4, 8192], k = ceil(bpc / 512) virtual
 //    512-byte blocks per chunk.  Each chunk is right-aligned into its k
 //    blocks (pad = 512 k - bpc leading zero bytes, which do not change the
-//    CRC's linear part), so every block is a whole 512-byte load.
+//    CRC's linear part), so every block is a whole 512-byte load.  The last
+//    general tile of a packet also carries the packet's short tail chunk
+//    (tl >= 4 bytes, kt = ceil(tl / 512) more blocks) when it has room.
 //  * GenItem: one chunk of any length / alignment (the short tail chunk of a
 //    packet, or every chunk whose bpc fits neither tile form), processed by
 //    half a wave.
@@ -36,17 +38,21 @@ constexpr uint32_t kMaxTileBpc = kTileBlocks * kBlockBytes;  // 8192
 constexpr uint32_t kGeneralTile = 0x80000000u;
 
 struct FastTile {
-    uint64_t src;   // payload byte offset of the tile's first chunk
+    // payload byte offset of the tile's first chunk (bits 0-47); general
+    // form: bits 48-63 = tl, the length of a tail chunk after the nch full
+    // ones (0 = none)
+    uint64_t src;
     uint32_t out;   // checksum index of the tile's first chunk
     // power-of-two form: bits 0-7 = blocks in tile (1..16), bits 8-15 = lg = log2(bpc / 512);
-    // general form: bit 31, bits 0-7 = nch * k, bits 8-12 = k, bits 13-17 = nch (chunks in the tile),
-    //               bits 18-26 = pad = 512 k - bpc
+    // general form: bit 31, bits 0-7 = blocks (nch * k + kt), bits 8-12 = k, bits 13-17 = nch (full chunks
+    //               in the tile), bits 18-26 = pad = 512 k - bpc
     uint32_t meta;
 };
 static_assert(sizeof(FastTile) == 16, "FastTile is 16 bytes");
+constexpr uint64_t kSrcMask = (1ull << 48) - 1;
 
-inline uint32_t general_meta(uint32_t nch, uint32_t k, uint32_t pad) {
-    return kGeneralTile | (nch * k) | (k << 8) | (nch << 13) | (pad << 18);
+inline uint32_t general_meta(uint32_t nch, uint32_t k, uint32_t pad, uint32_t kt = 0) {
+    return kGeneralTile | (nch * k + kt) | (k << 8) | (nch << 13) | (pad << 18);
 }
 
 struct GenItem {

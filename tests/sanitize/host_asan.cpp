@@ -159,21 +159,25 @@ void plans_and_framing(std::mt19937_64 &rng) {
         std::vector<int> seen(nsums, 0);
         for (uint64_t i = 0; i < nt; ++i) {
             const uint32_t meta = tiles[i].meta;
+            const uint64_t src = tiles[i].src & hdfs_crc::kSrcMask;
+            const uint32_t tl = uint32_t(tiles[i].src >> 48), kt = (tl + 511u) / 512u;
             uint32_t nch, bpc;
             if (meta & hdfs_crc::kGeneralTile) {
                 const uint32_t k = (meta >> 8) & 31u, pad = (meta >> 18) & 511u;
                 nch = (meta >> 13) & 31u;
                 bpc = k * 512u - pad;
-                CHECK(nch >= 1 && nch * k <= 16 && (meta & 0xffu) == nch * k && bpc >= 4, "general tile meta %x", meta);
-                CHECK(pad == 0 || tiles[i].src >= 16, "padded tile too close to the payload start");
+                CHECK(nch >= 1 && nch * k + kt <= 16 && (meta & 0xffu) == nch * k + kt && bpc >= 4,
+                      "general tile meta %x", meta);
+                CHECK(pad == 0 || src >= 16, "padded tile too close to the payload start");
+                CHECK(tl == 0 || (tl >= 4 && tl < bpc), "tail chunk length %u", tl);
             } else {
                 const uint32_t nb = meta & 0xffu, lg = (meta >> 8) & 0xffu;
-                CHECK(nb >= 1 && nb <= 16 && lg <= 4 && (nb % (1u << lg)) == 0, "tile meta %x", meta);
+                CHECK(nb >= 1 && nb <= 16 && lg <= 4 && (nb % (1u << lg)) == 0 && tl == 0, "tile meta %x", meta);
                 nch = nb >> lg;
                 bpc = 512u << lg;
             }
-            CHECK(tiles[i].src + uint64_t(bpc) * nch <= extent, "tile past the payload");
-            for (uint32_t c = 0; c < nch; ++c)
+            CHECK(src + uint64_t(bpc) * nch + tl <= extent, "tile past the payload");
+            for (uint32_t c = 0; c < nch + (tl ? 1u : 0u); ++c)
                 if (tiles[i].out + c < nsums) seen[tiles[i].out + c]++;
         }
         for (uint64_t i = 0; i < ng; ++i) {
@@ -280,15 +284,19 @@ void write_plans(std::mt19937_64 &rng) {
         };
         for (const auto &t : hp.tiles) {
             uint32_t nch, tb;
+            const uint64_t src = t.src & hdfs_crc::kSrcMask;
+            const uint32_t tl = uint32_t(t.src >> 48);
             if (t.meta & hdfs_crc::kGeneralTile) {
                 nch = (t.meta >> 13) & 31u;
                 tb = ((t.meta >> 8) & 31u) * 512u - ((t.meta >> 18) & 511u);
-                CHECK(((t.meta >> 18) & 511u) == 0 || (t.src & 4095u) >= 16, "padded tile page rule");
+                CHECK(((t.meta >> 18) & 511u) == 0 || (src & 4095u) >= 16, "padded tile page rule");
             } else {
                 nch = (t.meta & 0xffu) >> ((t.meta >> 8) & 0xffu);
                 tb = 512u << ((t.meta >> 8) & 0xffu);
+                CHECK(tl == 0, "tail on a power-of-two tile");
             }
-            for (uint32_t c = 0; c < nch; ++c) put(t.out + c, crc_at(t.src + uint64_t(c) * tb, tb));
+            for (uint32_t c = 0; c < nch; ++c) put(t.out + c, crc_at(src + uint64_t(c) * tb, tb));
+            if (tl) put(t.out + nch, crc_at(src + uint64_t(nch) * tb, tl));
         }
         for (const auto &g : hp.gen) put(g.out, crc_at(g.src, g.len));
         for (const auto &sg : hp.seg) {

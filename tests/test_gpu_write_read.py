@@ -67,14 +67,19 @@ def test_general_tiles_any_bpc(hdfs, gpu_ctx, orc, bpc):
     and verify against the oracle."""
     torch = _torch()
     rows, off, out = [], 0, 0
+    tails = [4, 5, 100, 508, 509, 511, 513, 1000, 1023, 1025, 4097]  # the tail chunk rides in the last tile
     for i in range(20):
         ln = 65536 - (0 if i % 3 else 777)
+        if i % 3 == 2:
+            ln = 65536 // bpc * bpc - bpc + tails[i % len(tails)] % bpc
         rows.append((off, out, ln, bpc))
         out += (ln + bpc - 1) // bpc
         off += ln + (i % 16) + 1
     pk = np.array(rows, hdfs.PACKET_DTYPE)
     tiles, gen = hdfs.debug_plan(pk)
     assert np.any(tiles["meta"] & 0x80000000)
+    if 16 <= bpc <= 7680:  # (8191: a 16-block chunk leaves a tile no room)
+        assert np.any(tiles["src"] >> np.uint64(48))  # tails in tiles
     payload = oracle.xorshift64_bytes(off + 64, 3000 + bpc)
     payload[:bpc * 2] = 0  # a zero chunk
     want = orc.batch(payload, pk, out)

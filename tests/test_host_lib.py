@@ -206,20 +206,21 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
     got = np.full(n, 0xDEADBEEF, np.uint32)
     seen = np.zeros(n, np.int32)
     for t in tiles:
-        meta = int(t["meta"])
+        meta, src, tl = int(t["meta"]), int(t["src"]) & ((1 << 48) - 1), int(t["src"]) >> 48
         if meta & 0x80000000:  # general tile: nch chunks of any bpc in [4, 8192], k virtual blocks each
             k, nch, pad = (meta >> 8) & 31, (meta >> 13) & 31, (meta >> 18) & 511
-            bpc = k * 512 - pad
-            assert meta & 0xFF == nch * k <= 16 and nch >= 1 and 4 <= bpc <= 8192 and pad < 512
+            bpc, kt = k * 512 - pad, (tl + 511) // 512
+            assert meta & 0xFF == nch * k + kt <= 16 and nch >= 1 and 4 <= bpc <= 8192 and pad < 512
             assert bpc & (bpc - 1) or bpc < 512  # powers of two >= 512 take the power-of-two tiles
-            assert pad == 0 or int(t["src"]) >= 16  # padded loads start up to 15 bytes early
+            assert pad == 0 or src >= 16  # padded loads start up to 15 bytes early
+            assert tl == 0 or 4 <= tl < bpc  # a packet's tail chunk after the full ones
         else:
             nb, lg = meta & 0xFF, (meta >> 8) & 0xFF
-            assert 1 <= nb <= 16 and nb % (1 << lg) == 0  # any alignment (unaligned tile loads)
+            assert 1 <= nb <= 16 and nb % (1 << lg) == 0 and tl == 0  # any alignment (unaligned tile loads)
             bpc, nch = 512 << lg, nb >> lg
-        for c in range(nch):
-            s = int(t["src"]) + c * bpc
-            got[int(t["out"]) + c] = orc.crc32c(payload[s:s + bpc])
+        for c in range(nch + (1 if tl else 0)):
+            s = src + c * bpc
+            got[int(t["out"]) + c] = orc.crc32c(payload[s:s + (bpc if c < nch else tl)])
             seen[int(t["out"]) + c] += 1
     for g in gen:
         s = int(g["src"])
