@@ -63,13 +63,16 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             plan->tiles.push_back(t);
         }
     } else if (p.bpc >= 4 && p.bpc <= kMaxTileBpc) {
-        // General tiles: 16 / k chunks of k virtual blocks each.  A padded
-        // tile's first loads start up to 15 bytes before its first chunk
-        // (masked to zero): allowed when those bytes are in the same
-        // allocation (offset >= 16) or, for device addresses, the same page.
+        // General items: up to 16 chunks of k virtual blocks each, processed
+        // as 16-block subtiles (a chunk may span two).  A padded item's
+        // first loads start up to 15 bytes before its first chunk (masked to
+        // zero): allowed when those bytes are in the same allocation
+        // (offset >= 16) or, for device addresses, the same page.
         const uint32_t k = (p.bpc + kBlockBytes - 1) / kBlockBytes;
         const uint32_t pad = k * kBlockBytes - p.bpc;
-        const uint64_t per = kTileBlocks / k;
+        // (k dividing 16: whole chunks fill subtiles exactly, and one subtile
+        // per item keeps the item loop out of the way)
+        const uint64_t per = kTileBlocks % k == 0 ? kTileBlocks / k : kGeneralChunks;
         for (uint64_t c = 0; c < nfull;) {
             const uint64_t src = p.payload_off + c * p.bpc;
             if (pad && !(absolute ? (src & 4095u) >= 16 : src >= 16)) {
@@ -82,11 +85,11 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             t.src = src;
             t.out = uint32_t(p.out_idx + c);
             t.meta = general_meta(uint32_t(nch), k, pad);
-            // The packet's tail chunk rides in its last tile when it fits:
-            // it starts right after the tile's full chunks, so its loads
-            // never reach before the packet.
+            // The packet's tail chunk rides in its last item: it starts
+            // right after the item's full chunks, so its loads never reach
+            // before the packet.
             const uint32_t kt = (tail + kBlockBytes - 1) / kBlockBytes;
-            if (c + nch == nfull && tail >= 4 && nch * k + kt <= kTileBlocks) {
+            if (c + nch == nfull && tail >= 4) {
                 t.src |= uint64_t(tail) << 48;
                 t.meta = general_meta(uint32_t(nch), k, pad, kt);
                 tail_done = true;

@@ -8,13 +8,15 @@
 //    one wave-tile) of FULL chunks of one packet whose bpc is 512 << lg
 //    (lg = 0..4), at any alignment.  A tile never straddles a chunk, so a
 //    wave finishes every chunk it starts.
-//  * FastTile, general form (meta bit 31): up to 16 / k FULL chunks of one
-//    packet with any other bpc in [4, 8192], k = ceil(bpc / 512) virtual
-//    512-byte blocks per chunk.  Each chunk is right-aligned into its k
-//    blocks (pad = 512 k - bpc leading zero bytes, which do not change the
-//    CRC's linear part), so every block is a whole 512-byte load.  The last
-//    general tile of a packet also carries the packet's short tail chunk
-//    (tl >= 4 bytes, kt = ceil(tl / 512) more blocks) when it has room.
+//  * FastTile, general form (meta bit 31): a general item of up to 16 FULL
+//    chunks of one packet with any other bpc in [4, 8192], k = ceil(bpc /
+//    512) virtual 512-byte blocks per chunk.  Each chunk is right-aligned
+//    into its k blocks (pad = 512 k - bpc leading zero bytes, which do not
+//    change the CRC's linear part), so every block is a whole 512-byte
+//    load.  The last item of a packet also carries the packet's short tail
+//    chunk (tl >= 4 bytes, kt = ceil(tl / 512) more blocks).  One wave runs
+//    the item's nch k + kt blocks as consecutive 16-block subtiles, so a
+//    chunk may span two subtiles (bpc 1536: 16 chunks in exactly 3).
 //  * GenItem: one chunk of any length / alignment (the short tail chunk of a
 //    packet, or every chunk whose bpc fits neither tile form), processed by
 //    half a wave.
@@ -44,15 +46,16 @@ struct FastTile {
     uint64_t src;
     uint32_t out;   // checksum index of the tile's first chunk
     // power-of-two form: bits 0-7 = blocks in tile (1..16), bits 8-15 = lg = log2(bpc / 512);
-    // general form: bit 31, bits 0-7 = blocks (nch * k + kt), bits 8-12 = k, bits 13-17 = nch (full chunks
-    //               in the tile), bits 18-26 = pad = 512 k - bpc
+    // general form: bit 31, bits 0-7 = subtiles ceil((nch * k + kt) / 16), bits 8-12 = k, bits 13-17 = nch
+    //               (full chunks in the item, 1..16), bits 18-26 = pad = 512 k - bpc
     uint32_t meta;
 };
 static_assert(sizeof(FastTile) == 16, "FastTile is 16 bytes");
 constexpr uint64_t kSrcMask = (1ull << 48) - 1;
+constexpr uint32_t kGeneralChunks = 16;  // full chunks per general item
 
 inline uint32_t general_meta(uint32_t nch, uint32_t k, uint32_t pad, uint32_t kt = 0) {
-    return kGeneralTile | (nch * k + kt) | (k << 8) | (nch << 13) | (pad << 18);
+    return kGeneralTile | ((nch * k + kt + kTileBlocks - 1) / kTileBlocks) | (k << 8) | (nch << 13) | (pad << 18);
 }
 
 struct GenItem {

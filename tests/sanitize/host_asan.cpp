@@ -166,7 +166,7 @@ void plans_and_framing(std::mt19937_64 &rng) {
                 const uint32_t k = (meta >> 8) & 31u, pad = (meta >> 18) & 511u;
                 nch = (meta >> 13) & 31u;
                 bpc = k * 512u - pad;
-                CHECK(nch >= 1 && nch * k + kt <= 16 && (meta & 0xffu) == nch * k + kt && bpc >= 4,
+                CHECK(nch >= 1 && nch <= 16 && (meta & 0xffu) == (nch * k + kt + 15) / 16 && bpc >= 4,
                       "general tile meta %x", meta);
                 CHECK(pad == 0 || src >= 16, "padded tile too close to the payload start");
                 CHECK(tl == 0 || (tl >= 4 && tl < bpc), "tail chunk length %u", tl);

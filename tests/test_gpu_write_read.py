@@ -94,6 +94,36 @@ def test_general_tiles_any_bpc(hdfs, gpu_ctx, orc, bpc):
     plan.close()
 
 
+@pytest.mark.parametrize("bpc", [100, 1000, 1536, 2560, 3000, 5000, 7000])
+def test_general_items_subtile_spans(hdfs, gpu_ctx, orc, bpc):
+    """Every chunk count 1..17 of a general item with tails of every block
+    count, so that full chunks and the tail chunk start, end and span 16-block
+    subtile boundaries at every position (padded and unpadded); one batch,
+    exec and verify against the oracle."""
+    torch = _torch()
+    rows, off, out = [], 64, 0
+    for nfull in range(1, 18):
+        for tl in (0, 4, 100, 509, 511, 513, 1000, 1283, 1532, 2047, 4100, 6000):
+            if tl >= bpc:
+                continue
+            ln = nfull * bpc + tl
+            rows.append((off, out, ln, bpc))
+            out += (ln + bpc - 1) // bpc
+            off += ln + (1 if nfull % 5 == 0 else 16 - ln % 16)
+    pk = np.array(rows, hdfs.PACKET_DTYPE)
+    tiles, gen = hdfs.debug_plan(pk)
+    assert np.any(tiles["src"] >> np.uint64(48)) and np.any((tiles["meta"] & 0xFF) > 1)
+    payload = oracle.xorshift64_bytes(off + 64, 4000 + bpc)
+    want = orc.batch(payload, pk, out)
+    dev = torch.from_numpy(payload).cuda()
+    stream = torch.cuda.current_stream()
+    plan = hdfs.Plan(gpu_ctx, pk)
+    got = _run_plan(plan, out, stream, dev.data_ptr())
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:10]
+    assert _verify(plan, want, stream, dev.data_ptr()) == [0, 0xFFFFFFFF]
+    plan.close()
+
+
 def test_general_tiles_device_addresses_near_page_start(hdfs, gpu_ctx, orc):
     """CRC32C_DEVICE_ADDRESSES plans with padded general tiles: packets
     starting 0..20 bytes into a fresh allocation (padded tiles load up to 15

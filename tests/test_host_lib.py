@@ -210,7 +210,7 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
         if meta & 0x80000000:  # general tile: nch chunks of any bpc in [4, 8192], k virtual blocks each
             k, nch, pad = (meta >> 8) & 31, (meta >> 13) & 31, (meta >> 18) & 511
             bpc, kt = k * 512 - pad, (tl + 511) // 512
-            assert meta & 0xFF == nch * k + kt <= 16 and nch >= 1 and 4 <= bpc <= 8192 and pad < 512
+            assert meta & 0xFF == (nch * k + kt + 15) // 16 and 1 <= nch <= 16 and 4 <= bpc <= 8192 and pad < 512
             assert bpc & (bpc - 1) or bpc < 512  # powers of two >= 512 take the power-of-two tiles
             assert pad == 0 or src >= 16  # padded loads start up to 15 bytes early
             assert tl == 0 or 4 <= tl < bpc  # a packet's tail chunk after the full ones
