@@ -60,6 +60,13 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             t.src = p.payload_off + b * kBlockBytes;
             t.out = uint32_t(p.out_idx + (b >> lg));
             t.meta = uint32_t(nb) | (uint32_t(lg) << 8);
+            if (b + nb == blocks && tail >= 4) {
+                // the packet's short tail chunk rides behind its last chunks:
+                // that tile becomes a general item (k = 2^lg, no pad)
+                t.src |= uint64_t(tail) << 48;
+                t.meta = general_meta(uint32_t(nb >> lg), 1u << lg, 0, (tail + kBlockBytes - 1) / kBlockBytes);
+                tail_done = true;
+            }
             plan->tiles.push_back(t);
         }
     } else if (p.bpc >= 4 && p.bpc <= kMaxTileBpc) {

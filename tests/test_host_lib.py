@@ -211,7 +211,8 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
             k, nch, pad = (meta >> 8) & 31, (meta >> 13) & 31, (meta >> 18) & 511
             bpc, kt = k * 512 - pad, (tl + 511) // 512
             assert meta & 0xFF == (nch * k + kt + 15) // 16 and 1 <= nch <= 16 and 4 <= bpc <= 8192 and pad < 512
-            assert bpc & (bpc - 1) or bpc < 512  # powers of two >= 512 take the power-of-two tiles
+            assert bpc & (bpc - 1) or bpc < 512 or tl  # powers of two >= 512: power-of-two tiles, but the
+            #                                           last one of a packet with a tail chunk is general
             assert pad == 0 or src >= 16  # padded loads start up to 15 bytes early
             assert tl == 0 or 4 <= tl < bpc  # a packet's tail chunk after the full ones
         else:
@@ -235,8 +236,10 @@ def test_plan_fast_path_shapes(hdfs):
     assert tiles.size == 4096 * 8 and gen.size == 0 and np.all(tiles["meta"] == 16)
     tiles, gen = hdfs.debug_plan(oracle.mixed_packets(3))
     assert list(tiles["meta"][:1]) == [16] and set(int(m) >> 8 for m in tiles["meta"]) == {0, 1, 3}
-    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65436))
-    assert gen.size == 1 and int(gen["len"][0]) == 65436 % 512
+    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65436))  # the tail rides in the last tile
+    assert gen.size == 0 and int(tiles["src"][-1]) >> 48 == 65436 % 512 and int(tiles["meta"][-1]) >> 31
+    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65539))  # a 3-byte tail: general path
+    assert gen.size == 1 and int(gen["len"][0]) == 3
 
 
 @pytest.fixture(scope="module")
