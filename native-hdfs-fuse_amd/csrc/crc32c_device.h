@@ -92,6 +92,8 @@ constexpr int kModeS4H = 128;       // A/B: half-column S4 image (64 KiB of T ta
 constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
 constexpr int kModeEarly = 1024;    // the first tile's loads are issued before the table staging
 constexpr int kModeItemsFirst = 2048;  // gen / seg / const items before the tiles instead of after
+constexpr int kModeQuarter = 4096;  // small batches: power-of-two tiles of chunks <= 2 KiB run as 4 work
+                                    // units of 4 blocks each (4x the waves, 1/4 of each wave's latency chain)
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
 
@@ -581,11 +583,11 @@ __device__ __forceinline__ uint4 chunk_start_mask(uint4 d, int m) {
 // lin() of a tile's 8 pieces (instruction i's 16 bytes per lane), each
 // piece first passed through prep(i, piece) (general tiles: the chunk-start
 // masks), so that piece i's lookups start as soon as its own load is back.
-template <int DIAG, bool S4, int IMG, typename Prep>
+template <int DIAG, bool S4, int IMG, typename Prep, int NP = 8>
 __device__ __forceinline__ void tile_pieces(const uint8_t *lds, uint4 v[8], uint32_t pc[8], int lane, Prep prep) {
     const LaneCols cols = lane_cols<IMG>(uint32_t(lane & 31));
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < NP; ++i) {
         prep(i, v[i]);
         pc[i] = piece<S4, DIAG, IMG>(lds, v[i], cols);
         opaque(pc[i]);
@@ -748,6 +750,63 @@ __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane,
         load_tile<AUX, COMPDIAG, VERIFY>(p, t, lane, v, ev);
 }
 
+// ---- quarter units (kModeQuarter): blocks 4u .. 4u + 3 of a tile ---------
+// A small batch leaves most of the chip's waves idle and each busy wave's
+// load -> 8 chained pieces -> reduce latency is the launch.  Unit j of a
+// launch is quarter u = j & 3 of tile j >> 2: for power-of-two chunks of at
+// most 4 blocks (bpc <= 2048) a quarter holds whole chunks, so it is an
+// ordinary tile of <= 4 blocks, loaded by 2 instructions and looked up as 2
+// pieces per lane.  General items and tiles of longer chunks run whole as
+// unit 0 of their tile (units 1-3 are empty).
+// Returns 0 (empty unit), 1 (a whole tile / item in ft) or 2 (a quarter in ft).
+template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL>
+__device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane, FastTile &ft, uint4 v[8],
+                                         uint32_t &ev) {
+    const FastTile x = tile_at(p, j >> 2);
+    const uint32_t u = j & 3u;
+    const uint32_t lg = (x.meta >> 8) & 0xffu;
+    if ((GENERAL && (x.meta & kGeneralTile)) || lg > 2) {
+        if (u) return 0;
+        ft = x;
+        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+        return 1;
+    }
+    const uint32_t nb = x.meta & 0xffu;
+    if (4u * u >= nb) return 0;
+    ft.src = x.src + 2048u * u;
+    ft.out = x.out + ((4u * u) >> lg);
+    ft.meta = min(nb - 4u * u, 4u) | (lg << 8);
+    if (COMPDIAG) {
+        load_tile<AUX, true, false>(p, ft, lane, v, ev);
+        return 2;
+    }
+    const uint32_t nbq = ft.meta & 0xffu;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + ft.src), 0, int(nbq * 512u), 0x00020000);
+    const uint32_t voff = 16u * uint32_t(lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
+        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+    if (VERIFY) {
+        const uint32_t blk = rep_block(lane);
+        if (rep_lane(lane, blk, nbq, lg)) ev = p.expect[ft.out + (blk >> lg)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    return 2;
+}
+
+template <int DIAG, bool S4, bool VERIFY, int IMG>
+__device__ __forceinline__ void finish_quarter(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                               uint4 v[8], uint32_t ev, int lane) {
+    uint32_t pc[8];
+    tile_pieces<DIAG, S4, IMG, NoPrep, 2>(lds, v, pc, lane, NoPrep{});
+#pragma unroll
+    for (int i = 2; i < 8; ++i) pc[i] = 0;  // blocks 4..15: none
+    reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
+}
+
 // One tile index from the workgroup's LDS counter (one ds_add_rtn per wave).
 __device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
     uint32_t t = 0;
@@ -901,6 +960,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool ITEMSFIRST = !EARLY && (MODE & kModeItemsFirst) != 0;
+    constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = !S4 ? kStageBytes : C ? kS4CStageBytes : kS4StageBytes;
@@ -921,8 +981,10 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
 
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
-    const uint32_t tbeg = uint32_t((uint64_t(p.ntiles) * blockIdx.x) / gridDim.x);
-    const uint32_t tend = uint32_t((uint64_t(p.ntiles) * (blockIdx.x + 1)) / gridDim.x);
+    // (QUARTER: units, 4 per tile)
+    const uint64_t nunits = QUARTER ? 4ull * p.ntiles : uint64_t(p.ntiles);
+    const uint32_t tbeg = uint32_t((nunits * blockIdx.x) / gridDim.x);
+    const uint32_t tend = uint32_t((nunits * (blockIdx.x + 1)) / gridDim.x);
     if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
     if (threadIdx.x == 0) {
         *pool_ctr = tbeg + kWaves;
@@ -935,14 +997,20 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     FastTile ft{0, 0, 0};
     uint4 v[8];
     uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
+    int kind = 1;     // QUARTER: what load_unit found (0 empty, 1 tile / item, 2 quarter)
+    auto load_next = [&](uint32_t j) {
+        if (QUARTER) {
+            kind = load_unit<AUX, COMPDIAG, VERIFY, GENERAL>(p, j, lane, ft, v, ev);
+        } else {
+            ft = tile_at(p, j);
+            load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+        }
+    };
     // EARLY: the first tile's loads go out before the staging (their latency
     // overlaps it).  Measured slower for large batches -- 3072 waves x 8 KiB
     // in flight queue the 152 KiB staging DMA behind them -- so only the
     // small-batch kernel (compact image, 28 KiB) does it.
-    if (EARLY && t < tend) {
-        ft = tile_at(p, t);
-        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
-    }
+    if (EARLY && t < tend) load_next(t);
     // Stage the tables by LDS-DMA (1 KiB per wave instruction, no VGPRs); a
     // launch of constant runs only needs none.
     const bool tables = (p.ntiles | p.ngen | p.nseg) != 0;
@@ -990,16 +1058,15 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     };
     if (ITEMSFIRST) items();
 
-    if (!EARLY && t < tend) {
-        ft = tile_at(p, t);
-        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
-    }
+    if (!EARLY && t < tend) load_next(t);
     while (t < tend) {
-        finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GENERAL>(p, lds, vacc, ft, v, ev, lane);
+        if (!QUARTER || kind == 1)
+            finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GENERAL>(p, lds, vacc, ft, v, ev, lane);
+        else if (kind == 2)
+            finish_quarter<DIAG, S4, VERIFY, IMG>(p, lds, vacc, ft, v, ev, lane);
         t = pool_grab(pool_ctr, lane);
         if (t >= tend) break;
-        ft = tile_at(p, t);
-        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+        load_next(t);
     }
     if (!ITEMSFIRST) items();
     if (VERIFY) {
@@ -1021,8 +1088,9 @@ namespace hdfs_crc {
 // Grid of a launch: one workgroup per CU, or one per work item when there
 // are fewer items than CUs (a small batch leaves most waves without a tile;
 // they still share the table staging, which is what bounds a small launch).
-inline uint32_t production_grid(const KParams &p, uint32_t num_cu) {
-    const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
+inline uint32_t production_grid(const KParams &p, uint32_t num_cu, bool quarter = false) {
+    const uint64_t items = uint64_t(p.ntiles) * (quarter ? 4 : 1) + (uint64_t(p.ngen) + 1) / 2 +
+                           (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     return uint32_t(items < num_cu ? (items ? items : 1) : num_cu);
 }
 }  // namespace hdfs_crc

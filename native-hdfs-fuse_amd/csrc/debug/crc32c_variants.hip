@@ -48,6 +48,11 @@ constexpr Variant kVariants[] = {
     {48, "s4c_nt_early_prodgrid", 768, 1, true, true},     // 41, first tile's loads before the staging
     {49, "s4_nt_general_prodgrid", 768, 1, true, true},    // the full-image production build, any batch size
     {50, "s4_nt_itemsfirst_prodgrid", 768, 1, true, true},  // 49 with gen / seg / const items before the tiles
+    {51, "s4c_nt_quarter_prodgrid", 768, 1, true, true},   // 41 with quarter units (4 per tile)
+    {52, "s4c_nt_quarter_early_prodgrid", 768, 1, true, true},  // 51, first unit's loads before the staging
+    {53, "s4_nt_quarter_prodgrid", 768, 1, true, true},    // 49 (full image) with quarter units
+    {54, "s4c_nt_quarter_stamps_prodgrid", 768, 1, true, true},  // 51 with per-wave timestamps
+    {55, "s4c_nt_quarter_early_stamps_prodgrid", 768, 1, true, true},  // 52 with per-wave timestamps
 };
 
 const Variant *find(int v) {
@@ -61,7 +66,8 @@ const Variant *find(int v) {
 hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
-    uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu) : (items + waves - 1) / waves;
+    const bool quarter = v.id >= 51 && v.id <= 55;
+    uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, quarter) : (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
@@ -88,6 +94,11 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 48: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeEarly); break;
     case 49: HDFS_LAUNCH(768, 3, kS4Nt); break;
     case 50: HDFS_LAUNCH(768, 3, kS4Nt | kModeItemsFirst); break;
+    case 51: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter); break;
+    case 52: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeEarly); break;
+    case 53: HDFS_LAUNCH(768, 3, kS4Nt | kModeQuarter); break;
+    case 54: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeStamps); break;
+    case 55: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeEarly | kModeStamps); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
