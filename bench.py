@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak (default): every rank checksums its own config batch; strong: the config-2/5 batch's "
                          "packets are split evenly over the ranks (SURVEY.md section 8e)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="issue the timed launches one by one from Python instead of replaying them from a graph")
     ap.add_argument("--two-streams", action="store_true",
                     help="also time 1000 batches alternated over two streams (their launches overlap, so a "
                          "rocprofv3 run of the bench would average overlapped durations: off by default)")
@@ -280,12 +282,13 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
 
-    def step(i):
+    def step(i, sp=None):
         b = i % nbuf
+        sp = sptr if sp is None else sp
         if c4:
-            mplan.exec([bufs[b].data_ptr()], root_out.data_ptr() if rank == 0 else 0, [sptr])
+            mplan.exec([bufs[b].data_ptr()], root_out.data_ptr() if rank == 0 else 0, [sp])
         else:
-            plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sptr)
+            plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sp)
 
     # correctness gate (outside the timed region): every buffer-0 checksum
     # (config 4: the whole file's, gathered on rank 0)
@@ -302,6 +305,23 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    # The K timed steps are captured once into a HIP graph and replayed:
+    # each step is still one launch of the plan over one batch, but the
+    # launches are issued by the GPU's command processor instead of one
+    # Python -> ctypes -> hipLaunchKernel call each (~4.1 us per launch on
+    # the host, which bounds one-block batches: DESIGN.md section 5).  The
+    # host-issued rate is reported beside it (eager_ms_per_step).  Config 4's
+    # step holds RCCL calls and stays host-issued.
+    use_graph = not c4 and not args.no_graph
+    graph = None
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            cap = torch.cuda.current_stream(dev).cuda_stream
+            for i in range(args.steps):
+                step(i, cap)
+        graph.replay()  # (first replay uploads the graph)
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -309,8 +329,11 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for i in range(args.steps):
-        step(i)
+    if use_graph:
+        graph.replay()
+    else:
+        for i in range(args.steps):
+            step(i)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -319,6 +342,17 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)  # avg per launch, on the launch stream
+    eager_ms = None
+    if use_graph:  # the same steps issued one by one from the host, for comparison
+        ne = min(args.steps, 500)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(ne):
+            step(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        eager_ms = e0.elapsed_time(e1) / ne
 
     cdev = dev if backend == "nccl" else torch.device("cpu")  # where collectives run
     if world > 1:
@@ -524,6 +558,9 @@ def main():
             "two_streams": two_streams,
             "box_read_probe": read_probe,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+            "launch": ("hip graph of the %d timed launches, replayed" % args.steps) if use_graph else
+                      "host-issued, one launch per step",
+            "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 5),
         }
         print(json.dumps(line), flush=True)
     if c4:

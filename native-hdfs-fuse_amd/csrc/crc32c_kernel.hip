@@ -8,8 +8,13 @@
 //   * full image, power-of-two tiles only: the bulk path (config 2);
 //   * full image with the general-tile code (bpc outside 512 * 2^k);
 //   * compact image (28 KiB staged instead of 152 KiB, with the general-tile
-//     code): batches of at most kSmallBatchItems work items, where the table
-//     staging is most of a launch (one 4 MiB block: 5.8 -> 5.2 us).
+//     code): batches of at most kSmallBatchItemsPerCu work items per CU,
+//     where the table staging is most of a launch (one 4 MiB block: 5.8 ->
+//     5.2 us);
+//   * the same with quarter units (each tile split over 4 waves, 2 pieces
+//     per lane): batches of at most kQuarterTilesPerCu tiles per CU, where
+//     one wave's load -> lookups chain is the launch (one 4 MiB block,
+//     graph-replayed: 4.36 -> 3.71 us).
 // A/B and diagnostic variants are built only into libhdfs_crc32c_debug.so
 // (debug/crc32c_variants.hip).
 #include "crc32c_device.h"
@@ -22,6 +27,10 @@ namespace {
 // once every CU has several tiles the full image's faster lookups pay back
 // its staging (small batches).
 constexpr uint64_t kSmallBatchItemsPerCu = 8;
+// Tiles per CU up to which quarter units win (tools/launch_probe.py,
+// profiles/r02/launch_probe_crossover.json: 512 tiles 3.71 vs 4.36 us, 768
+// tiles 4.24 vs 4.72, 1024 tiles 5.56 vs 4.95).
+constexpr uint64_t kQuarterTilesPerCu = 3;
 }  // namespace
 
 hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream) {
@@ -29,19 +38,25 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     constexpr int kProd = kModeS4 | kModeNt;
     constexpr int kGen = kModeGeneral;
     constexpr int kSmall = kModeS4C | kModeGeneral;
-    const dim3 g{production_grid(p, num_cu), 1, 1}, b{768, 1, 1};
+    constexpr int kQuarter = kSmall | kModeQuarter;
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const bool small = items <= kSmallBatchItemsPerCu * num_cu;
+    const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
+    const dim3 g{production_grid(p, num_cu, quarter), 1, 1}, b{768, 1, 1};
     if (p.expect) {
         if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
-        if (small)
+        if (quarter)
+            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>), g, b, 0, stream, p);
+        else if (small)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>), g, b, 0, stream, p);
         else if (p.general)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeVerify>), g, b, 0, stream, p);
         else
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeVerify>), g, b, 0, stream, p);
     } else {
-        if (small)
+        if (quarter)
+            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>), g, b, 0, stream, p);
+        else if (small)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>), g, b, 0, stream, p);
         else if (p.general)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen>), g, b, 0, stream, p);
