@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Per-launch durations of one kernel from a rocprofv3 kernel trace
 (run_kernel_trace.csv), averaged over bench.py's timed window: launch 0 is
-the correctness gate, then `--warmup` warm-up launches, then `--steps` timed
-ones.  Writes the window's average / median / min / max (ns) so it can be
+the correctness gate, then `--warmup` warm-up launches, then (graph-replayed
+bench, the default) one untimed replay of the `--steps` captured launches,
+then the `--steps` timed ones.  Writes the window's average / median / min / max (ns) so it can be
 compared with bench.py's own HIP-event average for the same run.
 
     python tools/trace_window.py gpurun_out/prof/run_kernel_trace.csv \
@@ -23,14 +24,16 @@ def main():
     ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--out")
+    ap.add_argument("--no-graph", action="store_true", help="the bench ran with --no-graph (no untimed replay)")
     args = ap.parse_args()
     rows = [r for r in csv.DictReader(open(args.trace)) if args.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-    win = dur[1 + args.warmup:1 + args.warmup + args.steps]
-    starts = [int(r["Start_Timestamp"]) for r in rows[1 + args.warmup:1 + args.warmup + args.steps]]
+    first = 1 + args.warmup + (0 if args.no_graph else args.steps)
+    win = dur[first:first + args.steps]
+    starts = [int(r["Start_Timestamp"]) for r in rows[first:first + args.steps]]
     res = {
-        "kernel": args.kernel, "launches_in_trace": len(dur), "window": [1 + args.warmup, 1 + args.warmup + len(win)],
+        "kernel": args.kernel, "launches_in_trace": len(dur), "window": [first, first + len(win)],
         "window_avg_ns": round(statistics.mean(win), 1), "window_median_ns": statistics.median(win),
         "window_min_ns": min(win), "window_max_ns": max(win),
         "window_span_per_launch_ns": round((starts[-1] - starts[0]) / max(len(starts) - 1, 1), 1),
