@@ -568,16 +568,20 @@ __device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
 // Chunk bytes before position 0 of the lane's dwords -> 0, chunk bytes 0..3
 // ^= 0xff (the register pre-inversion of crc32c.c:237 moved into the data).
 // m = position in the lane's 16 bytes where the chunk starts (may be < 0).
+// Dword j's bytes with index < m - 4 j is M_j = 0xffffffff >> (32 - 8 c),
+// c = clamp(m - 4 j, 0, 4): one 64-bit shift of 0x00000000ffffffff by
+// clamp(32 - 8 (m - 4 j), 0, 32).  Dword k keeps its bytes outside M_k and
+// XORs 0xff into M_{k-1} & ~M_k (the bytes m .. m + 3): ~M_k & (w ^ M_{k-1}),
+// one v_bitop3.
+__device__ __forceinline__ uint32_t bytes_below(int s) {  // s = 32 - 8 (m - 4 j), any value
+    const int c = min(max(s, 0), 32);
+    return uint32_t(0xffffffffull >> c);
+}
 __device__ __forceinline__ uint4 chunk_start_mask(uint4 d, int m) {
-    uint32_t w[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int dm = m - 4 * k;
-        const uint32_t lo = bytes_mask(dm);
-        const uint32_t ff = bytes_mask(dm + 4) & ~lo;
-        w[k] = (w[k] & ~lo) ^ ff;
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    const int s = 32 - 8 * m;
+    const uint32_t mm1 = bytes_below(s - 32), m0 = bytes_below(s), m1 = bytes_below(s + 32),
+                   m2 = bytes_below(s + 64), m3 = bytes_below(s + 96);
+    return make_uint4(~m0 & (d.x ^ mm1), ~m1 & (d.y ^ m0), ~m2 & (d.z ^ m1), ~m3 & (d.w ^ m2));
 }
 
 // lin() of a tile's 8 pieces (instruction i's 16 bytes per lane), each
