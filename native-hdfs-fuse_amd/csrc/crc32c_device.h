@@ -623,7 +623,8 @@ __device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g,
             const int pcl = int(((th >> (2 * i)) & 1u) ? g.padt : g.pad);
             const bool first = (sth >> (2 * i)) & 1u, second = (s2h >> (2 * i)) & 1u;
             const int m = first ? pcl - int(16u * q) : pcl - 512 - int(16u * q);
-            if ((first || (second && q == 0)) && m > -4 && m < 16) x = chunk_start_mask(x, m);
+            // (branch-free: m = -64 leaves the piece as it is)
+            x = chunk_start_mask(x, (first || (second && q == 0)) ? m : -64);
         });
     } else {
         const uint32_t sth = q == 0 ? gs.start >> h : 0u;
