@@ -543,7 +543,8 @@ __device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, con
         const uint32_t d = g.pad * (gs.before + __builtin_popcount(gs.sfull & ((upto << (2 * i)) - 1u))) +
                            (tail ? g.padt : 0u);
         const bool skip = !((vh >> (2 * i)) & 1u) || (((sth >> (2 * i)) & 1u) && qs <= pc);
-        const uint32_t voff = skip ? 0x80000000u : base + 1024u * i - d;
+        // (bit 31: past any descriptor range -- arithmetic, so no branch around the offset math)
+        const uint32_t voff = (base + 1024u * i - d) | (uint32_t(skip) << 31);
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
