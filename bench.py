@@ -388,10 +388,10 @@ def main():
         res = torch.zeros(2, dtype=torch.int32, device=dev)
         for i in range(50):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
+        nv = 200  # (even: a plan's verify launches alternate between two scratch slots)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        nv = 200
         for i in range(nv):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         e1.record(stream)
@@ -399,7 +399,31 @@ def main():
         r = res.cpu().numpy().view(np.uint32)
         verify = {"gib_s": round(nbytes * nv / (e0.elapsed_time(e1) * 1e-3) / GIB, 1),
                   "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
-                  "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF)}
+                  "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF),
+                  "launch": "host-issued"}
+        vgraph = None
+        if use_graph:  # also replayed from a graph like the timed exec steps
+            # A plan orders its verify launches across streams with an event
+            # wait when the stream changes; one launch on the capture stream
+            # first keeps that wait out of the capture.
+            cs = torch.cuda.Stream(device=dev)
+            torch.cuda.synchronize()
+            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), cs.cuda_stream)
+            torch.cuda.synchronize()
+            vgraph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(vgraph, stream=cs):
+                for i in range(nv):
+                    plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), cs.cuda_stream)
+            vgraph.replay()
+            torch.cuda.synchronize()
+            e0.record(stream)
+            vgraph.replay()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            r = res.cpu().numpy().view(np.uint32)
+            verify["graph_kernel_avg_us"] = round(e0.elapsed_time(e1) / nv * 1e3, 2)
+            verify["graph_clean"] = bool(r[0] == 0 and r[1] == 0xFFFFFFFF)
+            verify["clean"] = verify["clean"] and verify["graph_clean"]
 
     # The box's own streaming-read rate over the same rotating buffers, right
     # after the timed region (same power state): a plain grid-stride read

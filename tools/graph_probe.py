@@ -5,7 +5,7 @@ capture through torch.cuda.CUDAGraph, i.e. hipStreamBeginCapture) and
 replayed.  Small batches are launch-bound (a 4 MiB block takes ~5 us, an
 empty-ish kernel ~3.5 us back to back), so this measures what a graph saves.
 
-    python tools/graph_probe.py [--config c3] [--per-graph 100] [--rounds 5]
+    python tools/graph_probe.py [--config c3] [--per-graph 100] [--rounds 5] [--op exec|verify]
 """
 from __future__ import annotations
 
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--replays", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--nbuf", type=int, default=4)
+    ap.add_argument("--op", default="exec", choices=["exec", "verify"])
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -48,10 +49,15 @@ def main():
     s = torch.cuda.Stream(device=dev)
     K = args.per_graph
 
-    def launches(stream):
+    res_buf = torch.zeros(2, dtype=torch.int32, device=dev)
+
+    def launches(stream, op="exec"):
         for i in range(K):
             b = i % args.nbuf
-            plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), stream.cuda_stream)
+            if op == "exec":
+                plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), stream.cuda_stream)
+            else:  # (expected = the checksums the exec launches left in outs)
+                plan.verify(bufs[b].data_ptr(), outs[b].data_ptr(), res_buf.data_ptr(), stream.cuda_stream)
 
     # reference checksums (plain launches), then clear and check the graph's
     with torch.cuda.stream(s):
@@ -59,13 +65,20 @@ def main():
     torch.cuda.synchronize()
     ref = [o.clone() for o in outs]
     graph = torch.cuda.CUDAGraph()
+    if args.op == "verify":
+        with torch.cuda.stream(s):
+            launches(s, "verify")  # (the plan's verify stream is now s: no cross-stream wait in the capture)
+        torch.cuda.synchronize()
     with torch.cuda.graph(graph, stream=s):
-        launches(torch.cuda.current_stream())
-    for o in outs:
-        o.zero_()
+        launches(torch.cuda.current_stream(), args.op)
+    if args.op == "exec":
+        for o in outs:
+            o.zero_()
     graph.replay()
     torch.cuda.synchronize()
     exact = all(torch.equal(a, b) for a, b in zip(ref, outs))
+    if args.op == "verify":
+        exact = exact and res_buf.cpu().tolist() == [0, -1]
 
     def timed(fn):
         e0 = torch.cuda.Event(enable_timing=True)
@@ -81,9 +94,9 @@ def main():
 
     res = {"stream": [], "graph": []}
     for _ in range(args.rounds):
-        res["stream"].append(timed(lambda: launches(s)))
+        res["stream"].append(timed(lambda: launches(s, args.op)))
         res["graph"].append(timed(graph.replay))
-    out = {"config": args.config, "bytes": nbytes, "launches_per_graph": K, "graph_exact": exact}
+    out = {"config": args.config, "op": args.op, "bytes": nbytes, "launches_per_graph": K, "graph_exact": exact}
     for k, v in res.items():
         v = sorted(v)
         out[k] = {"us_per_launch_median": round(v[len(v) // 2], 3), "us_min": round(v[0], 3),
