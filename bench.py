@@ -316,7 +316,9 @@ def main():
     graph = None
     if use_graph:
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        # (thread_local: other threads of the process -- e.g. the process
+        # group's watchdog -- may make CUDA calls while this thread captures)
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             cap = torch.cuda.current_stream(dev).cuda_stream
             for i in range(args.steps):
                 step(i, cap)
@@ -411,7 +413,7 @@ def main():
             plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), cs.cuda_stream)
             torch.cuda.synchronize()
             vgraph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(vgraph, stream=cs):
+            with torch.cuda.graph(vgraph, stream=cs, capture_error_mode="thread_local"):
                 for i in range(nv):
                     plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), cs.cuda_stream)
             vgraph.replay()
