@@ -105,7 +105,52 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     return p;
 }
 
-int upload_plan(const HostPlan &hp, DevicePlan *dp) {
+namespace {
+
+size_t pool_class(size_t bytes) {
+    size_t c = 4096;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+// A block of at least `bytes` from the pool (caller holds ctx->pool_mu).
+int pool_get(crc32c_ctx *ctx, BlockPool &pool, size_t bytes, uint8_t **out, size_t *cap) {
+    const size_t c = pool_class(bytes);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (size_t i = 0; i < pool.free.size(); ++i)
+            if (pool.free[i].second == c) {
+                *out = pool.free[i].first;
+                *cap = c;
+                pool.free[i] = pool.free.back();
+                pool.free.pop_back();
+                return 0;
+            }
+        // Epoch: once enough released blocks wait, one device synchronisation
+        // makes every one of them (in both pools) reusable.
+        if (pass == 0 && ctx->dev_pool.deferred.size() + ctx->host_pool.deferred.size() >= kEpochBlocks) {
+            HIP_TRY(hipDeviceSynchronize());
+            for (BlockPool *bp : {&ctx->dev_pool, &ctx->host_pool}) {
+                bp->free.insert(bp->free.end(), bp->deferred.begin(), bp->deferred.end());
+                bp->deferred.clear();
+            }
+            continue;
+        }
+        break;
+    }
+    uint8_t *p = nullptr;
+    if (pool.pinned)
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&p), c, hipHostMallocDefault));
+    else
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p), c));
+    pool.all.emplace_back(p, c);
+    *out = p;
+    *cap = c;
+    return 0;
+}
+
+}  // namespace
+
+int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     if (hp.tiles.size() > UINT32_MAX || hp.gen.size() > UINT32_MAX || hp.seg.size() > UINT32_MAX ||
         hp.consts.size() > UINT32_MAX)
         return fail(-E2BIG, "batch too large");
@@ -114,27 +159,79 @@ int upload_plan(const HostPlan &hp, DevicePlan *dp) {
     dp->nseg = uint32_t(hp.seg.size());
     dp->nconst = uint32_t(hp.consts.size());
     dp->general = has_general(hp);
-    dp->tiles_off = 0;
+    dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
+    dp->tiles_off = (2 * kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
     dp->seg_off = dp->gen_off + hp.gen.size() * sizeof(GenItem);
     dp->pieces_off = dp->seg_off + hp.seg.size() * sizeof(SegItem);
     dp->consts_off = dp->pieces_off + hp.pieces.size() * sizeof(GenPiece);
     const size_t bytes = dp->consts_off + hp.consts.size() * sizeof(ConstRun);
-    if (!bytes) return 0;
-    std::vector<uint8_t> img(bytes);
-    std::memcpy(img.data() + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
-    std::memcpy(img.data() + dp->gen_off, hp.gen.data(), hp.gen.size() * sizeof(GenItem));
-    std::memcpy(img.data() + dp->seg_off, hp.seg.data(), hp.seg.size() * sizeof(SegItem));
-    std::memcpy(img.data() + dp->pieces_off, hp.pieces.data(), hp.pieces.size() * sizeof(GenPiece));
-    std::memcpy(img.data() + dp->consts_off, hp.consts.data(), hp.consts.size() * sizeof(ConstRun));
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&dp->d), bytes));
-    HIP_TRY(hipMemcpy(dp->d, img.data(), bytes, hipMemcpyHostToDevice));
+    {
+        std::lock_guard<std::mutex> lock(ctx->pool_mu);
+        if (int rc = pool_get(ctx, ctx->dev_pool, bytes, &dp->d, &dp->cap)) return rc;
+        if (int rc = pool_get(ctx, ctx->host_pool, bytes, &dp->h, &dp->hcap)) return rc;
+        if (!ctx->spare_events.empty()) {
+            dp->uploaded = ctx->spare_events.back();
+            ctx->spare_events.pop_back();
+        }
+    }
+    if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDisableTiming));
+    uint8_t *img = dp->h;
+    init_sched_slots(reinterpret_cast<uint32_t *>(img + dp->slots_off));
+    std::memcpy(img + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
+    std::memcpy(img + dp->gen_off, hp.gen.data(), hp.gen.size() * sizeof(GenItem));
+    std::memcpy(img + dp->seg_off, hp.seg.data(), hp.seg.size() * sizeof(SegItem));
+    std::memcpy(img + dp->pieces_off, hp.pieces.data(), hp.pieces.size() * sizeof(GenPiece));
+    std::memcpy(img + dp->consts_off, hp.consts.data(), hp.consts.size() * sizeof(ConstRun));
+    HIP_TRY(hipMemcpyAsync(dp->d, img, bytes, hipMemcpyHostToDevice, ctx->upload_stream));
+    HIP_TRY(hipEventRecord(dp->uploaded, ctx->upload_stream));
+    dp->ready.store(false, std::memory_order_release);
     return 0;
 }
 
-void free_device_plan(DevicePlan *dp) {
-    if (dp->d) (void)hipFree(dp->d);
-    *dp = DevicePlan();
+// Orders a launch on `stream` after the plan's upload: nothing once the
+// upload is known complete; else a stream wait on its event (or, while the
+// stream is being captured into a graph, a host wait: a capture cannot wait
+// on work outside it).
+int plan_ready(DevicePlan *dp, hipStream_t stream) {
+    if (dp->ready.load(std::memory_order_acquire) || !dp->uploaded) return 0;
+    const hipError_t q = hipEventQuery(dp->uploaded);
+    if (q == hipSuccess) {
+        dp->ready.store(true, std::memory_order_release);
+        return 0;
+    }
+    if (q != hipErrorNotReady) HIP_TRY(q);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+        HIP_TRY(hipEventSynchronize(dp->uploaded));
+        dp->ready.store(true, std::memory_order_release);
+        return 0;
+    }
+    HIP_TRY(hipStreamWaitEvent(stream, dp->uploaded, 0));
+    return 0;
+}
+
+void free_device_plan(crc32c_ctx *ctx, DevicePlan *dp) {
+    std::lock_guard<std::mutex> lock(ctx->pool_mu);
+    if (dp->d) ctx->dev_pool.deferred.emplace_back(dp->d, dp->cap);
+    if (dp->h) ctx->host_pool.deferred.emplace_back(dp->h, dp->hcap);
+    if (dp->uploaded) ctx->spare_events.push_back(dp->uploaded);
+    dp->d = dp->h = nullptr;
+    dp->cap = dp->hcap = 0;
+    dp->uploaded = nullptr;
+}
+
+// Context teardown (device idle): every pooled block and spare event.
+void release_pools(crc32c_ctx *ctx) {
+    std::lock_guard<std::mutex> lock(ctx->pool_mu);
+    for (auto &b : ctx->dev_pool.all) (void)hipFree(b.first);
+    for (auto &b : ctx->host_pool.all) (void)hipHostFree(b.first);
+    for (hipEvent_t e : ctx->spare_events) (void)hipEventDestroy(e);
+    ctx->dev_pool = BlockPool();
+    ctx->host_pool = BlockPool();
+    ctx->host_pool.pinned = true;
+    ctx->spare_events.clear();
 }
 
 }  // namespace hdfs_crc
@@ -185,6 +282,7 @@ int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
 
 int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     std::lock_guard<std::mutex> lock(plan->mu);
+    if (int rc = plan_ready(&plan->dp, stream)) return rc;
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
@@ -495,7 +593,8 @@ int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute
     p->abs_base = abs_base;
     p->absolute = absolute;
     DeviceGuard guard(ctx->device);
-    if (int rc = upload_plan(hp, &p->dp)) return rc;
+    if (int rc = upload_plan(ctx, hp, &p->dp)) return rc;
+    p->sched.d = reinterpret_cast<uint32_t *>(p->dp.d + p->dp.slots_off);  // uploaded initialised with the items
     *out = p.release();
     return 0;
 }
@@ -531,6 +630,8 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
+    c->host_pool.pinned = true;
+    HIP_TRY(hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking));
     for (int ty = 0; ty < 2; ++ty) {
         const uint32_t poly = ty ? kPolyIeee : kPoly;
         std::vector<uint8_t> img(kTableAlloc, 0);
@@ -567,6 +668,12 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
             (void)hipStreamSynchronize(ctx->copy_stream);
             (void)hipStreamDestroy(ctx->copy_stream);
         }
+        if (ctx->upload_stream) {
+            (void)hipStreamSynchronize(ctx->upload_stream);
+            (void)hipStreamDestroy(ctx->upload_stream);
+        }
+        (void)hipDeviceSynchronize();  // (plans' launches may still read pooled blocks)
+        release_pools(ctx);
         for (int ty = 0; ty < 2; ++ty) {
             if (ctx->d_table[ty]) (void)hipFree(ctx->d_table[ty]);
             if (ctx->d_table_s4[ty]) (void)hipFree(ctx->d_table_s4[ty]);
@@ -680,8 +787,7 @@ int crc32c_plan_destroy(crc32c_plan *plan) {
     if (!plan) return 0;
     {
         DeviceGuard guard(plan->ctx->device);
-        free_device_plan(&plan->dp);
-        if (plan->sched.d) (void)hipFree(plan->sched.d);
+        free_device_plan(plan->ctx, &plan->dp);  // (the verify slots live in the same block)
         if (plan->last_done) (void)hipEventDestroy(plan->last_done);
     }
     delete plan;

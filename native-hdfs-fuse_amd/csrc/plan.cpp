@@ -181,11 +181,34 @@ int build_write_plan(const crc32c_buffer *buffers, uint32_t n_buffers, uint64_t 
         const uint64_t pos = bufferoffset + sent;  // stream offset of the packet
         const uint64_t nch = (plen + bpc - 1) / bpc;
         if (out + nch > (1ull << 32)) return -E2BIG;
+        const uint64_t nfullp = plen / bpc;  // full-length chunks of the packet
         for (uint64_t c = 0; c < nch; ++c) {
             const uint64_t a = pos + c * bpc;
+            while (bi + 1 < n_buffers && start[bi + 1] <= a) ++bi;
+            // Bulk: the full chunks c .. c + nf - 1 lie wholly inside buffer bi
+            // (O(packets), not O(chunks), for the common case).
+            const uint64_t nf = c < nfullp ? std::min<uint64_t>(nfullp - c, (start[bi + 1] - a) / bpc) : 0;
+            if (nf >= 2) {
+                if (buffers[bi].data) {
+                    const uint64_t addr = uint64_t(uintptr_t(buffers[bi].data)) + (a - start[bi]);
+                    if (in_run && run_buf == bi && c > 0 && run.payload_off + run.len == addr) {
+                        run.len += uint32_t(nf * bpc);
+                    } else {
+                        if (int rc = flush()) return rc;
+                        run = crc32c_packet{addr, out + c, uint32_t(nf * bpc), bpc};
+                        run_buf = bi;
+                        in_run = true;
+                    }
+                } else {
+                    if (int rc = flush()) return rc;
+                    const uint32_t z = zero(bpc);
+                    for (uint64_t k = 0; k < nf; ++k) push_const(plan, out + c + k, z);
+                }
+                c += nf - 1;
+                continue;
+            }
             const uint32_t clen = uint32_t(std::min<uint64_t>(bpc, plen - c * bpc));
             const uint64_t b = a + clen;
-            while (bi + 1 < n_buffers && start[bi + 1] <= a) ++bi;
             // (zero-length buffers are skipped by the loop above)
             if (b <= start[bi + 1]) {  // inside one buffer
                 if (buffers[bi].data) {

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -68,13 +69,32 @@ struct Stage {
     SchedSlots sched;  // this stage's launches are serialised on its stream
 };
 
-// Device copy of a HostPlan's work items, one allocation.
+// Device copy of a HostPlan's work items and its verify scheduler slots, one
+// block of the context's descriptor pool, uploaded asynchronously from a
+// pinned staging block on the context's upload stream (`uploaded`).
 struct DevicePlan {
     uint8_t *d = nullptr;
+    size_t cap = 0;
+    uint8_t *h = nullptr;  // pinned staging of the same image
+    size_t hcap = 0;
+    hipEvent_t uploaded = nullptr;
+    std::atomic<bool> ready{false};  // the upload is known complete: launches need no wait
     uint32_t ntiles = 0, ngen = 0, nseg = 0, nconst = 0;
     bool general = false;  // some tile is a general tile
-    size_t tiles_off = 0, gen_off = 0, seg_off = 0, pieces_off = 0, consts_off = 0;
+    size_t tiles_off = 0, gen_off = 0, seg_off = 0, pieces_off = 0, consts_off = 0, slots_off = 0;
 };
+
+// Blocks of descriptor memory (device) or of its pinned staging (host),
+// recycled instead of freed: hipFree costs ~12 us and hipMemcpy from pageable
+// memory ~15 us, several times a short plan's whole launch.  A released block
+// may still be read by launches in flight, so it is reusable only after the
+// next epoch (a device synchronisation the pool takes once kEpochBlocks
+// blocks wait, instead of the one hipFree took for every plan).
+struct BlockPool {
+    bool pinned = false;
+    std::vector<std::pair<uint8_t *, size_t>> free, deferred, all;
+};
+constexpr size_t kEpochBlocks = 32;
 
 }  // namespace hdfs_crc
 
@@ -93,6 +113,12 @@ struct crc32c_ctx {
     // link, finish together and leave it idle while both stages drain.
     hipStream_t copy_stream = nullptr;
     hdfs_crc::Stage stage[2];
+    // Plan descriptors: pooled device / pinned blocks, the stream their
+    // uploads go on, and spare events (all under pool_mu).
+    std::mutex pool_mu;
+    hdfs_crc::BlockPool dev_pool, host_pool;
+    hipStream_t upload_stream = nullptr;
+    std::vector<hipEvent_t> spare_events;
 };
 
 struct crc32c_plan {
@@ -119,9 +145,12 @@ namespace hdfs_crc {
 
 // Kernel parameters of a plan's launch on (payload, out); checks nothing.
 KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out);
-// Uploads a HostPlan's items to the context's device (into *dp).
-int upload_plan(const HostPlan &hp, DevicePlan *dp);
-void free_device_plan(DevicePlan *dp);
+// Uploads a HostPlan's items (and fresh verify slots) to the context's
+// device (into *dp), asynchronously; plan_ready orders a launch after it.
+int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
+int plan_ready(DevicePlan *dp, hipStream_t stream);
+void free_device_plan(crc32c_ctx *ctx, DevicePlan *dp);
+void release_pools(crc32c_ctx *ctx);
 // Creates a plan object from a built HostPlan (absolute: rebased, base given).
 int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute, uint64_t abs_base,
               crc32c_plan **out);

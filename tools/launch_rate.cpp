@@ -8,12 +8,17 @@
 // (hipEvents around the N launches), device-resident payload.
 //
 //   tools/launch_rate [packets=64] [launches=4000]
-// prints one JSON line.
+//   tools/launch_rate write [iterations=2000]
+// prints one JSON line.  `write`: one FUSE-shaped 4 MiB block write per
+// iteration (TRUNCATE / NULLPADDING / THEDATA / TRAILINGDATA buffers,
+// src/fuse.c:1348-1354) through crc32c_plan_create_buffers -> exec ->
+// stream sync -> destroy: the per-write host cost of the buffer-list path.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "hdfs_crc32c.h"
@@ -26,7 +31,76 @@
         }                                                                  \
     } while (0)
 
+static int write_mode(int iters) {
+    const uint64_t mb4 = 4u << 20;
+    crc32c_ctx *ctx = nullptr;
+    CHECK(crc32c_ctx_create(0, &ctx) == 0);
+    uint8_t *d = nullptr;
+    uint32_t *out = nullptr;
+    CHECK(hipMalloc(reinterpret_cast<void **>(&d), mb4 + 64) == hipSuccess);
+    CHECK(hipMemset(d, 0x3c, mb4 + 64) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&out), 8192 * 4) == hipSuccess);
+    const crc32c_buffer bufs[4] = {{d, 100000}, {nullptr, 300000}, {d + 400000, 3000000},
+                                   {d + 3400017, mb4 - 3400000}};
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    double t_create = 0, t_exec = 0, t_sync = 0, t_destroy = 0;
+    for (int it = -50; it < iters; ++it) {
+        const auto a = std::chrono::steady_clock::now();
+        crc32c_plan *plan = nullptr;
+        CHECK(crc32c_plan_create_buffers(ctx, bufs, 4, 0, mb4, 0, 65536, 512, 0, &plan) == 0);
+        const auto b = std::chrono::steady_clock::now();
+        CHECK(crc32c_plan_exec(plan, nullptr, out, s) == 0);
+        const auto c = std::chrono::steady_clock::now();
+        CHECK(hipStreamSynchronize(s) == hipSuccess);
+        const auto e = std::chrono::steady_clock::now();
+        CHECK(crc32c_plan_destroy(plan) == 0);
+        const auto f = std::chrono::steady_clock::now();
+        if (it < 0) continue;
+        t_create += std::chrono::duration<double, std::micro>(b - a).count();
+        t_exec += std::chrono::duration<double, std::micro>(c - b).count();
+        t_sync += std::chrono::duration<double, std::micro>(e - c).count();
+        t_destroy += std::chrono::duration<double, std::micro>(f - e).count();
+    }
+    // the HIP calls a plan's life is made of, alone (16 KiB of descriptors)
+    double t_malloc = 0, t_free = 0, t_copy = 0, t_copy_async = 0;
+    std::vector<uint8_t> host(16384, 1);
+    uint8_t *pinned = nullptr;
+    CHECK(hipHostMalloc(reinterpret_cast<void **>(&pinned), 16384, 0) == hipSuccess);
+    for (int it = 0; it < 200; ++it) {
+        const auto a = std::chrono::steady_clock::now();
+        void *x = nullptr;
+        CHECK(hipMalloc(&x, 16384) == hipSuccess);
+        const auto b = std::chrono::steady_clock::now();
+        CHECK(hipMemcpy(x, host.data(), 16384, hipMemcpyHostToDevice) == hipSuccess);
+        const auto c = std::chrono::steady_clock::now();
+        CHECK(hipMemcpyAsync(x, pinned, 16384, hipMemcpyHostToDevice, s) == hipSuccess);
+        const auto e = std::chrono::steady_clock::now();
+        CHECK(hipStreamSynchronize(s) == hipSuccess);
+        const auto f = std::chrono::steady_clock::now();
+        CHECK(hipFree(x) == hipSuccess);
+        const auto g = std::chrono::steady_clock::now();
+        t_malloc += std::chrono::duration<double, std::micro>(b - a).count();
+        t_copy += std::chrono::duration<double, std::micro>(c - b).count();
+        t_copy_async += std::chrono::duration<double, std::micro>(e - c).count();
+        t_free += std::chrono::duration<double, std::micro>(g - f).count();
+    }
+    (void)hipHostFree(pinned);
+    std::printf("{\"mode\": \"write\", \"iterations\": %d, \"create_us\": %.2f, \"exec_issue_us\": %.2f, "
+                "\"sync_us\": %.2f, \"destroy_us\": %.2f, \"total_us\": %.2f, \"hipMalloc_16KiB_us\": %.2f, "
+                "\"hipMemcpy_pageable_16KiB_us\": %.2f, \"hipMemcpyAsync_pinned_issue_us\": %.2f, "
+                "\"hipFree_us\": %.2f}\n",
+                iters, t_create / iters, t_exec / iters, t_sync / iters, t_destroy / iters,
+                (t_create + t_exec + t_sync + t_destroy) / iters, t_malloc / 200, t_copy / 200, t_copy_async / 200,
+                t_free / 200);
+    (void)hipFree(d);
+    (void)hipFree(out);
+    crc32c_ctx_destroy(ctx);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && std::string(argv[1]) == "write") return write_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
     const size_t npk = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 64;
     const int n = argc > 2 ? std::atoi(argv[2]) : 4000;
     const uint32_t len = 65536, bpc = 512;
