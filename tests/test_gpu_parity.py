@@ -589,3 +589,35 @@ def test_plan_launches_across_streams(hdfs, gpu_ctx, orc):
     for k in range(8):
         assert np.array_equal(outs[k].cpu().numpy().view(np.uint32), orc.batch(pays[k], pk, 64 * 128)), k
     plan.close()
+
+
+def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
+    """Plan descriptors come from a recycled pool and are uploaded
+    asynchronously: 100 plans of different shapes are each created, launched
+    at once on a fresh non-blocking stream (the launch must wait for the
+    upload) and destroyed while their launch may still run; their blocks are
+    reused by later plans only after an epoch.  Every output is exact."""
+    torch = _torch()
+    ctx = hdfs.Context(0)
+    rng = np.random.default_rng(5)
+    s = torch.cuda.Stream()
+    jobs = []
+    try:
+        for i in range(100):
+            npk = int(rng.integers(1, 40))
+            pk = oracle.uniform_packets(npk, pkt_len=int(rng.integers(1, 65537)), bpc=int(rng.choice([512, 1536, 4096])),
+                                        stride=65536 + 16)
+            n = hdfs.total_checksums(pk)
+            payload = oracle.xorshift64_bytes(npk * (65536 + 16) + 64, 900 + i)
+            dev = torch.from_numpy(payload).cuda()
+            out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            plan = hdfs.Plan(ctx, pk)
+            plan.exec(dev.data_ptr(), out.data_ptr(), s.cuda_stream)
+            plan.close()  # (launch possibly still in flight)
+            jobs.append((payload, pk, n, dev, out))
+        torch.cuda.synchronize()
+        for payload, pk, n, _, out in jobs:
+            assert np.array_equal(out.cpu().numpy().view(np.uint32)[:n], orc.batch(payload, pk, n))
+    finally:
+        ctx.close()
