@@ -88,10 +88,8 @@ constexpr int kModeMemDiag = 8;     // DIAGNOSTIC, wrong results: no lookups (me
 constexpr int kModeCompDiag = 16;   // DIAGNOSTIC, wrong results: no payload loads (compute ceiling)
 constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table staging
 constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
-constexpr int kModeS4H = 128;       // A/B: half-column S4 image (64 KiB of T tables, 88 KiB staged)
 constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
 constexpr int kModeEarly = 1024;    // the first tile's loads are issued before the table staging
-constexpr int kModeItemsFirst = 2048;  // gen / seg / const items before the tiles instead of after
 constexpr int kModeQuarter = 4096;  // small batches: power-of-two tiles of chunks <= 2 KiB run as 4 work
                                     // units of 4 blocks each (4x the waves, 1/4 of each wave's latency chain)
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
@@ -171,23 +169,20 @@ struct LaneCols {
     uint32_t col4;  // (lane & 31) * 4
     uint32_t hi;    // col4 | 65536
     uint32_t nib;   // col4 | kS4NibOff
-    uint32_t toff;  // T1 - T0 (= T3 - T2) in bytes: 128, or 64 in the half-column image
+    uint32_t toff;  // T1 - T0 (= T3 - T2) in bytes: 128, or 1024 in the compact image
 };
 
 // S4 image layouts (template parameter IMG): the full image (32 replica
-// columns of T0..T3), the half-column image (A/B), and the compact image
-// (T0..T3 once each, for small batches: crc_math.h kS4C*).
-constexpr int kImgFull = 0, kImgHalf = 1, kImgCompact = 2;
+// columns of T0..T3) and the compact image (T0..T3 once each, for small
+// batches: crc_math.h kS4C*).  (A half-column image -- 16 replica columns,
+// 88 KiB staged -- measured +-0 and was removed)
+constexpr int kImgFull = 0, kImgCompact = 2;
 constexpr uint32_t kS4CNibOff = uint32_t(hdfs_crc::kS4CNibOff);
 constexpr uint32_t kS4CShiftOff = uint32_t(hdfs_crc::kS4CShiftOff);
 constexpr uint32_t kS4CStageBytes = (uint32_t(hdfs_crc::kS4CBytes) + 1023u) / 1024u * 1024u;
 
 template <int IMG>
 __device__ __forceinline__ LaneCols lane_cols(uint32_t q) {
-    if (IMG == kImgHalf) {  // half-column S4 image (A/B, kModeS4H): T0..T3 share one 256-byte row per byte value
-        const uint32_t c4 = (q & 15u) << 2;
-        return LaneCols{c4, c4 | 128u, (q << 2) | kS4NibOff, 64u};
-    }
     if (IMG == kImgCompact)  // T_m[b] at m * 1024 + 4 b: col4 = T0 base, hi = T2 base
         return LaneCols{0u, 2048u, (q << 2) | kS4CNibOff, 1024u};
     return LaneCols{q << 2, (q << 2) | 65536u, (q << 2) | kS4NibOff, 128u};
@@ -960,12 +955,10 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : 0;
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
     constexpr bool VERIFY = (MODE & kModeVerify) != 0;
-    constexpr bool H = S4 && (MODE & kModeS4H) != 0;
     constexpr bool C = S4 && (MODE & kModeS4C) != 0;
-    constexpr int IMG = H ? kImgHalf : C ? kImgCompact : kImgFull;
+    constexpr int IMG = C ? kImgCompact : kImgFull;
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
-    constexpr bool ITEMSFIRST = !EARLY && (MODE & kModeItemsFirst) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
@@ -975,7 +968,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
-    const uint8_t *table = !S4 ? p.table : H ? p.table_s4 + hdfs_crc::kS4HOff : C ? p.table_s4 + hdfs_crc::kS4COff : p.table_s4;
+    const uint8_t *table = !S4 ? p.table : C ? p.table_s4 + hdfs_crc::kS4COff : p.table_s4;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
 
@@ -1021,7 +1014,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     // launch of constant runs only needs none.
     const bool tables = (p.ntiles | p.ngen | p.nseg) != 0;
     constexpr uint32_t kStageChunks = kStage / 1024u;
-    if (!NOSTAGE && tables && !H) {
+    if (!NOSTAGE && tables) {
         // Every workgroup copies the same 152 chunks: start each one at a
         // different chunk (the 32 CUs of an XCD would otherwise walk the same
         // L2 lines, hence the same L2 channel, in lock step).
@@ -1033,21 +1026,13 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                 (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
         }
     }
-    if (!NOSTAGE && tables && H) {
-        for (uint32_t c = wv; c < kStageChunks; c += (c + kWaves >= 64u && c + kWaves < 128u) ? kWaves + 64u : kWaves) {
-            // (half-column image: its T region is the first 64 KiB; chunks 64-127 are unused)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
-                (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
-        }
-    }
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
 
     // Gen pairs, seg pairs and constant runs, dealt over every wave of the
-    // grid: after the tiles, or (ITEMSFIRST) before them, so that their
-    // latency-bound loads overlap the other waves' tile streaming instead of
-    // the launch's tail.
+    // grid after the tiles.  (Before the tiles, so that their latency-bound
+    // loads would overlap the other waves' tile streaming, measured -2.8 ..
+    // +1 %: not kept)
     const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wv);
     const uint32_t nwaves = gridDim.x * kWaves;
     auto items = [&]() {
@@ -1062,7 +1047,6 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                 const_run<VERIFY>(p, vacc, g - ngp - nsp, lane);
         }
     };
-    if (ITEMSFIRST) items();
 
     if (!EARLY && t < tend) load_next(t);
     while (t < tend) {
@@ -1074,7 +1058,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         if (t >= tend) break;
         load_next(t);
     }
-    if (!ITEMSFIRST) items();
+    items();
     if (VERIFY) {
         __syncthreads();
         if (threadIdx.x == 0) verify_finish(p, vacc);

@@ -641,16 +641,6 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         HIP_TRY(hipMemcpy(c->d_table[ty], img.data(), kTableAlloc, hipMemcpyHostToDevice));
         std::vector<uint8_t> img4(kTableAllocS4Full, 0);
         build_lds_image_s4(img4.data(), poly);
-        {  // half-column image (A/B, debug library): same N_q / Z, T0..T3 in one row per byte value
-            uint8_t *h = img4.data() + kS4HOff;
-            std::memcpy(h, img4.data(), kTableAllocS4);
-            std::memset(h, 0, kS4NibOff);
-            for (uint32_t b = 0; b < 256; ++b)
-                for (uint32_t m = 0; m < 4; ++m)
-                    for (uint32_t q = 0; q < 16; ++q)
-                        std::memcpy(h + b * 256u + m * 64u + 4u * q,
-                                    img4.data() + (m >> 1) * 65536u + b * 256u + (m & 1u) * 128u, 4);
-        }
         compact_s4_image(img4.data(), img4.data() + kS4COff);  // small batches
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4Full));
         HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4Full, hipMemcpyHostToDevice));

@@ -34,8 +34,6 @@ constexpr Variant kVariants[] = {
     {6, "s4_wg768x1_nt_memonly_stamps", 768, 1, false},    // 3 with per-wave timestamps
     {7, "s4_wg768x1_nt_memonly_nostage", 768, 1, false},   // 3 without the table staging
     {9, "s4_wg512x1_nt", 512, 1, true},                    // 0 with 8 waves per CU
-    {35, "s4h_nt", 768, 1, true},                          // half-column image (88 KiB staged)
-    {36, "s4h_nt_stamps", 768, 1, true},                   // 35 with per-wave timestamps
     {40, "s4_nt_memonly_nostage_prodgrid", 768, 1, false, true},  // 7 on the production grid (launch floor)
     {41, "s4c_nt_prodgrid", 768, 1, true, true},           // compact image (28 KiB staged), production grid
     {42, "s4c_nt_stamps_prodgrid", 768, 1, true, true},    // 41 with per-wave timestamps
@@ -47,7 +45,6 @@ constexpr Variant kVariants[] = {
     {47, "s4c_wg128_nt_early", 128, 8, true},              // 45, first tile's loads before the staging
     {48, "s4c_nt_early_prodgrid", 768, 1, true, true},     // 41, first tile's loads before the staging
     {49, "s4_nt_general_prodgrid", 768, 1, true, true},    // the full-image production build, any batch size
-    {50, "s4_nt_itemsfirst_prodgrid", 768, 1, true, true},  // 49 with gen / seg / const items before the tiles
     {51, "s4c_nt_quarter_prodgrid", 768, 1, true, true},   // 41 with quarter units (4 per tile)
     {52, "s4c_nt_quarter_early_prodgrid", 768, 1, true, true},  // 51, first unit's loads before the staging
     {53, "s4_nt_quarter_prodgrid", 768, 1, true, true},    // 49 (full image) with quarter units
@@ -81,8 +78,6 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 6: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeStamps); break;
     case 7: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeNoStage); break;
     case 9: HDFS_LAUNCH(512, 2, kS4Nt); break;
-    case 35: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H); break;
-    case 36: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4H | kModeStamps); break;
     case 40: HDFS_LAUNCH(768, 3, kS4Nt | kModeMemDiag | kModeNoStage); break;
     case 41: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C); break;
     case 42: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeStamps); break;
@@ -93,7 +88,6 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 47: HDFS_LAUNCH(128, 4, kS4Nt | kModeS4C | kModeEarly); break;
     case 48: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeEarly); break;
     case 49: HDFS_LAUNCH(768, 3, kS4Nt); break;
-    case 50: HDFS_LAUNCH(768, 3, kS4Nt | kModeItemsFirst); break;
     case 51: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter); break;
     case 52: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeEarly); break;
     case 53: HDFS_LAUNCH(768, 3, kS4Nt | kModeQuarter); break;

@@ -14,13 +14,9 @@ constexpr uint32_t kKernelShiftOff = uint32_t(kLdsShiftOff);
 // 1024-thread workgroup (16 B per thread per round) is in bounds.
 constexpr uint32_t kTableAlloc = ((kKernelLdsBytes + 16384 - 1) / 16384) * 16384;
 constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 16384;
-// After the S4 image (at kTableAllocS4): the half-column S4 image (A/B only,
-// debug library): the full image with its T region re-laid out as
-// b*256 + m*64 + 4*(q & 15) (the first 64 KiB).
-constexpr uint32_t kS4HOff = kTableAllocS4;
-// Then the compact S4 image (crc_math.h kS4C*), padded to whole 1 KiB
-// staging pieces.
-constexpr uint32_t kS4COff = kS4HOff + kTableAllocS4;
+// After the S4 image (at kTableAllocS4): the compact S4 image (crc_math.h
+// kS4C*), padded to whole 1 KiB staging pieces.
+constexpr uint32_t kS4COff = kTableAllocS4;
 constexpr uint32_t kTableAllocS4C = ((uint32_t(kS4CBytes) + 16384 - 1) / 16384) * 16384;
 constexpr uint32_t kTableAllocS4Full = kS4COff + kTableAllocS4C;
 
