@@ -90,6 +90,7 @@ constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table stagin
 constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
 constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
 constexpr int kModeEarly = 1024;    // the first tile's loads are issued before the table staging
+constexpr int kModeHalves = 16384;  // A/B: with kModeQuarter, 2 units of 8 blocks per tile instead of 4
 constexpr int kModeQuarter = 4096;  // small batches: power-of-two tiles of chunks <= 2 KiB run as 4 work
                                     // units of 4 blocks each (4x the waves, 1/4 of each wave's latency chain)
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
@@ -759,24 +760,27 @@ __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane,
 // ordinary tile of <= 4 blocks, loaded by 2 instructions and looked up as 2
 // pieces per lane.  General items and tiles of longer chunks run whole as
 // unit 0 of their tile (units 1-3 are empty).
-// Returns 0 (empty unit), 1 (a whole tile / item in ft) or 2 (a quarter in ft).
-template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL>
+// SPLIT 2 (A/B, debug library): halves of 8 blocks instead (chunks <= 4 KiB).
+// Returns 0 (empty unit), 1 (a whole tile / item in ft) or 2 (a unit in ft).
+template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL, int SPLIT = 4>
 __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane, FastTile &ft, uint4 v[8],
                                          uint32_t &ev) {
-    const FastTile x = tile_at(p, j >> 2);
-    const uint32_t u = j & 3u;
+    constexpr uint32_t kUB = 16 / SPLIT;  // blocks per unit
+    constexpr int kNP = 8 / SPLIT;        // load instructions (pieces per lane) per unit
+    const FastTile x = tile_at(p, j / SPLIT);
+    const uint32_t u = j % SPLIT;
     const uint32_t lg = (x.meta >> 8) & 0xffu;
-    if ((GENERAL && (x.meta & kGeneralTile)) || lg > 2) {
+    if ((GENERAL && (x.meta & kGeneralTile)) || (1u << lg) > kUB) {
         if (u) return 0;
         ft = x;
         load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
         return 1;
     }
     const uint32_t nb = x.meta & 0xffu;
-    if (4u * u >= nb) return 0;
-    ft.src = x.src + 2048u * u;
-    ft.out = x.out + ((4u * u) >> lg);
-    ft.meta = min(nb - 4u * u, 4u) | (lg << 8);
+    if (kUB * u >= nb) return 0;
+    ft.src = x.src + 512u * kUB * u;
+    ft.out = x.out + ((kUB * u) >> lg);
+    ft.meta = min(nb - kUB * u, kUB) | (lg << 8);
     if (COMPDIAG) {
         load_tile<AUX, true, false>(p, ft, lane, v, ev);
         return 2;
@@ -786,7 +790,7 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + ft.src), 0, int(nbq * 512u), 0x00020000);
     const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < kNP; ++i) {
         const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
@@ -798,13 +802,14 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     return 2;
 }
 
-template <int DIAG, bool S4, bool VERIFY, int IMG>
+template <int DIAG, bool S4, bool VERIFY, int IMG, int SPLIT = 4>
 __device__ __forceinline__ void finish_quarter(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                                uint4 v[8], uint32_t ev, int lane) {
+    constexpr int kNP = 8 / SPLIT;
     uint32_t pc[8];
-    tile_pieces<DIAG, S4, IMG, NoPrep, 2>(lds, v, pc, lane, NoPrep{});
+    tile_pieces<DIAG, S4, IMG, NoPrep, kNP>(lds, v, pc, lane, NoPrep{});
 #pragma unroll
-    for (int i = 2; i < 8; ++i) pc[i] = 0;  // blocks 4..15: none
+    for (int i = kNP; i < 8; ++i) pc[i] = 0;  // blocks past the unit: none
     reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
 }
 
@@ -960,6 +965,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
+    constexpr int SPLIT = (MODE & kModeHalves) ? 2 : 4;  // units per tile
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = !S4 ? kStageBytes : C ? kS4CStageBytes : kS4StageBytes;
@@ -981,7 +987,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     // This workgroup's equal, contiguous range of tiles [tbeg, tend).  Wave
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
     // (QUARTER: units, 4 per tile)
-    const uint64_t nunits = QUARTER ? 4ull * p.ntiles : uint64_t(p.ntiles);
+    const uint64_t nunits = QUARTER ? uint64_t(SPLIT) * p.ntiles : uint64_t(p.ntiles);
     const uint32_t tbeg = uint32_t((nunits * blockIdx.x) / gridDim.x);
     const uint32_t tend = uint32_t((nunits * (blockIdx.x + 1)) / gridDim.x);
     if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
@@ -999,7 +1005,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     int kind = 1;     // QUARTER: what load_unit found (0 empty, 1 tile / item, 2 quarter)
     auto load_next = [&](uint32_t j) {
         if (QUARTER) {
-            kind = load_unit<AUX, COMPDIAG, VERIFY, GENERAL>(p, j, lane, ft, v, ev);
+            kind = load_unit<AUX, COMPDIAG, VERIFY, GENERAL, SPLIT>(p, j, lane, ft, v, ev);
         } else {
             ft = tile_at(p, j);
             load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
@@ -1053,7 +1059,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         if (!QUARTER || kind == 1)
             finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GENERAL>(p, lds, vacc, ft, v, ev, lane);
         else if (kind == 2)
-            finish_quarter<DIAG, S4, VERIFY, IMG>(p, lds, vacc, ft, v, ev, lane);
+            finish_quarter<DIAG, S4, VERIFY, IMG, SPLIT>(p, lds, vacc, ft, v, ev, lane);
         t = pool_grab(pool_ctr, lane);
         if (t >= tend) break;
         load_next(t);
@@ -1078,8 +1084,8 @@ namespace hdfs_crc {
 // Grid of a launch: one workgroup per CU, or one per work item when there
 // are fewer items than CUs (a small batch leaves most waves without a tile;
 // they still share the table staging, which is what bounds a small launch).
-inline uint32_t production_grid(const KParams &p, uint32_t num_cu, bool quarter = false) {
-    const uint64_t items = uint64_t(p.ntiles) * (quarter ? 4 : 1) + (uint64_t(p.ngen) + 1) / 2 +
+inline uint32_t production_grid(const KParams &p, uint32_t num_cu, uint32_t units_per_tile = 1) {
+    const uint64_t items = uint64_t(p.ntiles) * units_per_tile + (uint64_t(p.ngen) + 1) / 2 +
                            (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     return uint32_t(items < num_cu ? (items ? items : 1) : num_cu);
 }

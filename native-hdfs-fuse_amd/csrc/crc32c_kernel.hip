@@ -24,9 +24,11 @@ namespace hdfs_crc {
 namespace {
 // Work items per CU up to which the compact image wins: its T lookups are
 // not conflict-free (one copy of each table instead of 32 lane columns), so
-// once every CU has several tiles the full image's faster lookups pay back
-// its staging (small batches).
-constexpr uint64_t kSmallBatchItemsPerCu = 8;
+// once every CU has many tiles the full image's faster lookups pay back its
+// staging (small batches; graph-replayed, 3072 tiles:
+// 7.89 vs 8.24 us, 4096: 9.05 vs 9.39, 8192: full image ahead,
+// profiles/r02/launch_probe_units_crossover.json).
+constexpr uint64_t kSmallBatchItemsPerCu = 16;
 // Tiles per CU up to which quarter units win (tools/launch_probe.py,
 // profiles/r02/launch_probe_crossover.json: 512 tiles 3.71 vs 4.36 us, 768
 // tiles 4.24 vs 4.72, 1024 tiles 5.56 vs 4.95).
@@ -42,7 +44,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const bool small = items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
-    const dim3 g{production_grid(p, num_cu, quarter), 1, 1}, b{768, 1, 1};
+    const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
     if (p.expect) {
         if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
         if (quarter)

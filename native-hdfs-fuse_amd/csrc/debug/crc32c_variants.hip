@@ -50,6 +50,8 @@ constexpr Variant kVariants[] = {
     {53, "s4_nt_quarter_prodgrid", 768, 1, true, true},    // 49 (full image) with quarter units
     {54, "s4c_nt_quarter_stamps_prodgrid", 768, 1, true, true},  // 51 with per-wave timestamps
     {55, "s4c_nt_quarter_early_stamps_prodgrid", 768, 1, true, true},  // 52 with per-wave timestamps
+    {60, "s4c_nt_halves_prodgrid", 768, 1, true, true},    // 51 with 2 units of 8 blocks per tile
+    {61, "s4_nt_halves_prodgrid", 768, 1, true, true},     // the same on the full image
 };
 
 const Variant *find(int v) {
@@ -63,8 +65,8 @@ const Variant *find(int v) {
 hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
-    const bool quarter = v.id >= 51 && v.id <= 55;
-    uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, quarter) : (items + waves - 1) / waves;
+    const uint32_t units = (v.id >= 51 && v.id <= 55) ? 4u : (v.id == 60 || v.id == 61) ? 2u : 1u;
+    uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, units) : (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
@@ -93,6 +95,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 53: HDFS_LAUNCH(768, 3, kS4Nt | kModeQuarter); break;
     case 54: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeStamps); break;
     case 55: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeEarly | kModeStamps); break;
+    case 60: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeHalves); break;
+    case 61: HDFS_LAUNCH(768, 3, kS4Nt | kModeQuarter | kModeHalves); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -399,7 +399,7 @@ def test_kernel_variant_env_has_no_effect(hdfs, golden, monkeypatch):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 5, 9, 41, 42, 43, 44, 45, 46, 47, 48, 49, 51, 52, 53, 54, 55])
+@pytest.mark.parametrize("variant", [0, 1, 2, 5, 9, 41, 42, 43, 44, 45, 46, 47, 48, 49, 51, 52, 53, 54, 55, 60, 61])
 def test_debug_library_variants_exact(hdfs, golden, orc, variant):
     """The A/B kernels of libhdfs_crc32c_debug.so that compute checksums (1 =
     positional nibble tables, 2 = 16 waves per CU, 5 = stamped, 9 = 8
