@@ -311,8 +311,9 @@ def main():
     # Python -> ctypes -> hipLaunchKernel call each (~4.1 us per launch on
     # the host, which bounds one-block batches: DESIGN.md section 5).  The
     # host-issued rate is reported beside it (eager_ms_per_step).  Config 4's
-    # step holds RCCL calls and stays host-issued.
-    use_graph = not c4 and not args.no_graph
+    # step holds RCCL calls at N > 1 and stays host-issued there (at N = 1 it
+    # is one plan launch).
+    use_graph = (not c4 or world == 1) and not args.no_graph
     graph = None
     if use_graph:
         graph = torch.cuda.CUDAGraph()
