@@ -732,24 +732,114 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ 0xffffffffu, ev);
 }
 
+// ---- power-of-two tiles off 16-byte alignment (GENERAL builds) ----------
+// A dwordx4 load that straddles a 16-byte boundary costs the memory pipeline
+// about twice an aligned one (config 2 five bytes off: 58 us memory-only
+// against 42.6).  Such a tile (r = its address mod 16, uniform) is instead
+// loaded from the aligned address below it, 16 bytes per lane as usual,
+// plus the 16 bytes after the window (for the last lane); lane q's own 16
+// bytes then start r bytes into its load and end r bytes into the next
+// lane's, which a wave shift (DPP wave_shl:1) and v_alignbyte reassemble.
+__device__ __forceinline__ uint32_t tile_misalign(const KParams &p, FastTile t) {
+    return uint32_t(reinterpret_cast<uintptr_t>(p.payload + t.src)) & 15u;
+}
+
+template <int AUX, bool VERIFY>
+__device__ __forceinline__ void load_tile_shifted(const KParams &p, FastTile t, uint32_t r, int lane, uint4 v[9],
+                                                  uint32_t &ev) {
+    const uint32_t nb = t.meta & 0xffu;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src - r),
+                                                                          0, int(r + nb * 512u), 0x00020000);
+    const uint32_t voff = 16u * uint32_t(lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
+        v[i] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    {  // lane 0 only: the tile's last 16 bytes (a load that straddles the end of
+       // the descriptor's range reads zeros, so the last lane cannot take its
+       // tail from the next lane's load)
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, lane == 0 ? r + nb * 512u - 16u : 0x80000000u, 0,
+                                                             AUX);
+        v[8] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if (VERIFY) {
+        const uint32_t lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
+        if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// Piece i of a shifted tile: bytes r .. r + 15 of (this lane's load, the
+// next lane's load); lane 63 takes lane 0 of load i + 1; the tile's last
+// lane (block nb - 1's lane 31) takes the tile's last 16 bytes (v[8]).
+struct ShiftPrep {
+    const uint4 *v;
+    uint32_t m, b;  // r = 4 m + b
+    int lane;
+    uint32_t last_i;  // load instruction and lane of the tile's last 16 bytes
+    int last_lane;
+    __device__ __forceinline__ uint32_t shl1(uint32_t own, uint32_t last) const {
+        // DPP wave_shl:1 -- lane l reads lane l + 1; lane 63 (no source) keeps `last`
+        return uint32_t(__builtin_amdgcn_update_dpp(int(last), int(own), 0x130, 0xF, 0xF, false));
+    }
+    __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo) const {
+        return __builtin_amdgcn_alignbyte(hi, lo, b);
+    }
+    __device__ __forceinline__ void operator()(int i, uint4 &x) const {
+        const uint4 nx = v[i + 1];
+        const uint32_t n0 = shl1(x.x, __builtin_amdgcn_readfirstlane(nx.x));
+        if (m == 0) {
+            x = make_uint4(ab(x.y, x.x), ab(x.z, x.y), ab(x.w, x.z), ab(n0, x.w));
+        } else if (m == 1) {
+            const uint32_t n1 = shl1(x.y, __builtin_amdgcn_readfirstlane(nx.y));
+            x = make_uint4(ab(x.z, x.y), ab(x.w, x.z), ab(n0, x.w), ab(n1, n0));
+        } else if (m == 2) {
+            const uint32_t n1 = shl1(x.y, __builtin_amdgcn_readfirstlane(nx.y));
+            const uint32_t n2 = shl1(x.z, __builtin_amdgcn_readfirstlane(nx.z));
+            x = make_uint4(ab(x.w, x.z), ab(n0, x.w), ab(n1, n0), ab(n2, n1));
+        } else {
+            const uint32_t n1 = shl1(x.y, __builtin_amdgcn_readfirstlane(nx.y));
+            const uint32_t n2 = shl1(x.z, __builtin_amdgcn_readfirstlane(nx.z));
+            const uint32_t n3 = shl1(x.w, __builtin_amdgcn_readfirstlane(nx.w));
+            x = make_uint4(ab(n0, x.w), ab(n1, n0), ab(n2, n1), ab(n3, n2));
+        }
+        if (uint32_t(i) == last_i) {
+            const uint4 t = v[8];
+            const uint4 f = make_uint4(__builtin_amdgcn_readfirstlane(t.x), __builtin_amdgcn_readfirstlane(t.y),
+                                       __builtin_amdgcn_readfirstlane(t.z), __builtin_amdgcn_readfirstlane(t.w));
+            if (lane == last_lane) x = f;
+        }
+    }
+};
+
 template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, bool GENERAL>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
-                                            uint4 v[8], uint32_t ev, int lane) {
+                                            uint4 v[9], uint32_t ev, int lane) {
     uint32_t pc[8];
     if (GENERAL && (t.meta & kGeneralTile)) {
         finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG>(p, lds, vacc, t, v, ev, lane);
-    } else {
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
-        reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
+        return;
     }
+    const uint32_t r = GENERAL && !COMPDIAG ? tile_misalign(p, t) : 0u;
+    if (r)
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane,
+                                   ShiftPrep{v, r >> 2, r & 3u, lane, ((t.meta & 0xffu) - 1u) >> 1,
+                                             int(((t.meta & 0xffu) - 1u) & 1u) * 32 + 31});
+    else
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
+    reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
 }
 
 template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL>
-__device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
-    if (GENERAL && (t.meta & kGeneralTile))
+__device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[9], uint32_t &ev) {
+    if (GENERAL && (t.meta & kGeneralTile)) {
         load_gtile<VERIFY>(p, t, lane, ev);
-    else
+    } else if (GENERAL && !COMPDIAG && tile_misalign(p, t)) {
+        load_tile_shifted<AUX, VERIFY>(p, t, tile_misalign(p, t), lane, v, ev);
+    } else {
         load_tile<AUX, COMPDIAG, VERIFY>(p, t, lane, v, ev);
+    }
 }
 
 // ---- quarter units (kModeQuarter): blocks 4u .. 4u + 3 of a tile ---------
@@ -763,7 +853,7 @@ __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane,
 // SPLIT 2 (A/B, debug library): halves of 8 blocks instead (chunks <= 4 KiB).
 // Returns 0 (empty unit), 1 (a whole tile / item in ft) or 2 (a unit in ft).
 template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL, int SPLIT = 4>
-__device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane, FastTile &ft, uint4 v[8],
+__device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane, FastTile &ft, uint4 v[9],
                                          uint32_t &ev) {
     constexpr uint32_t kUB = 16 / SPLIT;  // blocks per unit
     constexpr int kNP = 8 / SPLIT;        // load instructions (pieces per lane) per unit
@@ -1000,7 +1090,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     }
     uint32_t t = tbeg + wv;
     FastTile ft{0, 0, 0};
-    uint4 v[8];
+    uint4 v[9];  // (v[8]: the bytes after a shifted tile's window)
     uint32_t ev = 0;  // VERIFY: expected checksum fetched with the tile
     int kind = 1;     // QUARTER: what load_unit found (0 empty, 1 tile / item, 2 quarter)
     auto load_next = [&](uint32_t j) {

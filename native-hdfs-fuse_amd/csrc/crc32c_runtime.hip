@@ -101,7 +101,8 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     p.ngen = dp.ngen;
     p.nseg = dp.nseg;
     p.nconst = dp.nconst;
-    p.general = dp.general ? 1u : 0u;
+    // the general build also carries the shifted loads of tiles off 16-byte alignment
+    p.general = (dp.general || dp.misaligned || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? 1u : 0u;
     return p;
 }
 
@@ -159,6 +160,12 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->nseg = uint32_t(hp.seg.size());
     dp->nconst = uint32_t(hp.consts.size());
     dp->general = has_general(hp);
+    dp->misaligned = false;
+    for (const FastTile &t : hp.tiles)
+        if (!(t.meta & kGeneralTile) && (t.src & 15u)) {
+            dp->misaligned = true;
+            break;
+        }
     dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
     dp->tiles_off = (2 * kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
