@@ -780,28 +780,32 @@ struct ShiftPrep {
     uint32_t last_i;  // load instruction and lane of the tile's last 16 bytes
     int last_lane;
     __device__ __forceinline__ uint32_t shl1(uint32_t own, uint32_t last) const {
-        // DPP wave_shl:1 -- lane l reads lane l + 1; lane 63 (no source) keeps `last`
+        // DPP wave_shl:1 -- lane l reads lane l + 1; lane 63 (no source) keeps `last`'s lane 63
         return uint32_t(__builtin_amdgcn_update_dpp(int(last), int(own), 0x130, 0xF, 0xF, false));
+    }
+    __device__ __forceinline__ static uint32_t rol1(uint32_t x) {
+        // DPP wave_rol:1 -- lane l reads lane (l + 1) mod 64: lane 63 gets lane 0
+        return uint32_t(__builtin_amdgcn_update_dpp(0, int(x), 0x134, 0xF, 0xF, false));
     }
     __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo) const {
         return __builtin_amdgcn_alignbyte(hi, lo, b);
     }
     __device__ __forceinline__ void operator()(int i, uint4 &x) const {
         const uint4 nx = v[i + 1];
-        const uint32_t n0 = shl1(x.x, __builtin_amdgcn_readfirstlane(nx.x));
+        const uint32_t n0 = shl1(x.x, rol1(nx.x));
         if (m == 0) {
             x = make_uint4(ab(x.y, x.x), ab(x.z, x.y), ab(x.w, x.z), ab(n0, x.w));
         } else if (m == 1) {
-            const uint32_t n1 = shl1(x.y, __builtin_amdgcn_readfirstlane(nx.y));
+            const uint32_t n1 = shl1(x.y, rol1(nx.y));
             x = make_uint4(ab(x.z, x.y), ab(x.w, x.z), ab(n0, x.w), ab(n1, n0));
         } else if (m == 2) {
-            const uint32_t n1 = shl1(x.y, __builtin_amdgcn_readfirstlane(nx.y));
-            const uint32_t n2 = shl1(x.z, __builtin_amdgcn_readfirstlane(nx.z));
+            const uint32_t n1 = shl1(x.y, rol1(nx.y));
+            const uint32_t n2 = shl1(x.z, rol1(nx.z));
             x = make_uint4(ab(x.w, x.z), ab(n0, x.w), ab(n1, n0), ab(n2, n1));
         } else {
-            const uint32_t n1 = shl1(x.y, __builtin_amdgcn_readfirstlane(nx.y));
-            const uint32_t n2 = shl1(x.z, __builtin_amdgcn_readfirstlane(nx.z));
-            const uint32_t n3 = shl1(x.w, __builtin_amdgcn_readfirstlane(nx.w));
+            const uint32_t n1 = shl1(x.y, rol1(nx.y));
+            const uint32_t n2 = shl1(x.z, rol1(nx.z));
+            const uint32_t n3 = shl1(x.w, rol1(nx.w));
             x = make_uint4(ab(n0, x.w), ab(n1, n0), ab(n2, n1), ab(n3, n2));
         }
         if (uint32_t(i) == last_i) {
