@@ -31,19 +31,24 @@
 //  * bpc = 1024..8192 (power of two): per-block results are shifted by
 //    Z^(512*s) (nibble tables in LDS) and XORed across the blocks of a chunk
 //    with DPP / swizzle steps.
-//  * Any other bpc in [4, 8192] (general tiles): each chunk is right-aligned
-//    into k = ceil(bpc / 512) virtual blocks (leading zeros do not change
-//    lin); the register pre-inversion (crc32c.c:237) is XORed into the
-//    chunk's first 4 bytes, so crc = lin ^ ~0; blocks are shifted by
-//    Z^(512*s) and a chunk's k blocks are XORed by ds_bpermute.
+//  * Any other bpc in [4, 8192], and packet tails (general items,
+//    crc32c_general.h): each chunk is right-aligned into k = ceil(bpc / 512)
+//    virtual blocks (leading zeros do not change lin); the register
+//    pre-inversion (crc32c.c:237) is XORed into the chunk's first 4 bytes,
+//    so crc = lin ^ ~0; one wave runs an item's blocks as 16-block subtiles
+//    (chunks may span two), shifting blocks by Z^(512*s) and gathering a
+//    chunk's blocks with a prefix XOR.
+//  * Tiles off 16-byte alignment (general builds): aligned loads, each
+//    lane's bytes reassembled with a DPP wave shift and v_alignbyte.
 //  * Work distribution: each workgroup owns an equal range of 8 KiB tiles;
 //    its waves pull tiles from an LDS counter (the SIMD arbiter's age
-//    priority makes static per-wave assignment finish 2x apart).
-//  * Tails / chunks fitting no tile: half a wave per chunk (GenItem), the
-//    chunk right-aligned into zero-prefixed virtual 512-byte blocks,
-//    Horner-combined with Z^512.  Chunks assembled from several buffers
-//    (SegItem) are read piece by piece into the same windows; chunks of
-//    zero fill only (ConstRun) are written from plan-time constants.
+//    priority makes static per-wave assignment finish 2x apart).  The
+//    smallest batches split each tile over 4 waves (quarter units).
+//  * Chunks fitting no tile (crc32c_items.h): half a wave per chunk
+//    (GenItem), the chunk right-aligned into zero-prefixed virtual 512-byte
+//    blocks, Horner-combined with Z^512.  Chunks assembled from several
+//    buffers (SegItem) are read piece by piece into the same windows; chunks
+//    of zero fill only (ConstRun) are written from plan-time constants.
 //  * Verification (crc32c_plan_verify): the same kernel compares instead of
 //    storing; the expected values are fetched with the tile and the last
 //    workgroup publishes the launch's result (sharded ticket reduction).
@@ -395,192 +400,6 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// General item geometry (plan.h general_meta): nch <= 16 full chunks of
-// bpc bytes (k virtual 512-byte blocks each, the data right-aligned behind
-// pad leading zeros), then optionally a tail chunk of tl bytes (kt blocks,
-// padt leading zeros) right after them.  Its nb = nch k + kt virtual blocks
-// are processed as ceil(nb / 16) subtiles of 16 blocks, one after another
-// by one wave, so a chunk may span two subtiles and no block slot is left
-// empty between chunks.
-struct GShape {
-    uint32_t k, nch, pad, bpc, tl, kt, padt, nfb, nb;
-    uint64_t src;  // payload offset of the first chunk
-};
-__device__ __forceinline__ GShape gshape(FastTile t) {
-    GShape g;
-    g.k = (t.meta >> 8) & 31u;
-    g.nch = (t.meta >> 13) & 31u;
-    g.pad = (t.meta >> 18) & 511u;
-    g.bpc = g.k * 512u - g.pad;
-    g.tl = uint32_t(t.src >> 48);
-    g.kt = (g.tl + 511u) >> 9;
-    g.padt = g.kt * 512u - g.tl;
-    g.nfb = g.nch * g.k;
-    g.nb = g.nfb + g.kt;
-    g.src = t.src & hdfs_crc::kSrcMask;
-    return g;
-}
-
-// Patterns of whole chunks of k blocks over 16 block slots, the first slot
-// being block phi (< k) of a chunk: start bit b = ((b + phi) % k == 0),
-// nibble b of dist = k - 1 - (b + phi) % k (the block's distance from its
-// chunk's end: the Z^512 power it is shifted by); mod16[k] = 16 % k.
-struct GPatterns {
-    uint64_t dist[17][16];
-    uint32_t start[17][16];
-    uint32_t mod16[17];
-    constexpr GPatterns() : dist(), start(), mod16() {
-        for (int k = 1; k <= 16; ++k) {
-            mod16[k] = uint32_t(16 % k);
-            for (int phi = 0; phi < k; ++phi)
-                for (int b = 0; b < 16; ++b) {
-                    dist[k][phi] |= uint64_t(k - 1 - (b + phi) % k) << (4 * b);
-                    if ((b + phi) % k == 0) start[k][phi] |= 1u << b;
-                }
-        }
-    }
-};
-__constant__ const GPatterns kGPat{};
-
-__device__ __forceinline__ uint32_t low_bits(uint32_t n) { return (1u << n) - 1u; }  // n <= 16
-__device__ __forceinline__ uint64_t low_nibbles(uint32_t n) { return n >= 16 ? ~0ull : (1ull << (4 * n)) - 1ull; }
-
-// Wave-uniform facts of subtile s (blocks 16 s .. 16 s + 15 of the item),
-// one bit or nibble per block, computed on the scalar unit from the
-// descriptor and the running state of the subtiles before it; lanes only
-// select their block's bit.
-struct GSub {
-    uint32_t sfull;   // bit b: block starts a full chunk
-    uint32_t start;   // ... or the tail chunk
-    uint32_t second;  // bit b: the block is its chunk's second
-    uint32_t tailm;   // bit b: block of the tail chunk
-    uint32_t valid;   // bit b: block < nb
-    uint32_t before;  // full chunks started before the subtile
-    uint64_t dist;    // nibble b: blocks to the chunk's end
-};
-struct GState {
-    uint32_t before = 0;  // full chunks started in earlier subtiles
-    uint32_t carry = 0;   // 1: the previous subtile's last block started a chunk
-    uint32_t phi = 0;     // (16 s) % k
-};
-__device__ __forceinline__ GSub gsub(const GShape &g, uint32_t s, const GState &st) {
-    GSub r;
-    const uint32_t base = 16u * s;
-    const uint32_t nf = g.nfb > base ? min(g.nfb - base, 16u) : 0u;
-    const uint32_t nv = g.nb > base ? min(g.nb - base, 16u) : 0u;
-    r.valid = low_bits(nv);
-    r.sfull = kGPat.start[g.k][st.phi] & low_bits(nf);
-    r.tailm = r.valid & ~low_bits(nf);
-    r.start = r.sfull;
-    r.dist = kGPat.dist[g.k][st.phi] & low_nibbles(nf);
-    if (g.kt) {
-        const uint32_t tr = g.nfb - base;  // the tail's first block (wraps when it began in an earlier subtile)
-        if (tr < 16u) r.start |= 1u << tr;
-        // tail block b: nb - 1 - base - b blocks to its end; kDesc has nibble b = 15 - b
-        constexpr uint64_t kDesc = 0x0123456789ABCDEFull;
-        const int e = min(max(int(g.nb) - 1 - int(base), 0), 30);  // the tail's last block, local (clamped)
-        const uint64_t pat = e <= 15 ? kDesc >> (4 * (15 - e)) : kDesc << (4 * (e - 15));
-        r.dist |= pat & low_nibbles(nv) & ~low_nibbles(nf);
-    }
-    r.second = ((r.start << 1) | st.carry) & r.valid & ~r.start;
-    r.before = st.before;
-    return r;
-}
-__device__ __forceinline__ void gstate_next(const GShape &g, const GSub &gs, GState &st) {
-    st.before += __builtin_popcount(gs.sfull);
-    st.carry = (gs.start >> 15) & 1u;
-    st.phi += kGPat.mod16[g.k];
-    if (st.phi >= g.k) st.phi -= g.k;
-}
-
-// Loads of subtile s of a general item: lane q of block b = 2i + h reads
-// bytes 512 (16 s + b) + 16 q - D .. +15 of the item, D = pad x (full chunks
-// started at or before the block) + (padt in the tail chunk): the virtual
-// blocks of chunk c start pad_c bytes before c's data.  The descriptor covers
-// [src - 16, src + nch * bpc + tl) (from src when no chunk is padded: then
-// the blocks are contiguous and load like a power-of-two tile's).  Lanes
-// wholly inside a chunk's zero prefix, or past the last chunk, read zeros
-// without touching memory; the straddling lane's bytes before the chunk are
-// masked in gsub_pieces.
-template <int AUX, bool COMPDIAG>
-__device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, const GSub &gs, uint32_t s, int lane,
-                                          uint4 v[8]) {
-    if (COMPDIAG) {  // synthetic data, no memory traffic
-        const uint32_t x = uint32_t(g.src) * 2654435761u + s * 97u + uint32_t(lane) * 40503u;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = make_uint4(x ^ i, x + i, x * 3u + i, x ^ (i << 16));
-        return;
-    }
-    const uint32_t bytes = g.nch * g.bpc + g.tl;
-    if (g.pad == 0 && g.padt == 0) {
-        const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + g.src), 0, int(bytes), 0x00020000);
-        const uint32_t voff = 8192u * s + 16u * uint32_t(lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 1024u * i, 0, AUX);
-            v[i] = make_uint4(r[0], r[1], r[2], r[3]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        return;
-    }
-    const uint32_t shift = 16u;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(p.payload + g.src - shift), 0, int(shift + bytes), 0x00020000);
-    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    const uint32_t upto = 2u << h;  // (upto << 2i) - 1: blocks 0 .. b
-    const uint32_t sth = gs.start >> h, vh = gs.valid >> h, th = gs.tailm >> h;
-    const uint32_t qs = 16u * q + 16u;
-    const uint32_t base = shift + 8192u * s + 16u * uint32_t(lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const bool tail = (th >> (2 * i)) & 1u;
-        const uint32_t pc = tail ? g.padt : g.pad;
-        const uint32_t d = g.pad * (gs.before + __builtin_popcount(gs.sfull & ((upto << (2 * i)) - 1u))) +
-                           (tail ? g.padt : 0u);
-        const bool skip = !((vh >> (2 * i)) & 1u) || (((sth >> (2 * i)) & 1u) && qs <= pc);
-        // (bit 31: past any descriptor range -- arithmetic, so no branch around the offset math)
-        const uint32_t voff = (base + 1024u * i - d) | (uint32_t(skip) << 31);
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, AUX);
-        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// Where a tile's loads go, a general item only fetches (VERIFY) the expected
-// checksums of its chunks: its subtiles are loaded inside finish_gtile's
-// loop, so the loaded registers are not carried around that loop (copying
-// them would wait for all 8 loads before the first lookup).
-template <bool VERIFY>
-__device__ __forceinline__ void load_gtile(const KParams &p, FastTile t, int lane, uint32_t &ev) {
-    const GShape g = gshape(t);
-    if (VERIFY && uint32_t(lane) < g.nch + (g.kt ? 1u : 0u)) ev = p.expect[t.out + uint32_t(lane)];
-}
-
-// Bytes of a dword with index < n (n clamped to 0..4).
-__device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
-    return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
-}
-
-// Chunk bytes before position 0 of the lane's dwords -> 0, chunk bytes 0..3
-// ^= 0xff (the register pre-inversion of crc32c.c:237 moved into the data).
-// m = position in the lane's 16 bytes where the chunk starts (may be < 0).
-// Dword j's bytes with index < m - 4 j is M_j = 0xffffffff >> (32 - 8 c),
-// c = clamp(m - 4 j, 0, 4): one 64-bit shift of 0x00000000ffffffff by
-// clamp(32 - 8 (m - 4 j), 0, 32).  Dword k keeps its bytes outside M_k and
-// XORs 0xff into M_{k-1} & ~M_k (the bytes m .. m + 3): ~M_k & (w ^ M_{k-1}),
-// one v_bitop3.
-__device__ __forceinline__ uint32_t bytes_below(int s) {  // s = 32 - 8 (m - 4 j), any value
-    const int c = min(max(s, 0), 32);
-    return uint32_t(0xffffffffull >> c);
-}
-__device__ __forceinline__ uint4 chunk_start_mask(uint4 d, int m) {
-    const int s = 32 - 8 * m;
-    const uint32_t mm1 = bytes_below(s - 32), m0 = bytes_below(s), m1 = bytes_below(s + 32),
-                   m2 = bytes_below(s + 64), m3 = bytes_below(s + 96);
-    return make_uint4(~m0 & (d.x ^ mm1), ~m1 & (d.y ^ m0), ~m2 & (d.z ^ m1), ~m3 & (d.w ^ m2));
-}
-
 // lin() of a tile's 8 pieces (instruction i's 16 bytes per lane), each
 // piece first passed through prep(i, piece) (general tiles: the chunk-start
 // masks), so that piece i's lookups start as soon as its own load is back.
@@ -602,33 +421,6 @@ __device__ __forceinline__ void tile_pieces(const uint8_t *lds, uint4 v[8], uint
 struct NoPrep {
     __device__ __forceinline__ void operator()(int, uint4 &) const {}
 };
-
-// General subtile pieces with the chunk-start masks (bytes before a chunk
-// zeroed, its first 4 bytes ^ 0xff).  The chunk starts at position
-// pad_c - 16 q of lane q's piece of the chunk's first block; its 4
-// pre-inverted bytes reach the second block's lane 0 when pad_c > 508.
-// Unpadded items (bpc = 512 k) only XOR ~0 into lane 0 of each chunk's
-// first block; the two forms are separate loops so that neither waits for
-// all 8 loads before its first lookup.
-template <int DIAG, bool S4, int IMG>
-__device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g, const GSub &gs, uint4 v[8],
-                                            uint32_t pc[8], int lane) {
-    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    if (g.pad || g.padt) {
-        const uint32_t sth = gs.start >> h, s2h = gs.second >> h, th = gs.tailm >> h;
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
-            const int pcl = int(((th >> (2 * i)) & 1u) ? g.padt : g.pad);
-            const bool first = (sth >> (2 * i)) & 1u, second = (s2h >> (2 * i)) & 1u;
-            const int m = first ? pcl - int(16u * q) : pcl - 512 - int(16u * q);
-            // (branch-free: m = -64 leaves the piece as it is)
-            x = chunk_start_mask(x, (first || (second && q == 0)) ? m : -64);
-        });
-    } else {
-        const uint32_t sth = q == 0 ? gs.start >> h : 0u;
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane,
-                                   [&](int i, uint4 &x) { x.x ^= uint32_t(-int32_t((sth >> (2 * i)) & 1u)); });
-    }
-}
 
 // The tile's 8 piece values -> one lin() per block: reduce-scatter over lane
 // bits 0, 1, 3 (8 values -> 1), then all-reduce over lane bits 2 and 4.
@@ -682,55 +474,11 @@ __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds
     if (rep_lane(lane, blk, nb, lg)) emit<VERIFY>(p, vacc, t.out + (blk >> lg), crc, ev);
 }
 
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a source read 0
-    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xF, 0xF, true));
-}
+}  // namespace hdfs_crc_dev
 
-// A general item: for every subtile, block b's lin (block_lin) is shifted
-// by Z^(512 dist_b) to its chunk's end; the blocks are permuted into block
-// order and prefix-XORed along 16-lane rows (DPP row_shr), and lane c adds
-// the XOR of its chunk's blocks in the subtile as P[hi - 1] ^ P[lo - 1].
-// After the last subtile lane c holds chunk c's lin; the data carried the
-// pre-inversion, so crc = lin ^ ~0.  Each subtile's loads are issued after
-// the previous one's lookups.
-template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG>
-__device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
-                                             uint4 v[8], uint32_t ev, int lane) {
-    const GShape g = gshape(t);
-    const uint32_t c = uint32_t(lane);
-    const uint32_t nout = g.nch + (g.kt ? 1u : 0u);
-    // lane c's chunk: virtual blocks [lo, hi)
-    const uint32_t lo = c < g.nch ? c * g.k : g.nfb;
-    const uint32_t hi = c < g.nch ? lo + g.k : (c < nout ? g.nb : lo);
-    const uint32_t blk = rep_block(lane);
-    const uint32_t from = block_lane(uint32_t(lane) & 15u) << 2;
-    const uint32_t nsub = (g.nb + 15u) >> 4;
-    GState st;
-    uint32_t acc = 0;
-    for (uint32_t s = 0; s < nsub; ++s) {
-        const GSub gs = gsub(g, s, st);
-        load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
-        uint32_t pc[8];
-        gsub_pieces<DIAG, S4, IMG>(lds, g, gs, v, pc, lane);
-        uint32_t x = block_lin(pc, lane);
-        const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
-        const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
-        if (sh) x = zshift<S4, IMG>(lds, sh, x);
-        uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(x)));  // lane l: block l & 15
-        y ^= dpp_zero<0x111>(y);  // row_shr:1
-        y ^= dpp_zero<0x112>(y);  // row_shr:2
-        y ^= dpp_zero<0x114>(y);  // row_shr:4
-        y ^= dpp_zero<0x118>(y);  // row_shr:8: lane l holds blocks 0 .. l & 15
-        const int base = int(16u * s);
-        const int l1 = min(max(int(lo) - base, 0), 16), h1 = min(max(int(hi) - base, 0), 16);
-        const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(y)));
-        const uint32_t pl = uint32_t(__builtin_amdgcn_ds_bpermute((max(l1, 1) - 1) << 2, int(y)));
-        if (h1 > l1) acc ^= ph ^ (l1 ? pl : 0u);
-        gstate_next(g, gs, st);
-    }
-    if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ 0xffffffffu, ev);
-}
+#include "crc32c_general.h"  // general items (needs the helpers above)
+
+namespace hdfs_crc_dev {
 
 // ---- power-of-two tiles off 16-byte alignment (GENERAL builds) ----------
 // A dwordx4 load that straddles a 16-byte boundary costs the memory pipeline
@@ -914,133 +662,9 @@ __device__ __forceinline__ uint32_t pool_grab(uint32_t *pool_ctr, int lane) {
     return __builtin_amdgcn_readfirstlane(t);
 }
 
-// ---- general path: half a wave per chunk of any length / alignment -------
-// Loads the aligned 16 bytes at a0 when they touch [cbeg, cend), zeroes the
-// bytes outside it and XORs 0xff into the bytes inside [cbeg, ffend)
-// (the register pre-inversion of crc32c.c:237 moved into the data).
-__device__ __forceinline__ void load_piece(uintptr_t a0, uintptr_t cbeg, uintptr_t cend, uintptr_t ffend,
-                                           uint32_t w[4]) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (a0 < cend && a0 + 16 > cbeg) v = *reinterpret_cast<const uint4 *>(a0);
-    const uint32_t dv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uintptr_t d = a0 + 4u * j;
-        const uint32_t lo = bytes_mask(int64_t(cbeg - d));
-        const uint32_t keep = bytes_mask(int64_t(cend - d)) & ~lo;
-        const uint32_t ff = bytes_mask(int64_t(ffend - d)) & ~lo;
-        w[j] = (dv[j] & keep) ^ ff;
-    }
-}
-
-// Bytes sh .. sh+15 of the 32 bytes w[0..7]: a two-stage dword select (by 2,
-// then by 1) and v_alignbyte.  Written out as values so the compiler cannot
-// turn it into an indexed scratch access.
-__device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
-    const bool by2 = (sh & 8u) != 0, by1 = (sh & 4u) != 0;
-    const uint32_t bi = sh & 3u;
-    const uint32_t t0 = by2 ? w[2] : w[0], t1 = by2 ? w[3] : w[1], t2 = by2 ? w[4] : w[2];
-    const uint32_t t3 = by2 ? w[5] : w[3], t4 = by2 ? w[6] : w[4], t5 = by2 ? w[7] : w[5];
-    const uint32_t s0 = by1 ? t1 : t0, s1 = by1 ? t2 : t1, s2 = by1 ? t3 : t2;
-    const uint32_t s3 = by1 ? t4 : t3, s4 = by1 ? t5 : t4;
-    return make_uint4(__builtin_amdgcn_alignbyte(s1, s0, bi), __builtin_amdgcn_alignbyte(s2, s1, bi),
-                      __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
-}
-
-template <bool S4, bool VERIFY, int IMG>
-__device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
-                                         int lane) {
-    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    const uint32_t idx = 2u * pair + h;
-    const bool valid = idx < p.ngen;
-    GenItem g{0, 0, 0};
-    if (valid) g = p.gen[idx];
-    const uint32_t r = g.len;
-    const uint32_t nbv = (r + 511u) >> 9;  // virtual 512-byte blocks
-    const uint32_t nmax = max(__builtin_amdgcn_readlane(nbv, 0), __builtin_amdgcn_readlane(nbv, 32));
-    const int64_t pad = int64_t(nbv) * 512 - int64_t(r);
-    const uintptr_t cbeg = reinterpret_cast<uintptr_t>(p.payload) + g.src;
-    const uintptr_t cend = cbeg + r;
-    const uintptr_t ffend = r >= 4 ? cbeg + 4 : cbeg;
-    const LaneCols cols = lane_cols<IMG>(q);
-    uint32_t acc = 0;
-    for (uint32_t m = 0; m < nmax; ++m) {
-        uint32_t lin = 0;
-        if (m < nbv) {
-            const int64_t o = int64_t(m) * 512 + int64_t(16 * q) - pad;  // may be negative (zero prefix)
-            const uintptr_t a = cbeg + uintptr_t(o);
-            const uintptr_t a0 = a & ~uintptr_t(15);
-            uint32_t w[8];
-            load_piece(a0, cbeg, cend, ffend, w);
-            load_piece(a0 + 16, cbeg, cend, ffend, w + 4);
-            lin = piece<S4, 0, IMG>(lds, funnel(w, uint32_t(a & 15u)), cols);
-        }
-        lin = allreduce32(lin);
-        if (m < nbv) acc = zshift<S4, IMG>(lds, 1, acc) ^ lin;
-    }
-    if (valid && q == 0) {
-        const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
-        emit<VERIFY>(p, vacc, g.out, crc, VERIFY ? p.expect[g.out] : 0u);
-    }
-}
-
-// A chunk assembled from several buffers (SegItem): like gen_pair, but each
-// lane's 16-byte window (chunk positions o .. o+15) is filled from every data
-// piece it overlaps; positions no piece covers are zero fill.
-template <bool S4, bool VERIFY, int IMG>
-__device__ __forceinline__ void seg_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
-                                         int lane) {
-    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    const uint32_t idx = 2u * pair + h;
-    const bool valid = idx < p.nseg;
-    SegItem s{0, 0, 0, 0};
-    if (valid) s = p.seg[idx];
-    const uint32_t r = s.len;
-    const uint32_t nbv = (r + 511u) >> 9;
-    const uint32_t nmax = max(__builtin_amdgcn_readlane(nbv, 0), __builtin_amdgcn_readlane(nbv, 32));
-    const int64_t pad = int64_t(nbv) * 512 - int64_t(r);
-    const uintptr_t base = reinterpret_cast<uintptr_t>(p.payload);
-    const LaneCols cols = lane_cols<IMG>(q);
-    uint32_t acc = 0;
-    for (uint32_t m = 0; m < nmax; ++m) {
-        uint32_t lin = 0;
-        if (m < nbv) {
-            const int64_t o = int64_t(m) * 512 + int64_t(16 * q) - pad;  // chunk position of the window
-            uint4 d = make_uint4(0, 0, 0, 0);
-            for (uint32_t u = 0; u < s.npieces; ++u) {
-                const GenPiece g = p.pieces[s.first + u];
-                if (o >= int64_t(g.start) + g.len || o + 16 <= int64_t(g.start)) continue;
-                const uintptr_t cbeg = base + g.src, cend = cbeg + g.len;
-                const uintptr_t a = cbeg + uintptr_t(o - int64_t(g.start));
-                const uintptr_t a0 = a & ~uintptr_t(15);
-                uint32_t w[8];
-                load_piece(a0, cbeg, cend, cbeg, w);
-                load_piece(a0 + 16, cbeg, cend, cbeg, w + 4);
-                const uint4 f = funnel(w, uint32_t(a & 15u));
-                d = make_uint4(d.x | f.x, d.y | f.y, d.z | f.z, d.w | f.w);
-            }
-            if (r >= 4) d = chunk_start_mask(d, int(-o));  // (o + 16 > 0 here: nothing before the chunk is loaded)
-            lin = piece<S4, 0, IMG>(lds, d, cols);
-        }
-        lin = allreduce32(lin);
-        if (m < nbv) acc = zshift<S4, IMG>(lds, 1, acc) ^ lin;
-    }
-    if (valid && q == 0) {
-        const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
-        emit<VERIFY>(p, vacc, s.out, crc, VERIFY ? p.expect[s.out] : 0u);
-    }
-}
-
-// Checksums known at plan time (chunks of zero fill only): stored (or compared).
-template <bool VERIFY>
-__device__ __forceinline__ void const_run(const KParams &p, uint32_t *vacc, uint32_t i, int lane) {
-    const ConstRuns c = (ConstRuns)(p.consts) + i;
-    const uint32_t out = c->out, count = c->count, value = c->value;
-    for (uint32_t k = uint32_t(lane); k < count; k += 64u)
-        emit<VERIFY>(p, vacc, out + k, value, VERIFY ? p.expect[out + k] : 0u);
-}
-
 }  // namespace hdfs_crc_dev
+
+#include "crc32c_items.h"  // GenItem / SegItem / ConstRun work items
 
 // THREADS per workgroup, WPS = waves per SIMD the launch bound asks for
 // (= workgroups per CU x THREADS / 256; it caps VGPRs at 512 / WPS).
