@@ -621,3 +621,37 @@ def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
             assert np.array_equal(out.cpu().numpy().view(np.uint32)[:n], orc.batch(payload, pk, n))
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("bpc", [512, 2048, 4096])
+def test_shifted_tiles_large_batch(hdfs, gpu_ctx, orc, bpc):
+    """A batch large enough for the full-image general build (> 16 tiles per
+    CU), every packet at a different offset mod 16 with partial last tiles:
+    the tiles off 16-byte alignment load from the aligned address below and
+    reassemble each lane's bytes (wave shift + alignbyte, the tile's last 16
+    bytes loaded apart).  Exec and verify against the oracle."""
+    torch = _torch()
+    n = 720
+    pk = np.zeros(n, hdfs.PACKET_DTYPE)
+    off = out = 0
+    for i in range(n):
+        off += i % 16 + 1  # every phase mod 16
+        ln = 65536 - (i % 7) * 512 * (bpc // 512) - (i % 3) * 37
+        pk[i] = (off, out, ln, bpc)
+        off += ln
+        out += (ln + bpc - 1) // bpc
+    tiles, _ = hdfs.debug_plan(pk)
+    assert len(tiles) > 16 * 256 and np.any(tiles["src"] & np.uint64(15))
+    payload = oracle.xorshift64_bytes(off + 64, 7000 + bpc)
+    want = orc.batch(payload, pk, out)
+    assert np.array_equal(run_dev(hdfs, gpu_ctx, payload, pk), want)
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    exp[[7, out - 1]] ^= 1
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [2, 7]
+    plan.close()
