@@ -315,16 +315,21 @@ def main():
     # is one plan launch).
     use_graph = (not c4 or world == 1) and not args.no_graph
     graph = None
+    graph_error = None
     if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        # (thread_local: other threads of the process -- e.g. the process
-        # group's watchdog -- may make CUDA calls while this thread captures)
-        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-            cap = torch.cuda.current_stream(dev).cuda_stream
-            for i in range(args.steps):
-                step(i, cap)
-        graph.replay()  # (first replay uploads the graph)
-        torch.cuda.synchronize()
+        try:
+            graph = torch.cuda.CUDAGraph()
+            # (thread_local: other threads of the process -- e.g. the process
+            # group's watchdog -- may make CUDA calls while this thread captures)
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                cap = torch.cuda.current_stream(dev).cuda_stream
+                for i in range(args.steps):
+                    step(i, cap)
+            graph.replay()  # (first replay uploads the graph)
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # no graph on this stack: time host-issued launches instead
+            graph, use_graph, graph_error = None, False, str(e)[:200]
+            torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -586,7 +591,8 @@ def main():
             "box_read_probe": read_probe,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             "launch": ("hip graph of the %d timed launches, replayed" % args.steps) if use_graph else
-                      "host-issued, one launch per step",
+                      ("host-issued, one launch per step" +
+                       ("" if graph_error is None else " (graph capture failed: %s)" % graph_error)),
             "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 5),
         }
         print(json.dumps(line), flush=True)
