@@ -418,12 +418,17 @@ def main():
             torch.cuda.synchronize()
             plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), cs.cuda_stream)
             torch.cuda.synchronize()
-            vgraph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(vgraph, stream=cs, capture_error_mode="thread_local"):
-                for i in range(nv):
-                    plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), cs.cuda_stream)
-            vgraph.replay()
+            try:
+                vgraph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(vgraph, stream=cs, capture_error_mode="thread_local"):
+                    for i in range(nv):
+                        plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(),
+                                    cs.cuda_stream)
+                vgraph.replay()
+            except RuntimeError:
+                vgraph = None
             torch.cuda.synchronize()
+        if vgraph is not None:
             e0.record(stream)
             vgraph.replay()
             e1.record(stream)
