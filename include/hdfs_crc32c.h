@@ -130,19 +130,25 @@ int crc32c_device_count(void);
  * 3. Device-resident batches.
  *
  * A plan is built once per batch SHAPE from host packet descriptors (work
- * decomposition into 8 KiB tiles, uploaded to the device) and executed on
- * any payload with that shape.  Payload and checksum buffers are device
+ * decomposition into 8 KiB tiles) and executed on any payload with that
+ * shape.  Its descriptors go to the device asynchronously (the first launch
+ * on a stream waits for that copy); destroying a plan whose launches are
+ * still in flight is safe (its device block is recycled only after a later
+ * device synchronisation).  Payload and checksum buffers are device
  * pointers; execution is asynchronous on `stream` (a hipStream_t, NULL =
  * the default stream).  Exec launches of one plan are not ordered with each
  * other: independent batches may run on several streams at once, and two
  * streams let one launch start on the CUs the previous one has released
  * (config 2: 41.2 instead of 43.4 us per batch, tools/overlap_probe.py).
- * Fast path: every full chunk of a packet with bpc in {512, 1024, 2048,
- * 4096, 8192}, at any alignment (off 16-byte alignment the tile loads are
- * unaligned: config 2 five bytes off takes 55 instead of 42.5 us); short
- * tail chunks and other bpc values take the general path (exact, ~4x
- * slower).  The payload buffer must be readable up to the next 16-byte
- * boundary after each packet's last byte (device allocations always are).
+ * Fast tiles: every full chunk of a packet with bpc in {512, 1024, 2048,
+ * 4096, 8192}, at any alignment (off 16-byte alignment, loaded from the
+ * aligned address below and shifted into place: config 2 five bytes off
+ * 48.7-50.5 instead of 42.0-43.0 us); every full chunk of any other bpc in
+ * [4, 8192] and every packet tail of at least 4 bytes (general items:
+ * config 2 with bpc 1536 in 1.1x the time of bpc 512); the rest (shorter
+ * tails, bpc outside [4, 8192]) takes the general path (exact, slower).
+ * The payload buffer must be readable up to the next 16-byte boundary after
+ * each packet's last byte (device allocations always are).
  * ------------------------------------------------------------------------- */
 typedef struct crc32c_plan crc32c_plan;
 
