@@ -148,7 +148,9 @@ __device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, con
     for (int i = 0; i < 8; ++i) {
         const bool tail = (th >> (2 * i)) & 1u;
         const uint32_t pc = tail ? g.padt : g.pad;
-        const uint32_t d = g.pad * (gs.before + __builtin_popcount(gs.sfull & ((upto << (2 * i)) - 1u))) +
+        // (unpadded full chunks: only the tail is offset)
+        const uint32_t d = (g.pad ? g.pad * (gs.before + __builtin_popcount(gs.sfull & ((upto << (2 * i)) - 1u)))
+                                  : 0u) +
                            (tail ? g.padt : 0u);
         const bool skip = !((vh >> (2 * i)) & 1u) || (((sth >> (2 * i)) & 1u) && qs <= pc);
         // (bit 31: past any descriptor range -- arithmetic, so no branch around the offset math)
@@ -204,7 +206,23 @@ template <int DIAG, bool S4, int IMG>
 __device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g, const GSub &gs, uint4 v[8],
                                             uint32_t pc[8], int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    if (g.pad || g.padt) {
+    if (g.pad == 0 && g.padt) {
+        // Only the tail chunk is padded (a power-of-two or 512 k packet with a
+        // short tail): the full chunks take the unpadded XOR, and the
+        // chunk-start mask runs only in the (at most two) piece rows that hold
+        // the tail's first block or the spill into its second.
+        const uint32_t fh = q == 0 ? (gs.start & ~gs.tailm) >> h : 0u;
+        const uint32_t trows = (gs.start | gs.second) & gs.tailm;  // the tail's first / second block
+        const uint32_t th1 = (gs.start & gs.tailm) >> h, th2 = (gs.second & gs.tailm) >> h;
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
+            x.x ^= uint32_t(-int32_t((fh >> (2 * i)) & 1u));
+            if ((trows >> (2 * i)) & 3u) {  // (uniform)
+                const bool first = (th1 >> (2 * i)) & 1u, second = (th2 >> (2 * i)) & 1u;
+                const int m = first ? int(g.padt) - int(16u * q) : int(g.padt) - 512 - int(16u * q);
+                x = chunk_start_mask(x, (first || (second && q == 0)) ? m : -64);
+            }
+        });
+    } else if (g.pad) {
         const uint32_t sth = gs.start >> h, s2h = gs.second >> h, th = gs.tailm >> h;
         tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
             const int pcl = int(((th >> (2 * i)) & 1u) ? g.padt : g.pad);
