@@ -9,6 +9,7 @@
 //
 //   tools/launch_rate [packets=64] [launches=4000]
 //   tools/launch_rate write [iterations=2000]
+//   tools/launch_rate raw [launches=4000]   (an empty kernel: HIP's own launch cost)
 // prints one JSON line.  `write`: one FUSE-shaped 4 MiB block write per
 // iteration (TRUNCATE / NULLPADDING / THEDATA / TRAILINGDATA buffers,
 // src/fuse.c:1348-1354) through crc32c_plan_create_buffers -> exec ->
@@ -30,6 +31,37 @@
             return 1;                                                      \
         }                                                                  \
     } while (0)
+
+// An empty kernel with a KParams-sized argument, on the production grid
+// shape: HIP's own launch cost, for comparison with crc32c_plan_exec's.
+struct BigArg {
+    uint64_t w[24];
+};
+__global__ void empty_kernel(BigArg a) {
+    if (a.w[0] == 12345u && threadIdx.x == 1000) a.w[1] = 0;  // (never true; keeps the argument live)
+}
+
+static int raw_mode(int n) {
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    BigArg a{};
+    for (int i = 0; i < 500; ++i) hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(768), 0, s, a);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess);
+    CHECK(hipEventRecord(e0, s) == hipSuccess);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; ++i) hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(768), 0, s, a);
+    const auto t1 = std::chrono::steady_clock::now();
+    CHECK(hipEventRecord(e1, s) == hipSuccess);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess);
+    std::printf("{\"mode\": \"raw_empty_kernel\", \"launches\": %d, \"host_issue_us\": %.3f, "
+                "\"gpu_us_per_launch\": %.3f}\n",
+                n, std::chrono::duration<double, std::micro>(t1 - t0).count() / n, ms * 1e3 / n);
+    return 0;
+}
 
 static int write_mode(int iters) {
     const uint64_t mb4 = 4u << 20;
@@ -101,6 +133,7 @@ static int write_mode(int iters) {
 
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "write") return write_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
+    if (argc > 1 && std::string(argv[1]) == "raw") return raw_mode(argc > 2 ? std::atoi(argv[2]) : 4000);
     const size_t npk = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 64;
     const int n = argc > 2 ? std::atoi(argv[2]) : 4000;
     const uint32_t len = 65536, bpc = 512;
