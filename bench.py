@@ -186,7 +186,7 @@ def main():
     # the 1.4 kW package cap).  2500 launches take ~0.1 s.
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "c2b1536", "c2b1000", "c2u", "c2t"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "c2b1536", "c2b1000", "c2u", "c2t", "c3u"])
     ap.add_argument("--nbuf", type=int, default=4, help="rotating payload buffers (defeat the 256 MiB L3)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -255,7 +255,7 @@ def main():
             pk["payload_off"] -= pk["payload_off"][0]
             pk["out_idx"] -= pk["out_idx"][0]
             workload += ", strong scaling: packets split over %d ranks" % world
-        nbuf = args.nbuf if args.config != "c3" else 1
+        nbuf = args.nbuf if args.config not in ("c3", "c3u") else 1
     nbytes = int(pk["len"].astype(np.int64).sum())
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)

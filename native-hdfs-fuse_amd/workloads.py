@@ -55,6 +55,10 @@ def config_packets(name: str):
         pk = uniform_packets(4096, stride=PACKET_BYTES + 16)
         pk["payload_off"] += np.uint64(5)
         return pk, "4096 x 64KiB packets at 16-byte-misaligned offsets, 512B chunks (general path)"
+    if name == "c3u":  # config 3 with every packet 5 bytes off 16-byte alignment
+        pk = uniform_packets(64, stride=PACKET_BYTES + 16)
+        pk["payload_off"] += np.uint64(5)
+        return pk, "one 4MiB block as 64 x 64KiB packets at 16-byte-misaligned offsets, 512B chunks"
     if name == "c2b1536":  # config 2 with bytesPerChecksum 1536 (not a power of two: general path)
         return uniform_packets(4096, bpc=1536), "4096 x 64KiB packets, 1536B chunks (general path)"
     if name == "c2b1000":  # config 2 with bytesPerChecksum 1000 (padded general tiles)
