@@ -265,8 +265,12 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     GState st;
     uint32_t acc = 0;
     for (uint32_t s = 0; s < nsub; ++s) {
+        // Unpadded items' loads need no block facts: issue them before the
+        // subtile's pattern-table fetches (two dependent scalar loads).
+        const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
+        if (contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
         const GSub gs = gsub(g, s, st);
-        load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
+        if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
         uint32_t pc[8];
         gsub_pieces<DIAG, S4, IMG>(lds, g, gs, v, pc, lane);
         uint32_t x = block_lin(pc, lane);
