@@ -655,3 +655,42 @@ def test_shifted_tiles_large_batch(hdfs, gpu_ctx, orc, bpc):
     stream.synchronize()
     assert res.cpu().numpy().view(np.uint32).tolist() == [2, 7]
     plan.close()
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_fuzz_mixed_batches(hdfs, gpu_ctx, orc, seed):
+    """Seeded random batches that mix every work-item kind the plan can
+    build -- power-of-two tiles at any alignment (shifted or not), general
+    items (padded and unpadded bpc, tails riding behind full chunks, chunks
+    spanning subtiles), GenItems (tails under 4 bytes, bpc > 8192) -- at
+    sizes that select each kernel build (quarter units, compact image, full
+    image); exec and verify against the oracle."""
+    torch = _torch()
+    rng = np.random.default_rng(seed)
+    for size in (12, 90, 700):  # packets: quarter-unit, compact and full-image builds
+        bpcs = rng.choice([512, 1024, 4096, 8192, 1536, 1000, 100, 3000, 513, 9000], size=size)
+        pk = np.zeros(size, hdfs.PACKET_DTYPE)
+        off = out = 0
+        for i in range(size):
+            bpc = int(bpcs[i])
+            off += int(rng.integers(16, 48)) if rng.random() < 0.5 else 16 - off % 16 + 16
+            ln = int(rng.integers(1, 65537)) if rng.random() < 0.4 else 65536 - int(rng.integers(0, 4)) * bpc
+            ln = max(ln, 1)
+            pk[i] = (off, out, ln, bpc)
+            off += ln
+            out += (ln + bpc - 1) // bpc
+        payload = oracle.xorshift64_bytes(off + 64, 100 * seed + size)
+        want = orc.batch(payload, pk, out)
+        got = run_dev(hdfs, gpu_ctx, payload, pk)
+        assert np.array_equal(got, want), (size, np.nonzero(got != want)[0][:8])
+        plan = hdfs.Plan(gpu_ctx, pk)
+        dev = torch.from_numpy(payload).cuda()
+        exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+        bad = int(rng.integers(0, out))
+        exp[bad] ^= 0x40
+        res = torch.zeros(2, dtype=torch.int32, device="cuda")
+        stream = torch.cuda.current_stream()
+        plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        assert res.cpu().numpy().view(np.uint32).tolist() == [1, bad], size
+        plan.close()
