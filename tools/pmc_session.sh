@@ -3,7 +3,7 @@
 # kernel-trace only beside --pmc).  Workload: tools/kbench.py, one variant.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/pmc
+OUT="${PMC_OUT:-gpurun_out/pmc}"
 mkdir -p $OUT
 export TMPDIR=/tmp
 V="${PMC_VARIANT:-0}"
