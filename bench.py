@@ -394,9 +394,11 @@ def main():
     verify = None
     if rank == 0 and plan is not None:
         res = torch.zeros(2, dtype=torch.int32, device=dev)
-        for i in range(50):
+        for i in range(200):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
-        nv = 200  # (even: a plan's verify launches alternate between two scratch slots)
+        # 1000 launches (~45 ms at config 2): a window of 200 fell inside the
+        # power controller's post-idle clamp on some boxes
+        nv = 1000  # (even: a plan's verify launches alternate between two scratch slots)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)

@@ -356,6 +356,65 @@ def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     assert np.array_equal(got2[:127], got[1:128])
 
 
+def test_batch_beyond_4GiB(hdfs, gpu_ctx, orc):
+    """One plan over 4.6 GiB of HBM (payload offsets past 2^31 and 2^32,
+    packets straddling both, some 16-byte-misaligned and ragged, bpc 512 and
+    1536): every straddling / first / last packet bit-exact against the
+    oracle, and the whole checksum vector equal to three plans over its thirds
+    (each below 2 GiB, so no offset wraps in them)."""
+    torch = _torch()
+    rng = np.random.default_rng(0x4614)
+    marks = (1 << 31, 1 << 32)
+    rows, off = [], 0
+    while off < (1 << 32) + (600 << 20):
+        n = 65536
+        near = any(abs(off - m) < (1 << 20) for m in marks)
+        if near:  # ragged and misaligned around the marks
+            n = int(rng.integers(1, 65537))
+            off += int(rng.integers(0, 16))
+        rows.append((off, n, 1536 if near and rng.integers(0, 3) == 0 else 512))
+        off += n
+    extent = off
+    pk = np.zeros(len(rows), hdfs.PACKET_DTYPE)
+    out = 0
+    for i, (o, n, b) in enumerate(rows):
+        pk[i] = (o, out, n, b)
+        out += (n + b - 1) // b
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4614)
+    dev = torch.randint(0, 256, (extent,), dtype=torch.uint8, device="cuda", generator=g)
+    stream = torch.cuda.current_stream()
+
+    def exec_plan(pks, base):
+        n = hdfs.total_checksums(pks)
+        res = torch.zeros(max(n, 1), dtype=torch.int32, device="cuda")
+        plan = hdfs.Plan(gpu_ctx, pks, 0)
+        plan.exec(dev.data_ptr() + base, res.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        plan.close()
+        return res.cpu().numpy().view(np.uint32)[:n]
+
+    got = exec_plan(pk, 0)
+    check = {0, len(rows) - 1}
+    for m in marks:
+        check |= {i for i, (o, n, _) in enumerate(rows) if o < m + (1 << 20) and o + n > m - (1 << 20)}
+    for i in sorted(check):
+        o, n, b = rows[i]
+        want = orc.chunks(dev[o:o + n].cpu().numpy(), b)
+        assert np.array_equal(got[pk["out_idx"][i]:pk["out_idx"][i] + want.size], want), (i, o, n, b)
+    parts = []
+    for part in np.array_split(pk, 3):
+        part = part.copy()
+        base = int(part["payload_off"][0]) & ~15
+        part["payload_off"] -= base
+        part["out_idx"] -= part["out_idx"][0]
+        assert int((part["payload_off"] + part["len"]).max()) < (1 << 31)
+        parts.append(exec_plan(part, base))
+    assert np.array_equal(got, np.concatenate(parts))
+    del dev
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("name", ["c1_one_packet", "c3_one_block_4MiB", "c5_mixed_bpc_96", "ragged_tail_257",
                                   "c2_4096_packets", "c5_mixed_bpc_4096", "c4_file_128MiB", "c2_bpc1536"])
 def test_golden_batches_verify_clean(hdfs, gpu_ctx, golden, name):
