@@ -199,6 +199,8 @@ def main():
     ap.add_argument("--two-streams", action="store_true",
                     help="also time 1000 batches alternated over two streams (their launches overlap, so a "
                          "rocprofv3 run of the bench would average overlapped durations: off by default)")
+    ap.add_argument("--host-multi-devices", type=int, default=1,
+                    help="GPUs crc32c_multi_batch_host deals the host-resident batch over at N = 1 (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -540,20 +542,25 @@ def main():
         h2d = round(world * pinned.numel() * reps / slowest(time.perf_counter() - h0) / GIB, 2)
         del dst
         # The N-link lever: crc32c_multi_batch_host deals the batch's 4 MiB
-        # blocks over every GPU this process sees, each over its own PCIe link
-        # (one process; N = 1 on a one-GPU box).
-        if world == 1:
-            ndev = torch.cuda.device_count()
-            m = hdfs.Multi(list(range(ndev)))
-            mout = m.batch_host(hp, pk, group_packets=64)
-            exact_multi = bool(np.array_equal(mout[:nout], want))
-            h0 = time.perf_counter()
-            for _ in range(reps):
-                m.batch_host(hp, pk, group_packets=64)
-            host_multi = {"gib_s": round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2), "devices": ndev,
-                          "bit_exact": exact_multi, "entry": "crc32c_multi_batch_host"}
-            bit_exact = bit_exact and exact_multi
-            m.close()
+        # blocks over --host-multi-devices GPUs from one process, each over
+        # its own PCIe link (default 1: an N = 1 line uses one GPU even on a
+        # node that shows eight; at N > 1 every rank's own link is measured
+        # above instead).
+        if world == 1 and args.host_multi_devices > 0:
+            ndev = min(args.host_multi_devices, torch.cuda.device_count())
+            devs = [(local_rank + k) % torch.cuda.device_count() for k in range(ndev)]
+            m = hdfs.Multi(devs)
+            try:
+                mout = m.batch_host(hp, pk, group_packets=64)
+                exact_multi = bool(np.array_equal(mout[:nout], want))
+                h0 = time.perf_counter()
+                for _ in range(reps):
+                    m.batch_host(hp, pk, group_packets=64)
+                host_multi = {"gib_s": round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2),
+                              "devices": ndev, "bit_exact": exact_multi, "entry": "crc32c_multi_batch_host"}
+                bit_exact = bit_exact and exact_multi
+            finally:
+                m.close()
 
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"))

@@ -177,6 +177,17 @@ uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream);
 
+/* crc32c_plan_verify plus a mismatch bitmap (SURVEY.md section 8f row 1:
+ * "compute + compare, emit a mismatch bitmap"): dev_bad_bits holds
+ * ceil(crc32c_plan_nchecksums(plan) / 32) device u32s; bit i % 32 of word
+ * i / 32 is set for every mismatching checksum i and cleared for every
+ * other one (the library zeroes the bitmap on `stream` before the launch).
+ * A reader that must report every corrupt chunk of a replica, not only the
+ * first (the ChecksumException of hadooprpc.c:497-584's caller), takes it
+ * from here; NULL = crc32c_plan_verify. */
+int crc32c_plan_verify_bitmap(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
+                              uint32_t *dev_result, uint32_t *dev_bad_bits, void *stream);
+
 /* Packet assembly from scatter buffers (hadooprpc.h:33-45, hadooprpc.c:666-725).
  * The bytes a block write sends are `len` bytes starting `bufferoffset` into
  * the concatenation of buffers[0 .. n_buffers); a buffer with data == NULL is

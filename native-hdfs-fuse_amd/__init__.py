@@ -145,6 +145,7 @@ def _bind(L):
         "crc32c_debug_lds_image": (sz, [vp, sz, vp, vp]),
         "crc32c_debug_lds_image_s4": (sz, [vp, sz, u32]),
         "crc32c_plan_verify": (i32, [vp, vp, vp, vp, vp]),
+        "crc32c_plan_verify_bitmap": (i32, [vp, vp, vp, vp, vp, vp]),
         "crc32c_frame_packets": (sz, [vp, sz, vp, u32, u64, ctypes.c_int64, u32, vp, sz, vp]),
         "crc32c_block_md5": (None, [vp, sz, u32, vp]),
         "crc32c_verify_host": (ctypes.c_int64, [vp, vp, vp, sz, vp, u32, vp]),
@@ -335,8 +336,17 @@ class Plan:
         _check(lib().crc32c_plan_exec(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
                                       ctypes.c_void_p(stream)), "crc32c_plan_exec")
 
-    def verify(self, dev_payload: int, dev_expected: int, dev_result: int, stream: int = 0) -> None:
-        """Compare instead of store: dev_result[0] = mismatches, [1] = lowest bad index (async)."""
+    def verify(self, dev_payload: int, dev_expected: int, dev_result: int, stream: int = 0,
+               dev_bad_bits: int = 0) -> None:
+        """Compare instead of store: dev_result[0] = mismatches, [1] = lowest bad index (async); with
+        dev_bad_bits (ceil(nchecksums / 32) u32s) also the bitmap of mismatching checksums
+        (crc32c_plan_verify_bitmap)."""
+        if dev_bad_bits:
+            _check(lib().crc32c_plan_verify_bitmap(self.handle, ctypes.c_void_p(dev_payload),
+                                                   ctypes.c_void_p(dev_expected), ctypes.c_void_p(dev_result),
+                                                   ctypes.c_void_p(dev_bad_bits), ctypes.c_void_p(stream)),
+                   "crc32c_plan_verify_bitmap")
+            return
         _check(lib().crc32c_plan_verify(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_expected),
                                         ctypes.c_void_p(dev_result), ctypes.c_void_p(stream)), "crc32c_plan_verify")
 

@@ -279,10 +279,13 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 }
 
 // A mismatch (VERIFY): bump the workgroup's LDS count and lower its LDS
-// first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish).
-__device__ __forceinline__ void mismatch(uint32_t *vacc, uint32_t idx) {
+// first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish), and
+// set the checksum's bit in the caller's bitmap when there is one (rare path:
+// a clean launch executes none of this).
+__device__ __forceinline__ void mismatch(const KParams &p, uint32_t *vacc, uint32_t idx) {
     atomicAdd(vacc, 1u);
     atomicMin(vacc + 1, idx);
+    if (p.bad_bits) atomicOr(p.bad_bits + (idx >> 5), 1u << (idx & 31u));
 }
 
 // Checksum `idx` of the batch: stored, or (VERIFY) compared with `expect`.
@@ -290,7 +293,7 @@ template <bool VERIFY>
 __device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t expect) {
     const uint32_t v = out_order(crc, p.flags);
     if (VERIFY) {
-        if (v != expect) mismatch(vacc, idx);
+        if (v != expect) mismatch(p, vacc, idx);
     } else {
         p.out[idx] = v;
     }

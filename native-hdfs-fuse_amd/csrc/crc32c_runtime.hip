@@ -735,11 +735,19 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
 
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream) {
+    return crc32c_plan_verify_bitmap(plan, dev_payload, dev_expected, dev_result, nullptr, stream);
+}
+
+int crc32c_plan_verify_bitmap(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
+                              uint32_t *dev_result, uint32_t *dev_bad_bits, void *stream) {
     if (!plan) return fail(-EINVAL, "plan == NULL");
     if (!dev_result) return fail(-EINVAL, "result == NULL");
     DeviceGuard guard(plan->ctx->device);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const DevicePlan &dp = plan->dp;
+    if (dev_bad_bits && plan->nchecksums)  // one bit per checksum, cleared in stream order
+        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_bad_bits), 0,
+                                  size_t((plan->nchecksums + 31) / 32), s));
     if (uint64_t(dp.ntiles) + dp.ngen + dp.nseg + dp.nconst == 0) {  // nothing to compare: set the result directly
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result), 0, 1, s));
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));
@@ -751,6 +759,7 @@ int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_
     KParams p = plan_params(plan, dev_payload, nullptr);
     p.expect = dev_expected;
     p.result = dev_result;
+    p.bad_bits = dev_bad_bits;
     return launch_plan(plan, p, s);
 }
 

@@ -44,6 +44,9 @@ struct KParams {
     // result[1] = min bad index.
     const uint32_t *expect;
     uint32_t *result;
+    // Optional (crc32c_plan_verify_bitmap): bit i set for every mismatching
+    // checksum i; zeroed by the runtime before the launch.
+    uint32_t *bad_bits;
     // Verification slot of this launch (kSlotWords u32s) and the other slot
     // of the pair, which this launch resets for the next one.
     uint32_t *sched;

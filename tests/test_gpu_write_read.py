@@ -401,3 +401,68 @@ def test_last_path_gpu(hdfs, orc):
     pkt = oracle.xorshift64_bytes(65536, 98)
     assert np.array_equal(hdfs.chunks(pkt, 512, hdfs.CRC32C_CPU_FALLBACK), orc.chunks(pkt, 512))
     assert hdfs.last_path() == hdfs.PATH_GPU
+
+
+# ---- verification with a mismatch bitmap -----------------------------------------
+def _bitmap_verify(plan, expected: np.ndarray, stream, payload=0):
+    torch = _torch()
+    n = expected.size
+    exp = torch.from_numpy(expected.view(np.int32).copy()).cuda()
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    words = (n + 31) // 32
+    bits = torch.full((max(words, 1),), -1, dtype=torch.int32, device="cuda")  # stale bits: must be cleared
+    plan.verify(payload, exp.data_ptr(), res.data_ptr(), stream.cuda_stream, dev_bad_bits=bits.data_ptr())
+    stream.synchronize()
+    b = bits.cpu().numpy().view(np.uint32)[:words]
+    flags = np.unpackbits(b.view(np.uint8), bitorder="little")
+    assert not flags[n:].any()  # bits past the last checksum stay clear
+    return res.cpu().numpy().view(np.uint32).tolist(), np.flatnonzero(flags[:n])
+
+
+def test_verify_bitmap_every_item_kind(hdfs, gpu_ctx, orc):
+    """crc32c_plan_verify_bitmap ("emit a mismatch
+    bitmap"): the set of mismatching checksums equals the set corrupted --
+    through power-of-two tiles, general tiles and items (bpc 1000, ragged
+    tails), and a FUSE-shaped buffer-list write plan (chunks spanning buffers,
+    zero-fill constants); corrupted payload bytes and expected values alike;
+    count and lowest index agree with the bitmap; a clean run sets no bit."""
+    torch = _torch()
+    s = torch.cuda.current_stream()
+    rng = np.random.default_rng(818)
+    pk = oracle.mixed_packets(48, bpcs=(512, 1000, 4096))
+    pk["len"] = rng.integers(1, 65537, pk.size).astype(np.uint32)
+    pk["len"][:24] = 65536
+    per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 818)
+    n = hdfs.total_checksums(pk)
+    want = orc.batch(payload, pk, n)
+    dev = torch.from_numpy(payload).cuda()
+    plan = hdfs.Plan(gpu_ctx, pk)
+    assert _bitmap_verify(plan, want, s, dev.data_ptr())[0] == [0, 0xFFFFFFFF]
+    bad = set(int(x) for x in rng.choice(n, 40, replace=False))
+    exp = want.copy()
+    for i in sorted(bad)[::2]:
+        exp[i] ^= np.uint32(1 << int(rng.integers(0, 32)))
+    for i in sorted(bad)[1::2]:  # the rest by a flipped payload byte inside that checksum's chunk
+        p = int(np.searchsorted(pk["out_idx"], i, side="right") - 1)
+        k = i - int(pk["out_idx"][p])
+        lo = k * int(pk["bpc"][p])
+        hi = min(lo + int(pk["bpc"][p]), int(pk["len"][p]))
+        dev[int(pk["payload_off"][p]) + int(rng.integers(lo, hi))] ^= 0x40
+    (cnt, first), idx = _bitmap_verify(plan, exp, s, dev.data_ptr())
+    assert set(idx.tolist()) == bad and cnt == len(bad) and first == min(bad)
+    plan.close()
+    # buffer-list write plan: TRUNCATE | NULLPADDING | THEDATA | TRAILINGDATA
+    bufs, devs, stream_bytes = _fuse_write_buffers(torch, rng, [10000, 300000, 1 << 20, 77777],
+                                                   [False, True, False, False], 900)
+    length = stream_bytes.size - 11
+    wplan = gpu_ctx.write_plan(bufs, 0, length, 0, 65536, 512)
+    want = _expected_write(orc, stream_bytes, 0, length, 0, 65536, 512)
+    assert _bitmap_verify(wplan, want, s)[0] == [0, 0xFFFFFFFF]
+    bad = sorted(set(int(x) for x in rng.choice(want.size, 25, replace=False)) | {0, want.size - 1})
+    exp = want.copy()
+    exp[bad] ^= np.uint32(0x80000000)
+    (cnt, first), idx = _bitmap_verify(wplan, exp, s)
+    assert idx.tolist() == bad and cnt == len(bad) and first == 0
+    wplan.close()
