@@ -25,7 +25,7 @@
  *   crc32c_multi_*()     no reference counterpart: blocks written in parallel
  *                        (src/fuse.c:580-647 writes them one at a time) sharded
  *                        over several GPUs of one node, RCCL gather.
- *   crc32c_verify_frames_host()
+ *   crc32c_plan_verify*(), crc32c_verify_frames_host()
  *                        hadoop_rpc_receive_packets (src/hadooprpc.c:497-584)
  *                        with sendChecksums (the reference asks for none,
  *                        src/fuse.c:1608-1609)
