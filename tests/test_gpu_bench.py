@@ -1,0 +1,58 @@
+"""bench.py's contract on the GPU, as the driver runs it: one JSON line with
+the metric, roofline and correctness fields at N = 1, and the N > 1 path
+(torch.distributed launch, barrier, max-over-ranks timing, gather to rank 0,
+every rank's host-resident run) rehearsed with two ranks on the one visible
+GPU, their collectives over gloo (BENCH_DIST_BACKEND; two RCCL ranks cannot
+share one GPU -- the RCCL transport itself is covered by the multi-plan
+self-send test).  Short step counts: these check the plumbing, not the rate.
+Children are started as subprocesses (never exec'd from this process)."""
+from __future__ import annotations
+
+import json
+import os
+import random
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert lines, out[-3000:]
+    return json.loads(lines[-1])
+
+
+def test_bench_one_gpu_contract():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "200", "--warmup", "20",
+                        "--no-cpu", "--no-host"], cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 1 and d["steps"] == 200 and d["unit"] == "GiB/s" and d["higher_is_better"]
+    assert d["bit_exact_vs_reference"] is True
+    assert d["verify"]["clean"] is True
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["algorithmic_bytes_per_launch"] == 4096 * 65536
+    assert 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
+    assert d["value"] > 0 and d["config"]["config"] == "c2"
+
+
+@pytest.mark.parametrize("config", ["c2", "c5"])
+def test_bench_two_ranks_rehearsal(config):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DIST_BACKEND="gloo")
+    port = 29500 + random.randrange(2000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "20", "--warmup", "5", "--config", config, "--no-cpu", "--nbuf", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=115)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["bit_exact_vs_reference"] is True  # MIN over ranks, host-resident runs included
+    assert d["host_resident_ranks"] == 2 and d["host_resident_gib_s"] > 0
+    assert d["gather_ms"] is not None and d["cpu_baseline"] is None
+    assert d["config"]["payload_bytes_per_rank"] > 0
