@@ -524,9 +524,13 @@ __device__ __forceinline__ void load_tile_shifted(const KParams &p, FastTile t, 
 // Piece i of a shifted tile: bytes r .. r + 15 of (this lane's load, the
 // next lane's load); lane 63 takes lane 0 of load i + 1; the tile's last
 // lane (block nb - 1's lane 31) takes the tile's last 16 bytes (v[8]).
+// r = 4 M + b, M a template parameter: each piece is straight-line code, so
+// piece i waits only for loads i and i + 1 (a branch on M inside every piece
+// made the compiler wait for all nine loads before the first lookup).
+template <uint32_t M>
 struct ShiftPrep {
     const uint4 *v;
-    uint32_t m, b;  // r = 4 m + b
+    uint32_t b;
     int lane;
     uint32_t last_i;  // load instruction and lane of the tile's last 16 bytes
     int last_lane;
@@ -544,12 +548,12 @@ struct ShiftPrep {
     __device__ __forceinline__ void operator()(int i, uint4 &x) const {
         const uint4 nx = v[i + 1];
         const uint32_t n0 = shl1(x.x, rol1(nx.x));
-        if (m == 0) {
+        if constexpr (M == 0) {
             x = make_uint4(ab(x.y, x.x), ab(x.z, x.y), ab(x.w, x.z), ab(n0, x.w));
-        } else if (m == 1) {
+        } else if constexpr (M == 1) {
             const uint32_t n1 = shl1(x.y, rol1(nx.y));
             x = make_uint4(ab(x.z, x.y), ab(x.w, x.z), ab(n0, x.w), ab(n1, n0));
-        } else if (m == 2) {
+        } else if constexpr (M == 2) {
             const uint32_t n1 = shl1(x.y, rol1(nx.y));
             const uint32_t n2 = shl1(x.z, rol1(nx.z));
             x = make_uint4(ab(x.w, x.z), ab(n0, x.w), ab(n1, n0), ab(n2, n1));
@@ -577,12 +581,18 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
         return;
     }
     const uint32_t r = GENERAL && !COMPDIAG ? tile_misalign(p, t) : 0u;
-    if (r)
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane,
-                                   ShiftPrep{v, r >> 2, r & 3u, lane, ((t.meta & 0xffu) - 1u) >> 1,
-                                             int(((t.meta & 0xffu) - 1u) & 1u) * 32 + 31});
-    else
+    if (r) {
+        const uint32_t b = r & 3u, li = ((t.meta & 0xffu) - 1u) >> 1;
+        const int ll = int(((t.meta & 0xffu) - 1u) & 1u) * 32 + 31;
+        switch (r >> 2) {
+            case 0: tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, ShiftPrep<0>{v, b, lane, li, ll}); break;
+            case 1: tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, ShiftPrep<1>{v, b, lane, li, ll}); break;
+            case 2: tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, ShiftPrep<2>{v, b, lane, li, ll}); break;
+            default: tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, ShiftPrep<3>{v, b, lane, li, ll}); break;
+        }
+    } else {
         tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
+    }
     reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
 }
 
