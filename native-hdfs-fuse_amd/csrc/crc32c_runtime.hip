@@ -293,6 +293,11 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
+        // the mismatch bitmap (one bit per checksum) is cleared after that
+        // wait, so a previous verify still setting bits in it has finished
+        if (p.bad_bits && plan->nchecksums)
+            HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.bad_bits), 0,
+                                      size_t((plan->nchecksums + 31) / 32), stream));
     }
     return launch(plan->ctx, p, plan->sched, stream);
 }
@@ -745,9 +750,6 @@ int crc32c_plan_verify_bitmap(crc32c_plan *plan, const void *dev_payload, const 
     DeviceGuard guard(plan->ctx->device);
     const hipStream_t s = static_cast<hipStream_t>(stream);
     const DevicePlan &dp = plan->dp;
-    if (dev_bad_bits && plan->nchecksums)  // one bit per checksum, cleared in stream order
-        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_bad_bits), 0,
-                                  size_t((plan->nchecksums + 31) / 32), s));
     if (uint64_t(dp.ntiles) + dp.ngen + dp.nseg + dp.nconst == 0) {  // nothing to compare: set the result directly
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result), 0, 1, s));
         HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(dev_result + 1), 0xffffffff, 1, s));

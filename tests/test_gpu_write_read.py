@@ -444,7 +444,8 @@ def test_verify_bitmap_every_item_kind(hdfs, gpu_ctx, orc):
     exp = want.copy()
     for i in sorted(bad)[::2]:
         exp[i] ^= np.uint32(1 << int(rng.integers(0, 32)))
-    for i in sorted(bad)[1::2]:  # the rest by a flipped payload byte inside that checksum's chunk
+    payload_bad = set(sorted(bad)[1::2])
+    for i in sorted(payload_bad):  # the rest by a flipped payload byte inside that checksum's chunk
         p = int(np.searchsorted(pk["out_idx"], i, side="right") - 1)
         k = i - int(pk["out_idx"][p])
         lo = k * int(pk["bpc"][p])
@@ -452,6 +453,25 @@ def test_verify_bitmap_every_item_kind(hdfs, gpu_ctx, orc):
         dev[int(pk["payload_off"][p]) + int(rng.integers(lo, hi))] ^= 0x40
     (cnt, first), idx = _bitmap_verify(plan, exp, s, dev.data_ptr())
     assert set(idx.tolist()) == bad and cnt == len(bad) and first == min(bad)
+    # one bitmap reused by back-to-back verifies on two streams: the second
+    # clears it only after the first (which sets other bits) has finished
+    exp_a = torch.from_numpy(exp.view(np.int32).copy()).cuda()
+    exp_b = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    exp_b[n - 1] ^= 1
+    bits = torch.zeros((n + 31) // 32, dtype=torch.int32, device="cuda")
+    res_a = torch.zeros(2, dtype=torch.int32, device="cuda")
+    res_b = torch.zeros(2, dtype=torch.int32, device="cuda")
+    s2 = torch.cuda.Stream()
+    for _ in range(3):
+        plan.verify(dev.data_ptr(), exp_a.data_ptr(), res_a.data_ptr(), s.cuda_stream, dev_bad_bits=bits.data_ptr())
+        plan.verify(dev.data_ptr(), exp_b.data_ptr(), res_b.data_ptr(), s2.cuda_stream,
+                    dev_bad_bits=bits.data_ptr())
+        torch.cuda.synchronize()
+        b = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:n]
+        want_b = sorted(payload_bad | {n - 1})  # the payload is still corrupted
+        assert np.flatnonzero(b).tolist() == want_b
+        assert res_b.cpu().numpy().view(np.uint32).tolist() == [len(want_b), want_b[0]]
+        assert res_a.cpu().numpy().view(np.uint32).tolist() == [len(bad), min(bad)]
     plan.close()
     # buffer-list write plan: TRUNCATE | NULLPADDING | THEDATA | TRAILINGDATA
     bufs, devs, stream_bytes = _fuse_write_buffers(torch, rng, [10000, 300000, 1 << 20, 77777],
