@@ -22,6 +22,7 @@ import argparse
 import glob
 import importlib.util
 import json
+import math
 import os
 import sys
 import time
@@ -142,7 +143,11 @@ def cpu_baseline(pk, payload_np: np.ndarray, seconds: float, nbuf: int = 4):
     nbytes = int(pk["len"].astype(np.int64).sum())
     ncpu = os.cpu_count() or 1
     sockets = host_sockets()
-    counts = sorted({1, max(1, ncpu // sockets), ncpu})
+    quota = cpu_quota()[1]
+    # full width, one socket, one core -- and, under a cgroup CPU quota, as
+    # many threads as the quota's CPUs (more threads than that only share the
+    # same CPU time)
+    counts = sorted({1, max(1, ncpu // sockets), ncpu} | ({max(1, min(ncpu, int(math.ceil(quota))))} if quota else set()))
     res = {}
     try:
         impl = oracle_mod.Reference()
@@ -166,11 +171,18 @@ def cpu_baseline(pk, payload_np: np.ndarray, seconds: float, nbuf: int = 4):
             cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), "")
     except Exception:
         pass
+    # The baseline is the best rate over the thread counts tried (never the
+    # understated one): on a box whose cgroup quota lends fewer CPUs' time
+    # than it shows, full width oversubscribes that time.
+    best = max(res, key=lambda t: res[t])
     return {
-        "value": round(res[ncpu], 3), "unit": "GiB/s", "cores": ncpu, "kind": kind,
+        "value": round(res[best], 3), "unit": "GiB/s", "cores": best, "kind": kind,
         "sample": "%s: the config batch (%d packets, %.0f MiB) in %d distinct first-touched host copies rotated "
-                  "per pass (DRAM-streaming), ~%.0fs per thread count; reference crc32c.c built -O2 (its Makefile "
-                  "builds -O0)" % (kind, pk.size, nbytes / 2**20, nbuf if kind == "reference" else 1, seconds),
+                  "per pass (DRAM-streaming), ~%.0fs per thread count, best of %s threads; reference crc32c.c "
+                  "built -O2 (its Makefile builds -O0)"
+                  % (kind, pk.size, nbytes / 2**20, nbuf if kind == "reference" else 1, seconds,
+                     "/".join(str(t) for t in counts)),
+        "full_width_gib_s": round(res[ncpu], 3),
         "per_threads_gib_s": {str(t): round(v, 3) for t, v in res.items()},
         "one_core_gib_s": round(res[1], 3), "one_socket_gib_s": round(res[max(1, ncpu // sockets)], 3),
         "host_cpus": ncpu, "sockets": sockets, "cpu_model": cpu_model,
