@@ -47,3 +47,29 @@ def test_c_caller_gpu(length, blockoffset, bpc):
     the framed prefixes carry them, verification finds 0 and then exactly
     the one flipped checksum."""
     _run([length, blockoffset, bpc], 120)
+
+
+FUSE_EXE = os.path.join(ROOT, "examples", "fuse_write")
+# (TRUNCATE, NULLPADDING, THEDATA, TRAILINGDATA lengths, blockoffset, bpc):
+# hadoop_fuse_write's four buffers (fuse.c:1348-1354) in the shapes a write
+# into an existing block, a write past EOF, a plain block write and a small
+# random write produce; packet cutting from a block offset off a chunk
+# boundary; bpc 1536.
+FUSE_CASES = [(10000, 300000, 1 << 20, 77777, 0, 512), (0, 0, 4 << 20, 0, 0, 512),
+              (5000, 20000, 200000, 3000, 1037, 512), (12345, 0, 100000, 0, 1536 * 3, 1536),
+              (3, 1, 700, 5, 0, 512), (0, 4096, 0, 0, 0, 512)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", FUSE_CASES)
+def test_c_caller_fuse_write_buffers(case):
+    """examples/fuse_write.c: the FUSE write path from C with the buffers in
+    device memory -- crc32c_plan_create_buffers / exec / verify_bitmap --
+    exact against crc32c() per chunk over the host-assembled stream, the
+    bitmap naming exactly the flipped checksums, and an all-NULL ftruncate
+    extension giving the zero-chunk constant."""
+    if not os.path.exists(FUSE_EXE):
+        pytest.fail(FUSE_EXE + " is not built (run __graft_entry__.build())")
+    r = subprocess.run([FUSE_EXE] + [str(a) for a in case], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok:"), r.stdout
