@@ -98,6 +98,8 @@ constexpr int kModeEarly = 1024;    // the first tile's loads are issued before 
 constexpr int kModeHalves = 16384;  // A/B: with kModeQuarter, 2 units of 8 blocks per tile instead of 4
 constexpr int kModeQuarter = 4096;  // small batches: power-of-two tiles of chunks <= 2 KiB run as 4 work
                                     // units of 4 blocks each (4x the waves, 1/4 of each wave's latency chain)
+constexpr int kModeXcdMap = 2048;   // A/B: workgroup ranges remapped so that each XCD's workgroups hold one
+                                    // contiguous 1/8 of the batch (instead of every eighth range)
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
 
@@ -696,6 +698,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
+    constexpr bool XCDMAP = (MODE & kModeXcdMap) != 0;
     constexpr int SPLIT = (MODE & kModeHalves) ? 2 : 4;  // units per tile
     constexpr int AUX = NT ? 2 : 0;
     constexpr uint32_t kWaves = THREADS / 64;
@@ -719,8 +722,12 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     // wv starts on tile tbeg + wv; the LDS counter hands out the rest.
     // (QUARTER: units, 4 per tile)
     const uint64_t nunits = QUARTER ? uint64_t(SPLIT) * p.ntiles : uint64_t(p.ntiles);
-    const uint32_t tbeg = uint32_t((nunits * blockIdx.x) / gridDim.x);
-    const uint32_t tend = uint32_t((nunits * (blockIdx.x + 1)) / gridDim.x);
+    // (XCDMAP: workgroup b runs on XCD b % 8; give XCD x the contiguous ranges
+    // x * G/8 .. (x + 1) * G/8 - 1)
+    const uint32_t rng = XCDMAP && (gridDim.x % 8u) == 0 ? (blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u
+                                                         : blockIdx.x;
+    const uint32_t tbeg = uint32_t((nunits * rng) / gridDim.x);
+    const uint32_t tend = uint32_t((nunits * (rng + 1)) / gridDim.x);
     if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
     if (threadIdx.x == 0) {
         *pool_ctr = tbeg + kWaves;

@@ -52,6 +52,8 @@ constexpr Variant kVariants[] = {
     {55, "s4c_nt_quarter_early_stamps_prodgrid", 768, 1, true, true},  // 52 with per-wave timestamps
     {60, "s4c_nt_halves_prodgrid", 768, 1, true, true},    // 51 with 2 units of 8 blocks per tile
     {61, "s4_nt_halves_prodgrid", 768, 1, true, true},     // the same on the full image
+    {62, "s4_nt_pow2only_prodgrid", 768, 1, true, true},   // the production power-of-two build (no general code)
+    {63, "s4_nt_pow2only_xcdmap_prodgrid", 768, 1, true, true},  // 62, each XCD's ranges contiguous
 };
 
 const Variant *find(int v) {
@@ -97,6 +99,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 55: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeEarly | kModeStamps); break;
     case 60: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeQuarter | kModeHalves); break;
     case 61: HDFS_LAUNCH(768, 3, kS4Nt | kModeQuarter | kModeHalves); break;
+    case 62: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt); break;
+    case 63: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeXcdMap); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
