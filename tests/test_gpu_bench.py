@@ -18,7 +18,15 @@ import pytest
 
 from conftest import ROOT
 
-pytestmark = pytest.mark.gpu
+# (generous limits: on a fresh box the first torch import pages the image in)
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(400)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _torch_paged_in():
+    import torch  # the children's imports then read a warm page cache
+
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
 
 
 def _line(out: str) -> dict:
@@ -29,7 +37,7 @@ def _line(out: str) -> dict:
 
 def test_bench_one_gpu_contract():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "200", "--warmup", "20",
-                        "--no-cpu", "--no-host"], cwd=ROOT, capture_output=True, text=True, timeout=110)
+                        "--no-cpu", "--no-host"], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["steps"] == 200 and d["unit"] == "GiB/s" and d["higher_is_better"]
@@ -48,7 +56,7 @@ def test_bench_two_ranks_rehearsal(config):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "20", "--warmup", "5", "--config", config, "--no-cpu", "--nbuf", "2"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=115)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
