@@ -59,6 +59,35 @@ Gf2Op op_zeros(uint64_t nbytes, uint32_t poly) {
     return acc;
 }
 
+namespace {
+// a * b mod P in the register's reflected representation (bit 31 = x^0).
+uint32_t mulmod(uint32_t a, uint32_t b, uint32_t poly) {
+    uint32_t p = 0;
+    for (uint32_t m = 1u << 31; m; m >>= 1) {
+        if (a & m) p ^= b;
+        b = (b & 1u) ? (b >> 1) ^ poly : b >> 1;
+    }
+    return p;
+}
+struct PowTable {  // x^(2^k) mod P, k = 0..63
+    uint32_t t[64];
+    explicit PowTable(uint32_t poly) {
+        t[0] = 1u << 30;  // x^1
+        for (int k = 1; k < 64; ++k) t[k] = mulmod(t[k - 1], t[k - 1], poly);
+    }
+};
+}  // namespace
+
+uint32_t shift_zeros(uint32_t reg, uint64_t nbytes, uint32_t poly) {
+    static const PowTable c(kPoly), ieee(kPolyIeee);
+    const PowTable &pt = poly == kPolyIeee ? ieee : c;
+    // x^(8 n) = product of x^(2^k) over the set bits k of 8 n
+    uint32_t x = 1u << 31;  // x^0
+    for (int k = 3; nbytes && k < 64; ++k, nbytes >>= 1)
+        if (nbytes & 1u) x = mulmod(pt.t[k], x, poly);
+    return mulmod(x, reg, poly);
+}
+
 uint32_t lin_bytes(const uint8_t *p, size_t n, uint32_t reg, uint32_t poly) {
     const uint32_t *t = byte_table(poly);
     for (size_t i = 0; i < n; ++i) reg = (reg >> 8) ^ t[(reg ^ p[i]) & 0xffu];

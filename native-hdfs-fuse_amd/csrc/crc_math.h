@@ -33,6 +33,10 @@ uint32_t append_zero_byte(uint32_t reg, uint32_t poly = kPoly);  // linear regis
 Gf2Op op_identity();
 Gf2Op op_compose(const Gf2Op &a, const Gf2Op &b);           // a after b
 Gf2Op op_zeros(uint64_t nbytes, uint32_t poly = kPoly);      // append nbytes zero bytes
+// The register after nbytes zero bytes, as op_zeros(nbytes).apply(reg) but
+// in O(log nbytes) 32-step products (reg * x^(8 nbytes) mod P) instead of
+// 32x32 operator compositions: what plan building uses per zero-fill chunk.
+uint32_t shift_zeros(uint32_t reg, uint64_t nbytes, uint32_t poly = kPoly);
 
 // Linear part of the CRC over bytes with register starting at 0 (no
 // conditioning): crc(0, M) == lin(M) ^ crc(0, zeros(len)).

@@ -129,22 +129,32 @@ struct ZeroCrc {
     uint32_t last_len = 0, last = 0;
     uint32_t operator()(uint32_t n) {
         if (n != last_len || !last_len) {
-            last = op_zeros(n, poly).apply(0xffffffffu) ^ 0xffffffffu;
+            last = shift_zeros(0xffffffffu, n, poly) ^ 0xffffffffu;
             last_len = n;
         }
         return last;
     }
 };
 
-void push_const(HostPlan *plan, uint64_t out, uint32_t value) {
-    if (!plan->consts.empty()) {
-        ConstRun &r = plan->consts.back();
-        if (r.value == value && uint64_t(r.out) + r.count == out && r.count < kConstRunMax) {
-            ++r.count;
-            return;
+// n consecutive checksums out .. out + n - 1 of one constant value: extends
+// the last run where it continues it, in runs of at most kConstRunMax.
+void push_const(HostPlan *plan, uint64_t out, uint32_t value, uint64_t n = 1) {
+    while (n) {
+        if (!plan->consts.empty()) {
+            ConstRun &r = plan->consts.back();
+            if (r.value == value && uint64_t(r.out) + r.count == out && r.count < kConstRunMax) {
+                const uint64_t k = std::min<uint64_t>(n, kConstRunMax - r.count);
+                r.count += uint32_t(k);
+                out += k;
+                n -= k;
+                continue;
+            }
         }
+        const uint64_t k = std::min<uint64_t>(n, kConstRunMax);
+        plan->consts.push_back(ConstRun{uint32_t(out), uint32_t(k), value, 0u});
+        out += k;
+        n -= k;
     }
-    plan->consts.push_back(ConstRun{uint32_t(out), 1u, value, 0u});
 }
 
 }  // namespace
@@ -201,8 +211,7 @@ int build_write_plan(const crc32c_buffer *buffers, uint32_t n_buffers, uint64_t 
                     }
                 } else {
                     if (int rc = flush()) return rc;
-                    const uint32_t z = zero(bpc);
-                    for (uint64_t k = 0; k < nf; ++k) push_const(plan, out + c + k, z);
+                    push_const(plan, out + c, zero(bpc), nf);
                 }
                 c += nf - 1;
                 continue;

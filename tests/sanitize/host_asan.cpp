@@ -381,6 +381,26 @@ void table_images() {
     std::free(img);
 }
 
+// shift_zeros (register * x^(8 n) mod P, what plan building uses for
+// zero-fill constants) equals the 32x32 operator op_zeros(n) for both
+// polynomials: every n below 1100, powers of two and random n up to 2^40.
+void zero_shifts(std::mt19937_64 &rng) {
+    for (uint32_t poly : {hdfs_crc::kPoly, hdfs_crc::kPolyIeee}) {
+        std::vector<uint64_t> ns;
+        for (uint64_t n = 0; n < 1100; ++n) ns.push_back(n);
+        for (int k = 0; k < 41; ++k) ns.push_back(uint64_t(1) << k);
+        for (int i = 0; i < 60; ++i) ns.push_back(rng() % (uint64_t(1) << 40));
+        for (uint64_t n : ns) {
+            const uint32_t r = uint32_t(rng());
+            const hdfs_crc::Gf2Op op = hdfs_crc::op_zeros(n, poly);
+            CHECK(hdfs_crc::shift_zeros(r, n, poly) == op.apply(r), "shift_zeros(%08x, %llu) poly %08x", r,
+                  (unsigned long long)n, poly);
+            CHECK(hdfs_crc::shift_zeros(0xffffffffu, n, poly) == op.apply(0xffffffffu), "shift_zeros(~0, %llu)",
+                  (unsigned long long)n);
+        }
+    }
+}
+
 }  // namespace
 
 int main() {
@@ -391,6 +411,7 @@ int main() {
     write_plans(rng);
     frames_parse(rng);
     table_images();
+    zero_shifts(rng);
     if (g_fail) {
         std::fprintf(stderr, "%d failures\n", g_fail);
         return 1;
