@@ -339,6 +339,33 @@ def test_multi_single_device(hdfs, orc):
     m.close()
 
 
+def test_multi_batch_host_dealt_over_contexts(hdfs, orc):
+    """crc32c_multi_batch_host's dealing (round-robin groups of packets, one
+    host thread and pipeline per device) on real launches: three contexts on
+    the box's one GPU stand in for three devices.  A config-4-shaped file
+    (32 x 4 MiB blocks) plus ragged blocks, a short last group, bpc 1536
+    packets and an unaligned packet, from pinned and pageable memory, equal
+    the oracle; group sizes 64 and 3."""
+    torch = _torch()
+    m = hdfs.Multi([0, 0, 0])
+    try:
+        pk = oracle.uniform_packets(32 * 64 + 37)
+        rng = np.random.default_rng(4)
+        pk["len"][rng.choice(pk.size, 40, replace=False)] = rng.integers(1, 65536, 40).astype(np.uint32)
+        pk["bpc"][5::97] = 1536
+        pk["payload_off"][1000:] += np.uint64(3)  # every packet from here on off 16-byte alignment
+        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 44)
+        want = orc.batch(payload, pk, hdfs.total_checksums(pk))
+        pinned = torch.from_numpy(payload).pin_memory()
+        for group in (64, 3):
+            assert np.array_equal(m.batch_host(payload, pk, group_packets=group), want), group
+            assert np.array_equal(m.batch_host(pinned.numpy(), pk, group_packets=group), want), group
+    finally:
+        m.close()
+
+
 def test_full_size_c2_against_reference_and_properties(hdfs, gpu_ctx, orc):
     """Config 2 at full size: bit-exact against the oracle, plus the
     size-independent properties (CRC of zero and 0xFF chunks, chunk-shift
