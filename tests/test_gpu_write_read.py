@@ -486,3 +486,83 @@ def test_verify_bitmap_every_item_kind(hdfs, gpu_ctx, orc):
     (cnt, first), idx = _bitmap_verify(wplan, exp, s)
     assert idx.tolist() == bad and cnt == len(bad) and first == 0
     wplan.close()
+
+
+# ---- an fsx-style sequence of writes (the reference's only integration test) ----
+def test_fsx_style_write_sequence(hdfs, gpu_ctx, orc):
+    """README.md:35-39's manual test runs fsx against a MiniCluster so that
+    writes span many blocks.  Here: 60 random file operations on a model
+    file (appends, writes inside the last block, writes past EOF, writes
+    into earlier blocks, ftruncate extensions and shrinks), each turned into
+    hadoop_fuse_write's buffers (fuse.c:1348-1480: TRUNCATE, NULLPADDING,
+    THEDATA, TRAILINGDATA) and hadoop_fuse_do_write's block writes
+    (fuse.c:466-647: the block under construction from its offset, then new
+    blocks from 0, bufferoffset advancing), every block write checksummed by
+    one crc32c_plan_create_buffers plan over the device buffers and compared
+    with the oracle over the bytes it sends.  256 KiB blocks, so writes span
+    many of them."""
+    torch = _torch()
+    s = torch.cuda.current_stream()
+    rng = np.random.default_rng(0xF5)
+    B, P = 256 << 10, 65536
+    f = np.zeros(0, np.uint8)
+    nwrites = 0
+    for op in range(60):
+        L = f.size
+        kind = rng.choice(["append", "last_block", "past_eof", "earlier", "extend", "shrink"],
+                          p=[0.3, 0.15, 0.15, 0.2, 0.1, 0.1])
+        if kind == "shrink":
+            f = f[:int(rng.integers(0, L + 1))]
+            continue
+        data = oracle.xorshift64_bytes(int(rng.integers(1, 700000)), 1000 + op)
+        last = (L - 1) // B * B if L else 0
+        if kind == "append":
+            off = L
+        elif kind == "last_block":
+            off = int(rng.integers(last, L + 1))
+        elif kind == "past_eof":
+            off = L + int(rng.integers(1, 300000))
+        elif kind == "earlier":
+            off = int(rng.integers(0, max(last, 1)))
+        else:  # ftruncate extension: a NULL buffer from EOF
+            off, data = L, None
+        parts = []  # (host bytes, is_null)
+        if kind == "extend":
+            parts.append((np.zeros(int(rng.integers(1, 900000)), np.uint8), True))
+            start = L
+        elif off < last:  # into an earlier block: keep its head, rewrite from there, re-append the tail
+            start = off // B * B
+            parts.append((f[start:off], False))
+            parts.append((data, False))
+            if off + data.size < L:
+                parts.append((f[off + data.size:], False))
+        else:
+            start = min(off, L)
+            if off > L:
+                parts.append((np.zeros(off - L, np.uint8), True))
+            parts.append((data, False))
+        bufs, devs = [], []
+        for host, is_null in parts:
+            if is_null:
+                bufs.append((0, host.size))
+                continue
+            skew = int(rng.integers(0, 16))
+            t = torch.zeros(host.size + 32, dtype=torch.uint8, device="cuda")
+            t[skew:skew + host.size].copy_(torch.from_numpy(np.ascontiguousarray(host)))
+            devs.append(t)
+            bufs.append((t.data_ptr() + skew, host.size))
+        stream_bytes = np.concatenate([h for h, _ in parts]) if parts else np.zeros(0, np.uint8)
+        # hadoop_fuse_do_write: the block under construction from its offset, then new blocks
+        total, boff, pos = stream_bytes.size, start % B, 0
+        while pos < total:
+            n = min(B - boff, total - pos)
+            plan = gpu_ctx.write_plan(bufs, pos, n, boff, P, 512)
+            want = _expected_write(orc, stream_bytes, pos, n, boff, P, 512)
+            assert plan.nchecksums == want.size, (op, kind, pos, n, boff)
+            assert np.array_equal(_run_plan(plan, want.size, s), want), (op, kind, pos, n, boff)
+            plan.close()
+            nwrites += 1
+            pos += n
+            boff = 0
+        f = np.concatenate([f[:start], stream_bytes])
+    assert nwrites > 60
