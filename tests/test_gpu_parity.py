@@ -780,3 +780,53 @@ def test_fuzz_mixed_batches(hdfs, gpu_ctx, orc, seed):
         stream.synchronize()
         assert res.cpu().numpy().view(np.uint32).tolist() == [1, bad], size
         plan.close()
+
+
+def test_entry_points_reject_bad_arguments(hdfs, gpu_ctx):
+    """The C ABI's argument checks on the GPU path: -EINVAL (never a launch)
+    for NULL plans / results / expected arrays, unknown flags, bpc 0, a
+    checksum range past 2^32, a buffer-list range past its buffers, and a
+    device-address plan given a payload pointer."""
+    import ctypes
+    import errno
+
+    torch = _torch()
+    L = hdfs.lib()
+    vp = ctypes.c_void_p
+    pk = oracle.uniform_packets(2)
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.zeros(2 * 65536, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    exp = torch.zeros(256, dtype=torch.int32, device="cuda")
+    bits = torch.zeros(8, dtype=torch.int32, device="cuda")
+    inval = -errno.EINVAL
+    assert L.crc32c_plan_verify_bitmap(None, vp(dev.data_ptr()), vp(exp.data_ptr()), vp(res.data_ptr()),
+                                       vp(bits.data_ptr()), None) == inval
+    assert L.crc32c_plan_verify_bitmap(plan.handle, vp(dev.data_ptr()), vp(exp.data_ptr()), None,
+                                       vp(bits.data_ptr()), None) == inval
+    assert L.crc32c_plan_verify_bitmap(plan.handle, vp(dev.data_ptr()), None, vp(res.data_ptr()),
+                                       vp(bits.data_ptr()), None) == inval
+    assert L.crc32c_plan_exec(None, vp(dev.data_ptr()), vp(exp.data_ptr()), None) == inval
+    plan.close()
+    bad = pk.copy()
+    bad["bpc"][1] = 0
+    with pytest.raises(hdfs.Crc32cError) as e:
+        hdfs.Plan(gpu_ctx, bad)
+    assert e.value.rc == inval
+    bad = pk.copy()
+    bad["out_idx"][1] = (1 << 32) - 10
+    with pytest.raises(hdfs.Crc32cError):
+        hdfs.Plan(gpu_ctx, bad)
+    with pytest.raises(hdfs.Crc32cError) as e:
+        hdfs.Plan(gpu_ctx, pk, 1 << 30)  # unknown flag
+    assert e.value.rc == inval
+    with pytest.raises(hdfs.Crc32cError) as e:
+        gpu_ctx.write_plan([(dev.data_ptr(), 1000)], 10, 1000)  # past the buffers
+    assert e.value.rc == inval
+    aplan = hdfs.Plan(gpu_ctx, np.array([(dev.data_ptr(), 0, 512, 512)], hdfs.PACKET_DTYPE),
+                      hdfs.CRC32C_DEVICE_ADDRESSES)
+    with pytest.raises(hdfs.Crc32cError):
+        aplan.exec(dev.data_ptr(), exp.data_ptr(), 0)  # a device-address plan takes payload NULL
+    aplan.exec(0, exp.data_ptr(), 0)
+    torch.cuda.synchronize()
+    aplan.close()
