@@ -86,7 +86,8 @@ def _worker(rank: int, world: int, port: int, nblocks: int, bpc: int, ragged: bo
 
 
 @pytest.mark.parametrize("world,nblocks,bpc,ragged", [(2, 7, 512, False), (2, 2, 4096, True), (3, 8, 512, True),
-                                                      (2, 1, 512, False), (3, 5, 1536, True)])
+                                                      (2, 1, 512, False), (3, 5, 1536, True),
+                                                      (8, 32, 512, False), (8, 11, 512, True)])
 def test_round_robin_gather_matches_oracle(tmp_path, world, nblocks, bpc, ragged):
     import oracle
 
