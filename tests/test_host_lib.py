@@ -70,6 +70,20 @@ def test_product_library_has_no_variant_switch(hdfs):
     assert len(set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", dblob))) >= 9
 
 
+def test_product_library_does_not_use_the_oracle(hdfs):
+    """The checker never ships: the product library (and the debug library
+    built beside it) neither links nor names anything under oracle/ -- no
+    oracle / reference-harness symbol, no oracle library in NEEDED."""
+    import subprocess
+
+    for path in (hdfs.LIB_PATH, hdfs.DEBUG_LIB_PATH):
+        blob = open(path, "rb").read()
+        for marker in (b"oracle_batch", b"oracle_crc32c", b"ref_batch", b"liboracle", b"crc32c_oracle", b"oracle/_ref"):
+            assert marker not in blob, (path, marker)
+        needed = subprocess.run(["readelf", "-d", path], capture_output=True, text=True).stdout
+        assert "oracle" not in needed and "_ref" not in needed, needed
+
+
 def test_scalar_dropin_known_answers(hdfs, golden):
     for e in golden["known_answers"]["published"]:
         assert "%08x" % hdfs.crc32c(bytes.fromhex(e["hex"])) == e["crc"]
