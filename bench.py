@@ -11,9 +11,13 @@ served from the 256 MiB Infinity Cache.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
 
-N > 1 is launched by torch.distributed.run (one rank per GPU).  After the
-timed region the ranks' checksum arrays are gathered to rank 0 over RCCL
-(the only collective; timed separately as "gather_ms").
+N > 1 runs one rank per GPU.  Launched by torch.distributed.run (WORLD_SIZE
+set, as the driver does) every process is one rank; launched plainly with
+--gpus N > 1 this process starts torch.distributed.run with N ranks as a
+child process (before any GPU call; never an exec), forwards its output and
+exits with its return code.  After the timed region the ranks' checksum
+arrays are gathered to rank 0 over RCCL (the only collective of configs 2/5;
+timed separately as "gather_ms"; config 4 gathers inside every step).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -190,6 +194,38 @@ def cpu_baseline(pk, payload_np: np.ndarray, seconds: float, nbuf: int = 4):
     }
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: N ranks under torch.distributed.run,
+    started as a child process before this process touches the GPU.  Their
+    stdout / stderr are this process's (rank 0's JSON line comes through
+    unchanged); the return code is the launcher's."""
+    import subprocess
+
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        # (counting devices does not initialise the GPU on this image)
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            print("bench.py: --gpus %d needs %d visible GPUs for one RCCL rank per GPU, found %d "
+                  "(BENCH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)" % (args.gpus, args.gpus, ndev),
+                  file=sys.stderr, flush=True)
+            return 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,6 +250,15 @@ def main():
     ap.add_argument("--host-multi-devices", type=int, default=1,
                     help="GPUs crc32c_multi_batch_host deals the host-resident batch over at N = 1 (0: skip)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        print("bench.py: WORLD_SIZE=%s but --gpus %d: the launcher and the flag disagree"
+              % (os.environ["WORLD_SIZE"], args.gpus), file=sys.stderr, flush=True)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -225,8 +270,13 @@ def main():
     # rehearses the N > 1 path with ranks sharing the visible GPUs (their
     # collectives then go through host memory); never used for a measurement.
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
     if backend != "nccl":
-        local_rank = local_rank % max(1, torch.cuda.device_count())
+        local_rank = local_rank % max(1, ndev)
+    elif local_rank >= ndev:
+        print("bench.py: rank %d (local rank %d) has no GPU of its own: %d visible; one RCCL rank per GPU"
+              % (rank, local_rank, ndev), file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local_rank)
     if world > 1:
         if backend == "nccl":
@@ -280,7 +330,9 @@ def main():
         plan = ctx.plan(pk)
     dev = torch.device("cuda", local_rank)
     # buffer 0: PCG64 host bytes (checked against the CPU
-    # path below); the rest: device-generated random bytes.
+    # path below); the rest: device-generated random bytes.  Config 4:
+    # buffer b is this rank's shard of the PCG64 file of seed 2024 + b, so
+    # rank 0 can rebuild whichever file a timed step checksummed.
     if c4:
         payload0 = shard.rank_payload(file_bytes, lay, shard_sizes, rank)
         extent = payload0.size
@@ -290,8 +342,13 @@ def main():
     bufs = [torch.from_numpy(payload0).to(dev)]
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    for _ in range(1, nbuf):
-        bufs.append(torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g))
+    for b in range(1, nbuf):
+        if c4:
+            fb = synthetic_bytes(32 * shard.BLOCK_BYTES, 2024 + b)
+            bufs.append(torch.from_numpy(shard.rank_payload(fb, lay, shard_sizes, rank)).to(dev))
+            del fb
+        else:
+            bufs.append(torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g))
     outs = [torch.zeros(max(nout, 1), dtype=torch.int32, device=dev) for _ in range(nbuf)]
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -315,6 +372,7 @@ def main():
         want = reference_checksums(payload0, pk, nout)
         got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
         bit_exact = bool(np.array_equal(got0, want))
+    gate_exact = bit_exact
 
     for i in range(args.warmup):
         step(i)
@@ -344,6 +402,11 @@ def main():
         except RuntimeError as e:  # no graph on this stack: time host-issued launches instead
             graph, use_graph, graph_error = None, False, str(e)[:200]
             torch.cuda.synchronize()
+    # Outputs cleared before the timed region (untimed), so the checks after
+    # it see only what the timed launches wrote.
+    for o in ([root_out] if c4 else outs):
+        o.zero_()
+    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -364,6 +427,28 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)  # avg per launch, on the launch stream
+
+    # Correctness of the timed launches themselves (outside the timed region):
+    # configs 2/3/5 -- the checksums the last timed launch on buffer 0 (PCG64
+    # host bytes) and on buffer 1 (device random bytes, copied back) wrote,
+    # against the reference's crc32c.c; config 4 -- the file-order array the
+    # last timed step gathered on rank 0, against the reference over the file
+    # that step checksummed.
+    timed_checks = {}
+    b_last = (args.steps - 1) % nbuf
+    if c4:
+        if rank == 0 and args.steps > 0:
+            fb = file_bytes if b_last == 0 else synthetic_bytes(32 * shard.BLOCK_BYTES, 2024 + b_last)
+            wb = want if b_last == 0 else reference_checksums(fb, file_pk, mplan.nchecksums)
+            timed_checks["timed_file_buf%d" % b_last] = bool(
+                np.array_equal(root_out.cpu().numpy().view(np.uint32)[:mplan.nchecksums], wb))
+    elif args.steps > 0:
+        timed_checks["timed_buf0"] = bool(np.array_equal(outs[0].cpu().numpy().view(np.uint32)[:nout], want))
+        if nbuf > 1 and args.steps > 1:
+            w1 = reference_checksums(bufs[1].cpu().numpy(), pk, nout)
+            timed_checks["timed_buf1_device_random"] = bool(
+                np.array_equal(outs[1].cpu().numpy().view(np.uint32)[:nout], w1))
+    timed_exact = all(timed_checks.values())
     eager_ms = None
     if use_graph:  # the same steps issued one by one from the host, for comparison
         ne = min(args.steps, 500)
@@ -381,7 +466,7 @@ def main():
         tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(tt[0]), float(tt[1])
-        ok = torch.tensor([1 if bit_exact else 0], dtype=torch.int32, device=cdev)
+        ok = torch.tensor([1 if bit_exact and timed_exact else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         bit_exact = bool(ok.item())
     # Configs 2/5 (weak scaling, independent batches): RCCL gather of every
@@ -540,7 +625,8 @@ def main():
         for _ in range(reps):
             ctx.batch_host(hp, pk, out=hout)
         host = round(world * nbytes * reps / slowest(time.perf_counter() - h0) / GIB, 2)
-        if not np.array_equal(hout[:nout], want):
+        timed_checks["host_resident"] = bool(np.array_equal(hout[:nout], want))
+        if not timed_checks["host_resident"]:
             bit_exact = False
         dst = torch.empty(pinned.numel(), dtype=torch.uint8, device=dev)
         dst.copy_(pinned, non_blocking=True)
@@ -570,6 +656,7 @@ def main():
                     m.batch_host(hp, pk, group_packets=64)
                 host_multi = {"gib_s": round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2),
                               "devices": ndev, "bit_exact": exact_multi, "entry": "crc32c_multi_batch_host"}
+                timed_checks["host_resident_multi"] = exact_multi
                 bit_exact = bit_exact and exact_multi
             finally:
                 m.close()
@@ -607,7 +694,8 @@ def main():
                          "kernel": KERNEL_NAME, "kernel_avg_us": round(kernel_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": nbytes},
             "cpu_baseline": cpu,
-            "bit_exact_vs_reference": bit_exact,
+            "bit_exact_vs_reference": bit_exact and timed_exact,
+            "bit_exact_checks": dict({"before_warmup_buf0": gate_exact}, **timed_checks),
             "host_resident_gib_s": host,
             "host_h2d_copy_gib_s": h2d,
             "host_resident_ranks": world if host is not None else None,

@@ -106,7 +106,11 @@ int crc32c_chunks_cpu(const void *packet, size_t len, uint32_t bpc, uint32_t *ou
 uint64_t crc32c_nchunks(uint64_t len, uint32_t bpc);
 
 /* Length of the checksum array a batch fills: max over packets with len > 0
- * of out_idx + crc32c_nchunks(len, bpc) (0 for none; bpc == 0 counts as 1). */
+ * of out_idx + crc32c_nchunks(len, bpc) (0 for none).  A packet with len == 0
+ * (the block's final empty packet, hadooprpc.c:853-856) has no checksums
+ * whatever its bpc, here and in every batch entry point; a packet with
+ * len > 0 and bpc == 0 is invalid (the batch entry points return -EINVAL) and
+ * counts nothing here. */
 uint64_t crc32c_batch_nchecksums(const crc32c_packet *pkts, size_t npkts);
 
 /* Packet lengths hadoop_rpc_send_packets produces for one block write of
@@ -132,9 +136,17 @@ int crc32c_device_count(void);
  * A plan is built once per batch SHAPE from host packet descriptors (work
  * decomposition into 8 KiB tiles) and executed on any payload with that
  * shape.  Its descriptors go to the device asynchronously (the first launch
- * on a stream waits for that copy); destroying a plan whose launches are
- * still in flight is safe (its device block is recycled only after a later
- * device synchronisation).  Payload and checksum buffers are device
+ * on a stream waits for that copy).  Destroying a plan whose launches are
+ * still in flight is safe: the destroy records an event on every stream the
+ * plan was launched on (so those streams must still exist, or the plan's
+ * block is simply never reused), and its device block is recycled only once
+ * those events have completed -- no device-wide synchronisation on any plan
+ * create / destroy path, so work of other streams and libraries is never
+ * waited on, and plans may be created and destroyed while another thread
+ * captures a graph.  A plan must outlive every HIP graph that captured its
+ * launches (the graph replays read its descriptors); the block of a plan
+ * whose launches were captured is not reused while the context lives.
+ * Payload and checksum buffers are device
  * pointers; execution is asynchronous on `stream` (a hipStream_t, NULL =
  * the default stream).  Exec launches of one plan are not ordered with each
  * other: independent batches may run on several streams at once, and two
@@ -272,6 +284,27 @@ int64_t crc32c_multi_layout(const crc32c_packet *pkts, size_t npkts, uint32_t gr
  * indices unchanged); returns their count (copies at most cap). */
 int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
                                    int rank, crc32c_packet *local, size_t cap);
+
+/* The two halves of crc32c_multi_plan_exec's gather, host only (no GPU), so
+ * that the N-rank exchange can be checked without N GPUs.
+ *
+ * crc32c_multi_rank_packets: the packets rank `rank`'s plan computes --
+ * payload offsets into its shard, out indices into the u32 array it sends to
+ * rank 0 (its groups' checksum ranges back to back, in group order); rank 0's
+ * out indices are the global ones (it writes its groups in place) unless
+ * flags has CRC32C_MULTI_SELF_SEND.  Returns their count (copies at most cap).
+ *
+ * crc32c_multi_gather_plan: local_nout[r] = length of the array rank r sends
+ * (0 for rank 0 in place), staging_off[r] = where rank 0 receives it in its
+ * staging area (both nranks entries, optional), and per received group s
+ * items[3s .. 3s+2] = {index in the staging area, index in the file-order
+ * output, count}.  Returns the number of items (fills at most cap).
+ * crc32c_multi_plan_exec issues exactly these sends, receives and copies. */
+int64_t crc32c_multi_rank_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                                  int rank, uint32_t flags, crc32c_packet *local, size_t cap);
+int64_t crc32c_multi_gather_plan(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                                 uint32_t flags, uint64_t *local_nout, uint64_t *staging_off, uint64_t *items,
+                                 size_t cap);
 
 /* Device-resident multi-GPU plan of a file's packets (offsets in the caller's
  * file layout; every process passes the same list).  Exec: dev_shards[i] =

@@ -159,6 +159,8 @@ def _bind(L):
         "crc32c_multi_sync": (i32, [vp]),
         "crc32c_multi_layout": (ctypes.c_int64, [vp, sz, u32, i32, vp, vp]),
         "crc32c_multi_shard_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, vp, sz]),
+        "crc32c_multi_rank_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, u32, vp, sz]),
+        "crc32c_multi_gather_plan": (ctypes.c_int64, [vp, sz, u32, i32, u32, vp, vp, vp, sz]),
         "crc32c_multi_plan_create": (i32, [vp, vp, sz, u32, u32, pp]),
         "crc32c_multi_plan_exec": (i32, [vp, vp, vp, vp]),
         "crc32c_multi_plan_destroy": (i32, [vp]),
@@ -277,11 +279,7 @@ class Context:
 
     def verify_frames(self, frames: np.ndarray, bpc: int, chunk_offset: int, flags: int = 0) -> FramesResult:
         """crc32c_verify_frames_host over a buffer of received packet frames."""
-        frames = np.ascontiguousarray(frames, dtype=np.uint8)
-        res = FramesResult()
-        _check(lib().crc32c_verify_frames_host(self.handle, _np_ptr(frames), frames.size, bpc, chunk_offset, flags,
-                                               ctypes.byref(res)), "crc32c_verify_frames_host")
-        return res
+        return verify_frames(frames, bpc, chunk_offset, flags, ctx=self)
 
     def batch_host(self, payload: np.ndarray, pkts, flags: int = 0, out: np.ndarray | None = None) -> np.ndarray:
         """Host-resident batch (crc32c_batch_host): H2D copy -> kernel -> checksums in host memory."""
@@ -476,6 +474,44 @@ def multi_shard_packets(pkts, group_packets: int, nranks: int, rank: int) -> np.
     out = np.zeros(max(n, 1), PACKET_DTYPE)
     lib().crc32c_multi_shard_packets(_np_ptr(pkts), pkts.size, group_packets, nranks, rank, _np_ptr(out), n)
     return out[:n]
+
+
+def multi_rank_packets(pkts, group_packets: int, nranks: int, rank: int, flags: int = 0) -> np.ndarray:
+    """crc32c_multi_rank_packets: the packets rank's plan computes (payload offsets into its shard, out
+    indices into the array it sends to rank 0; rank 0's global unless CRC32C_MULTI_SELF_SEND)."""
+    pkts = as_packets(pkts)
+    n = int(lib().crc32c_multi_rank_packets(_np_ptr(pkts), pkts.size, group_packets, nranks, rank, flags, None, 0))
+    if n < 0:
+        _check(n, "crc32c_multi_rank_packets")
+    out = np.zeros(max(n, 1), PACKET_DTYPE)
+    lib().crc32c_multi_rank_packets(_np_ptr(pkts), pkts.size, group_packets, nranks, rank, flags, _np_ptr(out), n)
+    return out[:n]
+
+
+def multi_gather_plan(pkts, group_packets: int, nranks: int, flags: int = 0):
+    """crc32c_multi_gather_plan: (local_nout[nranks], staging_off[nranks], items[S, 3] = {staging index,
+    file index, count}) -- the exchange crc32c_multi_plan_exec performs."""
+    pkts = as_packets(pkts)
+    n = int(lib().crc32c_multi_gather_plan(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, None, None, None,
+                                           0))
+    if n < 0:
+        _check(n, "crc32c_multi_gather_plan")
+    ln = np.zeros(nranks, np.uint64)
+    so = np.zeros(nranks, np.uint64)
+    items = np.zeros((max(n, 1), 3), np.uint64)
+    lib().crc32c_multi_gather_plan(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, _np_ptr(ln), _np_ptr(so),
+                                   _np_ptr(items), n)
+    return ln, so, items[:n]
+
+
+def verify_frames(frames: np.ndarray, bpc: int, chunk_offset: int, flags: int = 0, ctx: Context | None = None):
+    """crc32c_verify_frames_host over a buffer of received packet frames; ctx None (no GPU) needs
+    CRC32C_CPU_FALLBACK."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    res = FramesResult()
+    _check(lib().crc32c_verify_frames_host(None if ctx is None else ctx.handle, _np_ptr(frames), frames.size, bpc,
+                                           chunk_offset, flags, ctypes.byref(res)), "crc32c_verify_frames_host")
+    return res
 
 
 def parse_frames(frames: np.ndarray):

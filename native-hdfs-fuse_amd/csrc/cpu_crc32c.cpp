@@ -215,7 +215,9 @@ extern "C" uint64_t crc32c_batch_nchecksums(const crc32c_packet *pkts, size_t np
     uint64_t n = 0;
     for (size_t i = 0; pkts && i < npkts; ++i)
         if (pkts[i].len) {
-            const uint64_t end = pkts[i].out_idx + crc32c_nchunks(pkts[i].len, pkts[i].bpc ? pkts[i].bpc : 1);
+            // (len > 0 with bpc == 0 is an invalid packet, which every batch
+            // entry point refuses with -EINVAL; it counts nothing here)
+            const uint64_t end = pkts[i].out_idx + crc32c_nchunks(pkts[i].len, pkts[i].bpc);
             if (end > n) n = end;
         }
     return n;

@@ -78,8 +78,8 @@ int build_layout(const crc32c_packet *pkts, size_t npkts, uint32_t gp, int nrank
         std::vector<std::pair<uint64_t, uint64_t>> outs;  // (out_idx, checksums) of its packets
         for (size_t i = g * gp; i < std::min<size_t>(npkts, (g + 1) * gp); ++i) {
             const crc32c_packet &p = pkts[i];
+            if (!p.len) continue;  // (no checksums, whatever its bpc)
             if (p.bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
-            if (!p.len) continue;
             const uint64_t c = crc32c_nchunks(p.len, p.bpc);
             lo = std::min(lo, p.payload_off);
             hi = std::max(hi, p.payload_off + p.len);
@@ -125,6 +125,44 @@ void shard_packets(const crc32c_packet *pkts, size_t npkts, uint32_t gp, const s
     }
 }
 
+// The gather step of a plan: what each rank's local array holds, where
+// rank 0's staging area receives it, and the scatter items that move every
+// received group into file order.  Rank 0's own groups are computed in place
+// (no transfer) unless self_send.  crc32c_multi_plan_create builds its
+// device plan from exactly this; crc32c_multi_gather_plan exports it.
+struct Gather {
+    std::vector<uint64_t> staging_off;  // per rank
+    std::vector<uint64_t> items;        // 3 per received group: {staging index, file index, count}
+    uint64_t staging_total = 0;
+};
+
+bool sends(int rank, bool self_send) { return rank != 0 || self_send; }
+
+void build_gather(const std::vector<Group> &groups, const std::vector<uint64_t> &local_nout, int nranks,
+                  bool self_send, Gather *g) {
+    g->staging_off.assign(size_t(nranks), 0);
+    g->items.clear();
+    uint64_t total = 0;
+    for (int r = 0; r < nranks; ++r) {
+        g->staging_off[size_t(r)] = total;
+        if (sends(r, self_send)) total += local_nout[size_t(r)];
+    }
+    g->staging_total = total;
+    for (const Group &G : groups)
+        if (G.n && sends(G.rank, self_send)) {
+            g->items.push_back(g->staging_off[size_t(G.rank)] + G.local_out);
+            g->items.push_back(G.omin);
+            g->items.push_back(G.n);
+        }
+}
+
+// The packets rank r's plan computes: payload offsets in its shard; out
+// indices in its local array, or the global ones when rank 0 works in place.
+void rank_plan_packets(const crc32c_packet *pkts, size_t npkts, uint32_t gp, const std::vector<Group> &groups, int r,
+                       bool self_send, std::vector<crc32c_packet> *out) {
+    shard_packets(pkts, npkts, gp, groups, r, sends(r, self_send), out);
+}
+
 int ensure_comms(crc32c_multi *m) {
     if (!m->comms.empty()) return 0;
     std::vector<int> devs;
@@ -160,6 +198,12 @@ struct crc32c_multi_plan {
     uint4 *d_scatter = nullptr;  // {src index in staging, dst index in root_out, count, 0}
     uint32_t nscatter = 0;
     int root_local = -1;  // local device index of rank 0 (-1: not in this process)
+    // Successive execs reuse d_local / d_staging: per local device, the
+    // stream of the previous exec and an event after its last step, so an
+    // exec on another stream first waits for it.
+    std::vector<hipStream_t> last_stream;
+    std::vector<hipEvent_t> last_done;
+    std::vector<char> launched;
 };
 
 namespace {
@@ -169,6 +213,22 @@ namespace {
 __global__ __launch_bounds__(256) void scatter_groups(const uint32_t *staging, const uint4 *items, uint32_t *out) {
     const uint4 it = items[blockIdx.x];
     for (uint32_t k = threadIdx.x; k < it.z; k += blockDim.x) out[it.y + k] = staging[it.x + k];
+}
+
+// Records where this exec ended on every local device (outside a capture:
+// a captured exec is ordered by its graph's own stream).
+int mark_execs(crc32c_multi_plan *mp, void *const *streams) {
+    crc32c_multi *m = mp->m;
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        const hipStream_t s = local_stream(m, i, streams);
+        DeviceGuard guard(m->ctxs[i]->device);
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(s, &cs));
+        if (cs == hipStreamCaptureStatusNone) HIP_TRY(hipEventRecord(mp->last_done[i], s));
+        mp->last_stream[i] = s;
+        mp->launched[i] = 1;
+    }
+    return 0;
 }
 
 }  // namespace
@@ -276,6 +336,36 @@ int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint
     return int64_t(v.size());
 }
 
+int64_t crc32c_multi_rank_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                                  int rank, uint32_t flags, crc32c_packet *local, size_t cap) {
+    std::vector<Group> groups;
+    std::vector<uint64_t> sb, ln;
+    if (int rc = build_layout(pkts, npkts, group_packets, nranks, &groups, &sb, &ln)) return rc;
+    if (rank < 0 || rank >= nranks) return fail(-EINVAL, "rank %d out of range", rank);
+    std::vector<crc32c_packet> v;
+    rank_plan_packets(pkts, npkts, group_packets, groups, rank, (flags & CRC32C_MULTI_SELF_SEND) != 0, &v);
+    if (local) std::copy(v.begin(), v.begin() + std::min(cap, v.size()), local);
+    return int64_t(v.size());
+}
+
+int64_t crc32c_multi_gather_plan(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                                 uint32_t flags, uint64_t *local_nout, uint64_t *staging_off, uint64_t *items,
+                                 size_t cap) {
+    std::vector<Group> groups;
+    std::vector<uint64_t> sb, ln;
+    if (int rc = build_layout(pkts, npkts, group_packets, nranks, &groups, &sb, &ln)) return rc;
+    const bool self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
+    Gather ga;
+    build_gather(groups, ln, nranks, self_send, &ga);
+    for (int r = 0; r < nranks; ++r) {
+        if (local_nout) local_nout[r] = sends(r, self_send) ? ln[size_t(r)] : 0;
+        if (staging_off) staging_off[r] = ga.staging_off[size_t(r)];
+    }
+    const size_t n = ga.items.size() / 3;
+    if (items) std::copy(ga.items.begin(), ga.items.begin() + 3 * std::min(cap, n), items);
+    return int64_t(n);
+}
+
 int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
                              uint32_t flags, crc32c_multi_plan **out) {
     if (!m || !out) return fail(-EINVAL, "multi/out == NULL");
@@ -283,9 +373,23 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
     if (flags & (CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK))
         return fail(-EINVAL, "flags 0x%x not valid for a multi-GPU plan", flags);
     if (group_packets == 0) group_packets = 64;
+    // RCCL has one rank per GPU: a one-process communicator (ncclCommInitAll)
+    // cannot list a device twice (crc32c_multi_batch_host can: it uses no RCCL)
+    for (size_t i = 0; i < m->ctxs.size(); ++i)
+        for (size_t j = 0; j < i; ++j)
+            if (m->ctxs[i]->device == m->ctxs[j]->device)
+                return fail(-EINVAL, "device %d is listed twice: a multi-GPU plan needs one rank per GPU",
+                            m->ctxs[i]->device);
     std::unique_ptr<crc32c_multi_plan, int (*)(crc32c_multi_plan *)> mp(new crc32c_multi_plan,
                                                                         crc32c_multi_plan_destroy);
     mp->m = m;
+    mp->last_stream.assign(m->ctxs.size(), nullptr);
+    mp->last_done.assign(m->ctxs.size(), nullptr);
+    mp->launched.assign(m->ctxs.size(), 0);
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        DeviceGuard guard(m->ctxs[i]->device);
+        HIP_TRY(hipEventCreateWithFlags(&mp->last_done[i], hipEventDisableTiming));
+    }
     mp->self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
     flags &= ~CRC32C_MULTI_SELF_SEND;
     if (int rc = build_layout(pkts, npkts, group_packets, m->nranks, &mp->groups, &mp->shard_bytes, &mp->local_nout))
@@ -295,9 +399,9 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
     for (size_t i = 0; i < m->ctxs.size(); ++i) {
         const int r = m->ranks[i];
         // rank 0 in place: its packets keep their global out indices
-        const bool in_place = r == 0 && !mp->self_send;
+        const bool in_place = !sends(r, mp->self_send);
         if (r == 0) mp->root_local = int(i);
-        shard_packets(pkts, npkts, group_packets, mp->groups, r, !in_place, &local);
+        rank_plan_packets(pkts, npkts, group_packets, mp->groups, r, mp->self_send, &local);
         crc32c_plan *p = nullptr;
         if (int rc = crc32c_plan_create(m->ctxs[i], local.data(), local.size(), flags, &p)) return rc;
         mp->plans.push_back(p);
@@ -309,18 +413,14 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
         mp->d_local.push_back(d);
     }
     if (mp->root_local >= 0) {  // staging slots and scatter list for the arrays rank 0 receives
-        mp->staging_off.assign(size_t(m->nranks), 0);
-        uint64_t total = 0;
-        for (int r = 0; r < m->nranks; ++r) {
-            mp->staging_off[size_t(r)] = total;
-            if (r != 0 || mp->self_send) total += mp->local_nout[size_t(r)];
-        }
-        std::vector<uint4> items;
-        for (const Group &G : mp->groups)
-            if (G.n && (G.rank != 0 || mp->self_send))
-                items.push_back(make_uint4(uint32_t(mp->staging_off[size_t(G.rank)] + G.local_out), uint32_t(G.omin),
-                                           uint32_t(G.n), 0u));
+        Gather ga;
+        build_gather(mp->groups, mp->local_nout, m->nranks, mp->self_send, &ga);
+        mp->staging_off = ga.staging_off;
+        const uint64_t total = ga.staging_total;
         if (total > UINT32_MAX || mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
+        std::vector<uint4> items;
+        for (size_t k = 0; k + 2 < ga.items.size(); k += 3)
+            items.push_back(make_uint4(uint32_t(ga.items[k]), uint32_t(ga.items[k + 1]), uint32_t(ga.items[k + 2]), 0u));
         DeviceGuard guard(m->ctxs[size_t(mp->root_local)]->device);
         if (total) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_staging), total * sizeof(uint32_t)));
         if (!items.empty()) {
@@ -349,6 +449,20 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
         if (mp->local_nout[size_t(m->ranks[i])] && (!dev_shards || !dev_shards[i]))
             return fail(-EINVAL, "local device %zu: shard payload == NULL", i);
     if (mp->root_local >= 0 && mp->nchecksums && !root_out) return fail(-EINVAL, "root_out == NULL on rank 0");
+    // 0. after the previous exec when it ran on another stream (its sends and
+    //    scatter may still read the buffers this one overwrites)
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        const hipStream_t s = local_stream(m, i, streams);
+        if (mp->launched[i] && mp->last_stream[i] != s) {
+            DeviceGuard guard(m->ctxs[i]->device);
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            HIP_TRY(hipStreamIsCapturing(s, &cs));
+            if (cs != hipStreamCaptureStatusNone)  // (a capture cannot wait on work outside it)
+                HIP_TRY(hipEventSynchronize(mp->last_done[i]));
+            else
+                HIP_TRY(hipStreamWaitEvent(s, mp->last_done[i], 0));
+        }
+    }
     // 1. every local device checksums its shard: rank 0 into place, the
     //    others into their local arrays
     for (size_t i = 0; i < m->ctxs.size(); ++i) {
@@ -360,8 +474,8 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
     //    local array to rank 0's staging slot for it
     bool any = false;
     for (int r = 0; r < m->nranks; ++r)
-        if ((r != 0 || mp->self_send) && mp->local_nout[size_t(r)]) any = true;
-    if (!any) return 0;
+        if (sends(r, mp->self_send) && mp->local_nout[size_t(r)]) any = true;
+    if (!any) return mark_execs(mp, streams);
     if (int rc = ensure_comms(m)) return rc;
     NCCL_TRY(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
@@ -371,7 +485,7 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
         if (mp->d_local[i]) r = ncclSend(mp->d_local[i], mp->local_nout[size_t(me)], ncclUint32, 0, m->comms[i], s);
         if (me != 0) continue;
         for (int peer = 0; peer < m->nranks && r == ncclSuccess; ++peer)
-            if ((peer != 0 || mp->self_send) && mp->local_nout[size_t(peer)])
+            if (sends(peer, mp->self_send) && mp->local_nout[size_t(peer)])
                 r = ncclRecv(mp->d_staging + mp->staging_off[size_t(peer)], mp->local_nout[size_t(peer)], ncclUint32,
                              peer, m->comms[i], s);
     }
@@ -386,11 +500,16 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
                            mp->d_staging, mp->d_scatter, root_out);
         HIP_TRY(hipGetLastError());
     }
-    return 0;
+    return mark_execs(mp, streams);
 }
 
 int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
     if (!mp) return 0;
+    for (size_t i = 0; i < mp->last_done.size(); ++i)
+        if (mp->last_done[i]) {
+            DeviceGuard guard(mp->m->ctxs[i]->device);
+            (void)hipEventDestroy(mp->last_done[i]);
+        }
     for (size_t i = 0; i < mp->plans.size(); ++i) {
         crc32c_plan_destroy(mp->plans[i]);
         if (i < mp->d_local.size() && mp->d_local[i]) {
@@ -411,7 +530,8 @@ int crc32c_multi_batch_host(crc32c_multi *m, const void *payload, const crc32c_p
                             uint32_t group_packets, uint32_t *out, uint32_t flags) {
     if (!m || m->ctxs.empty()) return fail(-EINVAL, "multi == NULL");
     for (size_t i = 0; i < npkts; ++i)
-        if (!pkts || pkts[i].bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
+        if (!pkts || (pkts[i].len && pkts[i].bpc == 0))
+            return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
     if (group_packets == 0) group_packets = 64;
     const size_t g = m->ctxs.size();
     // Groups of consecutive packets (an HDFS block's worth) dealt round-robin

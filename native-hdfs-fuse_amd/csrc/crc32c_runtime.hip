@@ -26,22 +26,9 @@
 #include "host_copy.h"
 #include "runtime_internal.h"
 
-namespace hdfs_crc {
-
 namespace {
-thread_local char g_err[512] = "";
 thread_local int g_last_path = CRC32C_PATH_NONE;
 }  // namespace
-
-int fail(int code, const char *fmt, ...) {
-    va_list ap;
-    va_start(ap, fmt);
-    std::vsnprintf(g_err, sizeof g_err, fmt, ap);
-    va_end(ap);
-    return code;
-}
-
-}  // namespace hdfs_crc
 
 using namespace hdfs_crc;
 
@@ -114,35 +101,79 @@ size_t pool_class(size_t bytes) {
     return c;
 }
 
-// A block of at least `bytes` from the pool (caller holds ctx->pool_mu).
-int pool_get(crc32c_ctx *ctx, BlockPool &pool, size_t bytes, uint8_t **out, size_t *cap) {
-    const size_t c = pool_class(bytes);
-    for (int pass = 0; pass < 2; ++pass) {
-        for (size_t i = 0; i < pool.free.size(); ++i)
-            if (pool.free[i].second == c) {
-                *out = pool.free[i].first;
-                *cap = c;
-                pool.free[i] = pool.free.back();
-                pool.free.pop_back();
-                return 0;
-            }
-        // Epoch: once enough released blocks wait, one device synchronisation
-        // makes every one of them (in both pools) reusable.
-        if (pass == 0 && ctx->dev_pool.deferred.size() + ctx->host_pool.deferred.size() >= kEpochBlocks) {
-            HIP_TRY(hipDeviceSynchronize());
-            for (BlockPool *bp : {&ctx->dev_pool, &ctx->host_pool}) {
-                bp->free.insert(bp->free.end(), bp->deferred.begin(), bp->deferred.end());
-                bp->deferred.clear();
-            }
+hipEvent_t take_event(crc32c_ctx *ctx) {  // caller holds ctx->pool_mu
+    if (ctx->spare_events.empty()) return nullptr;
+    hipEvent_t e = ctx->spare_events.back();
+    ctx->spare_events.pop_back();
+    return e;
+}
+
+void drop_block(BlockPool &pool, uint8_t *p) {
+    for (size_t i = 0; i < pool.all.size(); ++i)
+        if (pool.all[i].first == p) {
+            pool.all[i] = pool.all.back();
+            pool.all.pop_back();
+            return;
+        }
+}
+
+// Moves every release whose events have all completed back into the pools
+// (non-blocking queries), then trims the free lists to kFreeBlocksMax.
+// Caller holds ctx->pool_mu.
+void reap_releases(crc32c_ctx *ctx) {
+    for (size_t i = 0; i < ctx->releases.size();) {
+        Release &r = ctx->releases[i];
+        bool done = true;
+        for (hipEvent_t e : r.events) {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipSuccess) continue;
+            if (q != hipErrorNotReady) (void)hipGetLastError();
+            done = false;
+            break;
+        }
+        if (!done) {
+            ++i;
             continue;
         }
-        break;
+        if (r.d) ctx->dev_pool.free.emplace_back(r.d, r.dcap);
+        if (r.h) ctx->host_pool.free.emplace_back(r.h, r.hcap);
+        ctx->spare_events.insert(ctx->spare_events.end(), r.events.begin(), r.events.end());
+        ctx->releases[i] = std::move(ctx->releases.back());
+        ctx->releases.pop_back();
     }
+    while (ctx->dev_pool.free.size() > kFreeBlocksMax) {  // stream-ordered: no device synchronisation
+        uint8_t *p = ctx->dev_pool.free.front().first;
+        ctx->dev_pool.free.erase(ctx->dev_pool.free.begin());
+        drop_block(ctx->dev_pool, p);
+        (void)hipFreeAsync(p, ctx->upload_stream);
+    }
+    while (ctx->host_pool.free.size() > kFreeBlocksMax) {
+        uint8_t *p = ctx->host_pool.free.front().first;
+        ctx->host_pool.free.erase(ctx->host_pool.free.begin());
+        drop_block(ctx->host_pool, p);
+        (void)hipHostFree(p);
+    }
+}
+
+// A block of at least `bytes` from the pool (caller holds ctx->pool_mu and
+// has reaped the releases).  New device blocks come from the stream-ordered
+// allocator on the upload stream (the upload that fills them follows on the
+// same stream; every launch waits for that upload).
+int pool_get(crc32c_ctx *ctx, BlockPool &pool, size_t bytes, uint8_t **out, size_t *cap) {
+    const size_t c = pool_class(bytes);
+    for (size_t i = 0; i < pool.free.size(); ++i)
+        if (pool.free[i].second == c) {
+            *out = pool.free[i].first;
+            *cap = c;
+            pool.free[i] = pool.free.back();
+            pool.free.pop_back();
+            return 0;
+        }
     uint8_t *p = nullptr;
     if (pool.pinned)
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&p), c, hipHostMallocDefault));
     else
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&p), c));
+        HIP_TRY(hipMallocAsync(reinterpret_cast<void **>(&p), c, ctx->upload_stream));
     pool.all.emplace_back(p, c);
     *out = p;
     *cap = c;
@@ -173,14 +204,13 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->pieces_off = dp->seg_off + hp.seg.size() * sizeof(SegItem);
     dp->consts_off = dp->pieces_off + hp.pieces.size() * sizeof(GenPiece);
     const size_t bytes = dp->consts_off + hp.consts.size() * sizeof(ConstRun);
+    RelaxedCapture relaxed;  // (another thread may be capturing a graph)
     {
         std::lock_guard<std::mutex> lock(ctx->pool_mu);
+        reap_releases(ctx);
         if (int rc = pool_get(ctx, ctx->dev_pool, bytes, &dp->d, &dp->cap)) return rc;
         if (int rc = pool_get(ctx, ctx->host_pool, bytes, &dp->h, &dp->hcap)) return rc;
-        if (!ctx->spare_events.empty()) {
-            dp->uploaded = ctx->spare_events.back();
-            ctx->spare_events.pop_back();
-        }
+        dp->uploaded = take_event(ctx);
     }
     if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDisableTiming));
     uint8_t *img = dp->h;
@@ -199,45 +229,101 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
 // Orders a launch on `stream` after the plan's upload: nothing once the
 // upload is known complete; else a stream wait on its event (or, while the
 // stream is being captured into a graph, a host wait: a capture cannot wait
-// on work outside it).
-int plan_ready(DevicePlan *dp, hipStream_t stream) {
-    if (dp->ready.load(std::memory_order_acquire) || !dp->uploaded) return 0;
-    const hipError_t q = hipEventQuery(dp->uploaded);
-    if (q == hipSuccess) {
-        dp->ready.store(true, std::memory_order_release);
-        return 0;
+// on work outside it).  Notes the launch stream for the plan's release.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream) {
+    RelaxedCapture relaxed;  // (the queries below while another thread captures a graph)
+    if (std::find(plan->launch_streams.begin(), plan->launch_streams.end(), stream) == plan->launch_streams.end())
+        plan->launch_streams.push_back(stream);
+    DevicePlan *dp = &plan->dp;
+    if (!plan->captured || !dp->ready.load(std::memory_order_acquire)) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(stream, &cs));
+        if (cs != hipStreamCaptureStatusNone) plan->captured = true;
+        if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
+            const hipError_t q = hipEventQuery(dp->uploaded);
+            if (q == hipSuccess) {
+                dp->ready.store(true, std::memory_order_release);
+            } else {
+                if (q != hipErrorNotReady) HIP_TRY(q);
+                if (cs != hipStreamCaptureStatusNone) {
+                    HIP_TRY(hipEventSynchronize(dp->uploaded));
+                    dp->ready.store(true, std::memory_order_release);
+                } else {
+                    HIP_TRY(hipStreamWaitEvent(stream, dp->uploaded, 0));
+                }
+            }
+        }
     }
-    if (q != hipErrorNotReady) HIP_TRY(q);
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    HIP_TRY(hipStreamIsCapturing(stream, &cs));
-    if (cs != hipStreamCaptureStatusNone) {
-        HIP_TRY(hipEventSynchronize(dp->uploaded));
-        dp->ready.store(true, std::memory_order_release);
-        return 0;
-    }
-    HIP_TRY(hipStreamWaitEvent(stream, dp->uploaded, 0));
     return 0;
 }
 
-void free_device_plan(crc32c_ctx *ctx, DevicePlan *dp) {
+void release_plan_blocks(crc32c_plan *plan) {
+    crc32c_ctx *ctx = plan->ctx;
+    DevicePlan *dp = &plan->dp;
+    RelaxedCapture relaxed;
+    Release r;
+    r.d = dp->d;
+    r.dcap = dp->cap;
+    r.h = dp->h;
+    r.hcap = dp->hcap;
+    bool held = plan->captured;
+    std::vector<hipEvent_t> evs;
+    {
+        std::lock_guard<std::mutex> lock(ctx->pool_mu);
+        for (size_t i = 0; i < plan->launch_streams.size(); ++i) evs.push_back(take_event(ctx));
+    }
+    // one event per launch stream, recorded now: it completes after every
+    // launch of the plan on that stream
+    for (size_t i = 0; i < plan->launch_streams.size() && !held; ++i) {
+        const hipStream_t s = plan->launch_streams[i];
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            (void)hipGetLastError();
+            held = true;  // (a capture in progress on it may hold the plan's launches)
+            break;
+        }
+        if (!evs[i] && hipEventCreateWithFlags(&evs[i], hipEventDisableTiming) != hipSuccess) evs[i] = nullptr;
+        if (!evs[i] || hipEventRecord(evs[i], s) != hipSuccess) {
+            (void)hipGetLastError();
+            held = true;  // (e.g. the stream no longer exists: the block is not reused)
+            break;
+        }
+        r.events.push_back(evs[i]);
+        evs[i] = nullptr;
+    }
+    if (dp->uploaded) r.events.push_back(dp->uploaded);
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
-    if (dp->d) ctx->dev_pool.deferred.emplace_back(dp->d, dp->cap);
-    if (dp->h) ctx->host_pool.deferred.emplace_back(dp->h, dp->hcap);
-    if (dp->uploaded) ctx->spare_events.push_back(dp->uploaded);
+    for (hipEvent_t e : evs)
+        if (e) ctx->spare_events.push_back(e);
+    if (held && r.d) {
+        ctx->held.emplace_back(r.d, r.dcap);
+        drop_block(ctx->dev_pool, r.d);
+        r.d = nullptr;
+    }
+    ctx->releases.push_back(std::move(r));
     dp->d = dp->h = nullptr;
     dp->cap = dp->hcap = 0;
     dp->uploaded = nullptr;
 }
 
-// Context teardown (device idle): every pooled block and spare event.
+// Context teardown (every plan destroyed): waits for the releases, then
+// frees every pooled block and spare event.
 void release_pools(crc32c_ctx *ctx) {
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
-    for (auto &b : ctx->dev_pool.all) (void)hipFree(b.first);
+    for (Release &r : ctx->releases)
+        for (hipEvent_t e : r.events) (void)hipEventSynchronize(e);
+    reap_releases(ctx);
+    if (!ctx->held.empty()) (void)hipDeviceSynchronize();  // (blocks graphs captured; graphs outlived by the context)
+    for (auto &b : ctx->dev_pool.all) (void)hipFreeAsync(b.first, ctx->upload_stream);
+    for (auto &b : ctx->held) (void)hipFreeAsync(b.first, ctx->upload_stream);
+    (void)hipStreamSynchronize(ctx->upload_stream);
     for (auto &b : ctx->host_pool.all) (void)hipHostFree(b.first);
     for (hipEvent_t e : ctx->spare_events) (void)hipEventDestroy(e);
     ctx->dev_pool = BlockPool();
     ctx->host_pool = BlockPool();
     ctx->host_pool.pinned = true;
+    ctx->releases.clear();
+    ctx->held.clear();
     ctx->spare_events.clear();
 }
 
@@ -289,7 +375,7 @@ int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
 
 int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     std::lock_guard<std::mutex> lock(plan->mu);
-    if (int rc = plan_ready(&plan->dp, stream)) return rc;
+    if (int rc = prepare_launch(plan, stream)) return rc;
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
@@ -312,7 +398,7 @@ int check_flags(uint32_t flags) {
 int check_packets(const crc32c_packet *pkts, size_t npkts) {
     if (npkts && !pkts) return fail(-EINVAL, "packets == NULL");
     for (size_t i = 0; i < npkts; ++i)
-        if (pkts[i].bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
+        if (pkts[i].len && pkts[i].bpc == 0) return fail(-EINVAL, "packet %zu: bytesPerChecksum == 0", i);
     return 0;
 }
 
@@ -615,7 +701,6 @@ int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute
 
 extern "C" {
 
-const char *crc32c_last_error(void) { return g_err; }
 int crc32c_last_path(void) { return g_last_path; }
 
 int crc32c_device_count(void) {
@@ -671,11 +756,9 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
             (void)hipStreamDestroy(ctx->copy_stream);
         }
         if (ctx->upload_stream) {
-            (void)hipStreamSynchronize(ctx->upload_stream);
+            release_pools(ctx);  // (waits for the destroyed plans' launches)
             (void)hipStreamDestroy(ctx->upload_stream);
         }
-        (void)hipDeviceSynchronize();  // (plans' launches may still read pooled blocks)
-        release_pools(ctx);
         for (int ty = 0; ty < 2; ++ty) {
             if (ctx->d_table[ty]) (void)hipFree(ctx->d_table[ty]);
             if (ctx->d_table_s4[ty]) (void)hipFree(ctx->d_table_s4[ty]);
@@ -768,7 +851,9 @@ int crc32c_plan_verify_bitmap(crc32c_plan *plan, const void *dev_payload, const 
 int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_packet *pkts, size_t npkts,
                            const uint32_t *expected, uint32_t flags, uint64_t *first_bad) {
     if (first_bad) *first_bad = UINT64_MAX;
-    if (!ctx) return fail(-EINVAL, "ctx == NULL");
+    // (ctx == NULL is a missing GPU: with CRC32C_CPU_FALLBACK crc32c_batch_host
+    // then computes on the host CPU)
+    if (!ctx && !(flags & CRC32C_CPU_FALLBACK)) return fail(-EINVAL, "ctx == NULL");
     uint64_t n = 0;
     for (size_t i = 0; i < npkts; ++i)
         if (pkts && pkts[i].bpc) n = std::max<uint64_t>(n, pkts[i].out_idx + crc32c_nchunks(pkts[i].len, pkts[i].bpc));
@@ -795,7 +880,7 @@ int crc32c_plan_destroy(crc32c_plan *plan) {
     if (!plan) return 0;
     {
         DeviceGuard guard(plan->ctx->device);
-        free_device_plan(plan->ctx, &plan->dp);  // (the verify slots live in the same block)
+        release_plan_blocks(plan);  // (the verify slots live in the same block)
         if (plan->last_done) (void)hipEventDestroy(plan->last_done);
     }
     delete plan;

@@ -124,7 +124,10 @@ extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev
     KParams p = plan_params(plan, dev_payload, dev_out);
     p.stamps = dev_stamps;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    if (int rc = plan_ready(&plan->dp, s)) return rc;
+    {
+        std::lock_guard<std::mutex> lock(plan->mu);
+        if (int rc = prepare_launch(plan, s)) return rc;
+    }
     HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
                          : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));
     return 0;

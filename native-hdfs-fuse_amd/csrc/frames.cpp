@@ -16,7 +16,10 @@
 #include <cstring>
 #include <vector>
 
+#include "errors.h"
 #include "hdfs_crc32c.h"
+
+using hdfs_crc::fail;
 
 namespace {
 
@@ -94,19 +97,22 @@ extern "C" int64_t crc32c_parse_frames(const void *frames, size_t bytes, crc32c_
     size_t o = 0;
     int64_t n = 0;
     if (consumed) *consumed = 0;
-    if (bytes && !b) return -EINVAL;
+    if (bytes && !b) return fail(-EINVAL, "frames == NULL");
     while (bytes - o >= 6) {
         const uint32_t plen = get_be32(b + o);
         const uint32_t hlen = uint32_t(b[o + 4]) << 8 | b[o + 5];
-        if (plen < 4) return -EBADMSG;
+        if (plen < 4) return fail(-EBADMSG, "frame %lld at %zu: PLEN %u < 4", (long long)n, o, plen);
         const uint64_t total = 6ull + hlen + (plen - 4ull);
         if (bytes - o < total) break;  // the rest has not arrived yet
         crc32c_frame_info f;
         std::memset(&f, 0, sizeof f);
-        if (!parse_header(b + o + 6, hlen, &f)) return -EBADMSG;
-        if (f.data_len > plen - 4u) return -EBADMSG;
+        if (!parse_header(b + o + 6, hlen, &f))
+            return fail(-EBADMSG, "frame %lld at %zu: malformed PacketHeaderProto", (long long)n, o);
+        if (f.data_len > plen - 4u)
+            return fail(-EBADMSG, "frame %lld at %zu: dataLen %u > PLEN - 4", (long long)n, o, f.data_len);
         const uint32_t sum_bytes = plen - 4u - f.data_len;
-        if (sum_bytes % 4) return -EBADMSG;
+        if (sum_bytes % 4)
+            return fail(-EBADMSG, "frame %lld at %zu: %u checksum bytes", (long long)n, o, sum_bytes);
         f.frame_off = o;
         f.sums_off = o + 6 + hlen;
         f.data_off = f.sums_off + sum_bytes;
@@ -122,7 +128,8 @@ extern "C" int64_t crc32c_parse_frames(const void *frames, size_t bytes, crc32c_
 
 extern "C" int crc32c_verify_frames_host(crc32c_ctx *ctx, const void *frames, size_t bytes, uint32_t bpc,
                                          uint64_t chunk_offset, uint32_t flags, crc32c_frames_result *res) {
-    if (!res || !bpc || (flags & ~(CRC32C_TYPE_CRC32 | CRC32C_CPU_FALLBACK))) return -EINVAL;
+    if (!res || !bpc || (flags & ~(CRC32C_TYPE_CRC32 | CRC32C_CPU_FALLBACK)))
+        return fail(-EINVAL, "res == NULL, bytesPerChecksum == 0 or unknown flags");
     std::memset(res, 0, sizeof *res);
     res->first_bad = UINT64_MAX;
     res->first_bad_offset = -1;
@@ -143,9 +150,13 @@ extern "C" int crc32c_verify_frames_host(crc32c_ctx *ctx, const void *frames, si
         if (f.data_len == 0) continue;
         // Every data packet starts on a chunk boundary, the first at
         // chunkOffset, the others where the previous one ended.
-        if (f.offset_in_block != next || uint64_t(f.offset_in_block) % bpc) return -EBADMSG;
+        if (f.offset_in_block != next || uint64_t(f.offset_in_block) % bpc)
+            return fail(-EBADMSG, "packet seqno %lld: offsetInBlock %lld, expected %lld on a %u-byte chunk boundary",
+                        (long long)f.seqno, (long long)f.offset_in_block, (long long)next, bpc);
         const uint64_t nch = crc32c_nchunks(f.data_len, bpc);
-        if (f.nsums != nch) return -EBADMSG;
+        if (f.nsums != nch)
+            return fail(-EBADMSG, "packet seqno %lld: %u checksums for %u bytes (%llu expected)", (long long)f.seqno,
+                        f.nsums, f.data_len, (unsigned long long)nch);
         crc32c_packet p;
         p.payload_off = f.data_off;
         p.out_idx = expected.size();

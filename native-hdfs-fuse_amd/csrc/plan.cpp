@@ -39,8 +39,10 @@ static void push_gen(HostPlan *plan, uint64_t src, uint64_t out, uint32_t len) {
 }
 
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
+    // A zero-length packet (the block's last-packet marker, hadooprpc.c:644,
+    // 853-856) has no checksums whatever its bpc; any other needs bpc > 0.
+    if (p.len == 0) return 0;
     if (p.bpc == 0) return -EINVAL;
-    if (p.len == 0) return 0;  // last-packet marker: no checksums (hadooprpc.c:644, 666)
     const uint64_t n = (uint64_t(p.len) + p.bpc - 1) / p.bpc;  // hadooprpc.c:639
     if (p.out_idx + n > (1ull << 32)) return -EINVAL;
     if (p.out_idx + n > plan->nchecksums) plan->nchecksums = p.out_idx + n;

@@ -9,14 +9,14 @@
 #include <mutex>
 #include <vector>
 
+#include "errors.h"
 #include "hdfs_crc32c.h"
 #include "kernel_abi.h"
 #include "plan.h"
 
 namespace hdfs_crc {
 
-// Thread-local error text (crc32c_last_error) and its setter.
-int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+// (fail(): errors.h)
 
 #define HIP_TRY(expr)                                                                                          \
     do {                                                                                                       \
@@ -87,15 +87,35 @@ struct DevicePlan {
 
 // Blocks of descriptor memory (device) or of its pinned staging (host),
 // recycled instead of freed: hipFree costs ~12 us and hipMemcpy from pageable
-// memory ~15 us, several times a short plan's whole launch.  A released block
-// may still be read by launches in flight, so it is reusable only after the
-// next epoch (a device synchronisation the pool takes once kEpochBlocks
-// blocks wait, instead of the one hipFree took for every plan).
+// memory ~15 us, several times a short plan's whole launch.
 struct BlockPool {
     bool pinned = false;
-    std::vector<std::pair<uint8_t *, size_t>> free, deferred, all;
+    std::vector<std::pair<uint8_t *, size_t>> free, all;
 };
-constexpr size_t kEpochBlocks = 32;
+// Free blocks a pool keeps; more are returned (device blocks stream-ordered,
+// hipFreeAsync on the upload stream, so no device-wide synchronisation).
+constexpr size_t kFreeBlocksMax = 48;
+
+// A destroyed plan's blocks, waiting for the GPU work that may still read
+// them: an event recorded at destroy time on every stream the plan was
+// launched on, and its upload's event.  Reusable once all have completed
+// (queried without blocking when a block is next needed) -- no device-wide
+// synchronisation, so other streams, other libraries' work and graph
+// captures on other threads are never waited on or disturbed.
+struct Release {
+    uint8_t *d = nullptr, *h = nullptr;  // device block / pinned staging block (either may be null)
+    size_t dcap = 0, hcap = 0;
+    std::vector<hipEvent_t> events;
+};
+
+// Makes the calling thread's potentially-unsafe HIP calls (allocation, event
+// records) legal while another thread captures a stream in global mode
+// (torch.cuda.graph's default); restores the thread's mode on exit.
+struct RelaxedCapture {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
+    ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&mode); }
+};
 
 }  // namespace hdfs_crc
 
@@ -118,6 +138,11 @@ struct crc32c_ctx {
     // uploads go on, and spare events (all under pool_mu).
     std::mutex pool_mu;
     hdfs_crc::BlockPool dev_pool, host_pool;
+    std::vector<hdfs_crc::Release> releases;
+    // device blocks of destroyed plans whose launches were captured into a
+    // graph: the graph may replay them at any time, so they are never
+    // reused (freed with the context)
+    std::vector<std::pair<uint8_t *, size_t>> held;
     hipStream_t upload_stream = nullptr;
     std::vector<hipEvent_t> spare_events;
 };
@@ -132,6 +157,10 @@ struct crc32c_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t last_done = nullptr;
     bool launched = false;
+    // every stream a launch of the plan went on (its blocks are recycled
+    // after an event on each), and whether one was a graph capture
+    std::vector<hipStream_t> launch_streams;
+    bool captured = false;
     hdfs_crc::DevicePlan dp;
     uint64_t nchecksums = 0, payload_bytes = 0;
     uint32_t flags = 0;
@@ -149,8 +178,12 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
 // Uploads a HostPlan's items (and fresh verify slots) to the context's
 // device (into *dp), asynchronously; plan_ready orders a launch after it.
 int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
-int plan_ready(DevicePlan *dp, hipStream_t stream);
-void free_device_plan(crc32c_ctx *ctx, DevicePlan *dp);
+// Before a launch of `plan` on `stream` (caller holds plan->mu): orders it
+// after the plan's upload and notes the stream for the plan's release.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream);
+// A destroyed plan's blocks back to the pools once its launches are done.
+void release_plan_blocks(crc32c_plan *plan);
+// Context teardown: waits for the releases, frees every pooled block.
 void release_pools(crc32c_ctx *ctx);
 // Creates a plan object from a built HostPlan (absolute: rebased, base given).
 int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute, uint64_t abs_base,

@@ -50,55 +50,56 @@ def rank_packets(pkts, group_packets: int, world: int, rank: int) -> np.ndarray:
     return _pkg().multi_shard_packets(pkts, group_packets, world, rank)
 
 
-def group_ranges(pkts, group_packets: int) -> list[tuple[int, int]]:
-    """Each group's checksum range (first global out index, count)."""
-    pkts = np.asarray(pkts)
-    out = []
-    for g in range(0, pkts.size, group_packets):
-        p = pkts[g:g + group_packets]
-        p = p[p["len"] > 0]
-        if not p.size:
-            out.append((0, 0))
-            continue
-        n = (p["len"].astype(np.int64) + p["bpc"] - 1) // p["bpc"]
-        out.append((int(p["out_idx"].min()), int(n.sum())))
-    return out
+def plan_packets(pkts, group_packets: int, world: int, rank: int, flags: int = 0) -> np.ndarray:
+    """The packets rank's plan computes: payload offsets into its shard, out
+    indices into the array it sends to rank 0 (rank 0: global, in place,
+    unless CRC32C_MULTI_SELF_SEND) -- crc32c_multi_rank_packets."""
+    return _pkg().multi_rank_packets(pkts, group_packets, world, rank, flags)
 
 
-def gather_checksums(local, pkts, group_packets: int, world: int, rank: int):
-    """Every group's checksum range from its rank's array (a torch int32
-    tensor indexed by GLOBAL out index, on the rank's device for nccl or on
-    the CPU for gloo) into place on rank 0, one send / receive per group, as
-    crc32c_multi_plan_exec does with RCCL.  Returns the file's checksums
-    (np.uint32) on rank 0, None elsewhere."""
+def gather_plan(pkts, group_packets: int, world: int, flags: int = 0):
+    """(local_nout, staging_off, scatter items {staging index, file index, count}) -- crc32c_multi_gather_plan."""
+    return _pkg().multi_gather_plan(pkts, group_packets, world, flags)
+
+
+def gather_checksums(local, pkts, group_packets: int, world: int, rank: int, flags: int = 0):
+    """The exchange of crc32c_multi_plan_exec, over torch.distributed: `local`
+    is the u32 array this rank's plan wrote (a torch int32 tensor laid out by
+    plan_packets -- rank 0's in place, indexed by global out index, unless
+    CRC32C_MULTI_SELF_SEND); every sending rank sends it whole in ONE send,
+    rank 0 receives each into its staging slot and applies the library's
+    scatter items to move every received group into file order -- the same
+    sends, receives and copies the library issues through RCCL and its scatter
+    kernel, driven by the library's own gather plan.  Returns the file's
+    checksums (np.uint32) on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
 
-    ranges = group_ranges(pkts, group_packets)
-    total = max((o + n for o, n in ranges), default=0)
-    full = torch.zeros(max(total, 1), dtype=torch.int32, device=local.device) if rank == 0 else None
+    ln, so, items = gather_plan(pkts, group_packets, world, flags)
+    total = int(_pkg().total_checksums(pkts))
     ops = []
-    for g, (o, n) in enumerate(ranges):
-        owner = g % world
-        if not n:
-            continue
-        if owner == rank and rank == 0:
-            full[o:o + n] = local[o:o + n]
-        elif owner == rank:
-            ops.append(dist.P2POp(dist.isend, local[o:o + n].contiguous(), 0))
-        elif rank == 0:
-            buf = torch.empty(n, dtype=torch.int32, device=local.device)
-            ops.append((dist.P2POp(dist.irecv, buf, owner), o, buf))
-    if world > 1:
-        p2p = [op if isinstance(op, dist.P2POp) else op[0] for op in ops]
-        if p2p:
-            for req in dist.batch_isend_irecv(p2p):
-                req.wait()
-        if rank == 0:
-            for op in ops:
-                if not isinstance(op, dist.P2POp):
-                    _, o, buf = op
-                    full[o:o + buf.numel()] = buf
+    staging = None
+    if rank == 0:
+        full = torch.zeros(max(total, 1), dtype=torch.int32, device=local.device)
+        if not ln[0]:  # rank 0 in place: its own groups are already at their file indices
+            full[:min(total, local.numel())] = local[:total]
+        staging = torch.zeros(max(int((so + ln).max()) if world else 0, 1), dtype=torch.int32, device=local.device)
+        for r in range(world):
+            n = int(ln[r])
+            if not n:
+                continue
+            dst = staging[int(so[r]):int(so[r]) + n]
+            if r == 0:  # self-send: RCCL copies rank 0's array to its own staging slot
+                dst.copy_(local[:n])
+            else:
+                ops.append(dist.P2POp(dist.irecv, dst, r))
+    elif int(ln[rank]):
+        ops.append(dist.P2POp(dist.isend, local[:int(ln[rank])].contiguous(), 0))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
     if rank != 0:
         return None
+    for src, dst, n in items.astype(np.int64):  # the scatter kernel, one group per item
+        full[dst:dst + n] = staging[src:src + n]
     return full[:total].cpu().numpy().view(np.uint32)

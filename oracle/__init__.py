@@ -243,6 +243,11 @@ def mixed_packets(npkts: int, pkt_len: int = 65536, bpcs=(512, 1024, 4096)) -> n
 
 
 def total_checksums(pkts: np.ndarray) -> int:
+    """Length of the checksum array a batch fills: max of out_idx + roundup(len, bpc)
+    (hadooprpc.c:639) over the packets with len > 0.  A zero-length packet (the
+    block's last-packet marker, hadooprpc.c:644 / 853-856) has no checksums, whatever
+    its bpc."""
+    pkts = pkts[pkts["len"] > 0]
     if pkts.size == 0:
         return 0
     per = (pkts["len"].astype(np.uint64) + pkts["bpc"].astype(np.uint64) - 1) // pkts["bpc"].astype(np.uint64)

@@ -1,19 +1,25 @@
-"""N > 1 path on CPU: world-size 2 and 3 process groups over gloo.
+"""N > 1 path on CPU: world-size 2, 3 and 8 process groups over gloo.
 
-The multi-GPU layout deals a file's blocks (groups of
-consecutive packets) round-robin over the ranks and gathers every group's
-u32 checksum range to rank 0 -- the path's only exchange.  Each rank here
-takes its shard and its packets from the library's own layout code
-(crc32c_multi_layout / crc32c_multi_shard_packets, the host half of
-crc32c_multi_plan_*), computes their checksums with the oracle (the GPU
-ranks run the HIP kernel), and the per-group send / receive of shard.py
-(the same pattern crc32c_multi_plan_exec issues through RCCL) lands them on
-rank 0, which checks the assembled array against the oracle over the whole
-file, bit for bit.  The bench's max-over-ranks timing reduction is checked
-the same way.
+The multi-GPU plan deals a file's blocks (groups of
+consecutive packets) round-robin over the ranks; each rank checksums its
+shard into one local u32 array, sends it to rank 0 in ONE send, and rank 0
+receives every array into a staging slot and scatters the groups into file
+order -- the path's only exchange.  Every part of that exchange that only
+N > 1 reaches is the library's own code here: each rank's shard and the
+packets its plan computes (payload offsets into the shard, out indices into
+its local array) come from crc32c_multi_layout / crc32c_multi_rank_packets,
+and the staging offsets and scatter items rank 0 applies from
+crc32c_multi_gather_plan -- the same host code crc32c_multi_plan_create
+builds its device plan from.  The checksums themselves come from the oracle
+(the GPU ranks run the HIP kernel); the transfers are gloo send / receive in
+place of RCCL's.  Rank 0's assembled array must equal the reference's golden
+digest of config 4's 128 MiB file, or the oracle over the whole file, bit for
+bit.  The bench's max-over-ranks timing reduction is checked the same way.
 """
 from __future__ import annotations
 
+import hashlib
+import json
 import os
 import socket
 
@@ -21,10 +27,11 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from conftest import load_package
+from conftest import GOLDEN, load_package
 
 PKTS_PER_BLOCK = 4  # 256 KiB blocks keep the CPU oracle fast; the layout is size-independent
 PKT = 65536
+SELF_SEND = 0x10  # CRC32C_MULTI_SELF_SEND
 
 
 def _free_port() -> int:
@@ -47,7 +54,12 @@ def _file_packets(nblocks: int, bpc: int, ragged: bool):
     return pk
 
 
-def _worker(rank: int, world: int, port: int, nblocks: int, bpc: int, ragged: bool, result_path: str):
+def _c4_spec():
+    with open(os.path.join(GOLDEN, "batches.json")) as f:
+        return [b for b in json.load(f) if b["name"] == "c4_file_128MiB"][0]
+
+
+def _worker(rank: int, world: int, port: int, case: tuple, flags: int, result_path: str):
     import torch
     import torch.distributed as dist
 
@@ -58,45 +70,93 @@ def _worker(rank: int, world: int, port: int, nblocks: int, bpc: int, ragged: bo
 
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     try:
-        pk = _file_packets(nblocks, bpc, ragged)
+        if case[0] == "c4":  # config 4: 32 x 4 MiB blocks of 64 packets, the reference's golden digest
+            spec = _c4_spec()
+            gp = 64
+            pk = oracle.uniform_packets(spec["packets"]["count"], spec["packets"]["len"][0], 512)
+            file_bytes = oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"])
+        else:
+            _, nblocks, bpc, ragged = case
+            gp = PKTS_PER_BLOCK
+            pk = _file_packets(nblocks, bpc, ragged)
+            file_bytes = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 16, oracle.SEED)
         total = oracle.total_checksums(pk)
-        file_bytes = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 16, oracle.SEED)
-        lay, sb = shard.layout(pk, PKTS_PER_BLOCK, world)
-        payload = shard.rank_payload(file_bytes, lay, sb, rank)
-        mine = shard.rank_packets(pk, PKTS_PER_BLOCK, world, rank)
+        lay, sb = shard.layout(pk, gp, world)
         assert set(int(x) for x in lay[:, 0]) <= set(range(world))
-        orc = oracle.Oracle()
-        local = np.zeros(max(total, 1), np.uint32)
-        if mine.size:
-            local = orc.batch(payload, mine, max(total, 1))  # global out indices, this rank's chunks only
-        got = shard.gather_checksums(torch.from_numpy(local.view(np.int32).copy()), pk, PKTS_PER_BLOCK, world,
-                                     rank)
+        payload = shard.rank_payload(file_bytes, lay, sb, rank)
+        ln, so, items = shard.gather_plan(pk, gp, world, flags)
+        mine = shard.plan_packets(pk, gp, world, rank, flags)
+        in_place = rank == 0 and not ln[0]
+        nlocal = total if in_place else int(ln[rank])
+        # the rank's plan output: its chunks at the indices the library's plan uses
+        local = oracle.Oracle().batch(payload, mine, max(nlocal, 1)) if mine.size else np.zeros(1, np.uint32)
+        if not in_place:
+            assert mine.size == 0 or oracle.total_checksums(mine) == nlocal  # the local array is dense
+        got = shard.gather_checksums(torch.from_numpy(local.view(np.int32).copy()), pk, gp, world, rank, flags)
 
         # bench.py's timing rule: the slowest rank's time is the job's
         t = torch.tensor([float(rank + 1)], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
 
         if rank == 0:
-            want = orc.batch(file_bytes, pk, total)
-            ok = bool(np.array_equal(got, want)) and float(t.item()) == float(world)
+            if case[0] == "c4":
+                ok = hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
+            else:
+                ok = bool(np.array_equal(got, oracle.Oracle().batch(file_bytes, pk, total)))
+            # every received group is one scatter item, every checksum covered exactly once
+            seen = np.zeros(total, np.int32)
+            for src, dst, n in items.astype(np.int64):
+                seen[dst:dst + n] += 1
+            if in_place:
+                for p in mine:
+                    n = (int(p["len"]) + int(p["bpc"]) - 1) // int(p["bpc"])
+                    seen[int(p["out_idx"]):int(p["out_idx"]) + n] += 1
+            ok = ok and bool(np.all(seen == 1)) and float(t.item()) == float(world)
             with open(result_path, "w") as f:
                 f.write("ok" if ok else "mismatch")
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,nblocks,bpc,ragged", [(2, 7, 512, False), (2, 2, 4096, True), (3, 8, 512, True),
-                                                      (2, 1, 512, False), (3, 5, 1536, True),
-                                                      (8, 32, 512, False), (8, 11, 512, True)])
-def test_round_robin_gather_matches_oracle(tmp_path, world, nblocks, bpc, ragged):
+@pytest.mark.parametrize("world,case,flags", [
+    (2, ("c4",), 0), (3, ("c4",), 0), (8, ("c4",), 0), (8, ("c4",), SELF_SEND),
+    (2, ("f", 7, 512, False), 0), (2, ("f", 2, 4096, True), SELF_SEND), (3, ("f", 8, 512, True), 0),
+    (2, ("f", 1, 512, False), 0), (3, ("f", 5, 1536, True), 0), (3, ("f", 5, 1536, True), SELF_SEND),
+    (8, ("f", 11, 512, True), 0)])
+def test_library_gather_plan_matches_reference(tmp_path, world, case, flags):
     import oracle
 
     oracle.build()
     res = str(tmp_path / "result")
-    mp.start_processes(_worker, args=(world, _free_port(), nblocks, bpc, ragged, res), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), case, flags, res), nprocs=world, join=True,
                        start_method="spawn")
     with open(res) as f:
         assert f.read() == "ok"
+
+
+def test_gather_plan_shape():
+    """crc32c_multi_gather_plan on config 4 at 8 ranks: 7 sending ranks of 4
+    blocks (32 768 checksums = 128 KiB each), staged back to back, 28 scatter
+    items of 8192 checksums; rank 0 in place sends nothing (with
+    CRC32C_MULTI_SELF_SEND it sends too: 32 items)."""
+    hdfs = load_package()
+    hdfs.lib()
+    import oracle
+    from hdfs_crc32c_amd import shard
+
+    pk = oracle.uniform_packets(2048, 65536, 512)
+    ln, so, items = shard.gather_plan(pk, 64, 8)
+    assert list(ln) == [0] + [32768] * 7 and list(so) == [0, 0] + [32768 * k for k in range(1, 7)]
+    assert items.shape == (28, 3) and set(items[:, 2]) == {8192}
+    # block g (on rank g % 8 > 0) lands at file index 8192 g from its rank's slot
+    for src, dst, n in items.astype(np.int64):
+        g = dst // 8192
+        assert g % 8 and src == so[g % 8] + (g // 8) * 8192
+    ln, so, items = shard.gather_plan(pk, 64, 8, SELF_SEND)
+    assert list(ln) == [32768] * 8 and items.shape == (32, 3)
+    p0 = shard.plan_packets(pk, 64, 8, 0, SELF_SEND)
+    assert p0.size == 256 and int(p0["out_idx"].max()) == 32768 - 128  # local indices when self-sending
+    assert int(shard.plan_packets(pk, 64, 8, 0)["out_idx"].max()) == 2048 * 128 - 128 - 7 * 64 * 128  # global
 
 
 def test_layout_helpers():

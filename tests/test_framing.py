@@ -92,3 +92,42 @@ def test_block_md5_of_crcs():
     assert hdfs.block_md5(sums.byteswap(), hdfs.CRC32C_BIG_ENDIAN) == want
     for n in (0, 1, 13, 255, 256, 257, 1000):
         assert hdfs.block_md5(sums[:n]) == hashlib.md5(sums[:n].astype(">u4").tobytes()).digest(), n
+
+
+def test_verify_frames_without_gpu_cpu_fallback():
+    """crc32c_verify_frames_host with ctx = NULL (no usable GPU) and
+    CRC32C_CPU_FALLBACK verifies on the host CPU (the product's
+    crc32c_chunks_cpu); without the flag it is refused.  Malformed or
+    misplaced frames fail with -EBADMSG and say why in crc32c_last_error()."""
+    hdfs = load_package()
+    bpc, chunk_offset = 512, 3 * 512
+    pk = _block_packets(hdfs, 300000, chunk_offset, bpc)
+    payload = oracle.xorshift64_bytes(300000 + 16, 5)
+    sums = oracle.Oracle().batch(payload, pk, hdfs.total_checksums(pk))
+    pre, offs = hdfs.frame_packets(pk, sums, 0, block_offset=chunk_offset)
+    parts = []
+    for i in range(pk.size):
+        parts.append(np.frombuffer(pre[int(offs[i]):int(offs[i + 1])], np.uint8))
+        parts.append(payload[int(pk["payload_off"][i]):int(pk["payload_off"][i]) + int(pk["len"][i])])
+    fr = np.concatenate(parts)
+    r = hdfs.verify_frames(fr, bpc, chunk_offset, hdfs.CRC32C_CPU_FALLBACK)
+    assert (r.packets, r.mismatches, r.first_bad, r.checksums, r.last_packet) == (
+        pk.size, 0, 2**64 - 1, hdfs.total_checksums(pk), 1)
+    assert hdfs.last_path() == hdfs.PATH_CPU
+    info, _ = hdfs.parse_frames(fr)
+    bad = fr.copy()
+    bad[int(info["data_off"][2]) + 3 * bpc + 1] ^= 4
+    r = hdfs.verify_frames(bad, bpc, chunk_offset, hdfs.CRC32C_CPU_FALLBACK)
+    assert (r.mismatches, r.first_bad) == (1, hdfs.total_checksums(pk[:2]) + 3)
+    assert r.first_bad_offset == chunk_offset + int(pk["payload_off"][2]) + 3 * bpc
+    with pytest.raises(hdfs.Crc32cError) as e:
+        hdfs.verify_frames(fr, bpc, chunk_offset)  # no GPU, no fallback
+    assert e.value.rc == -22
+    with pytest.raises(hdfs.Crc32cError) as e:
+        hdfs.verify_frames(fr, bpc, chunk_offset + bpc, hdfs.CRC32C_CPU_FALLBACK)
+    assert e.value.rc == -74 and "offsetInBlock" in str(e.value)
+    trunc = fr.copy()
+    trunc[:4] = np.frombuffer(struct.pack(">I", 3), np.uint8)  # PLEN < 4
+    with pytest.raises(hdfs.Crc32cError) as e:
+        hdfs.parse_frames(trunc)
+    assert e.value.rc == -74 and "PLEN" in str(e.value)

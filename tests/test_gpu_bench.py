@@ -42,6 +42,9 @@ def test_bench_one_gpu_contract():
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["steps"] == 200 and d["unit"] == "GiB/s" and d["higher_is_better"]
     assert d["bit_exact_vs_reference"] is True
+    # the gate before warm-up, the timed launches on buffer 0 and on a device-random buffer
+    assert d["bit_exact_checks"] == {"before_warmup_buf0": True, "timed_buf0": True,
+                                     "timed_buf1_device_random": True}
     assert d["verify"]["clean"] is True
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["algorithmic_bytes_per_launch"] == 4096 * 65536
@@ -64,3 +67,34 @@ def test_bench_two_ranks_rehearsal(config):
     assert d["host_resident_ranks"] == 2 and d["host_resident_gib_s"] > 0
     assert d["gather_ms"] is not None and d["cpu_baseline"] is None
     assert d["config"]["payload_bytes_per_rank"] > 0
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python3 bench.py --gpus 2` (the driver's form, no launcher): bench.py
+    starts torch.distributed.run with two ranks as a child process and
+    forwards rank 0's line -- here rehearsed as two gloo ranks on the one GPU."""
+    env = dict(os.environ, BENCH_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c2", "--steps", "20",
+                        "--warmup", "5", "--no-cpu", "--nbuf", "2"], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["bit_exact_vs_reference"] is True
+    assert d["bit_exact_checks"]["timed_buf0"] is True and d["bit_exact_checks"]["timed_buf1_device_random"] is True
+    assert len([ln for ln in r.stdout.splitlines() if ln.startswith("{")]) == 1
+
+
+def test_bench_gpus_flag_refuses_more_rccl_ranks_than_gpus():
+    """--gpus N with RCCL needs N GPUs: on a box with fewer it fails fast with
+    a message instead of printing an n_gpus: 1 line."""
+    import torch
+
+    n = torch.cuda.device_count() + 1
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("BENCH_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "5"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "visible GPUs" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

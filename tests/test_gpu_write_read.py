@@ -287,8 +287,10 @@ def test_verify_received_frames(hdfs, gpu_ctx, orc, bpc):
     n = 48
     pk = oracle.uniform_packets(n, pkt_len=65536 - 65536 % bpc, bpc=bpc)
     pk["len"][-1] = 12345
-    pk = np.concatenate([pk, np.zeros(1, pk.dtype)])
+    pk = np.concatenate([pk, np.zeros(1, pk.dtype)])  # the block's final empty packet (hadooprpc.c:853-856)
     pk["payload_off"][-1] = pk["payload_off"][-2] + pk["len"][-2]
+    pk["bpc"][-1] = bpc
+    pk["out_idx"][-1] = oracle.total_checksums(pk[:-1])
     payload = oracle.xorshift64_bytes(int(pk["payload_off"][-1]) + 16, 4242 + bpc)
     chunk_offset = 8 * bpc
     fr = _frames(hdfs, orc, payload, pk, bpc, chunk_offset)
@@ -391,7 +393,36 @@ def test_multi_rank_mode_single_rank(hdfs, orc):
     mp.exec([shard.data_ptr()], out.data_ptr())
     m.sync()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, mp.nchecksums, big_endian=True))
+    # successive execs on alternating streams (they reuse the plan's staging
+    # buffers: each waits for the previous one), two different shards
+    torch_streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    host2 = host.copy()
+    host2[:host2.size - 16] ^= 0x5C
+    payload2 = payload.copy()
+    for rank, soff, poff, nbytes in layout.astype(np.int64):
+        payload2[poff:poff + nbytes] = host2[soff:soff + nbytes]
+    shard2 = torch.from_numpy(host2).cuda()
+    outs = [torch.zeros_like(out) for _ in range(6)]
+    torch.cuda.synchronize()
+    for k in range(6):
+        mp.exec([(shard if k % 2 == 0 else shard2).data_ptr()], outs[k].data_ptr(), [torch_streams[k % 2].cuda_stream])
+    torch.cuda.synchronize()
+    want2 = orc.batch(payload2, pk, mp.nchecksums, big_endian=True)
+    for k in range(6):
+        assert np.array_equal(outs[k].cpu().numpy().view(np.uint32),
+                              want2 if k % 2 else orc.batch(payload, pk, mp.nchecksums, big_endian=True)), k
     mp.close()
+    m.close()
+
+
+def test_multi_plan_refuses_a_device_twice(hdfs):
+    """RCCL has one rank per GPU: a one-process multi handle listing a device
+    twice can deal host batches (crc32c_multi_batch_host) but its plan is
+    refused at creation, not at the first exec."""
+    m = hdfs.Multi([0, 0])
+    with pytest.raises(hdfs.Crc32cError) as e:
+        m.plan(oracle.uniform_packets(128), 64)
+    assert e.value.rc == -22 and "twice" in str(e.value)
     m.close()
 
 
@@ -566,3 +597,67 @@ def test_fsx_style_write_sequence(hdfs, gpu_ctx, orc):
             boff = 0
         f = np.concatenate([f[:start], stream_bytes])
     assert nwrites > 60
+
+
+def test_plans_created_while_another_thread_captures(hdfs, gpu_ctx, orc):
+    """Plan create / exec / destroy on one thread while another thread
+    captures a graph in global mode (torch.cuda.graph's default): no
+    device-wide synchronisation and no call that would invalidate the
+    capture.  48 plans of growing shapes (new pool blocks, more than the old
+    32-block epoch) are created, run on their own stream and destroyed during
+    the capture; the captured launch replays exactly afterwards, and every
+    plan's checksums are right."""
+    import threading
+
+    torch = _torch()
+    payload = oracle.xorshift64_bytes(200 * 65536 + 16, 55)
+    dpay = torch.from_numpy(payload).cuda()
+    pk = oracle.uniform_packets(64)
+    want = orc.batch(payload, pk, 8192)
+    plan = gpu_ctx.plan(pk)
+    out_g = torch.zeros(8192, dtype=torch.int32, device="cuda")
+    plan.exec(dpay.data_ptr(), out_g.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    shapes = []
+    for k in range(48):
+        q = oracle.uniform_packets(1 + (k * 37) % 199, 65536, (512, 1536, 1024)[k % 3])
+        q["len"][-1] -= 7 * k
+        shapes.append(q)
+    outs = [torch.zeros(max(oracle.total_checksums(q), 1), dtype=torch.int32, device="cuda") for q in shapes]
+    side = torch.cuda.Stream()
+    started, finished, errs = threading.Event(), threading.Event(), []
+
+    def worker():
+        started.wait(60)
+        try:
+            for q, o in zip(shapes, outs):
+                p = gpu_ctx.plan(q)
+                p.exec(dpay.data_ptr(), o.data_ptr(), side.cuda_stream)
+                p.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+        finished.set()
+
+    t = threading.Thread(target=worker)
+    t.start()
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    try:
+        with torch.cuda.graph(g, stream=cap):  # capture_error_mode="global"
+            plan.exec(dpay.data_ptr(), out_g.data_ptr(), cap.cuda_stream)
+            started.set()
+            assert finished.wait(120)
+    finally:
+        started.set()
+        t.join()
+    assert not errs, errs
+    out_g.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out_g.cpu().numpy().view(np.uint32), want)
+    for q, o in zip(shapes, outs):
+        n = oracle.total_checksums(q)
+        assert np.array_equal(o.cpu().numpy().view(np.uint32)[:n], orc.batch(payload, q, n))
+    del g
+    plan.close()

@@ -132,6 +132,27 @@ def test_nchunks_and_packetize(hdfs, orc):
         assert hdfs.packetize(*args) == orc.packetize(*args), args
 
 
+def test_zero_length_and_zero_bpc_packets_agree(hdfs):
+    """One rule across the ABI: a zero-length packet (the block's final empty
+    packet, hadooprpc.c:853-856) has no checksums whatever its bpc -- it is
+    counted by nothing and accepted by the plan builder; a packet with data
+    and bpc == 0 is refused by the plan builder and counts nothing."""
+    pk = oracle.uniform_packets(3, 65536, 512)
+    end = np.zeros(1, pk.dtype)  # len 0, bpc 0: as the reference's last packet could be written
+    end["payload_off"] = 3 * 65536
+    for tail_bpc in (0, 512):
+        end["bpc"] = tail_bpc
+        b = np.concatenate([pk, end])
+        assert hdfs.total_checksums(b) == oracle.total_checksums(b) == 3 * 128
+        tiles, gen = hdfs.debug_plan(b)
+        assert tiles.size == 3 * 8 and gen.size == 0
+    bad = pk.copy()
+    bad["bpc"][1] = 0
+    assert hdfs.total_checksums(bad) == 3 * 128  # packet 1 counts nothing; packet 2 ends at 384
+    with pytest.raises(hdfs.Crc32cError):
+        hdfs.debug_plan(bad)
+
+
 def test_chunks_cpu_matches_reference_loop(hdfs, orc, golden):
     """crc32c_chunks_cpu (the per-packet loop of hadooprpc.c:733-742 on the
     host, whole chunks as 3 interleaved crc32q chains): every golden packet
@@ -446,3 +467,21 @@ def test_workloads_match_oracle_shapes(hdfs):
         assert pk.dtype == hdfs.PACKET_DTYPE and text
     a, b = workloads.synthetic_bytes(1000, 3), workloads.synthetic_bytes(1000, 3)
     assert a.dtype == np.uint8 and np.array_equal(a, b)
+
+
+def test_no_device_wide_sync_on_plan_paths():
+    """Plan blocks are recycled after per-stream events, not a device-wide
+    synchronisation: hipDeviceSynchronize appears in the runtime only in the
+    context teardown (release_pools, and there only for blocks a graph
+    captured), never on a plan create / exec / destroy path (which would wait
+    for every stream of the device and break a global-mode graph capture on
+    another thread)."""
+    csrc = os.path.join(ROOT, "native-hdfs-fuse_amd", "csrc")
+    sig = re.compile(r"^(?:[A-Za-z_][\w:<>\*&]*\s+)+\**([A-Za-z_]\w*)\(", re.M)
+    for name in ("crc32c_runtime.hip", "crc32c_multi.hip", "crc32c_kernel.hip"):
+        text = re.sub(r"//[^\n]*", "", open(os.path.join(csrc, name)).read())
+        for m in re.finditer(r"hipDeviceSynchronize", text):
+            funcs = [f.group(1) for f in sig.finditer(text[:m.start()])]
+            assert funcs and funcs[-1] == "release_pools", (name, funcs[-1:])
+    text = open(os.path.join(csrc, "runtime_internal.h")).read()
+    assert "kEpochBlocks" not in text

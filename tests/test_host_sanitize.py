@@ -22,7 +22,7 @@ def test_host_sources_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "host_asan")
     subprocess.run(["gcc", *SAN, "-c", os.path.join(ROOT, "oracle", "crc32c_oracle.c"), "-o", oracle_o],
                    check=True)
-    srcs = [os.path.join(CSRC, f) for f in ("crc_math.cpp", "cpu_crc32c.cpp", "plan.cpp", "framing.cpp", "frames.cpp")]
+    srcs = [os.path.join(CSRC, f) for f in ("errors.cpp", "crc_math.cpp", "cpu_crc32c.cpp", "plan.cpp", "framing.cpp", "frames.cpp")]
     subprocess.run(["g++", *SAN, "-std=c++17", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
                     "-I/opt/rocm/include", os.path.join(ROOT, "tests", "sanitize", "host_asan.cpp"), *srcs,
                     oracle_o, "-lpthread", "-o", exe], check=True)
@@ -46,7 +46,7 @@ def test_host_threads_under_tsan(tmp_path):
     exe = str(tmp_path / "host_tsan")
     subprocess.run(["gcc", *TSAN, "-fPIC", "-c", os.path.join(ROOT, "oracle", "crc32c_oracle.c"), "-o", oracle_o],
                    check=True)
-    srcs = [os.path.join(CSRC, f) for f in ("crc_math.cpp", "cpu_crc32c.cpp", "plan.cpp", "framing.cpp", "frames.cpp")]
+    srcs = [os.path.join(CSRC, f) for f in ("errors.cpp", "crc_math.cpp", "cpu_crc32c.cpp", "plan.cpp", "framing.cpp", "frames.cpp")]
     subprocess.run(["g++", *TSAN, "-std=c++17", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC,
                     "-I/opt/rocm/include", os.path.join(ROOT, "tests", "sanitize", "host_tsan.cpp"), *srcs,
                     oracle_o, "-lpthread", "-o", exe], check=True)
