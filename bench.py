@@ -226,6 +226,64 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def timed_calls(fn, budget_s: float = 0.25, min_reps: int = 5, max_reps: int = 2000) -> float:
+    """Median wall seconds of one call of fn(), over about budget_s of calls."""
+    fn()
+    t0 = time.perf_counter()
+    fn()
+    one = max(time.perf_counter() - t0, 1e-7)
+    reps = int(min(max_reps, max(min_reps, budget_s / one)))
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def host_block_latency(hdfs, ctx, pk, payload: np.ndarray, want, ref_threads: int, with_ref: bool):
+    """The host-resident path at the reference's unit of work (one call over
+    one batch that starts and ends in host memory, e.g. one 4 MiB block:
+    hadoop_fuse_write_block, src/fuse.c:336-449, one libfuse thread; packets
+    cut by hadooprpc.c:815-860): median microseconds per call of
+      gpu_pinned / gpu_pageable -- crc32c_batch_host (H2D copy, kernel,
+                                   checksums back in host memory),
+      product_cpu_1t            -- the product's host path (crc32c_chunks_cpu
+                                   per packet on the calling thread),
+      reference_1t / _Nt        -- the reference's crc32c.c per chunk as
+                                   hadooprpc.c:739 calls it, on 1 thread and
+                                   split over N persistent threads (the CPU
+                                   baseline leg: oracle/_ref, in-cache),
+    each bit-exact against `want` (the reference's checksums)."""
+    import torch
+
+    nbytes = int(pk["len"].astype(np.int64).sum())
+    nout = hdfs.total_checksums(pk)
+    pinned = torch.from_numpy(payload).pin_memory().numpy()
+    out = np.zeros(max(nout, 1), np.uint32)
+    res = {"bytes": nbytes}
+    exact = True
+    for name, buf in (("gpu_pinned", pinned), ("gpu_pageable", payload)):
+        res[name + "_us"] = round(timed_calls(lambda: ctx.batch_host(buf, pk, out=out)) * 1e6, 2)
+        exact = exact and bool(np.array_equal(out[:nout], want))
+    res["product_cpu_1t_us"] = round(timed_calls(lambda: hdfs.batch_host_cpu(payload, pk, out=out)) * 1e6, 2)
+    exact = exact and bool(np.array_equal(out[:nout], want))
+    if with_ref:
+        import oracle as oracle_mod
+
+        try:
+            ref = oracle_mod.Reference()
+            for t in sorted({1, ref_threads}):
+                one = ref.block_latency_seconds(payload, pk, out, t, 3)
+                reps = int(min(5000, max(5, 0.25 / max(one, 1e-7))))
+                res["reference_%dt_us" % t] = round(ref.block_latency_seconds(payload, pk, out, t, reps) * 1e6, 2)
+                exact = exact and bool(np.array_equal(out[:nout], want))
+        except (FileNotFoundError, OSError):
+            pass
+    res["bit_exact"] = exact
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -247,6 +305,9 @@ def main():
     ap.add_argument("--two-streams", action="store_true",
                     help="also time 1000 batches alternated over two streams (their launches overlap, so a "
                          "rocprofv3 run of the bench would average overlapped durations: off by default)")
+    ap.add_argument("--host-sweep", action="store_true",
+                    help="also time the host-resident path per call against the host CPU over batch sizes from "
+                         "one 64 KiB packet to 256 MiB (N = 1; adds host_sweep to the line)")
     ap.add_argument("--host-multi-devices", type=int, default=1,
                     help="GPUs crc32c_multi_batch_host deals the host-resident batch over at N = 1 (0: skip)")
     args = ap.parse_args()
@@ -604,7 +665,7 @@ def main():
     # checksums in host memory), every rank at once on its own GPU and PCIe
     # link; the node-level rate is all ranks' bytes / the slowest rank's time.
     # Beside it, the link's ceiling: a plain pinned H2D copy of the same bytes.
-    host = h2d = host_multi = None
+    host = h2d = host_multi = host_latency = host_sweep = None
     if not args.no_host and args.config != "c4":
         pinned = torch.from_numpy(payload0).pin_memory()
         hp = pinned.numpy()
@@ -660,6 +721,25 @@ def main():
                 bit_exact = bit_exact and exact_multi
             finally:
                 m.close()
+        # Per call, at this config's batch (config 3: the reference's unit,
+        # one 4 MiB block), against the host CPU; --host-sweep: over sizes.
+        if world == 1:
+            quota = cpu_quota()[1]
+            qthreads = max(1, min(os.cpu_count() or 1, int(math.ceil(quota)) if quota else 16))
+            host_latency = host_block_latency(hdfs, ctx, pk, payload0, want, qthreads, not args.no_cpu)
+            timed_checks["host_latency"] = host_latency["bit_exact"]
+            if args.host_sweep:
+                host_sweep = []
+                for npk in (1, 4, 16, 64, 256, 1024, 4096):
+                    spk = uniform_packets(npk)
+                    sp = synthetic_bytes(npk * 65536, 77 + npk)
+                    sw = reference_checksums(sp, spk, hdfs.total_checksums(spk))
+                    r = host_block_latency(hdfs, ctx, spk, sp, sw, qthreads, not args.no_cpu)
+                    host_sweep.append(r)
+                    timed_checks["host_sweep_%d" % npk] = r["bit_exact"]
+                cross = [r["bytes"] for r in host_sweep if "reference_1t_us" in r and r["gpu_pinned_us"] < r["reference_1t_us"]]
+                host_sweep = {"sizes": host_sweep,
+                              "gpu_pinned_beats_reference_1t_from_bytes": min(cross) if cross else None}
 
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"))
@@ -700,6 +780,8 @@ def main():
             "host_h2d_copy_gib_s": h2d,
             "host_resident_ranks": world if host is not None else None,
             "host_resident_multi": host_multi,
+            "host_resident_per_call": host_latency,
+            "host_sweep": host_sweep,
             "verify": verify,
             "two_streams": two_streams,
             "box_read_probe": read_probe,

@@ -226,6 +226,47 @@ int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, ui
                                uint64_t bufferoffset, uint64_t len, uint64_t blockoffset, uint32_t packetsize,
                                uint32_t bpc, uint32_t flags, crc32c_plan **out);
 
+/* ---------------------------------------------------------------------------
+ * 3b. Many blocks of one shape in one launch (concurrent block writes).
+ *
+ * libfuse runs hadoop_fuse_write_block (src/fuse.c:336-449) on many worker
+ * threads at once (fuse.c:1771, no -s); each writes one block, cut into
+ * packets by hadoop_rpc_send_packets (hadooprpc.c:815-860).  A launch per
+ * 4 MiB block is bound by HIP's launch path (~3.5-4 us per block); one launch
+ * over many blocks is not.  `plan` here describes ONE block's packets
+ * (offsets from the block's start; not CRC32C_DEVICE_ADDRESSES).
+ *
+ * crc32c_plan_exec_blocks: the plan run once per block, block i's payload at
+ * dev_payloads[i] and its checksums to dev_outs[i] (4-byte aligned), as ONE
+ * launch per up to 32 blocks (the block table rides in the kernel arguments:
+ * nothing is built or uploaded per call).  A plan with items other than
+ * tiles (tails under 4 bytes, bpc outside [4, 8192]) runs one launch per
+ * block instead.  Asynchronous on `stream`.
+ *
+ * crc32c_blocks: a coalescing queue for block writes arriving from several
+ * threads without any batching by the caller.  crc32c_block_submit queues a
+ * block (its bytes already in device memory) and returns a ticket; the
+ * queue goes out as one crc32c_plan_exec_blocks launch on the queue's own
+ * stream when it holds max_blocks blocks, on crc32c_block_flush, or when a
+ * thread waits for a queued block (crc32c_block_wait) and window_us have
+ * passed since the queue's first block (group commit).  crc32c_block_wait
+ * returns when the ticket's checksums are in device memory;
+ * crc32c_block_checksums is submit + wait.  Thread-safe.  Destroy the queue
+ * (it flushes and waits) before its plan.  crc32c_blocks_stats: launches
+ * (flushes) made and blocks they carried.
+ * ------------------------------------------------------------------------- */
+int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
+                            size_t nblocks, void *stream);
+
+typedef struct crc32c_blocks crc32c_blocks;
+int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window_us, crc32c_blocks **out);
+int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket);
+int crc32c_block_flush(crc32c_blocks *q);
+int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket);
+int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out);
+int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blocks);
+int crc32c_blocks_destroy(crc32c_blocks *q);
+
 /* One-shot device batch: builds a plan, runs it on `stream` and waits for it. */
 int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,
                       uint32_t *dev_out, uint32_t flags, void *stream);

@@ -167,6 +167,14 @@ def _bind(L):
         "crc32c_multi_plan_nchecksums": (u64, [vp]),
         "crc32c_multi_plan_shard_bytes": (u64, [vp, i32]),
         "crc32c_parse_frames": (ctypes.c_int64, [vp, sz, vp, sz, ctypes.POINTER(u64)]),
+        "crc32c_plan_exec_blocks": (i32, [vp, vp, vp, sz, vp]),
+        "crc32c_blocks_create": (i32, [vp, u32, u32, pp]),
+        "crc32c_block_submit": (i32, [vp, vp, vp, ctypes.POINTER(u64)]),
+        "crc32c_block_flush": (i32, [vp]),
+        "crc32c_block_wait": (i32, [vp, u64]),
+        "crc32c_block_checksums": (i32, [vp, vp, vp]),
+        "crc32c_blocks_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
+        "crc32c_blocks_destroy": (i32, [vp]),
         "crc32c_verify_frames_host": (i32, [vp, vp, sz, u32, u64, u32, ctypes.POINTER(FramesResult)]),
     }
     for name, (res, args) in sig.items():
@@ -348,6 +356,17 @@ class Plan:
         _check(lib().crc32c_plan_verify(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_expected),
                                         ctypes.c_void_p(dev_result), ctypes.c_void_p(stream)), "crc32c_plan_verify")
 
+    def exec_blocks(self, dev_payloads, dev_outs, stream: int = 0) -> None:
+        """crc32c_plan_exec_blocks: this plan (one block's shape) on every block, one launch per <= 32."""
+        n = len(dev_payloads)
+        pays = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(x) for x in dev_payloads])
+        outs = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(x) for x in dev_outs])
+        _check(lib().crc32c_plan_exec_blocks(self.handle, pays, outs, n, ctypes.c_void_p(stream)),
+               "crc32c_plan_exec_blocks")
+
+    def blocks(self, max_blocks: int = 16, window_us: int = 20) -> "Blocks":
+        return Blocks(self, max_blocks, window_us)
+
     def exec_variant(self, dev_payload: int, dev_out: int, variant: int, dev_stamps: int = 0, stream: int = 0) -> None:
         """Diagnostic (debug library): run an explicit kernel variant (5/6/36 write per-wave timestamps)."""
         _check(debug_lib().crc32c_debug_plan_exec_variant(self.handle, ctypes.c_void_p(dev_payload),
@@ -358,6 +377,49 @@ class Plan:
     def close(self) -> None:
         if self.handle:
             lib().crc32c_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Blocks:
+    """crc32c_blocks: block writes from several threads coalesced into one launch (group commit)."""
+
+    def __init__(self, plan: Plan, max_blocks: int = 16, window_us: int = 20):
+        h = ctypes.c_void_p()
+        _check(lib().crc32c_blocks_create(plan.handle, max_blocks, window_us, ctypes.byref(h)), "crc32c_blocks_create")
+        self.plan = plan  # the plan outlives the queue
+        self.handle = h
+
+    def submit(self, dev_payload: int, dev_out: int) -> int:
+        t = ctypes.c_uint64(0)
+        _check(lib().crc32c_block_submit(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
+                                         ctypes.byref(t)), "crc32c_block_submit")
+        return int(t.value)
+
+    def flush(self) -> None:
+        _check(lib().crc32c_block_flush(self.handle), "crc32c_block_flush")
+
+    def wait(self, ticket: int) -> None:
+        _check(lib().crc32c_block_wait(self.handle, ticket), "crc32c_block_wait")
+
+    def checksums(self, dev_payload: int, dev_out: int) -> None:
+        """Submit + wait: returns when the block's checksums are in dev_out."""
+        _check(lib().crc32c_block_checksums(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out)),
+               "crc32c_block_checksums")
+
+    def stats(self):
+        f, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(lib().crc32c_blocks_stats(self.handle, ctypes.byref(f), ctypes.byref(b)), "crc32c_blocks_stats")
+        return int(f.value), int(b.value)
+
+    def close(self) -> None:
+        if self.handle:
+            lib().crc32c_blocks_destroy(self.handle)
             self.handle = None
 
     def __del__(self):
@@ -551,6 +613,19 @@ def chunks_cpu(packet: np.ndarray, bpc: int, flags: int = 0) -> np.ndarray:
     n = nchunks(packet.size, bpc)
     out = np.zeros(max(n, 1), np.uint32)
     _check(lib().crc32c_chunks_cpu(_np_ptr(packet), packet.size, bpc, _np_ptr(out), flags), "crc32c_chunks_cpu")
+    return out[:n]
+
+
+def batch_host_cpu(payload: np.ndarray, pkts, flags: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+    """The product's host-CPU path over a host batch (crc32c_batch_host with no GPU context and
+    CRC32C_CPU_FALLBACK: crc32c_chunks_cpu per packet on the calling thread)."""
+    pkts = as_packets(pkts)
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    n = total_checksums(pkts)
+    if out is None:
+        out = np.zeros(max(n, 1), np.uint32)
+    _check(lib().crc32c_batch_host(None, _np_ptr(payload), _np_ptr(pkts), pkts.size, _np_ptr(out),
+                                   flags | CRC32C_CPU_FALLBACK), "crc32c_batch_host (CPU)")
     return out[:n]
 
 

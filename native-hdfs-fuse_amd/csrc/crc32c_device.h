@@ -111,11 +111,20 @@ typedef const __attribute__((address_space(4))) FastTile *ConstTiles;
 typedef const __attribute__((address_space(4))) ConstRun *ConstRuns;
 
 __device__ __forceinline__ FastTile tile_at(const KParams &p, uint32_t i) {
+    uint32_t b = 0;
+    if (p.nblocks) {  // multi-block launch (wave-uniform): tile i of the plan's block shape, block b's copy
+        b = i / p.block_tiles;
+        i -= b * p.block_tiles;
+    }
     const ConstTiles t = (ConstTiles)(p.tiles) + i;
     FastTile r;
     r.src = t->src;
     r.out = t->out;
     r.meta = t->meta;
+    if (p.nblocks) {
+        r.src += p.blocks[b].payload_delta;
+        r.out += p.blocks[b].out_delta;
+    }
     return r;
 }
 

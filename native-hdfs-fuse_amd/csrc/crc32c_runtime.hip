@@ -821,6 +821,58 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
     return launch_plan(plan, plan_params(plan, dev_payload, dev_out), static_cast<hipStream_t>(stream));
 }
 
+int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
+                            size_t nblocks, void *stream) {
+    if (!plan) return fail(-EINVAL, "plan == NULL");
+    if (plan->absolute) return fail(-EINVAL, "a multi-block launch takes a plan of one block's shape, not device addresses");
+    if (nblocks && (!dev_payloads || !dev_outs)) return fail(-EINVAL, "payloads/outs == NULL");
+    if (plan->nchecksums == 0 || nblocks == 0) return 0;
+    for (size_t i = 0; i < nblocks; ++i)
+        if ((!dev_payloads[i] && plan_reads_payload(plan)) || !dev_outs[i] || (uintptr_t(dev_outs[i]) & 3u))
+            return fail(-EINVAL, "block %zu: payload NULL, or out NULL / not 4-byte aligned", i);
+    DeviceGuard guard(plan->ctx->device);
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const DevicePlan &dp = plan->dp;
+    if (dp.ngen || dp.nseg || dp.nconst || dp.ntiles == 0) {
+        // (items other than tiles -- tails under 4 bytes, bpc outside [4, 8192]
+        // -- have no multi-block form: one launch per block)
+        for (size_t i = 0; i < nblocks; ++i)
+            if (int rc = launch_plan(plan, plan_params(plan, dev_payloads[i], dev_outs[i]), s)) return rc;
+        return 0;
+    }
+    const uint64_t max_launch_tiles = UINT32_MAX;
+    size_t i = 0;
+    while (i < nblocks) {
+        // Up to kMaxLaunchBlocks blocks whose payloads and outputs are within
+        // reach of the launch's bases: payload deltas below 2^47 (tile
+        // offsets keep a tail length in bits 48-63), output indices below 2^32.
+        uintptr_t plo = UINTPTR_MAX, olo = UINTPTR_MAX, ohi = 0, phi = 0;
+        size_t j = i;
+        for (; j < nblocks && j - i < kMaxLaunchBlocks && uint64_t(j - i + 1) * dp.ntiles <= max_launch_tiles; ++j) {
+            const uintptr_t pp = uintptr_t(dev_payloads[j]) & ~uintptr_t(15), oo = uintptr_t(dev_outs[j]);
+            const uintptr_t nplo = std::min(plo, pp), nphi = std::max(phi, pp);
+            const uintptr_t nolo = std::min(olo, oo), nohi = std::max(ohi, oo);
+            if (j > i && (nphi - nplo >= (uintptr_t(1) << 47) || (nohi - nolo) / 4 + plan->nchecksums > (1ull << 32)))
+                break;
+            plo = nplo, phi = nphi, olo = nolo, ohi = nohi;
+        }
+        KParams p = plan_params(plan, reinterpret_cast<const void *>(plo), reinterpret_cast<uint32_t *>(olo));
+        p.nblocks = uint32_t(j - i);
+        p.block_tiles = dp.ntiles;
+        p.ntiles = uint32_t(uint64_t(j - i) * dp.ntiles);
+        for (size_t k = i; k < j; ++k) {
+            BlockRef &b = p.blocks[k - i];
+            b.payload_delta = uint64_t(uintptr_t(dev_payloads[k]) - plo);
+            b.out_delta = uint32_t((uintptr_t(dev_outs[k]) - olo) / 4);
+            b.reserved = 0;
+            if (b.payload_delta & 15u) p.general = 1u;  // (shifted loads for blocks off 16-byte alignment)
+        }
+        if (int rc = launch_plan(plan, p, s)) return rc;
+        i = j;
+    }
+    return 0;
+}
+
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream) {
     return crc32c_plan_verify_bitmap(plan, dev_payload, dev_expected, dev_result, nullptr, stream);

@@ -20,6 +20,17 @@ constexpr uint32_t kS4COff = kTableAllocS4;
 constexpr uint32_t kTableAllocS4C = ((uint32_t(kS4CBytes) + 16384 - 1) / 16384) * 16384;
 constexpr uint32_t kTableAllocS4Full = kS4COff + kTableAllocS4C;
 
+// One block of a multi-block launch (crc32c_plan_exec_blocks): the plan's
+// work items describe one block's shape; block b's copy of item i reads at
+// payload + src_i + payload_delta and writes out[out_i + out_delta].
+struct BlockRef {
+    uint64_t payload_delta;
+    uint32_t out_delta;
+    uint32_t reserved;
+};
+// Blocks one launch carries (in the kernel arguments: 16 B each).
+constexpr uint32_t kMaxLaunchBlocks = 32;
+
 struct KParams {
     const FastTile *tiles;  // power-of-two and general tiles
     const GenItem *gen;
@@ -51,6 +62,12 @@ struct KParams {
     // of the pair, which this launch resets for the next one.
     uint32_t *sched;
     uint32_t *sched_next;
+    // Multi-block launch: nblocks > 0 runs the plan's block_tiles tiles once
+    // per block (tile j = block j / block_tiles, tile j % block_tiles); the
+    // plan has tiles only.  0: an ordinary launch.
+    uint32_t nblocks;
+    uint32_t block_tiles;
+    BlockRef blocks[kMaxLaunchBlocks];
 };
 
 // Device state of one verification launch ("slot"), u32 words, each on its

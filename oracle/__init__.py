@@ -176,6 +176,8 @@ class Reference:
         lib.ref_batch_mt.argtypes = [vp, vp, u64, vp, ctypes.c_int, ctypes.c_int]
         lib.ref_batch_mt_rot.restype = ctypes.c_double
         lib.ref_batch_mt_rot.argtypes = [vp, u64, vp, u64, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        lib.ref_block_latency.restype = ctypes.c_double
+        lib.ref_block_latency.argtypes = [vp, vp, u64, vp, ctypes.c_int, ctypes.c_int]
         self.lib = lib
 
     @staticmethod
@@ -196,6 +198,11 @@ class Reference:
 
     def batch_mt_seconds(self, payload, pkts, out, nthreads: int, reps: int) -> float:
         return float(self.lib.ref_batch_mt(_ptr(payload), _ptr(pkts), pkts.size, _ptr(out), nthreads, reps))
+
+    def block_latency_seconds(self, payload, pkts, out, nthreads: int, reps: int) -> float:
+        """Mean wall seconds of one call over the batch split over nthreads
+        persistent threads (ref_harness.c ref_block_latency; in-cache)."""
+        return float(self.lib.ref_block_latency(_ptr(payload), _ptr(pkts), pkts.size, _ptr(out), nthreads, reps))
 
     def batch_rot_seconds(self, payload, pkts, out, nthreads: int, nbuf: int, reps: int) -> float:
         """Full-width timing: nbuf distinct first-touched copies rotated over reps

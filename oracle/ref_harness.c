@@ -192,3 +192,79 @@ double ref_batch_mt_rot(const void *payload, uint64_t bytes, const ref_packet *p
         free(bufs[b]);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---- per-block latency: one batch split over nthreads, reps times ---------
+ * The reference's unit of work is one block written by one libfuse worker
+ * (src/fuse.c:336-449); this times one call over the batch (e.g. one 4 MiB
+ * block) as a caller would issue it: the batch split into nthreads
+ * contiguous packet slices computed at once by persistent threads (the
+ * calling thread is slice 0), each rep between two barriers.  Returns the
+ * mean wall seconds per rep (in-cache: the same buffer every rep, as a block
+ * just written by the application). */
+typedef struct {
+    const uint8_t *payload;
+    const ref_packet *pkts;
+    uint64_t lo, hi;
+    uint32_t *out;
+    int reps;
+    pthread_barrier_t *bar;
+} ref_lat_job;
+
+static void ref_lat_slice(const ref_lat_job *j)
+{
+    for (uint64_t i = j->lo; i < j->hi; i++)
+        ref_packet_chunks(j->payload + j->pkts[i].payload_off, j->pkts[i].len, j->pkts[i].bpc,
+                          j->out + j->pkts[i].out_idx);
+}
+
+static void *ref_lat_worker(void *arg)
+{
+    ref_lat_job *j = (ref_lat_job *)arg;
+    for (int r = 0; r < j->reps; r++) {
+        pthread_barrier_wait(j->bar);
+        ref_lat_slice(j);
+        pthread_barrier_wait(j->bar);
+    }
+    return NULL;
+}
+
+double ref_block_latency(const void *payload, const ref_packet *pkts, uint64_t npkts, uint32_t *out, int nthreads,
+                         int reps)
+{
+    enum { MAXT = 256 };
+    pthread_t th[MAXT];
+    ref_lat_job jobs[MAXT];
+    pthread_barrier_t bar;
+    struct timespec t0, t1;
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > MAXT)
+        nthreads = MAXT;
+    if (reps < 1)
+        reps = 1;
+    (void)crc32c(0, "", 0);
+    pthread_barrier_init(&bar, NULL, (unsigned)nthreads);
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].payload = (const uint8_t *)payload;
+        jobs[t].pkts = pkts;
+        jobs[t].lo = npkts * (uint64_t)t / (uint64_t)nthreads;
+        jobs[t].hi = npkts * (uint64_t)(t + 1) / (uint64_t)nthreads;
+        jobs[t].out = out;
+        jobs[t].reps = reps;
+        jobs[t].bar = &bar;
+        if (t)
+            pthread_create(&th[t], NULL, ref_lat_worker, &jobs[t]);
+    }
+    ref_lat_slice(&jobs[0]); /* (warm: caches, page mappings) */
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int r = 0; r < reps; r++) {
+        pthread_barrier_wait(&bar);
+        ref_lat_slice(&jobs[0]);
+        pthread_barrier_wait(&bar);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (int t = 1; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&bar);
+    return ((double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec)) / reps;
+}

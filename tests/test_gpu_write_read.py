@@ -661,3 +661,110 @@ def test_plans_created_while_another_thread_captures(hdfs, gpu_ctx, orc):
         assert np.array_equal(o.cpu().numpy().view(np.uint32)[:n], orc.batch(payload, q, n))
     del g
     plan.close()
+
+
+# ---- many blocks of one shape in one launch (concurrent block writes) -------
+def _block_shape(kind):
+    if kind == "full":  # one 4 MiB block of 64 x 64 KiB packets
+        return oracle.uniform_packets(64)
+    if kind == "ragged":  # a short block: 15 packets + a 1000-byte tail packet (general tile)
+        pk = oracle.uniform_packets(16)
+        pk["len"][-1] = 1000
+        return pk
+    if kind == "bpc1536":
+        return oracle.uniform_packets(8, 65536, 1536)
+    if kind == "tiny_tail":  # a 2-byte tail: no multi-block form, one launch per block
+        pk = oracle.uniform_packets(4)
+        pk["len"][-1] = 65536 - 510
+        return pk
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("kind", ["full", "ragged", "bpc1536", "tiny_tail"])
+def test_plan_exec_blocks(hdfs, gpu_ctx, orc, kind):
+    """crc32c_plan_exec_blocks: one block's plan run over 40 blocks in
+    separate device buffers (some off 16-byte alignment, outputs in separate
+    arrays and inside one shared array) -- two launches of <= 32 blocks --
+    every block bit-exact against the oracle."""
+    torch = _torch()
+    pk = _block_shape(kind)
+    n = oracle.total_checksums(pk)
+    ext = int((pk["payload_off"] + pk["len"]).max())
+    bufs, pays, outs, wants = [], [], [], []
+    shared = torch.zeros(20 * n + 8, dtype=torch.int32, device="cuda")
+    for b in range(40):
+        skew = (b * 5) % 16 if b % 3 == 0 else 0
+        host = oracle.xorshift64_bytes(ext + 32, 900 + b)
+        t = torch.from_numpy(host).cuda()
+        bufs.append(t)
+        pays.append(t.data_ptr() + skew)
+        wants.append(orc.batch(host[skew:], pk, n))
+        if b % 2:
+            o = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            bufs.append(o)
+            outs.append((o, 0))
+        else:
+            outs.append((shared, (b // 2) * n))
+    plan = gpu_ctx.plan(pk)
+    stream = torch.cuda.current_stream()
+    plan.exec_blocks(pays, [o.data_ptr() + 4 * off for o, off in outs], stream.cuda_stream)
+    torch.cuda.synchronize()
+    for b, (o, off) in enumerate(outs):
+        got = o.cpu().numpy().view(np.uint32)[off:off + n]
+        assert np.array_equal(got, wants[b]), (kind, b)
+    plan.close()
+
+
+def test_block_queue_threads(hdfs, gpu_ctx, orc):
+    """crc32c_blocks: 12 threads, each writing 6 blocks of 4 MiB one after
+    another through crc32c_block_checksums (no batching by the caller): every
+    block bit-exact against the oracle, and the queue carried them in far
+    fewer launches than blocks (group commit)."""
+    import threading
+
+    torch = _torch()
+    pk = _block_shape("full")
+    n = oracle.total_checksums(pk)
+    nthreads, per = 12, 6
+    hosts = [oracle.xorshift64_bytes(64 * 65536, 7000 + k) for k in range(nthreads * per)]
+    devs = [torch.from_numpy(h).cuda() for h in hosts]
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in hosts]
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    q = plan.blocks(max_blocks=12, window_us=200)
+    errs = []
+    go = threading.Barrier(nthreads)
+
+    def worker(k):
+        try:
+            go.wait()
+            for j in range(per):
+                i = k * per + j
+                q.checksums(devs[i].data_ptr(), outs[i].data_ptr())
+                # the checksums are in device memory now: check this block right away
+                assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), orc.batch(hosts[i], pk, n)), i
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    flushes, blocks = q.stats()
+    assert blocks == nthreads * per and flushes < blocks // 2, (flushes, blocks)
+    # explicit submit / flush / wait
+    for i in range(5):
+        outs[i].zero_()
+    torch.cuda.synchronize()
+    tickets = [q.submit(devs[i].data_ptr(), outs[i].data_ptr()) for i in range(5)]
+    q.flush()
+    for t in reversed(tickets):
+        q.wait(t)
+    for i in range(5):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), orc.batch(hosts[i], pk, n))
+    with pytest.raises(hdfs.Crc32cError):
+        q.wait(10**9)
+    q.close()
+    plan.close()

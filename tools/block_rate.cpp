@@ -1,0 +1,162 @@
+// block_rate.cpp -- diagnostic: concurrent 4 MiB block writes from C, the
+// shape of libfuse's worker threads each running hadoop_fuse_write_block
+// (src/fuse.c:336-449, many threads: fuse.c:1771).  Every thread checksums
+// one device-resident 4 MiB block (64 x 64 KiB packets, bpc 512) per
+// iteration and waits for it, T threads at once; prints one JSON line per
+// mode with the wall time per block over all threads:
+//   single  -- one crc32c_plan_exec per block on the thread's own stream, then
+//              a stream synchronisation (what a caller does without batching)
+//   queue   -- crc32c_block_checksums through one crc32c_blocks queue
+//              (group commit into multi-block launches), one block in flight
+//              per thread
+//   queue2  -- the same with two blocks in flight per thread (submit the next,
+//              then wait for the previous)
+//   kernel  -- one thread issuing crc32c_plan_exec_blocks of B blocks back to
+//              back: the GPU's time per block in a multi-block launch (events)
+//
+//   tools/block_rate [threads=16] [iterations=400] [max_blocks=16] [window_us=30]
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
+#include <vector>
+
+#include "hdfs_crc32c.h"
+
+#define CHECK(x)                                                                      \
+    do {                                                                              \
+        if (!(x)) {                                                                   \
+            std::fprintf(stderr, "block_rate: %s failed (line %d): %s\n", #x, __LINE__, \
+                         crc32c_last_error());                                        \
+            std::exit(1);                                                             \
+        }                                                                             \
+    } while (0)
+
+using Clock = std::chrono::steady_clock;
+
+static double seconds(Clock::time_point a, Clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+}
+
+int main(int argc, char **argv) {
+    const int nthreads = argc > 1 ? std::atoi(argv[1]) : 16;
+    const int iters = argc > 2 ? std::atoi(argv[2]) : 400;
+    const uint32_t max_blocks = argc > 3 ? uint32_t(std::atoi(argv[3])) : 16u;
+    const uint32_t window_us = argc > 4 ? uint32_t(std::atoi(argv[4])) : 30u;
+    constexpr size_t kBlock = 4u << 20;
+    constexpr int kPkts = 64;
+    std::vector<crc32c_packet> pk(kPkts);
+    for (int i = 0; i < kPkts; ++i) pk[i] = crc32c_packet{uint64_t(i) * 65536u, uint64_t(i) * 128u, 65536u, 512u};
+    const size_t nout = kPkts * 128;
+
+    crc32c_ctx *ctx = nullptr;
+    CHECK(crc32c_ctx_create(0, &ctx) == 0);
+    crc32c_plan *plan = nullptr;
+    CHECK(crc32c_plan_create(ctx, pk.data(), pk.size(), 0, &plan) == 0);
+    const int nbuf = 2 * nthreads;
+    std::vector<uint8_t *> bufs(nbuf);
+    std::vector<uint32_t *> outs(nbuf);
+    for (int i = 0; i < nbuf; ++i) {
+        CHECK(hipMalloc(&bufs[i], kBlock) == hipSuccess);
+        CHECK(hipMemset(bufs[i], i * 37 + 1, kBlock) == hipSuccess);
+        CHECK(hipMalloc(&outs[i], nout * 4) == hipSuccess);
+    }
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+
+    auto run = [&](const char *mode, auto body) {
+        std::atomic<int> ready{0};
+        std::atomic<bool> go{false};
+        std::vector<std::thread> th;
+        Clock::time_point t0, t1;
+        for (int k = 0; k < nthreads; ++k)
+            th.emplace_back([&, k] {
+                ready++;
+                while (!go.load()) std::this_thread::yield();
+                body(k);
+            });
+        while (ready.load() < nthreads) std::this_thread::yield();
+        t0 = Clock::now();
+        go = true;
+        for (auto &t : th) t.join();
+        t1 = Clock::now();
+        const double s = seconds(t0, t1);
+        const double blocks = double(nthreads) * iters;
+        std::printf("{\"mode\": \"%s\", \"threads\": %d, \"blocks\": %.0f, \"us_per_block\": %.3f, \"gib_s\": %.1f",
+                    mode, nthreads, blocks, s / blocks * 1e6, blocks * kBlock / s / double(1 << 30));
+    };
+
+    // single: one launch per block
+    std::vector<hipStream_t> streams(nthreads);
+    for (auto &s : streams) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    for (int w = 0; w < 2; ++w) {
+        run("single", [&](int k) {
+            for (int i = 0; i < iters; ++i) {
+                CHECK(crc32c_plan_exec(plan, bufs[k], outs[k], streams[k]) == 0);
+                CHECK(hipStreamSynchronize(streams[k]) == hipSuccess);
+            }
+        });
+        std::printf(", \"pass\": %d}\n", w);
+    }
+
+    for (int depth = 1; depth <= 2; ++depth)
+        for (int w = 0; w < 2; ++w) {
+            crc32c_blocks *q = nullptr;
+            CHECK(crc32c_blocks_create(plan, max_blocks, window_us, &q) == 0);
+            run(depth == 1 ? "queue" : "queue2", [&](int k) {
+                if (depth == 1) {
+                    for (int i = 0; i < iters; ++i) CHECK(crc32c_block_checksums(q, bufs[k], outs[k]) == 0);
+                    return;
+                }
+                uint64_t prev = 0;
+                for (int i = 0; i < iters; ++i) {
+                    const int b = 2 * k + (i & 1);
+                    uint64_t t = 0;
+                    CHECK(crc32c_block_submit(q, bufs[b], outs[b], &t) == 0);
+                    if (i) CHECK(crc32c_block_wait(q, prev) == 0);
+                    prev = t;
+                }
+                CHECK(crc32c_block_wait(q, prev) == 0);
+            });
+            uint64_t flushes = 0, blocks = 0;
+            CHECK(crc32c_blocks_stats(q, &flushes, &blocks) == 0);
+            std::printf(", \"max_blocks\": %u, \"window_us\": %u, \"launches\": %llu, \"blocks_per_launch\": %.2f, "
+                        "\"pass\": %d}\n",
+                        max_blocks, window_us, (unsigned long long)flushes, double(blocks) / double(flushes ? flushes : 1),
+                        w);
+            CHECK(crc32c_blocks_destroy(q) == 0);
+        }
+
+    // kernel: the GPU's time per block in back-to-back multi-block launches
+    for (uint32_t nb : {1u, 4u, 8u, 16u, 32u}) {
+        if (nb > uint32_t(nbuf)) break;
+        hipStream_t s = streams[0];
+        hipEvent_t e0, e1;
+        CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess);
+        const void *pays[32];
+        uint32_t *os[32];
+        for (uint32_t i = 0; i < nb; ++i) pays[i] = bufs[i], os[i] = outs[i];
+        for (int i = 0; i < 200; ++i) CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s) == 0);
+        const int n = 1000;
+        CHECK(hipEventRecord(e0, s) == hipSuccess);
+        for (int i = 0; i < n; ++i) CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s) == 0);
+        CHECK(hipEventRecord(e1, s) == hipSuccess);
+        CHECK(hipStreamSynchronize(s) == hipSuccess);
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess);
+        std::printf("{\"mode\": \"kernel\", \"blocks_per_launch\": %u, \"us_per_launch\": %.3f, \"us_per_block\": %.3f}\n",
+                    nb, ms * 1e3 / n, ms * 1e3 / n / nb);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    for (auto &s : streams) (void)hipStreamDestroy(s);
+    for (int i = 0; i < nbuf; ++i) {
+        (void)hipFree(bufs[i]);
+        (void)hipFree(outs[i]);
+    }
+    crc32c_plan_destroy(plan);
+    crc32c_ctx_destroy(ctx);
+    return 0;
+}

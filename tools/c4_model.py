@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Measured parts of a model of config 4 at N = 8.
+
+At N = 8 every rank checksums 4 of the 32 blocks (a 16 MiB shard: 256
+packets of 64 KiB) and ranks 1-7 each send 4 x 8192 checksums (128 KiB) to
+rank 0, which scatters them into file order.  On a one-GPU box this times,
+per step (HIP events on the launch stream, 1000 steps after 200 warm-up):
+
+  shard_graph / shard_eager -- the production kernel over one rank's 16 MiB
+                               shard, graph-replayed / host-issued;
+  multi_in_place            -- crc32c_multi_plan_exec over the same shard on
+                               a 1-rank communicator (rank 0 writes in place:
+                               no RCCL call);
+  multi_self_send           -- the same with CRC32C_MULTI_SELF_SEND: the
+                               shard's 128 KiB go through one RCCL send/recv
+                               group to rank 0's own staging slot, then the
+                               scatter kernel -- a lower bound for one peer's
+                               gather at N = 8.
+
+Prints one JSON line.  The model: step(N = 8) ~= shard time + gather time,
+with the gather at least (multi_self_send - multi_in_place)."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+
+    import bench
+
+    hdfs = bench.load_package()
+    hdfs.lib()
+    from hdfs_crc32c_amd.workloads import synthetic_bytes, uniform_packets
+
+    dev = torch.device("cuda", 0)
+    pk = uniform_packets(256)  # one rank's shard at N = 8: 4 blocks x 64 packets
+    nbytes = 256 * 65536
+    payload = torch.from_numpy(synthetic_bytes(nbytes + 16, 5)).to(dev)
+    out = torch.zeros(256 * 128, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(fn, n=1000, warm=200):
+        for _ in range(warm):
+            fn()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(n):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / n * 1e3  # us per call
+
+    res = {"shard_bytes": nbytes, "shard_packets": 256}
+    ctx = hdfs.Context(0)
+    plan = ctx.plan(pk)
+    res["shard_eager_us"] = round(timed(lambda: plan.exec(payload.data_ptr(), out.data_ptr(), stream.cuda_stream)), 3)
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream(device=dev)
+    plan.exec(payload.data_ptr(), out.data_ptr(), cs.cuda_stream)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=cs, capture_error_mode="thread_local"):
+        for _ in range(100):
+            plan.exec(payload.data_ptr(), out.data_ptr(), cs.cuda_stream)
+    g.replay()
+    torch.cuda.synchronize()
+    res["shard_graph_us"] = round(timed(lambda: g.replay(), n=50, warm=5) / 100, 3)
+    plan.close()
+    for name, flags in (("multi_in_place_us", 0), ("multi_self_send_us", hdfs.CRC32C_MULTI_SELF_SEND)):
+        m = hdfs.Multi([0])
+        mp = m.plan(pk, 64, flags)
+        res[name] = round(timed(lambda: mp.exec([payload.data_ptr()], out.data_ptr(), [stream.cuda_stream])), 3)
+        mp.close()
+        m.close()
+    res["gather_lower_bound_us"] = round(res["multi_self_send_us"] - res["multi_in_place_us"], 3)
+    res["model_step_n8_us"] = round(res["shard_eager_us"] + res["gather_lower_bound_us"], 3)
+    res["model_value_n8_gib_s"] = round(32 * (4 << 20) / (res["model_step_n8_us"] * 1e-6) / 2**30, 1)
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
