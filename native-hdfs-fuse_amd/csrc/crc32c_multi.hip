@@ -18,6 +18,7 @@
 // (crc32c_multi_create, ncclCommInitAll) or one process per device
 // (crc32c_multi_create_rank, ncclCommInitRank with an id from
 // crc32c_multi_unique_id passed between the processes by the caller).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -28,6 +29,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "hdfs_crc32c.h"
@@ -36,11 +38,70 @@
 
 using namespace hdfs_crc;
 
+// RCCL is loaded on first use (dlopen by SONAME, so a process that already
+// holds torch's RCCL shares it), not linked: a single-GPU caller of the
+// library -- the FUSE daemon's write path -- needs no RCCL at load time.
+namespace {
+
+struct Rccl {
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommInitAll) CommInitAll = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    std::string error;
+};
+
+const Rccl &rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = nullptr;
+        for (const char *name : {"librccl.so.1", "librccl.so"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+        if (!h) {
+            const char *e = dlerror();
+            r.error = e ? e : "librccl.so.1 not found";
+            return;
+        }
+        bool ok = true;
+        auto sym = [&](auto &fn, const char *name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+            ok = ok && fn;
+        };
+        sym(r.GetUniqueId, "ncclGetUniqueId");
+        sym(r.CommInitRank, "ncclCommInitRank");
+        sym(r.CommInitAll, "ncclCommInitAll");
+        sym(r.CommDestroy, "ncclCommDestroy");
+        sym(r.GroupStart, "ncclGroupStart");
+        sym(r.GroupEnd, "ncclGroupEnd");
+        sym(r.Send, "ncclSend");
+        sym(r.Recv, "ncclRecv");
+        sym(r.GetErrorString, "ncclGetErrorString");
+        if (!ok) {
+            r.error = "librccl is missing a symbol";
+            r.GetUniqueId = nullptr;
+        }
+    });
+    return r;
+}
+
+}  // namespace
+
+#define RCCL_LOADED()                                                                          \
+    do {                                                                                       \
+        if (!rccl().GetUniqueId) return fail(-ENOSYS, "RCCL unavailable: %s", rccl().error.c_str()); \
+    } while (0)
+
 #define NCCL_TRY(expr)                                                                                  \
     do {                                                                                                \
         ncclResult_t r_ = (expr);                                                                       \
         if (r_ != ncclSuccess)                                                                          \
-            return fail(-EIO, "%s: %s (%s:%d)", #expr, ncclGetErrorString(r_), __FILE__, __LINE__);     \
+            return fail(-EIO, "%s: %s (%s:%d)", #expr, rccl().GetErrorString(r_), __FILE__, __LINE__);  \
     } while (0)
 
 struct crc32c_multi {
@@ -168,7 +229,8 @@ int ensure_comms(crc32c_multi *m) {
     std::vector<int> devs;
     for (crc32c_ctx *c : m->ctxs) devs.push_back(c->device);
     std::vector<ncclComm_t> comms(devs.size());
-    NCCL_TRY(ncclCommInitAll(comms.data(), int(devs.size()), devs.data()));
+    RCCL_LOADED();
+    NCCL_TRY(rccl().CommInitAll(comms.data(), int(devs.size()), devs.data()));
     m->comms = comms;
     return 0;
 }
@@ -258,7 +320,8 @@ int crc32c_multi_unique_id(uint8_t id[128]) {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
     if (!id) return fail(-EINVAL, "id == NULL");
     ncclUniqueId u;
-    NCCL_TRY(ncclGetUniqueId(&u));
+    RCCL_LOADED();
+    NCCL_TRY(rccl().GetUniqueId(&u));
     std::memcpy(id, &u, sizeof u);
     return 0;
 }
@@ -279,7 +342,8 @@ int crc32c_multi_create_rank(int device, int rank, int nranks, const uint8_t id[
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     ncclComm_t comm = nullptr;
-    NCCL_TRY(ncclCommInitRank(&comm, nranks, u, rank));
+    RCCL_LOADED();
+    NCCL_TRY(rccl().CommInitRank(&comm, nranks, u, rank));
     m->comms.push_back(comm);
     *out = m.release();
     return 0;
@@ -293,7 +357,7 @@ int crc32c_multi_destroy(crc32c_multi *m) {
             (void)hipStreamSynchronize(m->streams[i]);
             (void)hipStreamDestroy(m->streams[i]);
         }
-        if (i < m->comms.size() && m->comms[i]) (void)ncclCommDestroy(m->comms[i]);
+        if (i < m->comms.size() && m->comms[i]) (void)rccl().CommDestroy(m->comms[i]);
     }
     for (crc32c_ctx *c : m->ctxs) crc32c_ctx_destroy(c);
     delete m;
@@ -477,19 +541,19 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
         if (sends(r, mp->self_send) && mp->local_nout[size_t(r)]) any = true;
     if (!any) return mark_execs(mp, streams);
     if (int rc = ensure_comms(m)) return rc;
-    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(rccl().GroupStart());
     ncclResult_t r = ncclSuccess;
     for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
         const hipStream_t s = local_stream(m, i, streams);
         const int me = m->ranks[i];
-        if (mp->d_local[i]) r = ncclSend(mp->d_local[i], mp->local_nout[size_t(me)], ncclUint32, 0, m->comms[i], s);
+        if (mp->d_local[i]) r = rccl().Send(mp->d_local[i], mp->local_nout[size_t(me)], ncclUint32, 0, m->comms[i], s);
         if (me != 0) continue;
         for (int peer = 0; peer < m->nranks && r == ncclSuccess; ++peer)
             if (sends(peer, mp->self_send) && mp->local_nout[size_t(peer)])
-                r = ncclRecv(mp->d_staging + mp->staging_off[size_t(peer)], mp->local_nout[size_t(peer)], ncclUint32,
+                r = rccl().Recv(mp->d_staging + mp->staging_off[size_t(peer)], mp->local_nout[size_t(peer)], ncclUint32,
                              peer, m->comms[i], s);
     }
-    const ncclResult_t e = ncclGroupEnd();
+    const ncclResult_t e = rccl().GroupEnd();
     NCCL_TRY(r);
     NCCL_TRY(e);
     // 3. rank 0: the received groups into file order

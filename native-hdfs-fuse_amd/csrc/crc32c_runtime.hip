@@ -76,6 +76,14 @@ static bool has_general(const HostPlan &hp) {
     return false;
 }
 
+// Some power-of-two tile starts off 16-byte alignment (the general build's
+// shifted loads read it from the aligned address below).
+static bool has_misaligned(const HostPlan &hp) {
+    for (const FastTile &t : hp.tiles)
+        if (!(t.meta & kGeneralTile) && (t.src & 15u)) return true;
+    return false;
+}
+
 KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out) {
     KParams p = base_params(plan->ctx, payload, out, plan->flags);
     const DevicePlan &dp = plan->dp;
@@ -191,12 +199,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->nseg = uint32_t(hp.seg.size());
     dp->nconst = uint32_t(hp.consts.size());
     dp->general = has_general(hp);
-    dp->misaligned = false;
-    for (const FastTile &t : hp.tiles)
-        if (!(t.meta & kGeneralTile) && (t.src & 15u)) {
-            dp->misaligned = true;
-            break;
-        }
+    dp->misaligned = has_misaligned(hp);
     dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
     dp->tiles_off = (2 * kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
@@ -628,7 +631,9 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         p.gen = reinterpret_cast<const GenItem *>(s.d_desc + plan.tiles.size() * 16);
         p.ntiles = uint32_t(plan.tiles.size());
         p.ngen = uint32_t(plan.gen.size());
-        p.general = has_general(plan) ? 1u : 0u;
+        // (the staged slices keep every packet's 16-byte phase: tiles off
+        // alignment take the general build's shifted loads, as in plans)
+        p.general = (has_general(plan) || has_misaligned(plan)) ? 1u : 0u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));

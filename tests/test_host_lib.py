@@ -485,3 +485,14 @@ def test_no_device_wide_sync_on_plan_paths():
             assert funcs and funcs[-1] == "release_pools", (name, funcs[-1:])
     text = open(os.path.join(csrc, "runtime_internal.h")).read()
     assert "kEpochBlocks" not in text
+
+
+def test_product_library_loads_rccl_only_for_multi_gpu(hdfs):
+    """A single-GPU caller (the FUSE write path) needs no RCCL at load time:
+    the product library does not link librccl; crc32c_multi.hip loads it by
+    SONAME on first use (sharing the copy torch already holds)."""
+    import subprocess
+
+    needed = subprocess.run(["readelf", "-d", hdfs.LIB_PATH], capture_output=True, text=True).stdout
+    assert "NEEDED" in needed and "rccl" not in needed, needed
+    assert b"librccl.so.1" in open(hdfs.LIB_PATH, "rb").read()
