@@ -558,7 +558,7 @@ def main():
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         # 1000 launches (~45 ms at config 2): a window of 200 fell inside the
         # power controller's post-idle clamp on some boxes
-        nv = 1000  # (even: a plan's verify launches alternate between two scratch slots)
+        nv = 1000
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)

@@ -311,16 +311,24 @@ __device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t 
 }
 
 // ---- launch-wide verification state (kernel_abi.h slots) -----------------
-// Start of a verification launch, one thread of workgroup 0: restore the
-// OTHER slot of the pair (used by the previous launch, which has completed)
-// for the next launch.
-__device__ __forceinline__ void reset_next_slot(const KParams &p) {
-    uint32_t *s = p.sched_next;
-    atomicExch(reinterpret_cast<unsigned long long *>(s + kTicketWord), 0ull);
-    atomicExch(s + kVFirstWord, 0xffffffffu);
+// End of a verification launch, the workgroup that took the last global
+// ticket, after publishing the result: every other workgroup has made its
+// last access to the slot (its shard ticket, and its first-bad update before
+// that), so the slot goes back to {0, ~0, 0} for the next launch -- which
+// runs after this one (a plan's verify launches are kept in GPU order).
+// (Round 2 reset the other slot of a pair at the START of a launch, on
+// workgroup 0's critical path: its staging wait also waited for those ten
+// atomics, so workgroup 0 -- and a small batch's whole launch -- started
+// its tiles late.)  Non-returning: nothing waits for these stores but the
+// end of the kernel.
+__device__ __forceinline__ void reset_slot(uint32_t *s) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(s + kTicketWord), 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(s + kVFirstWord, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
     for (uint32_t i = 0; i < kTicketShards; ++i)
-        atomicExch(reinterpret_cast<unsigned long long *>(s + kShardWord + 32 * i), 0ull);
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(s + kShardWord + 32 * i), 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Waits until every vector-memory operation of the wave has completed; for a
@@ -364,6 +372,7 @@ __device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *
     const unsigned long long total = (g & kCountMask) + shard_total;
     p.result[0] = uint32_t(total);
     p.result[1] = total ? atomicAdd(s + kVFirstWord, 0u) : 0xffffffffu;
+    reset_slot(s);
 }
 
 // ---- tiles: one wave, 16 blocks ------------------------------------------
@@ -737,7 +746,6 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                                                          : blockIdx.x;
     const uint32_t tbeg = uint32_t((nunits * rng) / gridDim.x);
     const uint32_t tend = uint32_t((nunits * (rng + 1)) / gridDim.x);
-    if (VERIFY && blockIdx.x == 0 && threadIdx.x == 0) reset_next_slot(p);
     if (threadIdx.x == 0) {
         *pool_ctr = tbeg + kWaves;
         if (VERIFY) {

@@ -46,7 +46,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
     if (p.expect) {
-        if (!p.result || !p.sched || !p.sched_next) return hipErrorInvalidValue;
+        if (!p.result || !p.sched) return hipErrorInvalidValue;
         if (quarter)
             hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>), g, b, 0, stream, p);
         else if (small)

@@ -201,7 +201,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->general = has_general(hp);
     dp->misaligned = has_misaligned(hp);
     dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
-    dp->tiles_off = (2 * kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
+    dp->tiles_off = (kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
     dp->seg_off = dp->gen_off + hp.gen.size() * sizeof(GenItem);
     dp->pieces_off = dp->seg_off + hp.seg.size() * sizeof(SegItem);
@@ -336,16 +336,16 @@ namespace {
 
 int alloc_slots(SchedSlots &s) {
     if (s.d) return 0;
-    std::vector<uint32_t> init(2 * kSlotWords);
+    std::vector<uint32_t> init(kSlotWords);
     init_sched_slots(init.data());
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s.d), init.size() * sizeof(uint32_t)));
     HIP_TRY(hipMemcpy(s.d, init.data(), init.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return 0;
 }
 
-// Launches p on `stream`.  Verification launches take the current slot,
-// reset the other one, and the pair flips; the caller keeps launches on
-// `slots` in GPU order.
+// Launches p on `stream`.  Verification launches use the sequence's slot
+// (left reset by the previous one); the caller keeps launches on `slots`
+// in GPU order.
 int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + p.ngen + p.nseg + p.nconst;
     if (!items) return 0;
@@ -353,11 +353,9 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
     if (sched) {
         int rc = alloc_slots(slots);
         if (rc) return rc;
-        p.sched = slots.d + slots.cur * kSlotWords;
-        p.sched_next = slots.d + (slots.cur ^ 1) * kSlotWords;
+        p.sched = slots.d;
     }
     HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream));
-    if (sched) slots.cur ^= 1;
     return 0;
 }
 

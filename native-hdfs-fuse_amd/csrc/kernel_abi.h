@@ -58,10 +58,9 @@ struct KParams {
     // Optional (crc32c_plan_verify_bitmap): bit i set for every mismatching
     // checksum i; zeroed by the runtime before the launch.
     uint32_t *bad_bits;
-    // Verification slot of this launch (kSlotWords u32s) and the other slot
-    // of the pair, which this launch resets for the next one.
+    // Verification slot of this launch (kSlotWords u32s); the launch's last
+    // workgroup leaves it reset for the next launch.
     uint32_t *sched;
-    uint32_t *sched_next;
     // Multi-block launch: nblocks > 0 runs the plan's block_tiles tiles once
     // per block (tile j = block j / block_tiles, tile j % block_tiles); the
     // plan has tiles only.  0: an ordinary launch.
@@ -72,10 +71,9 @@ struct KParams {
 
 // Device state of one verification launch ("slot"), u32 words, each on its
 // own 128-B line: the grid-wide merge of the workgroups' mismatch counts.
-// Launches of one plan (or one host-pipeline stage) alternate between two
-// slots and run in GPU order, so a launch resets the slot its predecessor
-// used: {global ticket, first bad, shard tickets} = {0, ~0, 0} at launch
-// start.  Ticket words are 64-bit: tickets taken (bits 40-63) and the
+// Launches of one plan (or one host-pipeline stage) share one slot and run
+// in GPU order; a launch's last workgroup leaves the slot as every launch
+// finds it: {global ticket, first bad, shard tickets} = {0, ~0, 0}.  Ticket words are 64-bit: tickets taken (bits 40-63) and the
 // mismatches they carried (bits 0-39).  Workgroup b first takes a ticket in
 // shard b % kTicketShards; the last of a shard takes one of the global
 // ticket (one counter per 32 workgroups instead of one for all 256: every
@@ -86,11 +84,10 @@ constexpr uint32_t kVFirstWord = 64;  // u32
 constexpr uint32_t kShardWord = 96;   // u64, + 32 * shard
 constexpr uint32_t kSlotWords = kShardWord + 32 * kTicketShards;
 
-// Fills two slots' initial state (2 * kSlotWords words).
+// Fills a slot's initial state (kSlotWords words).
 inline void init_sched_slots(uint32_t *w) {
-    for (uint32_t i = 0; i < 2 * kSlotWords; ++i) w[i] = 0;
+    for (uint32_t i = 0; i < kSlotWords; ++i) w[i] = 0;
     w[kVFirstWord] = 0xffffffffu;
-    w[kSlotWords + kVFirstWord] = 0xffffffffu;
 }
 
 // The production kernel (crc32c_kernel.hip): one 12-wave workgroup per CU,

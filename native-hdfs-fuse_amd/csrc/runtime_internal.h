@@ -38,11 +38,10 @@ struct DeviceGuard {
     }
 };
 
-// The two device scheduler slots (kernel_abi.h) of one launch sequence that
+// The device verification slot (kernel_abi.h) of one launch sequence that
 // the GPU runs in order: a plan, or a host-pipeline stage.
 struct SchedSlots {
-    uint32_t *d = nullptr;  // 2 * kSlotWords u32
-    int cur = 0;
+    uint32_t *d = nullptr;  // kSlotWords u32
 };
 
 struct Stage {
