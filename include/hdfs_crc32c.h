@@ -137,10 +137,10 @@ int crc32c_device_count(void);
  * decomposition into 8 KiB tiles) and executed on any payload with that
  * shape.  Its descriptors go to the device asynchronously (the first launch
  * on a stream waits for that copy).  Destroying a plan whose launches are
- * still in flight is safe: the destroy records an event on every stream the
- * plan was launched on (so those streams must still exist, or the plan's
- * block is simply never reused), and its device block is recycled only once
- * those events have completed -- no device-wide synchronisation on any plan
+ * still in flight is safe, also after their streams were destroyed: every
+ * launch completes a per-(plan, stream) event (the kernel dispatch's own
+ * stop event), and the plan's device block is recycled only once those
+ * events have completed -- no device-wide synchronisation on any plan
  * create / destroy path, so work of other streams and libraries is never
  * waited on, and plans may be created and destroyed while another thread
  * captures a graph.  A plan must outlive every HIP graph that captured its

@@ -17,6 +17,8 @@
 //     graph-replayed: 4.36 -> 3.71 us).
 // A/B and diagnostic variants are built only into libhdfs_crc32c_debug.so
 // (debug/crc32c_variants.hip).
+#include <hip/hip_ext.h>
+
 #include "crc32c_device.h"
 
 namespace hdfs_crc {
@@ -35,7 +37,7 @@ constexpr uint64_t kSmallBatchItemsPerCu = 16;
 constexpr uint64_t kQuarterTilesPerCu = 3;
 }  // namespace
 
-hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream) {
+hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop) {
     using namespace hdfs_crc_dev;
     constexpr int kProd = kModeS4 | kModeNt;
     constexpr int kGen = kModeGeneral;
@@ -45,26 +47,34 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     const bool small = items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
+#define LAUNCH(K)                                                                  \
+    do {                                                                           \
+        if (stop)                                                                  \
+            hipExtLaunchKernelGGL(K, g, b, 0, stream, nullptr, stop, 0u, p);       \
+        else                                                                       \
+            hipLaunchKernelGGL(K, g, b, 0, stream, p);                             \
+    } while (0)
     if (p.expect) {
         if (!p.result || !p.sched) return hipErrorInvalidValue;
         if (quarter)
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>));
         else if (small)
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>));
         else if (p.general)
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeVerify>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeVerify>));
         else
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeVerify>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeVerify>));
     } else {
         if (quarter)
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>));
         else if (small)
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>));
         else if (p.general)
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen>));
         else
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<768, 3, kProd>), g, b, 0, stream, p);
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd>));
     }
+#undef LAUNCH
     return hipGetLastError();
 }
 

@@ -215,7 +215,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
         if (int rc = pool_get(ctx, ctx->host_pool, bytes, &dp->h, &dp->hcap)) return rc;
         dp->uploaded = take_event(ctx);
     }
-    if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDisableTiming));
+    if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDefault));  // (pooled: also used as stop events)
     uint8_t *img = dp->h;
     init_sched_slots(reinterpret_cast<uint32_t *>(img + dp->slots_off));
     std::memcpy(img + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
@@ -232,73 +232,61 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
 // Orders a launch on `stream` after the plan's upload: nothing once the
 // upload is known complete; else a stream wait on its event (or, while the
 // stream is being captured into a graph, a host wait: a capture cannot wait
-// on work outside it).  Notes the launch stream for the plan's release.
-int prepare_launch(crc32c_plan *plan, hipStream_t stream) {
+// on work outside it).  Hands out the stream's completion event.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream, hipEvent_t *stop) {
     RelaxedCapture relaxed;  // (the queries below while another thread captures a graph)
-    if (std::find(plan->launch_streams.begin(), plan->launch_streams.end(), stream) == plan->launch_streams.end())
-        plan->launch_streams.push_back(stream);
+    *stop = nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(stream, &cs));
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    if (capturing) plan->captured = true;
     DevicePlan *dp = &plan->dp;
-    if (!plan->captured || !dp->ready.load(std::memory_order_acquire)) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        HIP_TRY(hipStreamIsCapturing(stream, &cs));
-        if (cs != hipStreamCaptureStatusNone) plan->captured = true;
-        if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
-            const hipError_t q = hipEventQuery(dp->uploaded);
-            if (q == hipSuccess) {
+    if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
+        const hipError_t q = hipEventQuery(dp->uploaded);
+        if (q == hipSuccess) {
+            dp->ready.store(true, std::memory_order_release);
+        } else {
+            if (q != hipErrorNotReady) HIP_TRY(q);
+            if (capturing) {
+                HIP_TRY(hipEventSynchronize(dp->uploaded));
                 dp->ready.store(true, std::memory_order_release);
             } else {
-                if (q != hipErrorNotReady) HIP_TRY(q);
-                if (cs != hipStreamCaptureStatusNone) {
-                    HIP_TRY(hipEventSynchronize(dp->uploaded));
-                    dp->ready.store(true, std::memory_order_release);
-                } else {
-                    HIP_TRY(hipStreamWaitEvent(stream, dp->uploaded, 0));
-                }
+                HIP_TRY(hipStreamWaitEvent(stream, dp->uploaded, 0));
             }
         }
     }
+    if (capturing) return 0;  // (a graph's replays are not tracked: the block is held)
+    for (auto &d : plan->done)
+        if (d.first == stream) {
+            *stop = d.second;
+            return 0;
+        }
+    hipEvent_t e = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(plan->ctx->pool_mu);
+        e = take_event(plan->ctx);
+    }
+    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDefault));  // (a stop event tracks the dispatch's end)
+    plan->done.emplace_back(stream, e);
+    *stop = e;
     return 0;
 }
 
 void release_plan_blocks(crc32c_plan *plan) {
     crc32c_ctx *ctx = plan->ctx;
     DevicePlan *dp = &plan->dp;
-    RelaxedCapture relaxed;
     Release r;
     r.d = dp->d;
     r.dcap = dp->cap;
     r.h = dp->h;
     r.hcap = dp->hcap;
-    bool held = plan->captured;
-    std::vector<hipEvent_t> evs;
-    {
-        std::lock_guard<std::mutex> lock(ctx->pool_mu);
-        for (size_t i = 0; i < plan->launch_streams.size(); ++i) evs.push_back(take_event(ctx));
-    }
-    // one event per launch stream, recorded now: it completes after every
-    // launch of the plan on that stream
-    for (size_t i = 0; i < plan->launch_streams.size() && !held; ++i) {
-        const hipStream_t s = plan->launch_streams[i];
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-            (void)hipGetLastError();
-            held = true;  // (a capture in progress on it may hold the plan's launches)
-            break;
-        }
-        if (!evs[i] && hipEventCreateWithFlags(&evs[i], hipEventDisableTiming) != hipSuccess) evs[i] = nullptr;
-        if (!evs[i] || hipEventRecord(evs[i], s) != hipSuccess) {
-            (void)hipGetLastError();
-            held = true;  // (e.g. the stream no longer exists: the block is not reused)
-            break;
-        }
-        r.events.push_back(evs[i]);
-        evs[i] = nullptr;
-    }
+    // every launch's completion event (already recorded by the launches
+    // themselves: no stream is touched here), and the upload's
+    for (auto &d : plan->done) r.events.push_back(d.second);
+    plan->done.clear();
     if (dp->uploaded) r.events.push_back(dp->uploaded);
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
-    for (hipEvent_t e : evs)
-        if (e) ctx->spare_events.push_back(e);
-    if (held && r.d) {
+    if (plan->captured && r.d) {
         ctx->held.emplace_back(r.d, r.dcap);
         drop_block(ctx->dev_pool, r.d);
         r.d = nullptr;
@@ -346,7 +334,7 @@ int alloc_slots(SchedSlots &s) {
 // Launches p on `stream`.  Verification launches use the sequence's slot
 // (left reset by the previous one); the caller keeps launches on `slots`
 // in GPU order.
-int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream) {
+int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream, hipEvent_t stop = nullptr) {
     const uint64_t items = uint64_t(p.ntiles) + p.ngen + p.nseg + p.nconst;
     if (!items) return 0;
     const bool sched = p.expect != nullptr;
@@ -355,7 +343,7 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
         if (rc) return rc;
         p.sched = slots.d;
     }
-    HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream));
+    HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream, stop));
     return 0;
 }
 
@@ -376,7 +364,8 @@ int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
 
 int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
     std::lock_guard<std::mutex> lock(plan->mu);
-    if (int rc = prepare_launch(plan, stream)) return rc;
+    hipEvent_t stop = nullptr;
+    if (int rc = prepare_launch(plan, stream, &stop)) return rc;
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
@@ -386,7 +375,7 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
             HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.bad_bits), 0,
                                       size_t((plan->nchecksums + 31) / 32), stream));
     }
-    return launch(plan->ctx, p, plan->sched, stream);
+    return launch(plan->ctx, p, plan->sched, stream, stop);
 }
 
 constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK;

@@ -124,12 +124,12 @@ extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev
     KParams p = plan_params(plan, dev_payload, dev_out);
     p.stamps = dev_stamps;
     const hipStream_t s = static_cast<hipStream_t>(stream);
-    {
-        std::lock_guard<std::mutex> lock(plan->mu);
-        if (int rc = prepare_launch(plan, s)) return rc;
-    }
-    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
+    std::lock_guard<std::mutex> lock(plan->mu);
+    hipEvent_t stop = nullptr;
+    if (int rc = prepare_launch(plan, s, &stop)) return rc;
+    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s, stop)
                          : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));
+    if (variant != 0 && stop) HIP_TRY(hipEventRecord(stop, s));  // (the plan's block outlives this launch)
     return 0;
 }
 

@@ -156,9 +156,13 @@ struct crc32c_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t last_done = nullptr;
     bool launched = false;
-    // every stream a launch of the plan went on (its blocks are recycled
-    // after an event on each), and whether one was a graph capture
-    std::vector<hipStream_t> launch_streams;
+    // Per stream a launch of the plan went on: an event every launch there
+    // passes as its stop event (hipExtLaunchKernel: the dispatch's own
+    // completion), so the plan's blocks are recycled once these have
+    // completed -- without touching the streams (which the caller may have
+    // destroyed by then).  The stream is only a key.  `captured`: a launch
+    // went into a graph capture (its block is never reused).
+    std::vector<std::pair<hipStream_t, hipEvent_t>> done;
     bool captured = false;
     hdfs_crc::DevicePlan dp;
     uint64_t nchecksums = 0, payload_bytes = 0;
@@ -178,8 +182,9 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
 // device (into *dp), asynchronously; plan_ready orders a launch after it.
 int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
 // Before a launch of `plan` on `stream` (caller holds plan->mu): orders it
-// after the plan's upload and notes the stream for the plan's release.
-int prepare_launch(crc32c_plan *plan, hipStream_t stream);
+// after the plan's upload; *stop = the event the launch must complete
+// (nullptr while the stream is being captured).
+int prepare_launch(crc32c_plan *plan, hipStream_t stream, hipEvent_t *stop);
 // A destroyed plan's blocks back to the pools once its launches are done.
 void release_plan_blocks(crc32c_plan *plan);
 // Context teardown: waits for the releases, frees every pooled block.
