@@ -390,6 +390,21 @@ __device__ __forceinline__ bool rep_lane(int lane, uint32_t blk, uint32_t nb, ui
     return ((lane & 0x14) == 0) && ((blk & ((1u << lg) - 1u)) == 0) && blk < nb;
 }
 
+// A buffer resource for a wave-uniform range, built from SGPRs.  The
+// compiler cannot always prove a work item's base and length uniform (in
+// the verify instances of the general builds it could not), and a resource
+// it believes divergent makes it wrap EVERY load in a readfirstlane
+// "waterfall" loop (16 of them per general item in those kernels, round 2).
+// readfirstlane of a value that is uniform is exact; on SGPR inputs it
+// folds away.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const uint8_t *base, uint32_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    const uint64_t ua = uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(a >> 32))) << 32 |
+                        __builtin_amdgcn_readfirstlane(uint32_t(a));
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(ua), 0,
+                                             int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
+}
+
 // Loads of one power-of-two tile: instruction i reads 1 KiB contiguous
 // (blocks 2i, 2i+1) through a buffer descriptor whose range is the tile's
 // nb * 512 valid bytes.  Lanes of blocks a partial tile does not have fall
@@ -408,7 +423,7 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
     }
     const uint32_t nb = t.meta & 0xffu;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src), 0, int(nb * 512u), 0x00020000);
+        uniform_rsrc(p.payload + t.src, nb * 512u);
     const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -519,8 +534,7 @@ template <int AUX, bool VERIFY>
 __device__ __forceinline__ void load_tile_shifted(const KParams &p, FastTile t, uint32_t r, int lane, uint4 v[9],
                                                   uint32_t &ev) {
     const uint32_t nb = t.meta & 0xffu;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + t.src - r),
-                                                                          0, int(r + nb * 512u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + t.src - r, r + nb * 512u);
     const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -662,7 +676,7 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     }
     const uint32_t nbq = ft.meta & 0xffu;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + ft.src), 0, int(nbq * 512u), 0x00020000);
+        uniform_rsrc(p.payload + ft.src, nbq * 512u);
     const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < kNP; ++i) {

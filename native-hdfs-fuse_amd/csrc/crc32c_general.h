@@ -126,7 +126,7 @@ __device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, con
     const uint32_t bytes = g.nch * g.bpc + g.tl;
     if (g.pad == 0 && g.padt == 0) {
         const __amdgpu_buffer_rsrc_t rsrc =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.payload + g.src), 0, int(bytes), 0x00020000);
+            uniform_rsrc(p.payload + g.src, bytes);
         const uint32_t voff = 8192u * s + 16u * uint32_t(lane);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -137,8 +137,7 @@ __device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, con
         return;
     }
     const uint32_t shift = 16u;
-    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(p.payload + g.src - shift), 0, int(shift + bytes), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + g.src - shift, shift + bytes);
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
     const uint32_t upto = 2u << h;  // (upto << 2i) - 1: blocks 0 .. b
     const uint32_t sth = gs.start >> h, vh = gs.valid >> h, th = gs.tailm >> h;
