@@ -41,6 +41,22 @@ constexpr uint64_t kMinRunBytes = 1ull << 20;
 // The first slice of a pageable batch is staged and copied in pieces of this
 // size, so that the copy engine starts after one piece instead of a slice.
 constexpr size_t kFirstPieceBytes = 8ull << 20;
+constexpr size_t kZeroCopyBytes = 4ull << 20;  // (zero_copy_bytes)
+
+// Batches up to this many bytes skip the copy command: the kernel reads the
+// payload straight from pinned, device-mapped host memory (pageable
+// payloads are first copied into pinned staging by the CPU).  A copy
+// command costs ~15 us of latency per call before the kernel can start
+// (host-resident per call); $HDFS_CRC32C_ZERO_COPY_KB
+// overrides the threshold (A/B only; 0 = never).
+size_t zero_copy_bytes() {
+    static const size_t v = [] {
+        const char *e = std::getenv("HDFS_CRC32C_ZERO_COPY_KB");
+        const long kb = e ? std::atol(e) : -1;
+        return kb >= 0 && kb <= (1 << 20) ? size_t(kb) << 10 : kZeroCopyBytes;
+    }();
+    return v;
+}
 
 // Host pipeline slice size: kSliceBytes, or $HDFS_CRC32C_SLICE_MB (A/B only).
 size_t slice_bytes() {
@@ -537,8 +553,29 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         // 1. The payload copy goes first: it needs no plan, and the copy
         //    stream runs the slices' copies back to back.  (This stage's
         //    previous kernel is done: drain_stage waited for it.)
+        //    A small batch (one slice) is not copied: the kernel reads it in
+        //    host memory (zero copy).
         local.assign(pkts + i, pkts + j);
-        if (ranged) {
+        const uint8_t *kpayload = s.d_payload;
+        bool zero_copy = ranged && i == 0 && j == npkts && (hi - lo) <= zero_copy_bytes();
+        if (zero_copy) {
+            const uint8_t *src = payload + lo;
+            if (!pinned) {  // (into pinned staging, which the device can read)
+                copy_range(s.h_payload, src, stage_bytes);
+                src = s.h_payload;
+            }
+            void *dptr = nullptr;
+            if (hipHostGetDevicePointer(&dptr, const_cast<uint8_t *>(src), 0) == hipSuccess && dptr &&
+                (reinterpret_cast<uintptr_t>(dptr) & 15u) == (reinterpret_cast<uintptr_t>(src) & 15u)) {
+                kpayload = static_cast<const uint8_t *>(dptr);
+            } else {
+                (void)hipGetLastError();
+                zero_copy = false;  // (e.g. registered without mapping: copy as usual)
+            }
+        }
+        if (zero_copy) {
+            for (crc32c_packet &pk : local) pk.payload_off -= lo;
+        } else if (ranged) {
             for (crc32c_packet &pk : local) pk.payload_off -= lo;
             if (pinned) {
                 HIP_TRY(hipMemcpyAsync(s.d_payload, payload + lo, stage_bytes, hipMemcpyHostToDevice,
@@ -590,7 +627,7 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
             });
             HIP_TRY(hipMemcpyAsync(s.d_payload, s.h_payload, stage_bytes, hipMemcpyHostToDevice, ctx->copy_stream));
         }
-        HIP_TRY(hipEventRecord(s.copied, ctx->copy_stream));
+        if (!zero_copy) HIP_TRY(hipEventRecord(s.copied, ctx->copy_stream));
         // 2. Plan and descriptors while the copy runs.
         uint64_t nout = 0;
         s.scatter.clear();
@@ -612,15 +649,16 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         std::memcpy(s.h_desc, plan.tiles.data(), plan.tiles.size() * 16);
         std::memcpy(s.h_desc + plan.tiles.size() * 16, plan.gen.data(), plan.gen.size() * 16);
         // 3. Kernel and checksums on the stage's stream, after the copy.
-        HIP_TRY(hipStreamWaitEvent(s.stream, s.copied, 0));
-        KParams p = base_params(ctx, s.d_payload, s.d_out, flags);
+        if (!zero_copy) HIP_TRY(hipStreamWaitEvent(s.stream, s.copied, 0));
+        KParams p = base_params(ctx, kpayload, s.d_out, flags);
         p.tiles = reinterpret_cast<const FastTile *>(s.d_desc);
         p.gen = reinterpret_cast<const GenItem *>(s.d_desc + plan.tiles.size() * 16);
         p.ntiles = uint32_t(plan.tiles.size());
         p.ngen = uint32_t(plan.gen.size());
         // (the staged slices keep every packet's 16-byte phase: tiles off
         // alignment take the general build's shifted loads, as in plans)
-        p.general = (has_general(plan) || has_misaligned(plan)) ? 1u : 0u;
+        // (zero copy: the caller's buffer may itself be off 16-byte alignment)
+        p.general = (has_general(plan) || has_misaligned(plan) || (reinterpret_cast<uintptr_t>(kpayload) & 15u)) ? 1u : 0u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));

@@ -207,6 +207,30 @@ def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
     assert np.array_equal(gpu_ctx.batch_host(payload, pk2), want2)
 
 
+@pytest.mark.parametrize("npk", [1, 5, 64, 65])
+def test_host_path_zero_copy(hdfs, gpu_ctx, orc, npk):
+    """Small host batches (up to 4 MiB: 1, 5 and 64 packets) are read by the
+    kernel in host memory (no copy command); 65 packets take the copy path.
+    Pinned and pageable, a buffer starting 0 / 5 / 8 bytes off 16-byte
+    alignment, ragged tails (general items and tails under 4 bytes), mixed
+    bpc with a padded bpc 1000; bit-exact against the oracle."""
+    torch = _torch()
+    pk = oracle.mixed_packets(npk, 65536, (512, 1000, 1536, 4096))
+    pk["len"][1::3] -= 777
+    pk["len"][2::5] = 65536 - 510  # a 2-byte tail at bpc 512
+    per = (pk["len"].astype(np.int64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    n = oracle.total_checksums(pk)
+    base = oracle.xorshift64_bytes(npk * 65536 + 64, 600 + npk)
+    pinned_all = torch.from_numpy(base).pin_memory().numpy()
+    for skew in (0, 5, 8):
+        for buf in (base, pinned_all):
+            view = buf[skew:skew + npk * 65536]
+            want = orc.batch(np.ascontiguousarray(view), pk, n)
+            got = gpu_ctx.batch_host(view, pk)
+            assert np.array_equal(got, want), (npk, skew, buf is pinned_all)
+
+
 def test_host_path_pinned_runs(hdfs, gpu_ctx, orc):
     """Scattered packets from pinned memory in long contiguous runs go H2D one
     copy per run (crc32c_batch_host): 4 MiB blocks taken in a shuffled

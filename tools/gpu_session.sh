@@ -34,6 +34,7 @@ for s in $STEPS; do
     kbench) run kbench_${KCFG:-c2} ${KB_TIMEOUT:-600} python tools/kbench.py --config ${KCFG:-c2} --variants ${KV:-0,1,2,3,4,5} ${KB_ARGS:-} ;;
     kbench5) run kbench5 600 python tools/kbench.py --config c5 --variants ${KV:-0,1} ;;
     bench3h) run bench3h 600 python bench.py --config c3 --host-sweep --cpu-seconds 2 ;;
+    sweepab) run sweep_zc0 600 env HDFS_CRC32C_ZERO_COPY_KB=0 python bench.py --config c3 --host-sweep --no-cpu --steps 200 --warmup 50 && run sweep_zc 600 python bench.py --config c3 --host-sweep --no-cpu --steps 200 --warmup 50 ;;
     brate) run brate 300 tools/block_rate ${BR_ARGS:-16 400 16 30} ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
     stash) for b in ${SB:-basewt stashwt stashB}; do run stash_$b 300 python tools/stash_repro.py $b ${SBPC:-4,7,100,1000,1536}; done ;;
