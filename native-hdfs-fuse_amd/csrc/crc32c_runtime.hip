@@ -41,14 +41,16 @@ constexpr uint64_t kMinRunBytes = 1ull << 20;
 // The first slice of a pageable batch is staged and copied in pieces of this
 // size, so that the copy engine starts after one piece instead of a slice.
 constexpr size_t kFirstPieceBytes = 8ull << 20;
-constexpr size_t kZeroCopyBytes = 4ull << 20;  // (zero_copy_bytes)
+constexpr size_t kZeroCopyBytes = 1ull << 20;  // (zero_copy_bytes)
 
-// Batches up to this many bytes skip the copy command: the kernel reads the
-// payload straight from pinned, device-mapped host memory (pageable
-// payloads are first copied into pinned staging by the CPU).  A copy
-// command costs ~15 us of latency per call before the kernel can start
-// (host-resident per call); $HDFS_CRC32C_ZERO_COPY_KB
-// overrides the threshold (A/B only; 0 = never).
+// Pageable batches up to this many bytes skip the copy command: the CPU
+// copies them into pinned, device-MAPPED staging and the kernel reads them
+// there (a copy command costs ~15 us of latency per call before the kernel
+// can start; DESIGN.md section 5, host-resident per call).  The caller's own
+// pinned memory is not read in place: hipHostMalloc's default allocation is
+// not guaranteed to be mapped for the device (a first version that read it
+// in place faulted).  $HDFS_CRC32C_ZERO_COPY_KB overrides the threshold
+// (A/B only; 0 = never).
 size_t zero_copy_bytes() {
     static const size_t v = [] {
         const char *e = std::getenv("HDFS_CRC32C_ZERO_COPY_KB");
@@ -452,6 +454,7 @@ int grow_mapped(T **h, T **d, size_t *cap, size_t need) {
 void free_stage(Stage &s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.h_payload) (void)hipHostFree(s.h_payload);
+    if (s.h_zc) (void)hipHostFree(s.h_zc);  // d_zc is its mapping
     if (s.d_payload) (void)hipFree(s.d_payload);
     if (s.h_desc) (void)hipHostFree(s.h_desc);  // d_desc is its mapping
     if (s.h_out) (void)hipHostFree(s.h_out);  // d_out is its mapping
@@ -557,21 +560,12 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         //    host memory (zero copy).
         local.assign(pkts + i, pkts + j);
         const uint8_t *kpayload = s.d_payload;
-        bool zero_copy = ranged && i == 0 && j == npkts && (hi - lo) <= zero_copy_bytes();
-        if (zero_copy) {
-            const uint8_t *src = payload + lo;
-            if (!pinned) {  // (into pinned staging, which the device can read)
-                copy_range(s.h_payload, src, stage_bytes);
-                src = s.h_payload;
-            }
-            void *dptr = nullptr;
-            if (hipHostGetDevicePointer(&dptr, const_cast<uint8_t *>(src), 0) == hipSuccess && dptr &&
-                (reinterpret_cast<uintptr_t>(dptr) & 15u) == (reinterpret_cast<uintptr_t>(src) & 15u)) {
-                kpayload = static_cast<const uint8_t *>(dptr);
-            } else {
-                (void)hipGetLastError();
-                zero_copy = false;  // (e.g. registered without mapping: copy as usual)
-            }
+        const bool zero_copy = !pinned && ranged && i == 0 && j == npkts && (hi - lo) <= zero_copy_bytes();
+        if (zero_copy) {  // (into mapped staging, which the kernel reads in place)
+            rc = grow_mapped(&s.h_zc, &s.d_zc, &s.zc_cap, stage_bytes + 16);
+            if (rc) return rc;
+            copy_range(s.h_zc, payload + lo, stage_bytes);
+            kpayload = s.d_zc;
         }
         if (zero_copy) {
             for (crc32c_packet &pk : local) pk.payload_off -= lo;
@@ -657,8 +651,7 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         p.ngen = uint32_t(plan.gen.size());
         // (the staged slices keep every packet's 16-byte phase: tiles off
         // alignment take the general build's shifted loads, as in plans)
-        // (zero copy: the caller's buffer may itself be off 16-byte alignment)
-        p.general = (has_general(plan) || has_misaligned(plan) || (reinterpret_cast<uintptr_t>(kpayload) & 15u)) ? 1u : 0u;
+        p.general = (has_general(plan) || has_misaligned(plan)) ? 1u : 0u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));

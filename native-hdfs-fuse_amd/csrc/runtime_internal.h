@@ -52,6 +52,10 @@ struct Stage {
     size_t payload_cap = 0;
     uint8_t *h_payload = nullptr;  // pinned staging, only for pageable or gathered payloads
     size_t staging_cap = 0;
+    // Small pageable batches: pinned, device-MAPPED staging the kernel reads
+    // in place (zero copy; d_zc is h_zc's mapping).
+    uint8_t *h_zc = nullptr, *d_zc = nullptr;
+    size_t zc_cap = 0;
     // Work descriptors: pinned host memory the kernel reads in place (d_desc
     // is its device mapping).  A slice's 64 KiB of descriptors are not worth
     // a copy of their own: on the copy stream each copy costs ~25 us (9 us

@@ -207,13 +207,14 @@ def test_host_path_pageable_and_pinned(hdfs, gpu_ctx, orc):
     assert np.array_equal(gpu_ctx.batch_host(payload, pk2), want2)
 
 
-@pytest.mark.parametrize("npk", [1, 5, 64, 65])
+@pytest.mark.parametrize("npk", [1, 5, 16, 17])
 def test_host_path_zero_copy(hdfs, gpu_ctx, orc, npk):
-    """Small host batches (up to 4 MiB: 1, 5 and 64 packets) are read by the
-    kernel in host memory (no copy command); 65 packets take the copy path.
-    Pinned and pageable, a buffer starting 0 / 5 / 8 bytes off 16-byte
-    alignment, ragged tails (general items and tails under 4 bytes), mixed
-    bpc with a padded bpc 1000; bit-exact against the oracle."""
+    """Small pageable host batches (up to 1 MiB: 1, 5 and 16 packets) are
+    copied by the CPU into mapped staging that the kernel reads in place (no
+    copy command); 17 packets, and pinned buffers, take the copy path.  A
+    buffer starting 0 / 5 / 8 bytes off 16-byte alignment, ragged tails
+    (general items and tails under 4 bytes), mixed bpc with a padded bpc
+    1000; bit-exact against the oracle."""
     torch = _torch()
     pk = oracle.mixed_packets(npk, 65536, (512, 1000, 1536, 4096))
     pk["len"][1::3] -= 777

@@ -79,26 +79,9 @@ def main():
         m = hdfs.Multi([0])
         mp = m.plan(pk, 64, flags)
         res[name] = round(timed(lambda: mp.exec([payload.data_ptr()], out.data_ptr(), [stream.cuda_stream])), 3)
-        # the same step replayed from a HIP graph (RCCL calls captured too):
-        # what a step costs the GPU once the host's per-call RCCL cost is gone
-        try:
-            gm = torch.cuda.CUDAGraph()
-            mp.exec([payload.data_ptr()], out.data_ptr(), [cs.cuda_stream])
-            torch.cuda.synchronize()
-            with torch.cuda.graph(gm, stream=cs, capture_error_mode="thread_local"):
-                for _ in range(50):
-                    mp.exec([payload.data_ptr()], out.data_ptr(), [cs.cuda_stream])
-            gm.replay()
-            torch.cuda.synchronize()
-            res[name.replace("_us", "_graph_us")] = round(timed(lambda: gm.replay(), n=40, warm=5) / 50, 3)
-        except RuntimeError as e:
-            res[name.replace("_us", "_graph_error")] = str(e)[:160]
-            torch.cuda.synchronize()
         mp.close()
         m.close()
     res["gather_lower_bound_us"] = round(res["multi_self_send_us"] - res["multi_in_place_us"], 3)
-    if "multi_self_send_graph_us" in res and "multi_in_place_graph_us" in res:
-        res["gather_graph_lower_bound_us"] = round(res["multi_self_send_graph_us"] - res["multi_in_place_graph_us"], 3)
     res["model_step_n8_us"] = round(res["shard_eager_us"] + res["gather_lower_bound_us"], 3)
     res["model_value_n8_gib_s"] = round(32 * (4 << 20) / (res["model_step_n8_us"] * 1e-6) / 2**30, 1)
     print(json.dumps(res), flush=True)
