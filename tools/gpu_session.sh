@@ -16,6 +16,7 @@ run() {  # name timeout cmd...
   echo "=== $name rc=$rc" | tee -a $OUT/session.log
   tail -5 $OUT/$name.log
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  if [ $rc -ne 0 ] && [ -n "${STOP_ON_FAIL:-}" ]; then echo "stopping after a failure (STOP_ON_FAIL)"; exit $rc; fi
   return 0
 }
 for s in $STEPS; do
