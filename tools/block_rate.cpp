@@ -17,6 +17,7 @@
 //   tools/block_rate [threads=16] [iterations=400] [max_blocks=16] [window_us=30]
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -128,6 +129,40 @@ int main(int argc, char **argv) {
                         w);
             CHECK(crc32c_blocks_destroy(q) == 0);
         }
+
+    // one thread: submit max_blocks blocks, wait for the last (a flush cycle
+    // with no thread hand-off), and the host's issue cost of one
+    // crc32c_plan_exec_blocks call of max_blocks blocks
+    {
+        crc32c_blocks *q = nullptr;
+        CHECK(crc32c_blocks_create(plan, max_blocks, window_us, &q) == 0);
+        const uint32_t nb = std::min<uint32_t>(max_blocks, uint32_t(nbuf));
+        const int cycles = 500;
+        Clock::time_point t0 = Clock::now();
+        for (int c = 0; c < cycles + 50; ++c) {
+            if (c == 50) t0 = Clock::now();
+            uint64_t t = 0;
+            for (uint32_t b = 0; b < nb; ++b) CHECK(crc32c_block_submit(q, bufs[b], outs[b], &t) == 0);
+            CHECK(crc32c_block_wait(q, t) == 0);
+        }
+        const double s = seconds(t0, Clock::now());
+        std::printf("{\"mode\": \"queue_one_thread\", \"blocks_per_flush\": %u, \"us_per_cycle\": %.3f, "
+                    "\"us_per_block\": %.3f}\n", nb, s / cycles * 1e6, s / cycles / nb * 1e6);
+        CHECK(crc32c_blocks_destroy(q) == 0);
+        const void *pays[32];
+        uint32_t *os[32];
+        for (uint32_t i = 0; i < nb && i < 32; ++i) pays[i] = bufs[i], os[i] = outs[i];
+        hipStream_t s0 = streams[0];
+        for (int i = 0; i < 50; ++i) CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s0) == 0);
+        CHECK(hipStreamSynchronize(s0) == hipSuccess);
+        const int n = 200;
+        t0 = Clock::now();
+        for (int i = 0; i < n; ++i) CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s0) == 0);
+        const double issue = seconds(t0, Clock::now());
+        CHECK(hipStreamSynchronize(s0) == hipSuccess);
+        std::printf("{\"mode\": \"exec_blocks_issue\", \"blocks_per_launch\": %u, \"host_us_per_call\": %.3f}\n", nb,
+                    issue / n * 1e6);
+    }
 
     // kernel: the GPU's time per block in back-to-back multi-block launches
     for (uint32_t nb : {1u, 4u, 8u, 16u, 32u}) {
