@@ -398,9 +398,12 @@ __device__ __forceinline__ bool rep_lane(int lane, uint32_t blk, uint32_t nb, ui
 // readfirstlane of a value that is uniform is exact; on SGPR inputs it
 // folds away.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const uint8_t *base, uint32_t bytes) {
+    // (readfirstlane returns int: each half goes through uint32_t before it
+    // is widened, or a low word >= 2^31 would sign-extend over the high one)
     const uint64_t a = reinterpret_cast<uint64_t>(base);
-    const uint64_t ua = uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(a >> 32))) << 32 |
-                        __builtin_amdgcn_readfirstlane(uint32_t(a));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a >> 32))));
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(a))));
+    const uint64_t ua = uint64_t(hi) << 32 | uint64_t(lo);
     return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(ua), 0,
                                              int(__builtin_amdgcn_readfirstlane(bytes)), 0x00020000);
 }

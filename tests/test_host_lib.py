@@ -496,3 +496,31 @@ def test_product_library_loads_rccl_only_for_multi_gpu(hdfs):
     needed = subprocess.run(["readelf", "-d", hdfs.LIB_PATH], capture_output=True, text=True).stdout
     assert "NEEDED" in needed and "rccl" not in needed, needed
     assert b"librccl.so.1" in open(hdfs.LIB_PATH, "rb").read()
+
+
+def test_kernel_buffer_resources_not_sign_extended(tmp_path):
+    """Regression guard (round 3): the payload loads' buffer resources are
+    built from SGPRs by uniform_rsrc (crc32c_device.h).  A first version
+    widened readfirstlane's int result directly, so a base address whose low
+    word was >= 2^31 sign-extended over the high word (an s_bfe_i64 of the
+    address into the resource) and the kernel faulted on such buffers.  The
+    production kernels' device assembly must contain no 64-bit sign
+    extension of that kind."""
+    import subprocess
+
+    csrc = os.path.join(ROOT, "native-hdfs-fuse_amd", "csrc")
+    out = str(tmp_path / "k.s")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
+                        "-S", "-I" + os.path.join(ROOT, "include"), "-I" + csrc,
+                        os.path.join(csrc, "crc32c_kernel.hip"), "-o", out], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    asm = open(out).read()
+    assert "hdfs_crc32c_plan_kernel" in asm
+    assert not re.search(r"s_bfe_i64\s+s\[\d+:\d+\], s\[\d+:\d+\], 0x200000", asm)
+    # and no waterfall (readfirstlane + execnz) loop around a payload load
+    lines = asm.split("\n")
+    for i, line in enumerate(lines):
+        if "buffer_load_dwordx4" in line:
+            window = lines[max(0, i - 12):i + 4]
+            assert not (any("v_readfirstlane" in w for w in window) and any("s_cbranch_execnz" in w for w in window)), i
