@@ -43,14 +43,13 @@ constexpr uint64_t kMinRunBytes = 1ull << 20;
 constexpr size_t kFirstPieceBytes = 8ull << 20;
 constexpr size_t kZeroCopyBytes = 1ull << 20;  // (zero_copy_bytes)
 
-// Pageable batches up to this many bytes skip the copy command: the CPU
-// copies them into pinned, device-MAPPED staging and the kernel reads them
-// there (a copy command costs ~15 us of latency per call before the kernel
-// can start; DESIGN.md section 5, host-resident per call).  The caller's own
-// pinned memory is not read in place: hipHostMalloc's default allocation is
-// not guaranteed to be mapped for the device (a first version that read it
-// in place faulted).  $HDFS_CRC32C_ZERO_COPY_KB overrides the threshold
-// (A/B only; 0 = never).
+// Batches up to this many bytes (pinned: a quarter of it) skip the copy
+// command: the CPU copies them into pinned, device-MAPPED staging and the
+// kernel reads them there (a copy command costs ~15 us of latency per call
+// before the kernel can start; DESIGN.md section 5, host-resident per call).
+// The caller's own pinned memory is not read in place: hipHostMalloc's
+// default allocation is not guaranteed to be mapped for the device.
+// $HDFS_CRC32C_ZERO_COPY_KB overrides the threshold (A/B only; 0 = never).
 size_t zero_copy_bytes() {
     static const size_t v = [] {
         const char *e = std::getenv("HDFS_CRC32C_ZERO_COPY_KB");
@@ -465,11 +464,15 @@ void free_stage(Stage &s) {
     s = Stage();
 }
 
-// Completes the slice in flight on `s`: wait, then scatter its checksums.
+// Completes the slice in flight on `s`: wait (polled: the caller blocks
+// anyway, and a polled wait returns as soon as the kernel ends), then
+// scatter its checksums.
 int drain_stage(Stage &s, uint32_t *out) {
     if (!s.pending) return 0;
     s.pending = false;
-    HIP_TRY(hipEventSynchronize(s.done));
+    hipError_t e;
+    while ((e = hipEventQuery(s.done)) == hipErrorNotReady) std::this_thread::yield();
+    HIP_TRY(e);
     for (size_t i = 0; i + 2 < s.scatter.size(); i += 3)
         std::memcpy(out + s.scatter[i], s.h_out + s.scatter[i + 1], s.scatter[i + 2] * sizeof(uint32_t));
     s.scatter.clear();
@@ -560,7 +563,10 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         //    host memory (zero copy).
         local.assign(pkts + i, pkts + j);
         const uint8_t *kpayload = s.d_payload;
-        const bool zero_copy = !pinned && ranged && i == 0 && j == npkts && (hi - lo) <= zero_copy_bytes();
+        // (pinned input: only small batches -- a CPU copy of 1 MiB already
+        // costs what the copy command saves; 64 KiB: 22 vs 40 us per call)
+        const bool zero_copy = ranged && i == 0 && j == npkts &&
+                               (hi - lo) <= (pinned ? zero_copy_bytes() / 4 : zero_copy_bytes());
         if (zero_copy) {  // (into mapped staging, which the kernel reads in place)
             rc = grow_mapped(&s.h_zc, &s.d_zc, &s.zc_cap, stage_bytes + 16);
             if (rc) return rc;

@@ -162,6 +162,33 @@ int main(int argc, char **argv) {
         CHECK(hipStreamSynchronize(s0) == hipSuccess);
         std::printf("{\"mode\": \"exec_blocks_issue\", \"blocks_per_launch\": %u, \"host_us_per_call\": %.3f}\n", nb,
                     issue / n * 1e6);
+        // where a call's host time goes: the same loop over single calls
+        auto issue_cost = [&](const char *what, auto fn) {
+            for (int i = 0; i < 50; ++i) fn();
+            CHECK(hipStreamSynchronize(s0) == hipSuccess);
+            const auto a = Clock::now();
+            for (int i = 0; i < n; ++i) fn();
+            const double us = seconds(a, Clock::now()) / n * 1e6;
+            CHECK(hipStreamSynchronize(s0) == hipSuccess);
+            std::printf("{\"mode\": \"issue_cost\", \"call\": \"%s\", \"host_us\": %.3f}\n", what, us);
+        };
+        issue_cost("crc32c_plan_exec 1 block", [&] { CHECK(crc32c_plan_exec(plan, bufs[0], outs[0], s0) == 0); });
+        issue_cost("crc32c_plan_exec_blocks 1", [&] { CHECK(crc32c_plan_exec_blocks(plan, pays, os, 1, s0) == 0); });
+        issue_cost("crc32c_plan_exec_blocks 16", [&] { CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s0) == 0); });
+        hipEvent_t ev;
+        CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess);
+        issue_cost("hipEventRecord", [&] { CHECK(hipEventRecord(ev, s0) == hipSuccess); });
+        issue_cost("hipStreamIsCapturing", [&] {
+            hipStreamCaptureStatus cs;
+            CHECK(hipStreamIsCapturing(s0, &cs) == hipSuccess);
+        });
+        issue_cost("hipThreadExchangeStreamCaptureMode x2", [&] {
+            hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+            CHECK(hipThreadExchangeStreamCaptureMode(&m) == hipSuccess);
+            CHECK(hipThreadExchangeStreamCaptureMode(&m) == hipSuccess);
+        });
+        issue_cost("hipEventQuery", [&] { (void)hipEventQuery(ev); });
+        (void)hipEventDestroy(ev);
     }
 
     // kernel: the GPU's time per block in back-to-back multi-block launches
