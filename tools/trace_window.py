@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-launch durations of one kernel from a rocprofv3 kernel trace
 (run_kernel_trace.csv), averaged over bench.py's timed window: launch 0 is
-the correctness gate, then `--warmup` warm-up launches, then (graph-replayed
+the correctness gate, then `--settle` power-settle launches (the line's
+`settle_launches`), then `--warmup` warm-up launches, then (graph-replayed
 bench, the default) one untimed replay of the `--steps` captured launches,
 then the `--steps` timed ones.  Writes the window's average / median / min / max (ns) so it can be
 compared with bench.py's own HIP-event average for the same run.
@@ -21,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--kernel", required=True)
+    ap.add_argument("--settle", type=int, default=0, help="the bench line's settle_launches")
     ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--out")
@@ -29,7 +31,7 @@ def main():
     rows = [r for r in csv.DictReader(open(args.trace)) if args.kernel in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-    first = 1 + args.warmup + (0 if args.no_graph else args.steps)
+    first = 1 + args.settle + args.warmup + (0 if args.no_graph else args.steps)
     win = dur[first:first + args.steps]
     starts = [int(r["Start_Timestamp"]) for r in rows[first:first + args.steps]]
     res = {
@@ -37,7 +39,9 @@ def main():
         "window_avg_ns": round(statistics.mean(win), 1), "window_median_ns": statistics.median(win),
         "window_min_ns": min(win), "window_max_ns": max(win),
         "window_span_per_launch_ns": round((starts[-1] - starts[0]) / max(len(starts) - 1, 1), 1),
-        "warmup_avg_ns": round(statistics.mean(dur[1:1 + args.warmup]), 1) if args.warmup else None,
+        "settle_avg_ns": round(statistics.mean(dur[1:1 + args.settle]), 1) if args.settle else None,
+        "warmup_avg_ns": round(statistics.mean(dur[1 + args.settle:1 + args.settle + args.warmup]), 1)
+        if args.warmup else None,
     }
     text = json.dumps(res, indent=1)
     print(text)
