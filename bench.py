@@ -443,20 +443,24 @@ def main():
     # steady state, so a short timed window (the
     # driver's 20 steps after 5) would measure the transient.  ~settle_ms of
     # the same step first, reported in the line; --settle-ms 0 disables it.
-    settle = 0
-    if args.settle_ms > 0 and c4 and world > 1:
-        # (config 4's steps hold RCCL calls: every rank makes the same count)
-        for settle in range(int(args.settle_ms * 10)):
-            step(settle)
-        settle += 1
-        torch.cuda.synchronize()
-    elif args.settle_ms > 0:
-        s0 = time.perf_counter()
-        while (time.perf_counter() - s0) * 1e3 < args.settle_ms:
-            for _ in range(20):
-                step(settle)
-                settle += 1
+    def settle_for(ms):  # untimed steps for ~ms; returns how many
+        n = 0
+        if ms > 0 and c4 and world > 1:
+            # (config 4's steps hold RCCL calls: every rank makes the same count)
+            for n in range(int(ms * 10)):
+                step(n)
+            n += 1
             torch.cuda.synchronize()
+        elif ms > 0:
+            s0 = time.perf_counter()
+            while (time.perf_counter() - s0) * 1e3 < ms:
+                for _ in range(20):
+                    step(n)
+                    n += 1
+                torch.cuda.synchronize()
+        return n
+
+    settle = settle_for(args.settle_ms)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -534,6 +538,9 @@ def main():
     timed_exact = all(timed_checks.values())
     eager_ms = None
     if use_graph:  # the same steps issued one by one from the host, for comparison
+        # (after the checks above the GPU sat idle for a while: settle again,
+        # or the host-issued launches ride the power transient)
+        settle_for(args.settle_ms)
         ne = min(args.steps, 500)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

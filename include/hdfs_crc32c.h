@@ -137,10 +137,12 @@ int crc32c_device_count(void);
  * decomposition into 8 KiB tiles) and executed on any payload with that
  * shape.  Its descriptors go to the device asynchronously (the first launch
  * on a stream waits for that copy).  Destroying a plan whose launches are
- * still in flight is safe, also after their streams were destroyed: every
- * launch completes a per-(plan, stream) event (the kernel dispatch's own
- * stop event), and the plan's device block is recycled only once those
- * events have completed -- no device-wide synchronisation on any plan
+ * still in flight is safe: for every stream a launch of the plan went on
+ * that is still busy at destroy time an event is recorded there, and the
+ * plan's device block is recycled only once those events (and its upload)
+ * have completed.  So a plan is destroyed BEFORE the streams it was
+ * launched on (an idle stream is only queried) -- no device-wide
+ * synchronisation on any plan
  * create / destroy path, so work of other streams and libraries is never
  * waited on, and plans may be created and destroyed while another thread
  * captures a graph.  A plan must outlive every HIP graph that captured its

@@ -15,8 +15,9 @@
 // Group commit: a submit that fills the queue (max_blocks) flushes it; a
 // thread waiting for a block still queued flushes when the window since the
 // queue's first block has passed, else sleeps until then or until another
-// thread's flush took its block.  Every flush records an event on the
-// queue's stream.  Completion: the first thread to wait for a flush is its
+// thread's flush took its block.  A flush's completion event is its last
+// launch's own stop event (hipExtLaunchKernel; an hipEventRecord after it
+// adds a command and ~6 us of host time per flush, tools/block_rate).  Completion: the first thread to wait for a flush is its
 // watcher -- the only one that waits on the HIP event -- and publishes the
 // flush's end (done_upto) to the others, which spin on it briefly and then
 // sleep on the condition variable.  (Every waiter on the event itself, 16
@@ -29,6 +30,7 @@
 #include <cerrno>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -63,11 +65,19 @@ struct crc32c_blocks {
     std::deque<Flush> inflight;
     std::vector<hipEvent_t> spare;
     uint64_t flushes = 0, blocks = 0;
+    bool record_events = false;  // A/B (HDFS_CRC32C_QUEUE_RECORD=1): an hipEventRecord after each flush
 };
 
 namespace {
 
-constexpr auto kSpin = std::chrono::microseconds(50);  // waiters spin this long before sleeping
+// Waiters spin this long before sleeping (HDFS_CRC32C_QUEUE_SPIN_US: A/B).
+std::chrono::microseconds spin_time() {
+    static const std::chrono::microseconds t = [] {
+        const char *e = std::getenv("HDFS_CRC32C_QUEUE_SPIN_US");
+        return std::chrono::microseconds(e ? std::atoi(e) : 50);
+    }();
+    return t;
+}
 
 void publish(crc32c_blocks *q, uint64_t hi) {  // caller holds q->mu
     if (hi > q->done_upto.load(std::memory_order_relaxed)) q->done_upto.store(hi, std::memory_order_release);
@@ -101,11 +111,15 @@ int flush_locked(crc32c_blocks *q) {
         ev = q->spare.back();
         q->spare.pop_back();
     } else {
-        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDefault));
     }
-    int rc = crc32c_plan_exec_blocks(q->plan, q->pend_payload.data(), q->pend_out.data(), q->pend_payload.size(),
-                                     q->stream);
-    if (!rc && hipEventRecord(ev, q->stream) != hipSuccess) rc = fail(-EIO, "hipEventRecord failed");
+    // the flush's event is the last launch's own stop event
+    int rc = q->record_events
+                 ? crc32c_plan_exec_blocks(q->plan, q->pend_payload.data(), q->pend_out.data(), q->pend_payload.size(),
+                                           q->stream)
+                 : exec_blocks(q->plan, q->pend_payload.data(), q->pend_out.data(), q->pend_payload.size(), q->stream,
+                               ev);
+    if (!rc && q->record_events && hipEventRecord(ev, q->stream) != hipSuccess) rc = fail(-EIO, "hipEventRecord failed");
     if (rc) {
         q->spare.push_back(ev);
         return rc;
@@ -132,6 +146,8 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
     q->device = plan->ctx->device;
     q->max_blocks = max_blocks ? std::min<uint32_t>(max_blocks, 1024u) : 16u;
     q->window = std::chrono::microseconds(window_us);
+    const char *rec = std::getenv("HDFS_CRC32C_QUEUE_RECORD");
+    q->record_events = rec && rec[0] == '1';
     q->pend_payload.reserve(q->max_blocks);
     q->pend_out.reserve(q->max_blocks);
     DeviceGuard guard(q->device);
@@ -197,7 +213,7 @@ int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
         return 0;
     }
     lock.unlock();
-    const Clock::time_point spin_end = Clock::now() + kSpin;
+    const Clock::time_point spin_end = Clock::now() + spin_time();
     while (Clock::now() < spin_end) {
         if (ticket < q->done_upto.load(std::memory_order_acquire)) return 0;
         std::this_thread::yield();
@@ -231,6 +247,7 @@ int crc32c_blocks_destroy(crc32c_blocks *q) {
     DeviceGuard guard(q->device);
     if (q->stream) {
         (void)hipStreamSynchronize(q->stream);
+        plan_forget_stream(q->plan, q->stream);  // (idle now; the plan must not touch it once destroyed)
         (void)hipStreamDestroy(q->stream);
     }
     for (const auto &f : q->inflight) (void)hipEventDestroy(f.ev);

@@ -232,7 +232,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
         if (int rc = pool_get(ctx, ctx->host_pool, bytes, &dp->h, &dp->hcap)) return rc;
         dp->uploaded = take_event(ctx);
     }
-    if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDefault));  // (pooled: also used as stop events)
+    if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDisableTiming));
     uint8_t *img = dp->h;
     init_sched_slots(reinterpret_cast<uint32_t *>(img + dp->slots_off));
     std::memcpy(img + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
@@ -249,14 +249,15 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
 // Orders a launch on `stream` after the plan's upload: nothing once the
 // upload is known complete; else a stream wait on its event (or, while the
 // stream is being captured into a graph, a host wait: a capture cannot wait
-// on work outside it).  Hands out the stream's completion event.
-int prepare_launch(crc32c_plan *plan, hipStream_t stream, hipEvent_t *stop) {
+// on work outside it).  Notes the stream for the plan's release.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream) {
     RelaxedCapture relaxed;  // (the queries below while another thread captures a graph)
-    *stop = nullptr;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(stream, &cs));
     const bool capturing = cs != hipStreamCaptureStatusNone;
     if (capturing) plan->captured = true;
+    if (std::find(plan->launch_streams.begin(), plan->launch_streams.end(), stream) == plan->launch_streams.end())
+        plan->launch_streams.push_back(stream);
     DevicePlan *dp = &plan->dp;
     if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
         const hipError_t q = hipEventQuery(dp->uploaded);
@@ -272,38 +273,64 @@ int prepare_launch(crc32c_plan *plan, hipStream_t stream, hipEvent_t *stop) {
             }
         }
     }
-    if (capturing) return 0;  // (a graph's replays are not tracked: the block is held)
-    for (auto &d : plan->done)
-        if (d.first == stream) {
-            *stop = d.second;
-            return 0;
-        }
-    hipEvent_t e = nullptr;
-    {
-        std::lock_guard<std::mutex> lock(plan->ctx->pool_mu);
-        e = take_event(plan->ctx);
-    }
-    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDefault));  // (a stop event tracks the dispatch's end)
-    plan->done.emplace_back(stream, e);
-    *stop = e;
     return 0;
+}
+
+void plan_forget_stream(crc32c_plan *plan, hipStream_t stream) {
+    std::lock_guard<std::mutex> lock(plan->mu);
+    auto &v = plan->launch_streams;
+    v.erase(std::remove(v.begin(), v.end(), stream), v.end());
 }
 
 void release_plan_blocks(crc32c_plan *plan) {
     crc32c_ctx *ctx = plan->ctx;
     DevicePlan *dp = &plan->dp;
+    RelaxedCapture relaxed;
     Release r;
     r.d = dp->d;
     r.dcap = dp->cap;
     r.h = dp->h;
     r.hcap = dp->hcap;
-    // every launch's completion event (already recorded by the launches
-    // themselves: no stream is touched here), and the upload's
-    for (auto &d : plan->done) r.events.push_back(d.second);
-    plan->done.clear();
+    bool held = plan->captured;
+    // Per launch stream: nothing when it is idle (its launches of the plan
+    // are done -- the usual case: exec, synchronise, destroy), else an event
+    // recorded now (it completes after them).  The streams must still exist:
+    // a plan is destroyed before the streams it was launched on.
+    for (hipStream_t s : plan->launch_streams) {
+        if (held) break;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            (void)hipGetLastError();
+            held = true;  // (a capture in progress on it may hold the plan's launches)
+            break;
+        }
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) continue;
+        if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            held = true;
+            break;
+        }
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> lock(ctx->pool_mu);
+            e = take_event(ctx);
+        }
+        if ((!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) || hipEventRecord(e, s) != hipSuccess) {
+            (void)hipGetLastError();
+            if (e) {
+                std::lock_guard<std::mutex> lock(ctx->pool_mu);
+                ctx->spare_events.push_back(e);
+            }
+            held = true;
+            break;
+        }
+        r.events.push_back(e);
+    }
+    plan->launch_streams.clear();
     if (dp->uploaded) r.events.push_back(dp->uploaded);
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
-    if (plan->captured && r.d) {
+    if (held && r.d) {
         ctx->held.emplace_back(r.d, r.dcap);
         drop_block(ctx->dev_pool, r.d);
         r.d = nullptr;
@@ -353,7 +380,10 @@ int alloc_slots(SchedSlots &s) {
 // in GPU order.
 int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream, hipEvent_t stop = nullptr) {
     const uint64_t items = uint64_t(p.ntiles) + p.ngen + p.nseg + p.nconst;
-    if (!items) return 0;
+    if (!items) {
+        if (stop) HIP_TRY(hipEventRecord(stop, stream));
+        return 0;
+    }
     const bool sched = p.expect != nullptr;
     if (sched) {
         int rc = alloc_slots(slots);
@@ -379,10 +409,9 @@ int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
     return 0;
 }
 
-int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream) {
+int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream, hipEvent_t stop = nullptr) {
     std::lock_guard<std::mutex> lock(plan->mu);
-    hipEvent_t stop = nullptr;
-    if (int rc = prepare_launch(plan, stream, &stop)) return rc;
+    if (int rc = prepare_launch(plan, stream)) return rc;
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
@@ -850,23 +879,31 @@ int crc32c_plan_exec(crc32c_plan *plan, const void *dev_payload, uint32_t *dev_o
     return launch_plan(plan, plan_params(plan, dev_payload, dev_out), static_cast<hipStream_t>(stream));
 }
 
-int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
-                            size_t nblocks, void *stream) {
+}  // extern "C"
+
+namespace hdfs_crc {
+
+int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs, size_t nblocks,
+                hipStream_t s, hipEvent_t stop) {
     if (!plan) return fail(-EINVAL, "plan == NULL");
     if (plan->absolute) return fail(-EINVAL, "a multi-block launch takes a plan of one block's shape, not device addresses");
     if (nblocks && (!dev_payloads || !dev_outs)) return fail(-EINVAL, "payloads/outs == NULL");
-    if (plan->nchecksums == 0 || nblocks == 0) return 0;
+    if (plan->nchecksums == 0 || nblocks == 0) {
+        if (stop) HIP_TRY(hipEventRecord(stop, s));
+        return 0;
+    }
     for (size_t i = 0; i < nblocks; ++i)
         if ((!dev_payloads[i] && plan_reads_payload(plan)) || !dev_outs[i] || (uintptr_t(dev_outs[i]) & 3u))
             return fail(-EINVAL, "block %zu: payload NULL, or out NULL / not 4-byte aligned", i);
     DeviceGuard guard(plan->ctx->device);
-    const hipStream_t s = static_cast<hipStream_t>(stream);
     const DevicePlan &dp = plan->dp;
     if (dp.ngen || dp.nseg || dp.nconst || dp.ntiles == 0) {
         // (items other than tiles -- tails under 4 bytes, bpc outside [4, 8192]
         // -- have no multi-block form: one launch per block)
         for (size_t i = 0; i < nblocks; ++i)
-            if (int rc = launch_plan(plan, plan_params(plan, dev_payloads[i], dev_outs[i]), s)) return rc;
+            if (int rc = launch_plan(plan, plan_params(plan, dev_payloads[i], dev_outs[i]), s,
+                                     i + 1 == nblocks ? stop : nullptr))
+                return rc;
         return 0;
     }
     const uint64_t max_launch_tiles = UINT32_MAX;
@@ -896,10 +933,19 @@ int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, 
             b.reserved = 0;
             if (b.payload_delta & 15u) p.general = 1u;  // (shifted loads for blocks off 16-byte alignment)
         }
-        if (int rc = launch_plan(plan, p, s)) return rc;
+        if (int rc = launch_plan(plan, p, s, j == nblocks ? stop : nullptr)) return rc;
         i = j;
     }
     return 0;
+}
+
+}  // namespace hdfs_crc
+
+extern "C" {
+
+int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
+                            size_t nblocks, void *stream) {
+    return exec_blocks(plan, dev_payloads, dev_outs, nblocks, static_cast<hipStream_t>(stream), nullptr);
 }
 
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,

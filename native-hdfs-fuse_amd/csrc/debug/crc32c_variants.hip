@@ -125,11 +125,9 @@ extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev
     p.stamps = dev_stamps;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lock(plan->mu);
-    hipEvent_t stop = nullptr;
-    if (int rc = prepare_launch(plan, s, &stop)) return rc;
-    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s, stop)
+    if (int rc = prepare_launch(plan, s)) return rc;
+    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
                          : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));
-    if (variant != 0 && stop) HIP_TRY(hipEventRecord(stop, s));  // (the plan's block outlives this launch)
     return 0;
 }
 

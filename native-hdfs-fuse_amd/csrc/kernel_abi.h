@@ -92,8 +92,8 @@ inline void init_sched_slots(uint32_t *w) {
 
 // The production kernel (crc32c_kernel.hip): one 12-wave workgroup per CU,
 // min(work items, CUs) of them; p.expect selects the verification mode.
-// `stop` (optional) tracks the launch's completion (hipExtLaunchKernel's
-// stop event: the dispatch's own completion, no extra command).
+// `stop` (optional): an event the launch itself completes (hipExtLaunchKernel's
+// stop event -- no extra command on the stream, unlike an hipEventRecord).
 hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop = nullptr);
 
 }  // namespace hdfs_crc

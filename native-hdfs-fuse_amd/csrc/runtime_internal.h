@@ -160,13 +160,12 @@ struct crc32c_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t last_done = nullptr;
     bool launched = false;
-    // Per stream a launch of the plan went on: an event every launch there
-    // passes as its stop event (hipExtLaunchKernel: the dispatch's own
-    // completion), so the plan's blocks are recycled once these have
-    // completed -- without touching the streams (which the caller may have
-    // destroyed by then).  The stream is only a key.  `captured`: a launch
-    // went into a graph capture (its block is never reused).
-    std::vector<std::pair<hipStream_t, hipEvent_t>> done;
+    // Every stream a launch of the plan went on (at destroy time: nothing to
+    // do for an idle one, else an event recorded on it gates the block's
+    // reuse), and whether a launch went into a graph capture (then the block
+    // is never reused).  (Round 3 first gave every launch a stop event to
+    // complete instead; that cost every launch)
+    std::vector<hipStream_t> launch_streams;
     bool captured = false;
     hdfs_crc::DevicePlan dp;
     uint64_t nchecksums = 0, payload_bytes = 0;
@@ -186,9 +185,14 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
 // device (into *dp), asynchronously; plan_ready orders a launch after it.
 int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
 // Before a launch of `plan` on `stream` (caller holds plan->mu): orders it
-// after the plan's upload; *stop = the event the launch must complete
-// (nullptr while the stream is being captured).
-int prepare_launch(crc32c_plan *plan, hipStream_t stream, hipEvent_t *stop);
+// after the plan's upload and notes the stream for the plan's release.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream);
+// `stream` (idle, about to be destroyed by the library itself: a block
+// queue's) no longer needs an event at the plan's release.
+void plan_forget_stream(crc32c_plan *plan, hipStream_t stream);
+// crc32c_plan_exec_blocks; `stop` (optional) is completed by the last launch.
+int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs, size_t nblocks,
+                hipStream_t stream, hipEvent_t stop);
 // A destroyed plan's blocks back to the pools once its launches are done.
 void release_plan_blocks(crc32c_plan *plan);
 // Context teardown: waits for the releases, frees every pooled block.

@@ -15,6 +15,7 @@
 //              back: the GPU's time per block in a multi-block launch (events)
 //
 //   tools/block_rate [threads=16] [iterations=400] [max_blocks=16] [window_us=30]
+//                    [max_depth=2] [queue_modes_only=0]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,6 +44,7 @@ static double seconds(Clock::time_point a, Clock::time_point b) {
 }
 
 int main(int argc, char **argv) {
+    std::setvbuf(stdout, nullptr, _IOLBF, 0);  // (lines survive a crash when stdout is a file)
     const int nthreads = argc > 1 ? std::atoi(argv[1]) : 16;
     const int iters = argc > 2 ? std::atoi(argv[2]) : 400;
     const uint32_t max_blocks = argc > 3 ? uint32_t(std::atoi(argv[3])) : 16u;
@@ -57,7 +59,9 @@ int main(int argc, char **argv) {
     CHECK(crc32c_ctx_create(0, &ctx) == 0);
     crc32c_plan *plan = nullptr;
     CHECK(crc32c_plan_create(ctx, pk.data(), pk.size(), 0, &plan) == 0);
-    const int nbuf = 2 * nthreads;
+    const int maxdepth = argc > 5 ? std::atoi(argv[5]) : 2;  // blocks in flight per thread (queue modes)
+    const bool sweep_only = argc > 6 && std::atoi(argv[6]) != 0;  // only the queue modes
+    const int nbuf = std::max(2, maxdepth) * nthreads;
     std::vector<uint8_t *> bufs(nbuf);
     std::vector<uint32_t *> outs(nbuf);
     for (int i = 0; i < nbuf; ++i) {
@@ -92,7 +96,7 @@ int main(int argc, char **argv) {
     // single: one launch per block
     std::vector<hipStream_t> streams(nthreads);
     for (auto &s : streams) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; w < (sweep_only ? 0 : 2); ++w) {
         run("single", [&](int k) {
             for (int i = 0; i < iters; ++i) {
                 CHECK(crc32c_plan_exec(plan, bufs[k], outs[k], streams[k]) == 0);
@@ -102,24 +106,27 @@ int main(int argc, char **argv) {
         std::printf(", \"pass\": %d}\n", w);
     }
 
-    for (int depth = 1; depth <= 2; ++depth)
+    // queue (depth 1), queue2, queue4, ...: `depth` blocks in flight per
+    // thread (submit the next, then wait for the oldest)
+    for (int depth = 1; depth <= maxdepth; depth *= 2)
         for (int w = 0; w < 2; ++w) {
             crc32c_blocks *q = nullptr;
             CHECK(crc32c_blocks_create(plan, max_blocks, window_us, &q) == 0);
-            run(depth == 1 ? "queue" : "queue2", [&](int k) {
+            char name[32];
+            std::snprintf(name, sizeof name, depth == 1 ? "queue" : "queue%d", depth);
+            run(name, [&](int k) {
                 if (depth == 1) {
                     for (int i = 0; i < iters; ++i) CHECK(crc32c_block_checksums(q, bufs[k], outs[k]) == 0);
                     return;
                 }
-                uint64_t prev = 0;
+                std::vector<uint64_t> ring(depth);
                 for (int i = 0; i < iters; ++i) {
-                    const int b = 2 * k + (i & 1);
-                    uint64_t t = 0;
-                    CHECK(crc32c_block_submit(q, bufs[b], outs[b], &t) == 0);
-                    if (i) CHECK(crc32c_block_wait(q, prev) == 0);
-                    prev = t;
+                    const int slot = i % depth;
+                    if (i >= depth) CHECK(crc32c_block_wait(q, ring[slot]) == 0);
+                    const int b = depth * k + slot;
+                    CHECK(crc32c_block_submit(q, bufs[b], outs[b], &ring[slot]) == 0);
                 }
-                CHECK(crc32c_block_wait(q, prev) == 0);
+                for (int i = std::max(0, iters - depth); i < iters; ++i) CHECK(crc32c_block_wait(q, ring[i % depth]) == 0);
             });
             uint64_t flushes = 0, blocks = 0;
             CHECK(crc32c_blocks_stats(q, &flushes, &blocks) == 0);
@@ -129,6 +136,11 @@ int main(int argc, char **argv) {
                         w);
             CHECK(crc32c_blocks_destroy(q) == 0);
         }
+    if (sweep_only) {
+        crc32c_plan_destroy(plan);
+        for (auto &s : streams) (void)hipStreamDestroy(s);
+        return 0;
+    }
 
     // one thread: submit max_blocks blocks, wait for the last (a flush cycle
     // with no thread hand-off), and the host's issue cost of one
@@ -163,14 +175,19 @@ int main(int argc, char **argv) {
         std::printf("{\"mode\": \"exec_blocks_issue\", \"blocks_per_launch\": %u, \"host_us_per_call\": %.3f}\n", nb,
                     issue / n * 1e6);
         // where a call's host time goes: the same loop over single calls
+        // (in bursts of 4 calls on an idle stream, so a full queue's
+        // back-pressure is not counted as issue cost)
         auto issue_cost = [&](const char *what, auto fn) {
             for (int i = 0; i < 50; ++i) fn();
             CHECK(hipStreamSynchronize(s0) == hipSuccess);
-            const auto a = Clock::now();
-            for (int i = 0; i < n; ++i) fn();
-            const double us = seconds(a, Clock::now()) / n * 1e6;
-            CHECK(hipStreamSynchronize(s0) == hipSuccess);
-            std::printf("{\"mode\": \"issue_cost\", \"call\": \"%s\", \"host_us\": %.3f}\n", what, us);
+            double tot = 0;
+            for (int r = 0; r < n / 4; ++r) {
+                const auto a = Clock::now();
+                for (int i = 0; i < 4; ++i) fn();
+                tot += seconds(a, Clock::now());
+                CHECK(hipStreamSynchronize(s0) == hipSuccess);
+            }
+            std::printf("{\"mode\": \"issue_cost\", \"call\": \"%s\", \"host_us\": %.3f}\n", what, tot / n * 1e6);
         };
         issue_cost("crc32c_plan_exec 1 block", [&] { CHECK(crc32c_plan_exec(plan, bufs[0], outs[0], s0) == 0); });
         issue_cost("crc32c_plan_exec_blocks 1", [&] { CHECK(crc32c_plan_exec_blocks(plan, pays, os, 1, s0) == 0); });
@@ -213,12 +230,12 @@ int main(int argc, char **argv) {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     }
+    crc32c_plan_destroy(plan);  // (before the streams it was launched on)
     for (auto &s : streams) (void)hipStreamDestroy(s);
     for (int i = 0; i < nbuf; ++i) {
         (void)hipFree(bufs[i]);
         (void)hipFree(outs[i]);
     }
-    crc32c_plan_destroy(plan);
     crc32c_ctx_destroy(ctx);
     return 0;
 }

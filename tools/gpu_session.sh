@@ -37,6 +37,14 @@ for s in $STEPS; do
     bench3h) run bench3h 600 python bench.py --config c3 --host-sweep --cpu-seconds 2 ;;
     sweepab) run sweep_zc0 600 env HDFS_CRC32C_ZERO_COPY_KB=0 python bench.py --config c3 --host-sweep --no-cpu --steps 200 --warmup 50 && run sweep_zc 600 python bench.py --config c3 --host-sweep --no-cpu --steps 200 --warmup 50 ;;
     brate) run brate 300 tools/block_rate ${BR_ARGS:-16 400 16 30} ;;
+    brateab) run brate_rec 300 env HDFS_CRC32C_QUEUE_RECORD=1 tools/block_rate ${BR_ARGS:-16 400 16 30} && run brate 300 tools/block_rate ${BR_ARGS:-16 400 16 30} ;;
+    ab02) for c in ${ABCFGS:-c5 c2b1536}; do
+            run ab_r02_$c 600 bash -c "cd scratch/r02 && python bench.py --config $c --no-cpu --no-host" &&
+            run ab_head_$c 600 python bench.py --config $c --no-cpu --no-host; done ;;
+    bsweep) for spin in ${BSPIN:-50 0}; do for mb in ${BMB:-8 16 32}; do for th in ${BTH:-16 32}; do
+              run bsw_s${spin}_mb${mb}_t${th} 120 env HDFS_CRC32C_QUEUE_SPIN_US=$spin tools/block_rate $th 300 $mb ${BWIN:-30} 4 1;
+            done; done; done ;;
+    lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
     stash) for b in ${SB:-basewt stashwt stashB}; do run stash_$b 300 python tools/stash_repro.py $b ${SBPC:-4,7,100,1000,1536}; done ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
