@@ -14,15 +14,15 @@
 //
 // Group commit: a submit that fills the queue (max_blocks) flushes it; a
 // thread waiting for a block still queued flushes when the window since the
-// queue's first block has passed, else sleeps until then or until another
-// thread's flush took its block.  A flush's completion event is its last
-// launch's own stop event (hipExtLaunchKernel; an hipEventRecord after it
-// adds a command and ~6 us of host time per flush, tools/block_rate).  Completion: the first thread to wait for a flush is its
-// watcher -- the only one that waits on the HIP event -- and publishes the
-// flush's end (done_upto) to the others, which spin on it briefly and then
-// sleep on the condition variable.  (Every waiter on the event itself, 16
-// threads in HIP's event wait at once, ran at 4.6-6.8 us per block, 5-8x the
-// GPU's time: tools/block_rate.)
+// queue's first block has passed (so does the queue's completion thread).
+// A flush's completion event is its last launch's own stop event
+// (hipExtLaunchKernel; an hipEventRecord after the launch costs more,
+// tools/launch_stop_probe).  Completion: one thread per queue (the
+// completer) polls the oldest flush's event, publishes its end (done_upto)
+// and wakes the waiters, which spin on done_upto briefly and then sleep on
+// the condition variable.  Only the completer queries the events: round 3's
+// first form made the first waiter of each flush poll its event, so several
+// threads polled HIP at once while others launched.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -50,7 +50,8 @@ struct crc32c_blocks {
     std::chrono::microseconds window{20};
     hipStream_t stream = nullptr;
     std::mutex mu;
-    std::condition_variable cv;
+    std::condition_variable cv;       // waiters: done_upto moved
+    std::condition_variable work_cv;  // completer: a flush or a pending block appeared, or stop
     std::vector<const void *> pend_payload;
     std::vector<uint32_t *> pend_out;
     Clock::time_point first_pending;
@@ -60,17 +61,20 @@ struct crc32c_blocks {
     struct Flush {
         uint64_t hi;  // tickets below hi
         hipEvent_t ev;
-        bool watched;  // a thread waits on ev and will publish hi
     };
     std::deque<Flush> inflight;
     std::vector<hipEvent_t> spare;
     uint64_t flushes = 0, blocks = 0;
+    std::atomic<int> error{0};            // a failed flush or event: every waiter returns it
+    std::atomic<bool> has_pending{false};  // pend_payload non-empty (read without the lock)
+    bool stop = false;
     bool record_events = false;  // A/B (HDFS_CRC32C_QUEUE_RECORD=1): an hipEventRecord after each flush
+    std::thread completer;
 };
 
 namespace {
 
-// Waiters spin this long before sleeping (HDFS_CRC32C_QUEUE_SPIN_US: A/B).
+// Waiters spin this long on done_upto before sleeping (HDFS_CRC32C_QUEUE_SPIN_US: A/B).
 std::chrono::microseconds spin_time() {
     static const std::chrono::microseconds t = [] {
         const char *e = std::getenv("HDFS_CRC32C_QUEUE_SPIN_US");
@@ -79,33 +83,10 @@ std::chrono::microseconds spin_time() {
     return t;
 }
 
-void publish(crc32c_blocks *q, uint64_t hi) {  // caller holds q->mu
-    if (hi > q->done_upto.load(std::memory_order_relaxed)) q->done_upto.store(hi, std::memory_order_release);
-}
-
-// Completed flushes off the front of the queue (non-blocking; a watched
-// flush only once its watcher has published it, so its event is not
-// recycled under the watcher).  Caller holds q->mu.
-void reap(crc32c_blocks *q) {
-    while (!q->inflight.empty()) {
-        auto &f = q->inflight.front();
-        if (f.hi > q->done_upto.load(std::memory_order_relaxed)) {
-            if (f.watched) return;
-            const hipError_t e = hipEventQuery(f.ev);
-            if (e == hipErrorNotReady) return;
-            if (e != hipSuccess) (void)hipGetLastError();
-            publish(q, f.hi);
-        }
-        q->spare.push_back(f.ev);
-        q->inflight.pop_front();
-    }
-}
-
 // One multi-block launch of everything queued.  Caller holds q->mu.
 int flush_locked(crc32c_blocks *q) {
     if (q->pend_payload.empty()) return 0;
     DeviceGuard guard(q->device);
-    reap(q);
     hipEvent_t ev = nullptr;
     if (!q->spare.empty()) {
         ev = q->spare.back();
@@ -124,14 +105,64 @@ int flush_locked(crc32c_blocks *q) {
         q->spare.push_back(ev);
         return rc;
     }
-    q->inflight.push_back({q->next_ticket, ev, false});
+    const bool was_idle = q->inflight.empty();
+    q->inflight.push_back({q->next_ticket, ev});
     q->flushes++;
     q->blocks += q->pend_payload.size();
     q->flushed_upto = q->next_ticket;
     q->pend_payload.clear();
     q->pend_out.clear();
-    q->cv.notify_all();
+    q->has_pending.store(false, std::memory_order_relaxed);
+    q->cv.notify_all();  // (waiters of these blocks stop flushing)
+    if (was_idle) q->work_cv.notify_one();
     return 0;
+}
+
+// The queue's one HIP waiter: completes flushes in launch order (polling the
+// front flush's event -- the only thread that queries the queue's events, so
+// the threads that submit and launch never contend with it in the runtime),
+// publishes done_upto, and flushes a partial queue once its window passed.
+void completer_loop(crc32c_blocks *q) {
+    DeviceGuard guard(q->device);
+    std::unique_lock<std::mutex> lock(q->mu);
+    for (;;) {
+        if (!q->pend_payload.empty() && Clock::now() >= q->first_pending + q->window) {
+            if (int rc = flush_locked(q)) {  // (the blocks are dropped: their waiters get the error)
+                q->error = rc;
+                q->pend_payload.clear();
+                q->pend_out.clear();
+                q->has_pending.store(false, std::memory_order_relaxed);
+                q->flushed_upto = q->next_ticket;
+                if (q->inflight.empty()) q->done_upto.store(q->next_ticket, std::memory_order_release);
+                q->cv.notify_all();
+            }
+        }
+        if (q->inflight.empty()) {
+            if (q->stop) return;
+            if (q->pend_payload.empty())
+                q->work_cv.wait(lock);
+            else
+                q->work_cv.wait_until(lock, q->first_pending + q->window);
+            continue;
+        }
+        const crc32c_blocks::Flush f = q->inflight.front();
+        lock.unlock();
+        hipError_t e;
+        int polls = 0;
+        while ((e = hipEventQuery(f.ev)) == hipErrorNotReady) {
+            // (a flush is ~15 us: poll; a partial queue's window may pass meanwhile)
+            if ((++polls & 63) == 0 && q->has_pending.load(std::memory_order_relaxed)) break;
+            std::this_thread::yield();
+        }
+        lock.lock();
+        if (e == hipErrorNotReady) continue;  // (back to check the window)
+        if (e != hipSuccess) q->error = fail(-EIO, "block flush: %s", hipGetErrorString(e));
+        q->inflight.pop_front();
+        q->spare.push_back(f.ev);
+        // (after a dropped partial queue, the last flush also completes its tickets)
+        q->done_upto.store(q->inflight.empty() && q->error ? q->flushed_upto : f.hi, std::memory_order_release);
+        q->cv.notify_all();
+    }
 }
 
 }  // namespace
@@ -152,6 +183,11 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
     q->pend_out.reserve(q->max_blocks);
     DeviceGuard guard(q->device);
     HIP_TRY(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
+    try {
+        q->completer = std::thread(completer_loop, q.get());
+    } catch (...) {
+        return fail(-ENOMEM, "cannot start the queue's completion thread");
+    }
     *out = q.release();
     return 0;
 }
@@ -159,12 +195,17 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
 int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
     if (!q || !dev_out) return fail(-EINVAL, "queue/out == NULL");
     std::lock_guard<std::mutex> lock(q->mu);
-    if (q->pend_payload.empty()) q->first_pending = Clock::now();
+    const bool first = q->pend_payload.empty();
+    if (first) q->first_pending = Clock::now();
     if (ticket) *ticket = q->next_ticket;
     q->next_ticket++;
     q->pend_payload.push_back(dev_payload);
     q->pend_out.push_back(dev_out);
     if (q->pend_payload.size() >= q->max_blocks) return flush_locked(q);
+    if (first) {
+        q->has_pending.store(true, std::memory_order_relaxed);
+        q->work_cv.notify_one();  // (the completer flushes it when the window passes)
+    }
     return 0;
 }
 
@@ -176,6 +217,7 @@ int crc32c_block_flush(crc32c_blocks *q) {
 
 int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
     if (!q) return fail(-EINVAL, "queue == NULL");
+    if (ticket < q->done_upto.load(std::memory_order_acquire)) return q->error;
     std::unique_lock<std::mutex> lock(q->mu);
     if (ticket >= q->next_ticket) return fail(-EINVAL, "ticket %llu was never handed out", (unsigned long long)ticket);
     while (ticket >= q->flushed_upto) {  // still queued: flush when full or when the window has passed
@@ -186,41 +228,15 @@ int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
         }
         q->cv.wait_until(lock, due);
     }
-    if (ticket < q->done_upto.load(std::memory_order_acquire)) return 0;
-    crc32c_blocks::Flush *f = nullptr;
-    for (auto &x : q->inflight)
-        if (ticket < x.hi) {
-            f = &x;
-            break;
-        }
-    if (!f) return 0;  // (reaped: complete)
-    if (!f->watched) {  // this thread watches the flush: the one HIP wait for it
-        f->watched = true;
-        const hipEvent_t ev = f->ev;
-        const uint64_t hi = f->hi;
-        lock.unlock();
-        hipError_t e;
-        {
-            // (polled: hipEventSynchronize's wake-up after a ~15 us launch
-            // was a large part of a flush cycle)
-            DeviceGuard guard(q->device);
-            while ((e = hipEventQuery(ev)) == hipErrorNotReady) std::this_thread::yield();
-        }
-        lock.lock();
-        publish(q, hi);  // (also on failure: the waiters must not hang)
-        q->cv.notify_all();
-        if (e != hipSuccess) return fail(-EIO, "hipEventSynchronize: %s", hipGetErrorString(e));
-        return 0;
-    }
     lock.unlock();
     const Clock::time_point spin_end = Clock::now() + spin_time();
     while (Clock::now() < spin_end) {
-        if (ticket < q->done_upto.load(std::memory_order_acquire)) return 0;
+        if (ticket < q->done_upto.load(std::memory_order_acquire)) return q->error;
         std::this_thread::yield();
     }
     lock.lock();
     q->cv.wait(lock, [&] { return ticket < q->done_upto.load(std::memory_order_acquire); });
-    return 0;
+    return q->error;
 }
 
 int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out) {
@@ -242,8 +258,11 @@ int crc32c_blocks_destroy(crc32c_blocks *q) {
     if (!q) return 0;
     {
         std::lock_guard<std::mutex> lock(q->mu);
-        (void)flush_locked(q);
+        if (q->stream) (void)flush_locked(q);
+        q->stop = true;
+        q->work_cv.notify_all();
     }
+    if (q->completer.joinable()) q->completer.join();  // (returns once every flush completed)
     DeviceGuard guard(q->device);
     if (q->stream) {
         (void)hipStreamSynchronize(q->stream);

@@ -23,6 +23,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <sys/resource.h>
 #include <thread>
 #include <vector>
 
@@ -38,6 +40,25 @@
     } while (0)
 
 using Clock = std::chrono::steady_clock;
+
+// The cgroup's CPU throttling so far (cgroup v2 cpu.stat; -1 if unreadable)
+// and the process's CPU time: a run that spins more threads than the
+// container's CPU quota is throttled, which shows here.
+static long long throttled_usec() {
+    FILE *f = std::fopen("/sys/fs/cgroup/cpu.stat", "r");
+    if (!f) return -1;
+    char key[64];
+    long long v, r = -1;
+    while (std::fscanf(f, "%63s %lld", key, &v) == 2)
+        if (!std::strcmp(key, "throttled_usec")) r = v;
+    std::fclose(f);
+    return r;
+}
+static double cpu_seconds() {
+    rusage u{};
+    getrusage(RUSAGE_SELF, &u);
+    return double(u.ru_utime.tv_sec + u.ru_stime.tv_sec) + 1e-6 * double(u.ru_utime.tv_usec + u.ru_stime.tv_usec);
+}
 
 static double seconds(Clock::time_point a, Clock::time_point b) {
     return std::chrono::duration<double>(b - a).count();
@@ -83,14 +104,20 @@ int main(int argc, char **argv) {
                 body(k);
             });
         while (ready.load() < nthreads) std::this_thread::yield();
+        const long long th0 = throttled_usec();
+        const double c0 = cpu_seconds();
         t0 = Clock::now();
         go = true;
         for (auto &t : th) t.join();
         t1 = Clock::now();
         const double s = seconds(t0, t1);
+        const double cpus = (cpu_seconds() - c0) / s;
+        const long long th1 = throttled_usec();
         const double blocks = double(nthreads) * iters;
-        std::printf("{\"mode\": \"%s\", \"threads\": %d, \"blocks\": %.0f, \"us_per_block\": %.3f, \"gib_s\": %.1f",
-                    mode, nthreads, blocks, s / blocks * 1e6, blocks * kBlock / s / double(1 << 30));
+        std::printf("{\"mode\": \"%s\", \"threads\": %d, \"blocks\": %.0f, \"us_per_block\": %.3f, \"gib_s\": %.1f, "
+                    "\"cpus_busy\": %.2f, \"throttled_us\": %lld",
+                    mode, nthreads, blocks, s / blocks * 1e6, blocks * kBlock / s / double(1 << 30), cpus,
+                    th0 < 0 || th1 < 0 ? -1ll : th1 - th0);
     };
 
     // single: one launch per block

@@ -44,6 +44,7 @@ for s in $STEPS; do
     bsweep) for spin in ${BSPIN:-50 0}; do for mb in ${BMB:-8 16 32}; do for th in ${BTH:-16 32}; do
               run bsw_s${spin}_mb${mb}_t${th} 120 env HDFS_CRC32C_QUEUE_SPIN_US=$spin tools/block_rate $th 300 $mb ${BWIN:-30} 4 1;
             done; done; done ;;
+    cgroup) run cgroup 30 bash -c 'cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat; nproc; cat /proc/self/status | grep -i cpus_allowed_list' ;;
     lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
     stash) for b in ${SB:-basewt stashwt stashB}; do run stash_$b 300 python tools/stash_repro.py $b ${SBPC:-4,7,100,1000,1536}; done ;;
