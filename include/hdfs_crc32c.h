@@ -249,13 +249,15 @@ int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, ui
  * threads without any batching by the caller.  crc32c_block_submit queues a
  * block (its bytes already in device memory) and returns a ticket; the
  * queue goes out as one crc32c_plan_exec_blocks launch on the queue's own
- * stream when it holds max_blocks blocks, on crc32c_block_flush, or when a
- * thread waits for a queued block (crc32c_block_wait) and window_us have
- * passed since the queue's first block (group commit).  crc32c_block_wait
- * returns when the ticket's checksums are in device memory;
+ * stream when it holds max_blocks blocks, on crc32c_block_flush, or when
+ * window_us have passed since the queue's first block (group commit).  The
+ * launches and their completion are made by one worker thread the queue
+ * owns (every HIP call of the queue is on it; crc32c_block_flush only asks
+ * it to launch now).  crc32c_block_wait returns when the ticket's checksums
+ * are in device memory (and complete for any later stream or copy);
  * crc32c_block_checksums is submit + wait.  Thread-safe.  Destroy the queue
- * (it flushes and waits) before its plan.  crc32c_blocks_stats: launches
- * (flushes) made and blocks they carried.
+ * (it launches what is queued and waits) before its plan.
+ * crc32c_blocks_stats: launches (flushes) made and blocks they carried.
  * ------------------------------------------------------------------------- */
 int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
                             size_t nblocks, void *stream);

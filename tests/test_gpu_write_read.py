@@ -766,5 +766,23 @@ def test_block_queue_threads(hdfs, gpu_ctx, orc):
         assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), orc.batch(hosts[i], pk, n))
     with pytest.raises(hdfs.Crc32cError):
         q.wait(10**9)
+    # a partial batch goes out when its window has passed (no flush call)
+    for i in range(3):
+        outs[i].zero_()
+    torch.cuda.synchronize()
+    tickets = [q.submit(devs[i].data_ptr(), outs[i].data_ptr()) for i in range(3)]
+    q.wait(tickets[-1])
+    for i in range(3):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), orc.batch(hosts[i], pk, n))
+    # destroy launches what is still queued and waits for it
+    for i in range(2):
+        outs[i].zero_()
+    torch.cuda.synchronize()
+    q2 = plan.blocks(max_blocks=12, window_us=10**6)
+    for i in range(2):
+        q2.submit(devs[i].data_ptr(), outs[i].data_ptr())
+    q2.close()
+    for i in range(2):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), orc.batch(hosts[i], pk, n))
     q.close()
     plan.close()

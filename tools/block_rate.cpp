@@ -236,6 +236,10 @@ int main(int argc, char **argv) {
     }
 
     // kernel: the GPU's time per block in back-to-back multi-block launches
+    // (kernel: the same nb buffers every launch -- nb x 4 MiB may stay in
+    // the 256 MiB last-level cache; kernel_rotating: consecutive launches
+    // take the next nb of all nbuf buffers, as the queue modes do)
+    for (int rot = 0; rot < 2; ++rot)
     for (uint32_t nb : {1u, 4u, 8u, 16u, 32u}) {
         if (nb > uint32_t(nbuf)) break;
         hipStream_t s = streams[0];
@@ -243,17 +247,24 @@ int main(int argc, char **argv) {
         CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess);
         const void *pays[32];
         uint32_t *os[32];
-        for (uint32_t i = 0; i < nb; ++i) pays[i] = bufs[i], os[i] = outs[i];
-        for (int i = 0; i < 200; ++i) CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s) == 0);
+        const uint32_t groups = rot ? std::max<uint32_t>(1u, uint32_t(nbuf) / nb) : 1u;
+        auto launch = [&](int i) {
+            const uint32_t g0 = (uint32_t(i) % groups) * nb;
+            for (uint32_t k = 0; k < nb; ++k) pays[k] = bufs[g0 + k], os[k] = outs[g0 + k];
+            CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s) == 0);
+        };
+        for (int i = 0; i < 200; ++i) launch(i);
         const int n = 1000;
         CHECK(hipEventRecord(e0, s) == hipSuccess);
-        for (int i = 0; i < n; ++i) CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s) == 0);
+        for (int i = 0; i < n; ++i) launch(i);
         CHECK(hipEventRecord(e1, s) == hipSuccess);
         CHECK(hipStreamSynchronize(s) == hipSuccess);
         float ms = 0;
         CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess);
-        std::printf("{\"mode\": \"kernel\", \"blocks_per_launch\": %u, \"us_per_launch\": %.3f, \"us_per_block\": %.3f}\n",
-                    nb, ms * 1e3 / n, ms * 1e3 / n / nb);
+        std::printf("{\"mode\": \"%s\", \"blocks_per_launch\": %u, \"bytes_rotated\": %llu, \"us_per_launch\": %.3f, "
+                    "\"us_per_block\": %.3f}\n",
+                    rot ? "kernel_rotating" : "kernel", nb, (unsigned long long)groups * nb * kBlock, ms * 1e3 / n,
+                    ms * 1e3 / n / nb);
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
     }

@@ -44,6 +44,10 @@ for s in $STEPS; do
     bsweep) for spin in ${BSPIN:-50 0}; do for mb in ${BMB:-8 16 32}; do for th in ${BTH:-16 32}; do
               run bsw_s${spin}_mb${mb}_t${th} 120 env HDFS_CRC32C_QUEUE_SPIN_US=$spin tools/block_rate $th 300 $mb ${BWIN:-30} 4 1;
             done; done; done ;;
+    btrace) for th in ${BTH:-4 16}; do run btrace_t$th 120 env HDFS_CRC32C_QUEUE_TRACE=gpurun_out/qtrace_t$th.jsonl tools/block_rate $th 300 16 30 4 1; done ;;
+    bpoll) for v in ${BPV:-p1 p5 p20 sync rec}; do
+             case $v in tim) E="HDFS_CRC32C_QUEUE_TIMING=1";; rec) E="HDFS_CRC32C_QUEUE_RECORD=1";; rectim) E="HDFS_CRC32C_QUEUE_RECORD=1 HDFS_CRC32C_QUEUE_TIMING=1";; s*) E="HDFS_CRC32C_QUEUE_SPIN_US=${v#s}";; p*) E="HDFS_CRC32C_QUEUE_POLL_US=${v#p}";; esac
+             run bpoll_$v 120 env $E HDFS_CRC32C_QUEUE_TRACE=gpurun_out/qtrace_$v.jsonl tools/block_rate ${BPT:-16} 300 16 30 4 1; done ;;
     cgroup) run cgroup 30 bash -c 'cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat; nproc; cat /proc/self/status | grep -i cpus_allowed_list' ;;
     lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
