@@ -33,9 +33,9 @@
 //    with DPP / swizzle steps.
 //  * Any other bpc in [4, 8192], and packet tails (general items,
 //    crc32c_general.h): each chunk is right-aligned into k = ceil(bpc / 512)
-//    virtual blocks (leading zeros do not change lin); the register
-//    pre-inversion (crc32c.c:237) is XORed into the chunk's first 4 bytes,
-//    so crc = lin ^ ~0; one wave runs an item's blocks as 16-block subtiles
+//    virtual blocks (leading zeros do not change lin; the bytes before a
+//    chunk in its first block are masked off), crc = lin ^ crc(0, zeros(n))
+//    from a table; one wave runs an item's blocks as 16-block subtiles
 //    (chunks may span two), shifting blocks by Z^(512*s) and gathering a
 //    chunk's blocks with a prefix XOR.
 //  * Tiles off 16-byte alignment (general builds): aligned loads, each

@@ -64,7 +64,6 @@ __device__ __forceinline__ uint64_t low_nibbles(uint32_t n) { return n >= 16 ? ~
 struct GSub {
     uint32_t sfull;   // bit b: block starts a full chunk
     uint32_t start;   // ... or the tail chunk
-    uint32_t second;  // bit b: the block is its chunk's second
     uint32_t tailm;   // bit b: block of the tail chunk
     uint32_t valid;   // bit b: block < nb
     uint32_t before;  // full chunks started before the subtile
@@ -72,7 +71,6 @@ struct GSub {
 };
 struct GState {
     uint32_t before = 0;  // full chunks started in earlier subtiles
-    uint32_t carry = 0;   // 1: the previous subtile's last block started a chunk
     uint32_t phi = 0;     // (16 s) % k
 };
 __device__ __forceinline__ GSub gsub(const GShape &g, uint32_t s, const GState &st) {
@@ -94,13 +92,11 @@ __device__ __forceinline__ GSub gsub(const GShape &g, uint32_t s, const GState &
         const uint64_t pat = e <= 15 ? kDesc >> (4 * (15 - e)) : kDesc << (4 * (e - 15));
         r.dist |= pat & low_nibbles(nv) & ~low_nibbles(nf);
     }
-    r.second = ((r.start << 1) | st.carry) & r.valid & ~r.start;
     r.before = st.before;
     return r;
 }
 __device__ __forceinline__ void gstate_next(const GShape &g, const GSub &gs, GState &st) {
     st.before += __builtin_popcount(gs.sfull);
-    st.carry = (gs.start >> 15) & 1u;
     st.phi += kGPat.mod16[g.k];
     if (st.phi >= g.k) st.phi -= g.k;
 }
@@ -175,14 +171,14 @@ __device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
     return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
 }
 
-// Chunk bytes before position 0 of the lane's dwords -> 0, chunk bytes 0..3
-// ^= 0xff (the register pre-inversion of crc32c.c:237 moved into the data).
-// m = position in the lane's 16 bytes where the chunk starts (may be < 0).
-// Dword j's bytes with index < m - 4 j is M_j = 0xffffffff >> (32 - 8 c),
-// c = clamp(m - 4 j, 0, 4): one 64-bit shift of 0x00000000ffffffff by
-// clamp(32 - 8 (m - 4 j), 0, 32).  Dword k keeps its bytes outside M_k and
-// XORs 0xff into M_{k-1} & ~M_k (the bytes m .. m + 3): ~M_k & (w ^ M_{k-1}),
-// one v_bitop3.
+// (GenItems and SegItems, crc32c_items.h) Chunk bytes before position 0 of
+// the lane's dwords -> 0, chunk bytes 0..3 ^= 0xff (the register
+// pre-inversion of crc32c.c:237 moved into the data).  m = position in the
+// lane's 16 bytes where the chunk starts (may be < 0).  Dword j's bytes with
+// index < m - 4 j is M_j = 0xffffffff >> (32 - 8 c), c = clamp(m - 4 j, 0,
+// 4): one 64-bit shift of 0x00000000ffffffff by clamp(32 - 8 (m - 4 j), 0,
+// 32).  Dword k keeps its bytes outside M_k and XORs 0xff into M_{k-1} &
+// ~M_k (the bytes m .. m + 3): ~M_k & (w ^ M_{k-1}), one v_bitop3.
 __device__ __forceinline__ uint32_t bytes_below(int s) {  // s = 32 - 8 (m - 4 j), any value
     const int c = min(max(s, 0), 32);
     return uint32_t(0xffffffffull >> c);
@@ -194,46 +190,54 @@ __device__ __forceinline__ uint4 chunk_start_mask(uint4 d, int m) {
     return make_uint4(~m0 & (d.x ^ mm1), ~m1 & (d.y ^ m0), ~m2 & (d.z ^ m1), ~m3 & (d.w ^ m2));
 }
 
-// General subtile pieces with the chunk-start masks (bytes before a chunk
-// zeroed, its first 4 bytes ^ 0xff).  The chunk starts at position
-// pad_c - 16 q of lane q's piece of the chunk's first block; its 4
-// pre-inverted bytes reach the second block's lane 0 when pad_c > 508.
-// Unpadded items (bpc = 512 k) only XOR ~0 into lane 0 of each chunk's
-// first block; the two forms are separate loops so that neither waits for
-// all 8 loads before its first lookup.
+// Keep masks of a lane's 16-byte piece whose chunk starts at position m of
+// it (m may be < 0 or > 15): dword j keeps its bytes with index >= m - 4 j,
+// i.e. K_j = ~(0xffffffff >> clamp(32 - 8 (m - 4 j), 0, 32)).  Chunk bytes
+// before position 0 are the zero prefix of the chunk's first virtual block
+// (leading zeros do not change lin; crc = lin ^ crc(0, zeros(n)) for a chunk
+// of n bytes, so no pre-inversion needs to reach the data).
+__device__ __forceinline__ uint32_t keep_from(int s) { return ~bytes_below(s); }
+__device__ __forceinline__ uint4 keep_masks(int m) {
+    const int s = 32 - 8 * m;
+    return make_uint4(keep_from(s), keep_from(s + 32), keep_from(s + 64), keep_from(s + 96));
+}
+// x & (K | ~f) per dword (one v_bitop3 each): the masks apply where f = ~0.
+__device__ __forceinline__ void apply_keep(uint4 &x, const uint4 &k, uint32_t f) {
+    x.x &= k.x | ~f;
+    x.y &= k.y | ~f;
+    x.z &= k.z | ~f;
+    x.w &= k.w | ~f;
+}
+
+// General subtile pieces: the bytes before a chunk's start in its first
+// block are zeroed.  The chunk starts at position pad_c - 16 q of lane q's
+// piece of the chunk's first block; every full chunk has the same pad, so
+// the lane's keep masks kp (keep_masks(pad - 16 q)) are computed once per
+// item and a piece only selects them by its block's start bit (5 VALU).  The
+// tail chunk (at most one start per item) takes its own masks in the piece
+// row that holds its first block (a wave-uniform branch).  Unpadded items
+// (bpc = 512 k, tail a multiple of 512) need nothing.
 template <int DIAG, bool S4, int IMG>
-__device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g, const GSub &gs, uint4 v[8],
-                                            uint32_t pc[8], int lane) {
+__device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g, const GSub &gs, const uint4 &kp,
+                                            uint4 v[8], uint32_t pc[8], int lane) {
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    if (g.pad == 0 && g.padt) {
-        // Only the tail chunk is padded (a power-of-two or 512 k packet with a
-        // short tail): the full chunks take the unpadded XOR, and the
-        // chunk-start mask runs only in the (at most two) piece rows that hold
-        // the tail's first block or the spill into its second.
-        const uint32_t fh = q == 0 ? (gs.start & ~gs.tailm) >> h : 0u;
-        const uint32_t trows = (gs.start | gs.second) & gs.tailm;  // the tail's first / second block
-        const uint32_t th1 = (gs.start & gs.tailm) >> h, th2 = (gs.second & gs.tailm) >> h;
+    const uint32_t tst = g.padt ? gs.start & gs.tailm : 0u;  // the tail's first block (uniform)
+    const uint32_t tsh = tst >> h;
+    const int mt = int(g.padt) - int(16u * q);
+    if (g.pad) {
+        const uint32_t sfh = gs.sfull >> h;
         tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
-            x.x ^= uint32_t(-int32_t((fh >> (2 * i)) & 1u));
-            if ((trows >> (2 * i)) & 3u) {  // (uniform)
-                const bool first = (th1 >> (2 * i)) & 1u, second = (th2 >> (2 * i)) & 1u;
-                const int m = first ? int(g.padt) - int(16u * q) : int(g.padt) - 512 - int(16u * q);
-                x = chunk_start_mask(x, (first || (second && q == 0)) ? m : -64);
-            }
+            apply_keep(x, kp, 0u - ((sfh >> (2 * i)) & 1u));
+            if ((tst >> (2 * i)) & 3u)  // (uniform)
+                apply_keep(x, keep_masks(mt), 0u - ((tsh >> (2 * i)) & 1u));
         });
-    } else if (g.pad) {
-        const uint32_t sth = gs.start >> h, s2h = gs.second >> h, th = gs.tailm >> h;
+    } else if (g.padt) {
+        // Only the tail chunk is padded (a power-of-two or 512 k packet with a short tail).
         tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
-            const int pcl = int(((th >> (2 * i)) & 1u) ? g.padt : g.pad);
-            const bool first = (sth >> (2 * i)) & 1u, second = (s2h >> (2 * i)) & 1u;
-            const int m = first ? pcl - int(16u * q) : pcl - 512 - int(16u * q);
-            // (branch-free: m = -64 leaves the piece as it is)
-            x = chunk_start_mask(x, (first || (second && q == 0)) ? m : -64);
+            if ((tst >> (2 * i)) & 3u) apply_keep(x, keep_masks(mt), 0u - ((tsh >> (2 * i)) & 1u));
         });
     } else {
-        const uint32_t sth = q == 0 ? gs.start >> h : 0u;
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane,
-                                   [&](int i, uint4 &x) { x.x ^= uint32_t(-int32_t((sth >> (2 * i)) & 1u)); });
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
     }
 }
 
@@ -246,8 +250,8 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
 // by Z^(512 dist_b) to its chunk's end; the blocks are permuted into block
 // order and prefix-XORed along 16-lane rows (DPP row_shr), and lane c adds
 // the XOR of its chunk's blocks in the subtile as P[hi - 1] ^ P[lo - 1].
-// After the last subtile lane c holds chunk c's lin; the data carried the
-// pre-inversion, so crc = lin ^ ~0.  Each subtile's loads are issued after
+// After the last subtile lane c holds chunk c's lin, and crc = lin ^
+// crc(0, zeros(n)) for its n bytes.  Each subtile's loads are issued after
 // the previous one's lookups.
 template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
@@ -261,6 +265,11 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     const uint32_t blk = rep_block(lane);
     const uint32_t from = block_lane(uint32_t(lane) & 15u) << 2;
     const uint32_t nsub = (g.nb + 15u) >> 4;
+    // lane c's affine constant crc(0, zeros(n)), n = bpc or tl (scalar loads)
+    typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
+    const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
+    const uint32_t cf = zc[g.bpc], ct = zc[g.tl];
+    const uint4 kp = keep_masks(int(g.pad) - int(16u * (uint32_t(lane) & 31u)));
     GState st;
     uint32_t acc = 0;
     for (uint32_t s = 0; s < nsub; ++s) {
@@ -271,7 +280,7 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         const GSub gs = gsub(g, s, st);
         if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
         uint32_t pc[8];
-        gsub_pieces<DIAG, S4, IMG>(lds, g, gs, v, pc, lane);
+        gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
         uint32_t x = block_lin(pc, lane);
         const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
         const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
@@ -288,7 +297,7 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         if (h1 > l1) acc ^= ph ^ (l1 ? pl : 0u);
         gstate_next(g, gs, st);
     }
-    if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ 0xffffffffu, ev);
+    if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ (c < g.nch ? cf : ct), ev);
 }
 
 }  // namespace hdfs_crc_dev

@@ -797,6 +797,7 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
         std::vector<uint8_t> img4(kTableAllocS4Full, 0);
         build_lds_image_s4(img4.data(), poly);
         compact_s4_image(img4.data(), img4.data() + kS4COff);  // small batches
+        zero_crc_table(reinterpret_cast<uint32_t *>(img4.data() + kZeroCrcOff), poly);  // general items
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&c->d_table_s4[ty]), kTableAllocS4Full));
         HIP_TRY(hipMemcpy(c->d_table_s4[ty], img4.data(), kTableAllocS4Full, hipMemcpyHostToDevice));
     }

@@ -175,4 +175,13 @@ void affine_constants(uint32_t c_lg[5], uint32_t c_small[4], uint32_t poly) {
     for (int r = 0; r < 4; ++r) c_small[r] = op_zeros(r, poly).apply(0xffffffffu) ^ 0xffffffffu;
 }
 
+void zero_crc_table(uint32_t *dst, uint32_t poly) {
+    // register ~0 (crc32c.c:237) through n zero bytes, ^ ~0 (crc32c.c:312)
+    uint32_t reg = 0xffffffffu;
+    for (uint32_t n = 0; n <= kZeroCrcMax; ++n) {
+        dst[n] = reg ^ 0xffffffffu;
+        reg = append_zero_byte(reg, poly);
+    }
+}
+
 }  // namespace hdfs_crc

@@ -91,4 +91,10 @@ uint32_t s4_step(uint32_t u, uint32_t poly = kPoly);
 // crc(0, zeros(512 << lg)) for lg = 0..4 and crc(0, zeros(r)) for r = 0..3.
 void affine_constants(uint32_t c_lg[5], uint32_t c_small[4], uint32_t poly = kPoly);
 
+// crc(0, zeros(n)) for n = 0 .. kZeroCrcMax: the affine constant of a chunk
+// of n bytes (crc(0, M) = lin(M) ^ crc(0, zeros(n))), which general items
+// add per chunk instead of folding the pre-inversion into the data.
+constexpr uint32_t kZeroCrcMax = 8192;
+void zero_crc_table(uint32_t *dst, uint32_t poly = kPoly);  // kZeroCrcMax + 1 entries
+
 }  // namespace hdfs_crc

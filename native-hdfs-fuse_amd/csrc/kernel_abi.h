@@ -18,7 +18,10 @@ constexpr uint32_t kTableAllocS4 = ((uint32_t(kS4Bytes) + 16384 - 1) / 16384) * 
 // kS4C*), padded to whole 1 KiB staging pieces.
 constexpr uint32_t kS4COff = kTableAllocS4;
 constexpr uint32_t kTableAllocS4C = ((uint32_t(kS4CBytes) + 16384 - 1) / 16384) * 16384;
-constexpr uint32_t kTableAllocS4Full = kS4COff + kTableAllocS4C;
+// After it (at kZeroCrcOff): crc(0, zeros(n)) for n = 0 .. kZeroCrcMax
+// (crc_math.h zero_crc_table), read by general items with scalar loads.
+constexpr uint32_t kZeroCrcOff = kS4COff + kTableAllocS4C;
+constexpr uint32_t kTableAllocS4Full = kZeroCrcOff + ((4 * (kZeroCrcMax + 1) + 16384 - 1) / 16384) * 16384;
 
 // One block of a multi-block launch (crc32c_plan_exec_blocks): the plan's
 // work items describe one block's shape; block b's copy of item i reads at

@@ -315,8 +315,10 @@ def test_kernel_model_general_chunks(orc, model):
 @pytest.mark.parametrize("bpc", [4, 5, 100, 511, 513, 1000, 1536, 2560, 4000, 7680, 8191])
 def test_kernel_model_general_tiles(hdfs, orc, bpc):
     """General tiles: each chunk right-aligned into k = ceil(bpc / 512)
-    virtual blocks, 0xff folded into its first 4 bytes, block b shifted by
-    Z^(512 (k - 1 - b)) from the S4 image's shift section, XORed, ^ ~0."""
+    virtual blocks (zero prefix, no pre-inversion in the data), block b
+    shifted by Z^(512 (k - 1 - b)) from the S4 image's shift section, XORed,
+    ^ crc(0, zeros(bpc)) -- the affine constant the kernel reads from the
+    zero-crc table (crc_math.h zero_crc_table)."""
     m4 = KernelModelS4(hdfs.debug_lds_image_s4())
     img, c_lg, c_small = hdfs.debug_lds_image()
     zm = KernelModel(img, c_lg, c_small)
@@ -324,17 +326,17 @@ def test_kernel_model_general_tiles(hdfs, orc, bpc):
     pad = k * 512 - bpc
     data = oracle.xorshift64_bytes(bpc * 5, bpc)
     data[:bpc] = 0
+    zero_crc = orc.crc32c(np.zeros(bpc, np.uint8))
     got = []
     for c in range(5):
         v = np.zeros(k * 512, np.uint8)
         v[pad:] = data[c * bpc:(c + 1) * bpc]
-        v[pad:pad + 4] ^= 0xFF
         lins = m4.block_lin(v.reshape(k, 512))
         x = 0
         for j in range(k):
             s = k - 1 - j
             x ^= zm.zshift(s, int(lins[j])) if s else int(lins[j])
-        got.append(x ^ 0xFFFFFFFF)
+        got.append(x ^ zero_crc)
     assert np.array_equal(np.array(got, np.uint32), orc.chunks(data, bpc))
 
 

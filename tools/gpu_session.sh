@@ -48,6 +48,10 @@ for s in $STEPS; do
     bpoll) for v in ${BPV:-p1 p5 p20 sync rec}; do
              case $v in tim) E="HDFS_CRC32C_QUEUE_TIMING=1";; rec) E="HDFS_CRC32C_QUEUE_RECORD=1";; rectim) E="HDFS_CRC32C_QUEUE_RECORD=1 HDFS_CRC32C_QUEUE_TIMING=1";; s*) E="HDFS_CRC32C_QUEUE_SPIN_US=${v#s}";; p*) E="HDFS_CRC32C_QUEUE_POLL_US=${v#p}";; esac
              run bpoll_$v 120 env $E HDFS_CRC32C_QUEUE_TRACE=gpurun_out/qtrace_$v.jsonl tools/block_rate ${BPT:-16} 300 16 30 4 1; done ;;
+    abwt) for c in ${ABCFGS:-c2b1000 c2b1536}; do
+            run abwt_base_$c 600 bash -c "cd scratch/wt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
+            run abwt_head_$c 600 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}; done ;;
+    qsum) run qsum 60 bash -c 'for f in gpurun_out/qtrace_*.jsonl; do echo "$f"; python tools/qtrace_summary.py "$f"; done' ;;
     cgroup) run cgroup 30 bash -c 'cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat; nproc; cat /proc/self/status | grep -i cpus_allowed_list' ;;
     lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
