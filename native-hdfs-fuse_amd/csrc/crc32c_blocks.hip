@@ -6,7 +6,7 @@
 // block per call, hadoop_rpc_send_packets cuts it into packets,
 // hadooprpc.c:815-860).  One launch per 4 MiB block is bound by HIP's launch
 // path (~3.5-4 us per block), while one launch over 16
-// blocks takes ~1.0 us per block from HBM.  A crc32c_blocks queue collects
+// blocks takes ~0.9 us per block from HBM.  A crc32c_blocks queue collects
 // the blocks several threads submit within a short window and sends them
 // out as ONE multi-block launch of the block's plan
 // (crc32c_plan_exec_blocks: the block table rides in the kernel arguments,
@@ -14,16 +14,18 @@
 //
 // One worker thread per queue makes every HIP call of the queue: it
 // launches a batch when it holds max_blocks blocks, on crc32c_block_flush,
-// or when window_us have passed since its first block (group commit), and
-// completes the launches in order by polling their events (a flush's event
-// is its last launch's own stop event, hipExtLaunchKernel).  Submitting and
-// waiting threads only touch the queue's lock and its done_upto counter
-// (waiters spin on it briefly, then sleep on a condition variable).
-// Round 3 first launched from the submitting threads and had every waiter
-// -- then one watcher per flush, then one poller -- query events: HIP's
-// launch path and its event queries contend, and with two or three flushes
-// outstanding a launch call took ~27 us instead of ~5 (tools/block_rate,
-// HDFS_CRC32C_QUEUE_TRACE).
+// or when window_us have passed since it saw the batch's first block (group
+// commit), and completes the launches in order by polling their events (a
+// flush's event is its last launch's own stop event, hipExtLaunchKernel).
+//
+// Submitting and waiting threads take no lock on the fast path: a ticket is
+// one atomic add, the block goes into the ring slot of its ticket, published
+// by the slot's sequence word; waiters spin on the completed-ticket counter
+// and only sleep (condition variable) after spin_time.  Round 3's first
+// queue kept the pending blocks under one mutex: 16 threads resubmitting
+// after a flush queued on it (a futex hand-off each), and a batch took ~40
+// us to fill against ~15 us of GPU time per flush (HDFS_CRC32C_QUEUE_TRACE,
+// DESIGN.md section 5).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,39 +47,48 @@
 using namespace hdfs_crc;
 using Clock = std::chrono::steady_clock;
 
+namespace {
+struct alignas(64) Slot {
+    std::atomic<uint64_t> seq{0};  // ticket + 1 once payload/out hold ticket's block
+    const void *payload = nullptr;
+    uint32_t *out = nullptr;
+};
+}  // namespace
+
 struct crc32c_blocks {
     crc32c_plan *plan = nullptr;
     int device = 0;
     uint32_t max_blocks = 16;
     std::chrono::microseconds window{20};
     hipStream_t stream = nullptr;
-    std::mutex mu;
+    // the ring: ticket t's block in slots[t & mask] (reusable once t is launched)
+    std::unique_ptr<Slot[]> slots;
+    uint64_t mask = 0;
+    alignas(64) std::atomic<uint64_t> next_ticket{0};   // tickets handed out
+    alignas(64) std::atomic<uint64_t> launched_upto{0}; // tickets below this are in a launch
+    alignas(64) std::atomic<uint64_t> done_upto{0};     // tickets below this are complete
+    alignas(64) std::atomic<uint64_t> flush_upto{0};    // crc32c_block_flush: launch tickets below this now
+    std::atomic<bool> stop{false};
+    std::atomic<bool> worker_sleeping{false};
+    std::atomic<int> sleepers{0};  // waiters asleep on cv
+    std::atomic<int> error{0};     // a failed flush or event: every later wait returns it
+    std::mutex mu;                  // only for the two condition variables
     std::condition_variable cv;       // waiters: done_upto moved
-    std::condition_variable work_cv;  // worker: a batch is due, or stop
-    std::vector<const void *> pend_payload;
-    std::vector<uint32_t *> pend_out;
-    Clock::time_point first_pending;
-    uint64_t next_ticket = 0;            // tickets handed out
-    std::atomic<uint64_t> done_upto{0};  // tickets below this are complete
-    std::atomic<bool> due{false};        // a batch is full or a flush was asked for
-    bool flush_req = false;
-    bool stop = false;
-    bool worker_sleeping = false;
+    std::condition_variable work_cv;  // worker: a ticket was handed out, or stop
     struct Flush {
         uint64_t hi;  // tickets below hi
         hipEvent_t ev;
         size_t trace_idx;
     };
-    std::deque<Flush> inflight;  // worker only
+    std::deque<Flush> inflight;     // worker only
     std::vector<hipEvent_t> spare;  // worker only
-    uint64_t flushes = 0, blocks = 0;
-    std::atomic<int> error{0};  // a failed flush or event: every later wait returns it
+    std::atomic<uint64_t> flushes{0}, blocks{0};
     bool record_events = false;  // A/B (HDFS_CRC32C_QUEUE_RECORD=1): an hipEventRecord after each flush
     unsigned event_flags = hipEventDisableTiming;  // A/B (HDFS_CRC32C_QUEUE_TIMING=1: timing events)
     std::thread worker;
     // Diagnostic (HDFS_CRC32C_QUEUE_TRACE=<file>): per flush, steady-clock
-    // ns of its first submit, issue start / end, completion seen; written
-    // as JSON lines at destroy.
+    // ns of its first block seen by the worker, issue start / end,
+    // completion seen; written as JSON lines at destroy.
     struct TraceRec {
         int64_t first, issue0, issue1, done;
         uint32_t nblocks, inflight_before;
@@ -97,37 +108,54 @@ std::chrono::microseconds spin_time() {
     static const std::chrono::microseconds t = env_us("HDFS_CRC32C_QUEUE_SPIN_US", 50);
     return t;
 }
-// The worker's time between event polls (HDFS_CRC32C_QUEUE_POLL_US: A/B).
-std::chrono::microseconds poll_gap() {
-    static const std::chrono::microseconds t = env_us("HDFS_CRC32C_QUEUE_POLL_US", 2);
+// The worker spins this long with nothing queued or in flight before it
+// sleeps (HDFS_CRC32C_QUEUE_IDLE_US: A/B).
+std::chrono::microseconds idle_spin() {
+    static const std::chrono::microseconds t = env_us("HDFS_CRC32C_QUEUE_IDLE_US", 200);
     return t;
+}
+
+// Launches the worker keeps in flight at most (HDFS_CRC32C_QUEUE_INFLIGHT:
+// A/B).  Two keep the GPU busy (one running, one queued behind it); with
+// three to six queued, HIP's launch call itself slowed from ~4 to 16-20 us
+// (tools/block_rate depth 4, HDFS_CRC32C_QUEUE_TRACE), so blocks wait in the
+// ring instead and go out in fuller launches.
+size_t max_inflight() {
+    static const size_t n = [] {
+        const char *e = std::getenv("HDFS_CRC32C_QUEUE_INFLIGHT");
+        const int v = e ? std::atoi(e) : 2;
+        return size_t(v > 0 ? v : 2);
+    }();
+    return n;
 }
 
 int64_t ns(Clock::time_point t) {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count();
 }
 
-// Launches the batch (worker thread; `lock` held on entry and exit, released
-// around the launch).
-void launch_batch(crc32c_blocks *q, std::unique_lock<std::mutex> &lock, std::vector<const void *> &pays,
-                  std::vector<uint32_t *> &outs) {
-    // (at most max_blocks: blocks submitted while the worker was busy wait
-    // for the next launch)
-    const size_t n = std::min<size_t>(q->pend_payload.size(), q->max_blocks);
-    pays.assign(q->pend_payload.begin(), q->pend_payload.begin() + n);
-    outs.assign(q->pend_out.begin(), q->pend_out.begin() + n);
-    q->pend_payload.erase(q->pend_payload.begin(), q->pend_payload.begin() + n);
-    q->pend_out.erase(q->pend_out.begin(), q->pend_out.begin() + n);
-    const uint64_t hi = q->next_ticket - q->pend_payload.size();
-    const int64_t first = ns(q->first_pending);
-    if (q->pend_payload.empty()) {
-        q->flush_req = false;
-        q->due.store(false, std::memory_order_relaxed);
-    } else {
-        q->first_pending = Clock::now();
-        q->due.store(q->flush_req || q->pend_payload.size() >= q->max_blocks, std::memory_order_relaxed);
+void relax() {
+    for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+}
+
+// Tickets from `from` whose blocks are published, contiguous, at most `cap`.
+uint32_t ready_from(const crc32c_blocks *q, uint64_t from, uint32_t cap) {
+    uint32_t n = 0;
+    while (n < cap && q->slots[(from + n) & q->mask].seq.load(std::memory_order_acquire) == from + n + 1) ++n;
+    return n;
+}
+
+// Launches tickets [from, from + n) (worker).
+void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point first,
+                  std::vector<const void *> &pays, std::vector<uint32_t *> &outs) {
+    pays.resize(n);
+    outs.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const Slot &s = q->slots[(from + i) & q->mask];
+        pays[i] = s.payload;
+        outs[i] = s.out;
     }
-    lock.unlock();
+    // (the kernel arguments hold copies: the slots may be reused from here)
+    q->launched_upto.store(from + n, std::memory_order_release);
     hipEvent_t ev = nullptr;
     if (!q->spare.empty()) {
         ev = q->spare.back();
@@ -141,28 +169,35 @@ void launch_batch(crc32c_blocks *q, std::unique_lock<std::mutex> &lock, std::vec
     const Clock::time_point issue0 = Clock::now();
     // the flush's event is the last launch's own stop event
     if (!rc)
-        rc = q->record_events ? crc32c_plan_exec_blocks(q->plan, pays.data(), outs.data(), pays.size(), q->stream)
-                              : exec_blocks(q->plan, pays.data(), outs.data(), pays.size(), q->stream, ev);
+        rc = q->record_events ? crc32c_plan_exec_blocks(q->plan, pays.data(), outs.data(), n, q->stream)
+                              : exec_blocks(q->plan, pays.data(), outs.data(), n, q->stream, ev);
     if (!rc && q->record_events && hipEventRecord(ev, q->stream) != hipSuccess) rc = fail(-EIO, "hipEventRecord failed");
     const Clock::time_point issue1 = Clock::now();
     size_t tidx = SIZE_MAX;
     if (!q->trace_path.empty()) {
         tidx = q->trace.size();
-        q->trace.push_back({first, ns(issue0), ns(issue1), 0, uint32_t(pays.size()), uint32_t(q->inflight.size())});
+        q->trace.push_back({ns(first), ns(issue0), ns(issue1), 0, n, uint32_t(q->inflight.size())});
     }
-    lock.lock();
-    q->flushes++;
-    q->blocks += pays.size();
+    q->flushes.fetch_add(1, std::memory_order_relaxed);
+    q->blocks.fetch_add(n, std::memory_order_relaxed);
     if (rc) {  // nothing to wait for: its tickets complete (with the error) once those before them have
         q->error = rc;
         if (ev) q->spare.push_back(ev);
         ev = nullptr;
     }
-    q->inflight.push_back({hi, ev, tidx});
+    q->inflight.push_back({from + n, ev, tidx});
 }
 
-// Completes the front flush if its event has (worker; lock NOT held).
-// Returns true when it did.
+// Publishes done_upto = hi, waking sleeping waiters (worker).
+void complete_upto(crc32c_blocks *q, uint64_t hi) {
+    q->done_upto.store(hi, std::memory_order_seq_cst);
+    if (q->sleepers.load(std::memory_order_seq_cst) > 0) {
+        { std::lock_guard<std::mutex> lock(q->mu); }
+        q->cv.notify_all();
+    }
+}
+
+// Completes the front flush if its event has (worker).  Returns true when it did.
 bool complete_front(crc32c_blocks *q) {
     const crc32c_blocks::Flush f = q->inflight.front();
     if (f.ev) {
@@ -173,11 +208,7 @@ bool complete_front(crc32c_blocks *q) {
     }
     q->inflight.pop_front();
     if (f.trace_idx != SIZE_MAX) q->trace[f.trace_idx].done = ns(Clock::now());
-    {
-        std::lock_guard<std::mutex> lock(q->mu);
-        q->done_upto.store(f.hi, std::memory_order_release);
-    }
-    q->cv.notify_all();
+    complete_upto(q, f.hi);
     return true;
 }
 
@@ -187,40 +218,57 @@ void worker_loop(crc32c_blocks *q) {
     std::vector<uint32_t *> outs;
     pays.reserve(q->max_blocks);
     outs.reserve(q->max_blocks);
-    std::unique_lock<std::mutex> lock(q->mu);
+    uint64_t launched = 0;
+    bool have_first = false;  // a ready block seen since the last launch
+    Clock::time_point first, idle_since = Clock::now();
     for (;;) {
-        const bool pending = !q->pend_payload.empty();
-        if (pending && (q->pend_payload.size() >= q->max_blocks || q->flush_req || q->stop ||
-                        Clock::now() >= q->first_pending + q->window)) {
-            launch_batch(q, lock, pays, outs);
+        const uint32_t n = q->inflight.size() < max_inflight() ? ready_from(q, launched, q->max_blocks) : 0u;
+        if (n) {
+            const Clock::time_point now = Clock::now();
+            if (!have_first) first = now, have_first = true;
+            const bool stopping = q->stop.load(std::memory_order_acquire);
+            if (n >= q->max_blocks || q->flush_upto.load(std::memory_order_acquire) > launched || stopping ||
+                now >= first + q->window) {
+                launch_batch(q, launched, n, first, pays, outs);
+                launched += n;
+                have_first = false;
+                idle_since = Clock::now();
+                continue;
+            }
+        }
+        if (!q->inflight.empty()) {
+            if (complete_front(q)) idle_since = Clock::now();
+            else relax();
             continue;
         }
-        if (q->inflight.empty()) {
-            if (q->stop) return;
-            q->worker_sleeping = true;
-            if (pending)
-                q->work_cv.wait_until(lock, q->first_pending + q->window);
-            else
-                q->work_cv.wait(lock);
-            q->worker_sleeping = false;
+        if (q->next_ticket.load(std::memory_order_acquire) != launched) {  // a submit in progress, or a window open
+            relax();
             continue;
         }
-        // a flush in flight: poll it (no lock held), watching for a due batch
-        lock.unlock();
-        while (!complete_front(q)) {
-            const Clock::time_point until = Clock::now() + poll_gap();
-            while (Clock::now() < until && !q->due.load(std::memory_order_relaxed)) __builtin_ia32_pause();
-            if (q->due.load(std::memory_order_relaxed)) break;
-            if (pending) break;  // (re-check the window)
+        if (q->stop.load(std::memory_order_acquire)) return;
+        if (Clock::now() < idle_since + idle_spin()) {
+            relax();
+            continue;
         }
-        lock.lock();
+        // idle: sleep until a ticket is handed out (Dekker with crc32c_block_submit)
+        q->worker_sleeping.store(true, std::memory_order_seq_cst);
+        {
+            std::unique_lock<std::mutex> lock(q->mu);
+            q->work_cv.wait(lock, [&] {
+                return q->next_ticket.load(std::memory_order_seq_cst) != launched ||
+                       q->stop.load(std::memory_order_seq_cst);
+            });
+        }
+        q->worker_sleeping.store(false, std::memory_order_relaxed);
+        idle_since = Clock::now();
     }
 }
 
-// Caller holds q->mu: wakes the worker for a due batch.
-void mark_due(crc32c_blocks *q) {
-    q->due.store(true, std::memory_order_relaxed);
-    if (q->worker_sleeping) q->work_cv.notify_one();
+void wake_worker(crc32c_blocks *q) {
+    if (q->worker_sleeping.load(std::memory_order_seq_cst)) {
+        { std::lock_guard<std::mutex> lock(q->mu); }
+        q->work_cv.notify_one();
+    }
 }
 
 }  // namespace
@@ -235,6 +283,10 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
     q->device = plan->ctx->device;
     q->max_blocks = max_blocks ? std::min<uint32_t>(max_blocks, 1024u) : 16u;
     q->window = std::chrono::microseconds(window_us);
+    uint64_t cap = 1024;
+    while (cap < 4ull * q->max_blocks) cap <<= 1;
+    q->slots.reset(new Slot[cap]);
+    q->mask = cap - 1;
     if (const char *tp = std::getenv("HDFS_CRC32C_QUEUE_TRACE")) {
         q->trace_path = tp;
         q->trace.reserve(1 << 16);
@@ -243,8 +295,6 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
     q->record_events = rec && rec[0] == '1';
     const char *tim = std::getenv("HDFS_CRC32C_QUEUE_TIMING");
     if (tim && tim[0] == '1') q->event_flags = hipEventDefault;
-    q->pend_payload.reserve(q->max_blocks);
-    q->pend_out.reserve(q->max_blocks);
     DeviceGuard guard(q->device);
     HIP_TRY(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
     try {
@@ -258,46 +308,49 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
 
 int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
     if (!q || !dev_out) return fail(-EINVAL, "queue/out == NULL");
-    std::lock_guard<std::mutex> lock(q->mu);
-    if (q->stop) return fail(-EINVAL, "queue is being destroyed");
-    const bool first = q->pend_payload.empty();
-    if (first) q->first_pending = Clock::now();
-    if (ticket) *ticket = q->next_ticket;
-    q->next_ticket++;
-    q->pend_payload.push_back(dev_payload);
-    q->pend_out.push_back(dev_out);
-    if (q->pend_payload.size() >= q->max_blocks)
-        mark_due(q);
-    else if (first && q->worker_sleeping)
-        q->work_cv.notify_one();  // (it flushes the batch when the window passes)
+    if (q->stop.load(std::memory_order_relaxed)) return fail(-EINVAL, "queue is being destroyed");
+    const uint64_t t = q->next_ticket.fetch_add(1, std::memory_order_seq_cst);
+    // the ring is full only with mask + 1 blocks queued and none launched yet
+    while (t - q->launched_upto.load(std::memory_order_acquire) > q->mask) std::this_thread::yield();
+    Slot &s = q->slots[t & q->mask];
+    s.payload = dev_payload;
+    s.out = dev_out;
+    s.seq.store(t + 1, std::memory_order_release);
+    if (ticket) *ticket = t;
+    wake_worker(q);
     return 0;
 }
 
 int crc32c_block_flush(crc32c_blocks *q) {
     if (!q) return fail(-EINVAL, "queue == NULL");
-    std::lock_guard<std::mutex> lock(q->mu);
-    if (!q->pend_payload.empty()) {
-        q->flush_req = true;
-        mark_due(q);
+    const uint64_t hi = q->next_ticket.load(std::memory_order_acquire);
+    uint64_t cur = q->flush_upto.load(std::memory_order_relaxed);
+    while (cur < hi && !q->flush_upto.compare_exchange_weak(cur, hi, std::memory_order_acq_rel)) {
     }
+    wake_worker(q);
     return 0;
 }
 
 int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
     if (!q) return fail(-EINVAL, "queue == NULL");
     if (ticket < q->done_upto.load(std::memory_order_acquire)) return q->error;
-    {
-        std::lock_guard<std::mutex> lock(q->mu);
-        if (ticket >= q->next_ticket)
-            return fail(-EINVAL, "ticket %llu was never handed out", (unsigned long long)ticket);
-    }
+    if (ticket >= q->next_ticket.load(std::memory_order_acquire))
+        return fail(-EINVAL, "ticket %llu was never handed out", (unsigned long long)ticket);
     const Clock::time_point spin_end = Clock::now() + spin_time();
-    while (Clock::now() < spin_end) {
+    for (int i = 0;; ++i) {
         if (ticket < q->done_upto.load(std::memory_order_acquire)) return q->error;
-        std::this_thread::yield();
+        if ((i & 63) == 63 && Clock::now() >= spin_end) break;
+        if ((i & 7) == 7)
+            std::this_thread::yield();
+        else
+            relax();
     }
-    std::unique_lock<std::mutex> lock(q->mu);
-    q->cv.wait(lock, [&] { return ticket < q->done_upto.load(std::memory_order_acquire); });
+    q->sleepers.fetch_add(1, std::memory_order_seq_cst);
+    {
+        std::unique_lock<std::mutex> lock(q->mu);
+        q->cv.wait(lock, [&] { return ticket < q->done_upto.load(std::memory_order_seq_cst); });
+    }
+    q->sleepers.fetch_sub(1, std::memory_order_relaxed);
     return q->error;
 }
 
@@ -309,20 +362,19 @@ int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *
 
 int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blocks) {
     if (!q) return fail(-EINVAL, "queue == NULL");
-    crc32c_blocks *m = const_cast<crc32c_blocks *>(q);
-    std::lock_guard<std::mutex> lock(m->mu);
-    if (flushes) *flushes = q->flushes;
-    if (blocks) *blocks = q->blocks;
+    if (flushes) *flushes = q->flushes.load(std::memory_order_relaxed);
+    if (blocks) *blocks = q->blocks.load(std::memory_order_relaxed);
     return 0;
 }
 
 int crc32c_blocks_destroy(crc32c_blocks *q) {
     if (!q) return 0;
+    // (the worker launches what is queued, completes everything, returns)
+    q->stop.store(true, std::memory_order_seq_cst);
     {
         std::lock_guard<std::mutex> lock(q->mu);
-        q->stop = true;  // (the worker launches what is queued, completes everything, returns)
-        mark_due(q);
     }
+    q->work_cv.notify_one();
     if (q->worker.joinable()) q->worker.join();
     DeviceGuard guard(q->device);
     if (q->stream) {

@@ -235,6 +235,41 @@ int main(int argc, char **argv) {
         (void)hipEventDestroy(ev);
     }
 
+    // pipelined: one thread keeps `depth` multi-block launches in flight on
+    // one stream, each followed by an event it polls (hipEventQuery), and
+    // launches the next batch when the oldest completes -- the queue
+    // worker's loop without any other thread: the rate a single issuing
+    // thread can sustain against the GPU's.
+    for (int depth : {1, 2, 3}) {
+        const uint32_t nb = std::min<uint32_t>(max_blocks, 32u);
+        const uint32_t groups = std::max<uint32_t>(1u, uint32_t(nbuf) / nb);
+        hipStream_t s = streams[0];
+        std::vector<hipEvent_t> evs(depth);
+        for (auto &e : evs) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess);
+        const void *pays[32];
+        uint32_t *os[32];
+        int issued = 0, done = 0;
+        auto launch = [&] {
+            const uint32_t g0 = (uint32_t(issued) % groups) * nb;
+            for (uint32_t k = 0; k < nb; ++k) pays[k] = bufs[g0 + k], os[k] = outs[g0 + k];
+            CHECK(crc32c_plan_exec_blocks(plan, pays, os, nb, s) == 0);
+            CHECK(hipEventRecord(evs[issued % depth], s) == hipSuccess);
+            issued++;
+        };
+        const int total = 1500, skip = 200;
+        Clock::time_point t0 = Clock::now();
+        while (done < total) {
+            while (issued < total && issued - done < depth) launch();
+            while (hipEventQuery(evs[done % depth]) == hipErrorNotReady) __builtin_ia32_pause();
+            if (++done == skip) t0 = Clock::now();
+        }
+        const double sec = seconds(t0, Clock::now());
+        std::printf("{\"mode\": \"pipelined\", \"depth\": %d, \"blocks_per_launch\": %u, \"us_per_launch\": %.3f, "
+                    "\"us_per_block\": %.3f}\n",
+                    depth, nb, sec / (total - skip) * 1e6, sec / (total - skip) / nb * 1e6);
+        for (auto &e : evs) (void)hipEventDestroy(e);
+    }
+
     // kernel: the GPU's time per block in back-to-back multi-block launches
     // (kernel: the same nb buffers every launch -- nb x 4 MiB may stay in
     // the 256 MiB last-level cache; kernel_rotating: consecutive launches

@@ -52,6 +52,10 @@ for s in $STEPS; do
             run abwt_base_$c 600 bash -c "cd scratch/wt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
             run abwt_head_$c 600 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}; done ;;
     qsum) run qsum 60 bash -c 'for f in gpurun_out/qtrace_*.jsonl; do echo "$f"; python tools/qtrace_summary.py "$f"; done' ;;
+    bq) run bq_t16_mb16 300 tools/block_rate 16 400 16 30 4 0 &&
+        run bq_t16_mb32 200 tools/block_rate 16 300 32 30 4 1 &&
+        run bq_t32_mb16 200 tools/block_rate 32 300 16 30 2 1 &&
+        run bq_t32_mb32 200 tools/block_rate 32 300 32 30 2 1 ;;
     cgroup) run cgroup 30 bash -c 'cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat; nproc; cat /proc/self/status | grep -i cpus_allowed_list' ;;
     lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
