@@ -51,7 +51,7 @@
 //    of zero fill only (ConstRun) are written from plan-time constants.
 //  * Verification (crc32c_plan_verify): the same kernel compares instead of
 //    storing; the expected values are fetched with the tile and the last
-//    workgroup publishes the launch's result (sharded ticket reduction).
+//    workgroup 0 initialises the result; only mismatching workgroups add to it.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -67,10 +67,7 @@ using hdfs_crc::GenPiece;
 using hdfs_crc::KParams;
 using hdfs_crc::SegItem;
 using hdfs_crc::kGeneralTile;
-using hdfs_crc::kShardWord;
-using hdfs_crc::kTicketShards;
-using hdfs_crc::kTicketWord;
-using hdfs_crc::kVFirstWord;
+using hdfs_crc::kEpochWord;
 
 constexpr uint32_t kLdsBytes = hdfs_crc::kKernelLdsBytes;
 constexpr uint32_t kShiftOff = hdfs_crc::kKernelShiftOff;
@@ -310,69 +307,55 @@ __device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t 
     }
 }
 
-// ---- launch-wide verification state (kernel_abi.h slots) -----------------
-// End of a verification launch, the workgroup that took the last global
-// ticket, after publishing the result: every other workgroup has made its
-// last access to the slot (its shard ticket, and its first-bad update before
-// that), so the slot goes back to {0, ~0, 0} for the next launch -- which
-// runs after this one (a plan's verify launches are kept in GPU order).
-// (Round 2 reset the other slot of a pair at the START of a launch, on
-// workgroup 0's critical path: its staging wait also waited for those ten
-// atomics, so workgroup 0 -- and a small batch's whole launch -- started
-// its tiles late.)  Non-returning: nothing waits for these stores but the
-// end of the kernel.
-__device__ __forceinline__ void reset_slot(uint32_t *s) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(s + kTicketWord), 0ull, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(s + kVFirstWord, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (uint32_t i = 0; i < kTicketShards; ++i)
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(s + kShardWord + 32 * i), 0ull, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-}
-
+// ---- launch-wide verification result (kernel_abi.h slots) ----------------
 // Waits until every vector-memory operation of the wave has completed; for a
 // returning device-scope atomic that means it has been performed.
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// A ticket word: tickets taken in bits 40-63, mismatches counted in 0-39.
-constexpr unsigned long long kTicket = 1ull << 40;
-constexpr unsigned long long kCountMask = kTicket - 1;
+// The queue's dispatch id of this launch (the AQL packet index; LLVM has the
+// intrinsic, clang no builtin for it).
+extern "C" __device__ uint64_t llvm_amdgcn_dispatch_id() __asm("llvm.amdgcn.dispatch.id");
 
-// End of a verification launch, thread 0 of every workgroup: take a ticket
-// in its shard that also adds the workgroup's mismatch count (one 64-bit
-// atomic); the last of a shard adds the shard's total to the global ticket
-// word the same way, and the last of those publishes the totals to
-// p.result[0..1] (no host-side reset of the result is needed).  The first-bad
-// index is lowered (and completed) before the ticket, and only read back when
-// something mismatched, so a clean launch's critical tail is two atomics.
-// Every word of the slot is only ever touched by device-scope atomics, which
-// are performed in one place, so ordering needs only completion waits, no
-// cache fences (a __threadfence() is an L2 writeback + invalidate, ~3.5 us
-// on the launch's critical tail).
+// A key unique to this launch (graph replays included): the address of its
+// dispatch packet in the queue's ring and the queue's dispatch id, mixed.
+__device__ __forceinline__ uint64_t launch_key() {
+    const uint64_t ptr = uint64_t(reinterpret_cast<uintptr_t>(__builtin_amdgcn_dispatch_ptr()));
+    return ptr + llvm_amdgcn_dispatch_id() * 0x9E3779B97F4A7C15ull;
+}
+
+// Start of a verification launch, one lane of workgroup 0 (dispatched
+// first, so a workgroup waiting for the key below never waits for a
+// workgroup that has not been placed): the result becomes {0, ~0} (returning
+// device-scope atomics, performed at the memory side once the wait returns),
+// then the slot takes this launch's key.  No host-side reset of the result.
+__device__ __forceinline__ void verify_init(const KParams &p) {
+    uint32_t a = __hip_atomic_exchange(p.result, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t b = __hip_atomic_exchange(p.result + 1, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" : "+v"(a), "+v"(b));  // (returning forms: the wait covers them)
+    wait_vmem();
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p.sched + kEpochWord),
+                       static_cast<unsigned long long>(launch_key()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// End of a verification launch, thread 0 of every workgroup.  A clean
+// workgroup does nothing; one with mismatches waits until workgroup 0 has
+// initialised the result for this launch (the slot holds this launch's key:
+// polled with a returning atomic, performed where the key was written), then
+// adds its count and lowers the first bad index.  The clean launch's tail is
+// therefore empty: round 2's sharded tickets (every workgroup one returning
+// atomic, the last of each shard a second, the last of those the publish)
+// cost a small batch ~1.4 us (config 3: 5.05 vs 3.58 us).
 __device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
-    uint32_t *s = p.sched;
-    const uint32_t cnt = vacc[0], first = vacc[1];
-    if (cnt) {
-        uint32_t b = atomicMin(s + kVFirstWord, first);
-        asm volatile("" : "+v"(b));  // returning form: the wait below covers it
-        wait_vmem();
-    }
-    const uint32_t shard = blockIdx.x % kTicketShards;
-    const uint32_t shards = min(gridDim.x, kTicketShards);
-    const uint32_t in_shard = (gridDim.x - shard + kTicketShards - 1u) / kTicketShards;
-    const unsigned long long o =
-        atomicAdd(reinterpret_cast<unsigned long long *>(s + kShardWord + 32u * shard), kTicket | cnt);
-    if ((o >> 40) != in_shard - 1u) return;
-    const unsigned long long shard_total = (o & kCountMask) + cnt;
-    const unsigned long long g =
-        atomicAdd(reinterpret_cast<unsigned long long *>(s + kTicketWord), kTicket | shard_total);
-    if ((g >> 40) != shards - 1u) return;
-    // every other workgroup's first-bad update completed before its ticket
-    const unsigned long long total = (g & kCountMask) + shard_total;
-    p.result[0] = uint32_t(total);
-    p.result[1] = total ? atomicAdd(s + kVFirstWord, 0u) : 0xffffffffu;
-    reset_slot(s);
+    const uint32_t cnt = vacc[0];
+    if (!cnt) return;
+    const unsigned long long key = launch_key();
+    unsigned long long *ep = reinterpret_cast<unsigned long long *>(p.sched + kEpochWord);
+    while (__hip_atomic_fetch_add(ep, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key)
+        __builtin_amdgcn_s_sleep(8);
+    uint32_t a = __hip_atomic_fetch_add(p.result, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t b = __hip_atomic_fetch_min(p.result + 1, vacc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" : "+v"(a), "+v"(b));
+    wait_vmem();
 }
 
 // ---- tiles: one wave, 16 blocks ------------------------------------------
@@ -806,6 +789,9 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     }
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
+    // (the last wave: idle in small batches; in large ones the workgroup's
+    // tile pool absorbs its late start)
+    if (VERIFY && blockIdx.x == 0 && wv == kWaves - 1 && lane == 0) verify_init(p);
 
     // Gen pairs, seg pairs and constant runs, dealt over every wave of the
     // grid after the tiles.  (Before the tiles, so that their latency-bound

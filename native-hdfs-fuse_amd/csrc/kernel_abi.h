@@ -61,8 +61,8 @@ struct KParams {
     // Optional (crc32c_plan_verify_bitmap): bit i set for every mismatching
     // checksum i; zeroed by the runtime before the launch.
     uint32_t *bad_bits;
-    // Verification slot of this launch (kSlotWords u32s); the launch's last
-    // workgroup leaves it reset for the next launch.
+    // Verification slot of this launch (kSlotWords u32s): the key of the
+    // launch that initialised p.result.
     uint32_t *sched;
     // Multi-block launch: nblocks > 0 runs the plan's block_tiles tiles once
     // per block (tile j = block j / block_tiles, tile j % block_tiles); the
@@ -72,25 +72,21 @@ struct KParams {
     BlockRef blocks[kMaxLaunchBlocks];
 };
 
-// Device state of one verification launch ("slot"), u32 words, each on its
-// own 128-B line: the grid-wide merge of the workgroups' mismatch counts.
-// Launches of one plan (or one host-pipeline stage) share one slot and run
-// in GPU order; a launch's last workgroup leaves the slot as every launch
-// finds it: {global ticket, first bad, shard tickets} = {0, ~0, 0}.  Ticket words are 64-bit: tickets taken (bits 40-63) and the
-// mismatches they carried (bits 0-39).  Workgroup b first takes a ticket in
-// shard b % kTicketShards; the last of a shard takes one of the global
-// ticket (one counter per 32 workgroups instead of one for all 256: every
-// add to one word serialises).
-constexpr uint32_t kTicketShards = 8;
-constexpr uint32_t kTicketWord = 0;   // u64
-constexpr uint32_t kVFirstWord = 64;  // u32
-constexpr uint32_t kShardWord = 96;   // u64, + 32 * shard
-constexpr uint32_t kSlotWords = kShardWord + 32 * kTicketShards;
+// Device state of verification launches ("slot", kSlotWords u32s, one
+// 128-B line): the 64-bit key of the launch that last initialised its
+// result (kernel: launch_key, from the dispatch packet's address and the
+// queue's dispatch id -- unique per launch, graph replays included).
+// Workgroup 0 of a verification launch writes {0, ~0} to p.result and then
+// its key; a workgroup with mismatches waits for the key before it adds to
+// the result, and a clean workgroup touches neither (no grid-wide ticket).
+// Launches sharing a slot run in GPU order (a plan's verify launches).
+constexpr uint32_t kEpochWord = 0;  // u64
+constexpr uint32_t kSlotWords = 32;
 
-// Fills a slot's initial state (kSlotWords words).
+// Fills a slot's initial state (kSlotWords words): no launch's key.
 inline void init_sched_slots(uint32_t *w) {
     for (uint32_t i = 0; i < kSlotWords; ++i) w[i] = 0;
-    w[kVFirstWord] = 0xffffffffu;
+    w[kEpochWord] = w[kEpochWord + 1] = 0xffffffffu;
 }
 
 // The production kernel (crc32c_kernel.hip): one 12-wave workgroup per CU,
