@@ -188,16 +188,20 @@ void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point
     q->inflight.push_back({from + n, ev, tidx});
 }
 
-// Publishes done_upto = hi, waking sleeping waiters (worker).
-void complete_upto(crc32c_blocks *q, uint64_t hi) {
-    q->done_upto.store(hi, std::memory_order_seq_cst);
+// Wakes waiters asleep on done_upto (worker).  Called after the launch
+// that a completion makes possible, never between them: a futex wake of
+// many sleepers takes the worker tens of us, which the GPU then idles
+// (16 threads x 4 blocks in flight, before this order: 2.2-2.8 us per block).
+void wake_sleepers(crc32c_blocks *q) {
     if (q->sleepers.load(std::memory_order_seq_cst) > 0) {
         { std::lock_guard<std::mutex> lock(q->mu); }
         q->cv.notify_all();
     }
 }
 
-// Completes the front flush if its event has (worker).  Returns true when it did.
+// Completes the front flush if its event has (worker): publishes
+// done_upto (spinning waiters see it at once; sleepers are woken by the
+// caller's wake_sleepers).  Returns true when it did.
 bool complete_front(crc32c_blocks *q) {
     const crc32c_blocks::Flush f = q->inflight.front();
     if (f.ev) {
@@ -208,7 +212,7 @@ bool complete_front(crc32c_blocks *q) {
     }
     q->inflight.pop_front();
     if (f.trace_idx != SIZE_MAX) q->trace[f.trace_idx].done = ns(Clock::now());
-    complete_upto(q, f.hi);
+    q->done_upto.store(f.hi, std::memory_order_seq_cst);
     return true;
 }
 
@@ -219,6 +223,7 @@ void worker_loop(crc32c_blocks *q) {
     pays.reserve(q->max_blocks);
     outs.reserve(q->max_blocks);
     uint64_t launched = 0;
+    bool wake = false;        // done_upto moved: sleepers to wake once nothing is to launch
     bool have_first = false;  // a ready block seen since the last launch
     Clock::time_point first, idle_since = Clock::now();
     for (;;) {
@@ -236,9 +241,17 @@ void worker_loop(crc32c_blocks *q) {
                 continue;
             }
         }
+        if (wake) {
+            wake_sleepers(q);
+            wake = false;
+        }
         if (!q->inflight.empty()) {
-            if (complete_front(q)) idle_since = Clock::now();
-            else relax();
+            if (complete_front(q)) {
+                wake = true;
+                idle_since = Clock::now();
+            } else {
+                relax();
+            }
             continue;
         }
         if (q->next_ticket.load(std::memory_order_acquire) != launched) {  // a submit in progress, or a window open

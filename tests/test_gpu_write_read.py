@@ -786,3 +786,50 @@ def test_block_queue_threads(hdfs, gpu_ctx, orc):
         assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), orc.batch(hosts[i], pk, n))
     q.close()
     plan.close()
+
+
+@pytest.mark.parametrize("npk", [64, 4096])
+def test_verify_result_per_launch_graph_replays(hdfs, gpu_ctx, orc, npk):
+    """Verification results are per launch, with no host reset: workgroup 0
+    initialises the result and stores the launch's key (dispatch packet
+    address + dispatch id), and only mismatching workgroups add after it.
+    Back-to-back launches into the SAME result buffer, alternating clean and
+    corrupt expected arrays, must each report their own counts (never a
+    sum); a captured graph of [corrupt, clean, corrupt] launches replayed
+    three times must leave each launch's own result after every replay (a
+    replay reuses the captured kernel arguments, so only a device-side key
+    tells its launches apart).  One 4 MiB block (256 workgroups) and config
+    2 (one per CU)."""
+    torch = _torch()
+    pk = oracle.uniform_packets(npk)
+    n = oracle.total_checksums(pk)
+    payload = oracle.xorshift64_bytes(int(pk["payload_off"][-1] + pk["len"][-1]) + 16, 777 + npk)
+    want = orc.batch(payload, pk, n)
+    dpay = torch.from_numpy(payload).cuda()
+    good = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    bad_idx = np.array([3, n // 2, n - 1, n // 3 + 7])
+    badv = want.copy()
+    badv[bad_idx] ^= 0x5A5A
+    bad = torch.from_numpy(badv.view(np.int32)).cuda()
+    plan = gpu_ctx.plan(pk)
+    s = torch.cuda.Stream()
+    res = torch.full((2,), 12345, dtype=torch.int32, device="cuda")
+    expect_bad = (len(bad_idx), int(bad_idx.min()))
+    for k in range(6):
+        exp = bad if k % 2 else good
+        plan.verify(dpay.data_ptr(), exp.data_ptr(), res.data_ptr(), s.cuda_stream)
+        s.synchronize()
+        r = tuple(int(x) for x in res.cpu().numpy().view(np.uint32))
+        assert r == (expect_bad if k % 2 else (0, 0xFFFFFFFF)), (k, r)
+    results = [torch.full((2,), 777, dtype=torch.int32, device="cuda") for _ in range(3)]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for exp, r in zip((bad, good, bad), results):
+            plan.verify(dpay.data_ptr(), exp.data_ptr(), r.data_ptr(), s.cuda_stream)
+    for rep in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        got = [tuple(int(x) for x in r.cpu().numpy().view(np.uint32)) for r in results]
+        assert got == [expect_bad, (0, 0xFFFFFFFF), expect_bad], (rep, got)
+    del g
+    plan.close()
