@@ -51,6 +51,12 @@ for s in $STEPS; do
     abwt) for c in ${ABCFGS:-c2b1000 c2b1536}; do
             run abwt_base_$c 600 bash -c "cd scratch/wt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
             run abwt_head_$c 600 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}; done ;;
+    abwt2) for c in ${ABCFGS:-c2b1000 c2b1536}; do
+            run abwt2_base_$c 600 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-} &&
+            run abwt2_cand_$c 600 bash -c "cd scratch/wt2 && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}"; done ;;
+    abwt3) for c in ${ABCFGS:-c2b1000 c2b1536}; do
+            run abwt3_base_$c 600 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-} &&
+            run abwt3_cand_$c 600 bash -c "cd scratch/wt3 && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}"; done ;;
     qsum) run qsum 60 bash -c 'for f in gpurun_out/qtrace_*.jsonl; do echo "$f"; python tools/qtrace_summary.py "$f"; done' ;;
     bq) run bq_t16_mb16 300 tools/block_rate 16 400 16 30 4 0 &&
         run bq_t16_mb32 200 tools/block_rate 16 300 32 30 4 1 &&
