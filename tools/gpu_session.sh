@@ -64,6 +64,10 @@ for s in $STEPS; do
         run bq_t32_mb32 200 tools/block_rate 32 300 32 30 2 1 ;;
     bqprof) run bq_mb8 200 tools/block_rate 16 400 8 30 1 1 &&
             run bq_prof 300 rocprofv3 --kernel-trace --stats -d $OUT/bq_prof -o run --output-format csv -- tools/block_rate 16 100 16 30 2 1 ;;
+    bqs) for ns in 1 2; do
+           run bqs${ns}_t16_mb16 200 env HDFS_CRC32C_QUEUE_STREAMS=$ns tools/block_rate 16 400 16 30 2 1 &&
+           run bqs${ns}_t16_mb8 200 env HDFS_CRC32C_QUEUE_STREAMS=$ns tools/block_rate 16 400 8 30 2 1 &&
+           run bqs${ns}_t32_mb16 200 env HDFS_CRC32C_QUEUE_STREAMS=$ns tools/block_rate 32 300 16 30 1 1 || break; done ;;
     cgroup) run cgroup 30 bash -c 'cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat; nproc; cat /proc/self/status | grep -i cpus_allowed_list' ;;
     lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
