@@ -97,6 +97,8 @@ constexpr int kModeQuarter = 4096;  // small batches: power-of-two tiles of chun
                                     // units of 4 blocks each (4x the waves, 1/4 of each wave's latency chain)
 constexpr int kModeXcdMap = 2048;   // A/B: workgroup ranges remapped so that each XCD's workgroups hold one
                                     // contiguous 1/8 of the batch (instead of every eighth range)
+constexpr int kModeGDiagNoGather = 128;  // DIAGNOSTIC, wrong results: general items skip the per-subtile gather
+constexpr int kModeGDiagNoMask = 8192;   // DIAGNOSTIC, wrong results: general items skip the chunk-start masks
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
 
@@ -708,7 +710,9 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool S4 = (MODE & kModeS4) != 0;
     constexpr bool STAMPS = (MODE & kModeStamps) != 0;
     constexpr bool COMPDIAG = (MODE & kModeCompDiag) != 0;
-    constexpr int DIAG = (MODE & kModeMemDiag) ? 1 : 0;
+    // (bit 0: no lookups; bits 1-2: general-item ablations -- diagnostic builds only)
+    constexpr int DIAG = ((MODE & kModeMemDiag) ? 1 : 0) | ((MODE & kModeGDiagNoGather) ? 2 : 0) |
+                         ((MODE & kModeGDiagNoMask) ? 4 : 0);
     constexpr bool NOSTAGE = (MODE & kModeNoStage) != 0;
     constexpr bool VERIFY = (MODE & kModeVerify) != 0;
     constexpr bool C = S4 && (MODE & kModeS4C) != 0;

@@ -220,6 +220,10 @@ __device__ __forceinline__ void apply_keep(uint4 &x, const uint4 &k, uint32_t f)
 template <int DIAG, bool S4, int IMG>
 __device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g, const GSub &gs, const uint4 &kp,
                                             uint4 v[8], uint32_t pc[8], int lane) {
+    if (DIAG & 4) {  // DIAGNOSTIC (debug variants only, wrong results): no chunk-start masks
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
+        return;
+    }
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
     const uint32_t tst = g.padt ? gs.start & gs.tailm : 0u;  // the tail's first block (uniform)
     const uint32_t tsh = tst >> h;
@@ -282,6 +286,11 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         uint32_t pc[8];
         gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
         uint32_t x = block_lin(pc, lane);
+        if (DIAG & 2) {  // DIAGNOSTIC (debug variants only, wrong results): no per-subtile gather
+            acc ^= x;
+            gstate_next(g, gs, st);
+            continue;
+        }
         const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
         const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
         if (sh) x = zshift<S4, IMG>(lds, sh, x);

@@ -54,6 +54,13 @@ constexpr Variant kVariants[] = {
     {61, "s4_nt_halves_prodgrid", 768, 1, true, true},     // the same on the full image
     {62, "s4_nt_pow2only_prodgrid", 768, 1, true, true},   // the production power-of-two build (no general code)
     {63, "s4_nt_pow2only_xcdmap_prodgrid", 768, 1, true, true},  // 62, each XCD's ranges contiguous
+    // general-item ablations (wrong results): what the per-subtile gather and
+    // the chunk-start masks cost, with and without the payload loads
+    {70, "s4_nt_compute_only_nogather", 768, 1, false},
+    {71, "s4_nt_compute_only_nomask", 768, 1, false},
+    {72, "s4_nt_compute_only_nogather_nomask", 768, 1, false},
+    {73, "s4_nt_nogather", 768, 1, false},
+    {74, "s4_nt_nomask", 768, 1, false},
 };
 
 const Variant *find(int v) {
@@ -101,6 +108,11 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 61: HDFS_LAUNCH(768, 3, kS4Nt | kModeQuarter | kModeHalves); break;
     case 62: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt); break;
     case 63: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeXcdMap); break;
+    case 70: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompDiag | kModeGDiagNoGather); break;
+    case 71: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompDiag | kModeGDiagNoMask); break;
+    case 72: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompDiag | kModeGDiagNoGather | kModeGDiagNoMask); break;
+    case 73: HDFS_LAUNCH(768, 3, kS4Nt | kModeGDiagNoGather); break;
+    case 74: HDFS_LAUNCH(768, 3, kS4Nt | kModeGDiagNoMask); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -68,6 +68,9 @@ for s in $STEPS; do
            run bqs${ns}_t16_mb16 200 env HDFS_CRC32C_QUEUE_STREAMS=$ns tools/block_rate 16 400 16 30 2 1 &&
            run bqs${ns}_t16_mb8 200 env HDFS_CRC32C_QUEUE_STREAMS=$ns tools/block_rate 16 400 8 30 2 1 &&
            run bqs${ns}_t32_mb16 200 env HDFS_CRC32C_QUEUE_STREAMS=$ns tools/block_rate 32 300 16 30 1 1 || break; done ;;
+    gabl) run kbench_gabl_c2b1000 400 python tools/kbench.py --config c2b1000 --variants 0,3,4,70,71,72,73,74 &&
+          run kbench_gabl_c2b1536 400 python tools/kbench.py --config c2b1536 --variants 0,3,4,70,72,73 &&
+          run kbench_gabl_c2 300 python tools/kbench.py --config c2 --variants 0,3,4 ;;
     cgroup) run cgroup 30 bash -c 'cat /sys/fs/cgroup/cpu.max /sys/fs/cgroup/cpu.stat; nproc; cat /proc/self/status | grep -i cpus_allowed_list' ;;
     lsp) run lsp 120 tools/launch_stop_probe ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
