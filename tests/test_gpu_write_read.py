@@ -788,6 +788,64 @@ def test_block_queue_threads(hdfs, gpu_ctx, orc):
     plan.close()
 
 
+def test_block_queue_ring_reuse_two_in_flight(hdfs, gpu_ctx, orc):
+    """crc32c_blocks with more tickets than its ring has slots (1024): 16
+    threads keep two blocks in flight each (submit the next, then wait for
+    the oldest), 80 blocks per thread = 1280 tickets, max_blocks 8 (launches
+    capped at two in flight, the rest waiting in the ring).  Every output is
+    zeroed before its block is submitted and checked right after its wait,
+    so a launch that carried a stale ring slot or completed out of order
+    shows."""
+    import threading
+
+    torch = _torch()
+    pk = _block_shape("full")
+    n = oracle.total_checksums(pk)
+    nthreads, per, depth = 16, 80, 2
+    hosts = [oracle.xorshift64_bytes(64 * 65536, 9100 + k) for k in range(nthreads * depth)]
+    want = [orc.batch(h, pk, n) for h in hosts]
+    devs = [torch.from_numpy(h).cuda() for h in hosts]
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in hosts]
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    q = plan.blocks(max_blocks=8, window_us=50)
+    errs = []
+    go = threading.Barrier(nthreads)
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            ring = [None] * depth
+            go.wait()
+            for i in range(per + depth):
+                slot = i % depth
+                b = k * depth + slot
+                if ring[slot] is not None:
+                    q.wait(ring[slot])
+                    got = outs[b].cpu().numpy().view(np.uint32)
+                    assert np.array_equal(got, want[b]), (k, i)
+                if i < per:
+                    with torch.cuda.stream(s):
+                        outs[b].zero_()
+                    s.synchronize()
+                    ring[slot] = q.submit(devs[b].data_ptr(), outs[b].data_ptr())
+                else:
+                    ring[slot] = None
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    flushes, blocks = q.stats()
+    assert blocks == nthreads * per and flushes <= blocks, (flushes, blocks)
+    q.close()
+    plan.close()
+
+
 @pytest.mark.parametrize("npk", [64, 4096])
 def test_verify_result_per_launch_graph_replays(hdfs, gpu_ctx, orc, npk):
     """Verification results are per launch, with no host reset: workgroup 0
