@@ -183,11 +183,13 @@ uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
  * the plan was created with CRC32C_BIG_ENDIAN) instead of storing it.
  * dev_result: 2 device u32s, set by this call (asynchronously on `stream`):
  * [0] = mismatching checksums, [1] = lowest mismatching index (0xffffffff
- * when none).  One launch: the last workgroup to finish publishes the result
- * (no separate reset of dev_result).  A plan's verify launches share its
- * device scratch, so the library keeps them in GPU order, also across
- * streams (a verify launch on another stream than the plan's previous one
- * waits for it). */
+ * when none).  One launch: its first workgroup initialises dev_result and
+ * tags the plan's device slot with the launch's key, and only workgroups
+ * that found mismatches add to the result after they see that key (no
+ * separate reset of dev_result, no grid-wide reduction; graph replays are
+ * told apart by their dispatch).  A plan's verify launches share that slot,
+ * so the library keeps them in GPU order, also across streams (a verify
+ * launch on another stream than the plan's previous one waits for it). */
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream);
 
@@ -247,13 +249,16 @@ int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, ui
  *
  * crc32c_blocks: a coalescing queue for block writes arriving from several
  * threads without any batching by the caller.  crc32c_block_submit queues a
- * block (its bytes already in device memory) and returns a ticket; the
- * queue goes out as one crc32c_plan_exec_blocks launch on the queue's own
- * stream when it holds max_blocks blocks, on crc32c_block_flush, or when
- * window_us have passed since the queue's first block (group commit).  The
- * launches and their completion are made by one worker thread the queue
- * owns (every HIP call of the queue is on it; crc32c_block_flush only asks
- * it to launch now).  crc32c_block_wait returns when the ticket's checksums
+ * block (its bytes already in device memory) and returns a ticket (one
+ * atomic add and a ring slot: no lock); the queue goes out as one
+ * crc32c_plan_exec_blocks launch on the queue's own stream when it holds
+ * max_blocks blocks, on crc32c_block_flush, or window_us after the queue's
+ * worker saw the batch's first block (group commit).  The launches and
+ * their completion are made by one worker thread the queue owns (every HIP
+ * call of the queue is on it; crc32c_block_flush only asks it to launch
+ * now); at most two launches are in flight, later blocks wait in the ring.
+ * The GPU stays busy when about 2 x max_blocks blocks are in flight (e.g.
+ * 16 writer threads keeping two blocks each in flight with submit / wait).  crc32c_block_wait returns when the ticket's checksums
  * are in device memory (and complete for any later stream or copy);
  * crc32c_block_checksums is submit + wait.  Thread-safe.  Destroy the queue
  * (it launches what is queued and waits) before its plan.
