@@ -437,42 +437,32 @@ def main():
         bit_exact = bool(np.array_equal(got0, want))
     gate_exact = bit_exact
 
-    # Power settle (untimed, before the W warm-up steps): back-to-back
-    # launches of this kernel push the package to its 1.4 kW cap; the first
-    # few hundred ride a boost-then-clamp transient 5-12 % slower than the
-    # steady state (DESIGN.md section 5), so a short timed window (the
-    # driver's 20 steps after 5) would measure the transient.  ~settle_ms of
-    # the same step first, reported in the line; --settle-ms 0 disables it.
-    def settle_for(ms):  # untimed steps for ~ms; returns how many
-        n = 0
-        if ms > 0 and c4 and world > 1:
-            # (config 4's steps hold RCCL calls: every rank makes the same count)
-            for n in range(int(ms * 10)):
-                step(n)
-            n += 1
-            torch.cuda.synchronize()
-        elif ms > 0:
-            s0 = time.perf_counter()
-            while (time.perf_counter() - s0) * 1e3 < ms:
-                for _ in range(20):
-                    step(n)
-                    n += 1
-                torch.cuda.synchronize()
-        return n
+    # Settle and warm-up steps write a scratch copy of the outputs (same
+    # payloads, same plan), so the outputs the timed steps write are zeroed
+    # BEFORE the settle phase and the checks after the timed region still see
+    # only what the timed launches wrote -- and the GPU goes from settle to
+    # warm-up to the timed steps with no idle gap beyond one synchronise
+    # (round 3 captured and zeroed between settle and timing: the GPU idled
+    # there and a 20-step window ran slower than the verify window after it).
+    scratch_outs = [torch.zeros_like(o) for o in ([root_out] if c4 else outs)]
 
-    settle = settle_for(args.settle_ms)
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
+    def warm_step(i):
+        b = i % nbuf
+        if c4:
+            mplan.exec([bufs[b].data_ptr()], scratch_outs[0].data_ptr() if rank == 0 else 0, [sptr])
+        else:
+            plan.exec(bufs[b].data_ptr(), scratch_outs[b].data_ptr(), sptr)
+
     # The K timed steps are captured once into a HIP graph and replayed:
-    # each step is still one launch of the plan over one batch, but the
-    # launches are issued by the GPU's command processor instead of one
-    # Python -> ctypes -> hipLaunchKernel call each (~4.1 us per launch on
-    # the host, which bounds one-block batches: DESIGN.md section 5).  The
-    # host-issued rate is reported beside it (eager_ms_per_step).  Config 4's
-    # step holds RCCL calls at N > 1 and stays host-issued there (at N = 1 it
-    # is one plan launch).
-    use_graph = (not c4 or world == 1) and not args.no_graph
+    # each step is still one launch of the plan over one batch (config 4:
+    # the shard launch + the RCCL group), but the launches are issued by the
+    # GPU's command processor instead of one Python -> ctypes -> hipLaunchKernel
+    # call each (~4.1 us per launch on the host, which bounds one-block
+    # batches: DESIGN.md section 5).  The host-issued rate is reported beside
+    # it (eager_ms_per_step).  Config 4 at N > 1 captures the RCCL group too
+    # (the communicator exists: the gate step above created it); if this
+    # stack cannot capture, the steps are host-issued instead.
+    use_graph = not args.no_graph
     graph = None
     graph_error = None
     if use_graph:
@@ -489,10 +479,44 @@ def main():
         except RuntimeError as e:  # no graph on this stack: time host-issued launches instead
             graph, use_graph, graph_error = None, False, str(e)[:200]
             torch.cuda.synchronize()
-    # Outputs cleared before the timed region (untimed), so the checks after
-    # it see only what the timed launches wrote.
+    # Outputs cleared before the settle phase (untimed): the checks after the
+    # timed region see only what the timed launches wrote.
     for o in ([root_out] if c4 else outs):
         o.zero_()
+    torch.cuda.synchronize()
+
+    # Power settle (untimed, before the W warm-up steps): back-to-back
+    # launches of this kernel push the package to its 1.4 kW cap; the first
+    # few hundred ride a boost-then-clamp transient 5-12 % slower than the
+    # steady state (DESIGN.md section 5), so a short timed window (the
+    # driver's 20 steps after 5) would measure the transient.  ~settle_ms of
+    # the same step first, reported in the line; --settle-ms 0 disables it.
+    def settle_for(ms, fn=warm_step):  # untimed steps for ~ms; returns how many
+        n = 0
+        if ms > 0 and c4 and world > 1:
+            # (config 4's steps hold RCCL calls: every rank makes the same count)
+            for n in range(int(ms * 10)):
+                fn(n)
+            n += 1
+        elif ms > 0:
+            # (chunks of 20 launches; the host waits for the chunk before the
+            # last one, so the GPU always has one queued and never idles)
+            s0 = time.perf_counter()
+            prev = None
+            while (time.perf_counter() - s0) * 1e3 < ms:
+                for _ in range(20):
+                    fn(n)
+                    n += 1
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                if prev is not None:
+                    prev.synchronize()
+                prev = ev
+        return n
+
+    settle = settle_for(args.settle_ms)
+    for i in range(args.warmup):
+        warm_step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -189,7 +189,13 @@ uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
  * separate reset of dev_result, no grid-wide reduction; graph replays are
  * told apart by their dispatch).  A plan's verify launches share that slot,
  * so the library keeps them in GPU order, also across streams (a verify
- * launch on another stream than the plan's previous one waits for it). */
+ * launch on another stream than the plan's previous one waits for it).  It
+ * cannot order a graph replay of captured verify launches against other
+ * verify launches of the same plan: the caller must not let those overlap.
+ * If they do, the kernels still finish (a mismatching workgroup waits for
+ * its launch's key a bounded time) and bit 31 of dev_result[0]
+ * (CRC32C_VERIFY_OVERLAP) marks the result indeterminate. */
+#define CRC32C_VERIFY_OVERLAP 0x80000000u
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream);
 
@@ -344,17 +350,19 @@ int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint
  * out indices are the global ones (it writes its groups in place) unless
  * flags has CRC32C_MULTI_SELF_SEND.  Returns their count (copies at most cap).
  *
- * crc32c_multi_gather_plan: local_nout[r] = length of the array rank r sends
- * (0 for rank 0 in place), staging_off[r] = where rank 0 receives it in its
- * staging area (both nranks entries, optional), and per received group s
- * items[3s .. 3s+2] = {index in the staging area, index in the file-order
- * output, count}.  Returns the number of items (fills at most cap).
- * crc32c_multi_plan_exec issues exactly these sends, receives and copies. */
+ * crc32c_multi_transfers: local_nout[r] = length of rank r's local array (0
+ * for rank 0 in place; nranks entries, optional), and per transfer t, in the
+ * order exec posts them, xfers[4t .. 4t+3] = {sending rank, index in its
+ * local array, index in the file-order output on rank 0, count} -- one per
+ * received group, merged with the previous one when both come from the same
+ * rank and stay contiguous on both sides.  Returns the number of transfers
+ * (fills at most cap).  crc32c_multi_plan_exec issues exactly these: each
+ * sender one ncclSend per transfer of its own, rank 0 one ncclRecv per
+ * transfer straight into root_out (no staging copy), all in one RCCL group. */
 int64_t crc32c_multi_rank_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
                                   int rank, uint32_t flags, crc32c_packet *local, size_t cap);
-int64_t crc32c_multi_gather_plan(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
-                                 uint32_t flags, uint64_t *local_nout, uint64_t *staging_off, uint64_t *items,
-                                 size_t cap);
+int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                               uint32_t flags, uint64_t *local_nout, uint64_t *xfers, size_t cap);
 
 /* Device-resident multi-GPU plan of a file's packets (offsets in the caller's
  * file layout; every process passes the same list).  Exec: dev_shards[i] =
@@ -363,10 +371,15 @@ int64_t crc32c_multi_gather_plan(const crc32c_packet *pkts, size_t npkts, uint32
  * only), streams[i] = the local device i's stream (NULL entry = its default
  * stream; streams == NULL = the library's own streams, see
  * crc32c_multi_sync).  Asynchronous: the
- * checksum launches, then the RCCL gather (every other rank's array in one
- * ncclSend; rank 0 computes its own groups in place and scatters the
- * received ones into file order), on the local devices' streams; root_out
- * is complete when rank 0's stream is.  flags: CRC32C_BIG_ENDIAN,
+ * checksum launches, then the RCCL gather (crc32c_multi_transfers: every
+ * other rank's group ranges sent straight into their file-order places in
+ * root_out; rank 0 computes its own groups in place), on the local devices'
+ * streams; root_out is complete when rank 0's stream is.  An exec may be
+ * captured into a HIP graph (kernels and the RCCL group; the communicator is
+ * created by the first exec, so run one exec before capturing).  Successive
+ * execs on the same stream cost no extra HIP call; an exec on another stream
+ * than the plan's previous one records an event on that previous stream, so
+ * that stream must still exist then.  flags: CRC32C_BIG_ENDIAN,
  * CRC32C_TYPE_CRC32, CRC32C_MULTI_SELF_SEND. */
 #define CRC32C_MULTI_SELF_SEND 0x10u /* crc32c_multi_plan_create: rank 0's own checksums also travel
                                        through RCCL (a send to itself) instead of being written in

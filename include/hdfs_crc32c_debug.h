@@ -51,6 +51,12 @@ size_t crc32c_debug_lds_image_s4(void *dst, size_t cap, uint32_t flags);
 /* The affine constants of the checksum type in `flags` (CRC32C_TYPE_CRC32 or not). */
 void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_small4);
 
+/* Fault injection for the block queue's error path (tests): the worker fails
+ * the issue of the next `n` flushes of q as if their launch had failed
+ * (-EIO, nothing launched); the waits of exactly those flushes' tickets
+ * return the error. */
+int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n);
+
 /* ---- 2. libhdfs_crc32c_debug.so only ---- */
 
 /* Launch of a plan with an explicit kernel variant (0 = production; see

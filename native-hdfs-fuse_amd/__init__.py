@@ -31,6 +31,7 @@ CRC32C_TYPE_CRC32 = 0x2  # Hadoop CHECKSUM_CRC32 (zlib polynomial) instead of CR
 CRC32C_DEVICE_ADDRESSES = 0x4  # plan flag: payload_off are device addresses; exec/verify take payload 0
 CRC32C_CPU_FALLBACK = 0x8  # crc32c_chunks / crc32c_batch_host: finish on the host CPU if the GPU fails
 CRC32C_MULTI_SELF_SEND = 0x10  # multi plan: rank 0's own checksums also go through RCCL (one-GPU transport test)
+CRC32C_VERIFY_OVERLAP = 0x80000000  # bit 31 of a verify result's count: overlapping verify launches
 PATH_NONE, PATH_GPU, PATH_CPU = 0, 1, 2  # crc32c_last_path()
 
 PACKET_DTYPE = np.dtype(
@@ -160,7 +161,7 @@ def _bind(L):
         "crc32c_multi_layout": (ctypes.c_int64, [vp, sz, u32, i32, vp, vp]),
         "crc32c_multi_shard_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, vp, sz]),
         "crc32c_multi_rank_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, u32, vp, sz]),
-        "crc32c_multi_gather_plan": (ctypes.c_int64, [vp, sz, u32, i32, u32, vp, vp, vp, sz]),
+        "crc32c_multi_transfers": (ctypes.c_int64, [vp, sz, u32, i32, u32, vp, vp, sz]),
         "crc32c_multi_plan_create": (i32, [vp, vp, sz, u32, u32, pp]),
         "crc32c_multi_plan_exec": (i32, [vp, vp, vp, vp]),
         "crc32c_multi_plan_destroy": (i32, [vp]),
@@ -175,6 +176,7 @@ def _bind(L):
         "crc32c_block_checksums": (i32, [vp, vp, vp]),
         "crc32c_blocks_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_blocks_destroy": (i32, [vp]),
+        "crc32c_debug_blocks_fail_flushes": (i32, [vp, u32]),
         "crc32c_verify_frames_host": (i32, [vp, vp, sz, u32, u64, u32, ctypes.POINTER(FramesResult)]),
     }
     for name, (res, args) in sig.items():
@@ -412,6 +414,10 @@ class Blocks:
         _check(lib().crc32c_block_checksums(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out)),
                "crc32c_block_checksums")
 
+    def debug_fail_flushes(self, n: int) -> None:
+        """crc32c_debug_blocks_fail_flushes: the next n flushes fail at issue (tests of the error path)."""
+        _check(lib().crc32c_debug_blocks_fail_flushes(self.handle, n), "crc32c_debug_blocks_fail_flushes")
+
     def stats(self):
         f, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
         _check(lib().crc32c_blocks_stats(self.handle, ctypes.byref(f), ctypes.byref(b)), "crc32c_blocks_stats")
@@ -550,20 +556,17 @@ def multi_rank_packets(pkts, group_packets: int, nranks: int, rank: int, flags: 
     return out[:n]
 
 
-def multi_gather_plan(pkts, group_packets: int, nranks: int, flags: int = 0):
-    """crc32c_multi_gather_plan: (local_nout[nranks], staging_off[nranks], items[S, 3] = {staging index,
-    file index, count}) -- the exchange crc32c_multi_plan_exec performs."""
+def multi_transfers(pkts, group_packets: int, nranks: int, flags: int = 0):
+    """crc32c_multi_transfers: (local_nout[nranks], transfers[T, 4] = {sending rank, index in its local array,
+    file index on rank 0, count}) -- the exchange crc32c_multi_plan_exec posts, in posting order."""
     pkts = as_packets(pkts)
-    n = int(lib().crc32c_multi_gather_plan(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, None, None, None,
-                                           0))
+    n = int(lib().crc32c_multi_transfers(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, None, None, 0))
     if n < 0:
-        _check(n, "crc32c_multi_gather_plan")
+        _check(n, "crc32c_multi_transfers")
     ln = np.zeros(nranks, np.uint64)
-    so = np.zeros(nranks, np.uint64)
-    items = np.zeros((max(n, 1), 3), np.uint64)
-    lib().crc32c_multi_gather_plan(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, _np_ptr(ln), _np_ptr(so),
-                                   _np_ptr(items), n)
-    return ln, so, items[:n]
+    xs = np.zeros((max(n, 1), 4), np.uint64)
+    lib().crc32c_multi_transfers(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, _np_ptr(ln), _np_ptr(xs), n)
+    return ln, xs[:n]
 
 
 def verify_frames(frames: np.ndarray, bpc: int, chunk_offset: int, flags: int = 0, ctx: Context | None = None):

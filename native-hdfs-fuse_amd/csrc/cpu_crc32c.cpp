@@ -3,7 +3,7 @@
 // Replaces src/crc32c.c:333-343 with identical semantics: `crc` is a finished
 // CRC32C (pre-inverted on entry, post-inverted on exit, crc32c.c:237/312),
 // any alignment, len == 0 returns crc, thread-safe, cannot fail.  It is the
-// host path for single calls; batches go to the GPU (crc32c_gpu.hip).
+// host path for single calls; batches go to the GPU (crc32c_runtime.hip).
 //
 // Two host implementations, chosen once by CPUID:
 //  * SSE4.2 `crc32` instruction (3-cycle latency, 1 per cycle): the buffer

@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "hdfs_crc32c.h"
+#include "hdfs_crc32c_debug.h"
 #include "runtime_internal.h"
 
 using namespace hdfs_crc;
@@ -64,25 +65,32 @@ struct crc32c_blocks {
     // the ring: ticket t's block in slots[t & mask] (reusable once t is launched)
     std::unique_ptr<Slot[]> slots;
     uint64_t mask = 0;
-    alignas(64) std::atomic<uint64_t> next_ticket{0};   // tickets handed out
+    alignas(64) std::atomic<uint64_t> next_ticket{0};   // tickets handed out (| kStopBit once destroy began)
     alignas(64) std::atomic<uint64_t> launched_upto{0}; // tickets below this are in a launch
     alignas(64) std::atomic<uint64_t> done_upto{0};     // tickets below this are complete
     alignas(64) std::atomic<uint64_t> flush_upto{0};    // crc32c_block_flush: launch tickets below this now
     std::atomic<bool> stop{false};
     std::atomic<bool> worker_sleeping{false};
     std::atomic<int> sleepers{0};  // waiters asleep on cv
-    std::atomic<int> error{0};     // a failed flush or event: every later wait returns it
+    // Failed flushes (rare): each one's ticket range and error, so a wait
+    // returns the error of its own flush only -- tickets before and after it
+    // succeed as their flushes do.
+    std::mutex err_mu;
+    std::vector<std::pair<std::pair<uint64_t, uint64_t>, int>> failed;
+    std::atomic<int> nfailed{0};
     std::mutex mu;                  // only for the two condition variables
     std::condition_variable cv;       // waiters: done_upto moved
     std::condition_variable work_cv;  // worker: a ticket was handed out, or stop
     struct Flush {
-        uint64_t hi;  // tickets below hi
+        uint64_t lo, hi;  // tickets [lo, hi)
         hipEvent_t ev;
+        int err;  // its issue failed (nothing to wait for)
         size_t trace_idx;
     };
     std::deque<Flush> inflight;     // worker only
     std::vector<hipEvent_t> spare;  // worker only
     std::atomic<uint64_t> flushes{0}, blocks{0};
+    std::atomic<uint32_t> inject_fail{0};  // crc32c_debug_blocks_fail_flushes
     bool record_events = false;  // A/B (HDFS_CRC32C_QUEUE_RECORD=1): an hipEventRecord after each flush
     unsigned event_flags = hipEventDisableTiming;  // A/B (HDFS_CRC32C_QUEUE_TIMING=1: timing events)
     std::thread worker;
@@ -98,6 +106,30 @@ struct crc32c_blocks {
 };
 
 namespace {
+
+// Set in next_ticket by crc32c_blocks_destroy: a submit sees it in the same
+// atomic word it takes its ticket from, so no ticket is handed out after the
+// worker may have seen the last one.
+constexpr uint64_t kStopBit = 1ull << 63;
+
+uint64_t tickets_out(const crc32c_blocks *q, std::memory_order o = std::memory_order_acquire) {
+    return q->next_ticket.load(o) & ~kStopBit;
+}
+
+void record_failure(crc32c_blocks *q, uint64_t lo, uint64_t hi, int err) {
+    std::lock_guard<std::mutex> lock(q->err_mu);
+    q->failed.push_back({{lo, hi}, err});
+    q->nfailed.store(int(q->failed.size()), std::memory_order_release);
+}
+
+// The error of the flush ticket t went out in (0 when it succeeded).
+int ticket_error(crc32c_blocks *q, uint64_t t) {
+    if (!q->nfailed.load(std::memory_order_acquire)) return 0;
+    std::lock_guard<std::mutex> lock(q->err_mu);
+    for (const auto &f : q->failed)
+        if (t >= f.first.first && t < f.first.second) return f.second;
+    return 0;
+}
 
 std::chrono::microseconds env_us(const char *name, int dflt) {
     const char *e = std::getenv(name);
@@ -162,7 +194,9 @@ void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point
         q->spare.pop_back();
     }
     int rc = 0;
-    if (!ev && hipEventCreateWithFlags(&ev, q->event_flags) != hipSuccess) {
+    for (uint32_t k = q->inject_fail.load(std::memory_order_relaxed); k && !rc;)
+        if (q->inject_fail.compare_exchange_weak(k, k - 1, std::memory_order_relaxed)) rc = fail(-EIO, "injected flush failure");
+    if (!rc && !ev && hipEventCreateWithFlags(&ev, q->event_flags) != hipSuccess) {
         ev = nullptr;
         rc = fail(-EIO, "hipEventCreate failed");
     }
@@ -181,11 +215,10 @@ void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point
     q->flushes.fetch_add(1, std::memory_order_relaxed);
     q->blocks.fetch_add(n, std::memory_order_relaxed);
     if (rc) {  // nothing to wait for: its tickets complete (with the error) once those before them have
-        q->error = rc;
         if (ev) q->spare.push_back(ev);
         ev = nullptr;
     }
-    q->inflight.push_back({from + n, ev, tidx});
+    q->inflight.push_back({from, from + n, ev, rc, tidx});
 }
 
 // Wakes waiters asleep on done_upto (worker).  Called after the launch
@@ -204,12 +237,14 @@ void wake_sleepers(crc32c_blocks *q) {
 // caller's wake_sleepers).  Returns true when it did.
 bool complete_front(crc32c_blocks *q) {
     const crc32c_blocks::Flush f = q->inflight.front();
+    int err = f.err;
     if (f.ev) {
         const hipError_t e = hipEventQuery(f.ev);
         if (e == hipErrorNotReady) return false;
-        if (e != hipSuccess) q->error = fail(-EIO, "block flush: %s", hipGetErrorString(e));
+        if (e != hipSuccess) err = fail(-EIO, "block flush: %s", hipGetErrorString(e));
         q->spare.push_back(f.ev);
     }
+    if (err) record_failure(q, f.lo, f.hi, err);  // (before done_upto: a waiter that sees it sees this)
     q->inflight.pop_front();
     if (f.trace_idx != SIZE_MAX) q->trace[f.trace_idx].done = ns(Clock::now());
     q->done_upto.store(f.hi, std::memory_order_seq_cst);
@@ -254,7 +289,7 @@ void worker_loop(crc32c_blocks *q) {
             }
             continue;
         }
-        if (q->next_ticket.load(std::memory_order_acquire) != launched) {  // a submit in progress, or a window open
+        if (tickets_out(q) != launched) {  // a submit in progress, or a window open
             relax();
             continue;
         }
@@ -268,7 +303,7 @@ void worker_loop(crc32c_blocks *q) {
         {
             std::unique_lock<std::mutex> lock(q->mu);
             q->work_cv.wait(lock, [&] {
-                return q->next_ticket.load(std::memory_order_seq_cst) != launched ||
+                return tickets_out(q, std::memory_order_seq_cst) != launched ||
                        q->stop.load(std::memory_order_seq_cst);
             });
         }
@@ -321,8 +356,11 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
 
 int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
     if (!q || !dev_out) return fail(-EINVAL, "queue/out == NULL");
-    if (q->stop.load(std::memory_order_relaxed)) return fail(-EINVAL, "queue is being destroyed");
-    const uint64_t t = q->next_ticket.fetch_add(1, std::memory_order_seq_cst);
+    // the stop check and the ticket are one atomic step (kStopBit)
+    uint64_t t = q->next_ticket.load(std::memory_order_relaxed);
+    do {
+        if (t & kStopBit) return fail(-EINVAL, "queue is being destroyed");
+    } while (!q->next_ticket.compare_exchange_weak(t, t + 1, std::memory_order_seq_cst, std::memory_order_relaxed));
     // the ring is full only with mask + 1 blocks queued and none launched yet
     while (t - q->launched_upto.load(std::memory_order_acquire) > q->mask) std::this_thread::yield();
     Slot &s = q->slots[t & q->mask];
@@ -336,7 +374,7 @@ int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev
 
 int crc32c_block_flush(crc32c_blocks *q) {
     if (!q) return fail(-EINVAL, "queue == NULL");
-    const uint64_t hi = q->next_ticket.load(std::memory_order_acquire);
+    const uint64_t hi = tickets_out(q);
     uint64_t cur = q->flush_upto.load(std::memory_order_relaxed);
     while (cur < hi && !q->flush_upto.compare_exchange_weak(cur, hi, std::memory_order_acq_rel)) {
     }
@@ -346,12 +384,12 @@ int crc32c_block_flush(crc32c_blocks *q) {
 
 int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
     if (!q) return fail(-EINVAL, "queue == NULL");
-    if (ticket < q->done_upto.load(std::memory_order_acquire)) return q->error;
-    if (ticket >= q->next_ticket.load(std::memory_order_acquire))
+    if (ticket < q->done_upto.load(std::memory_order_acquire)) return ticket_error(q, ticket);
+    if (ticket >= tickets_out(q))
         return fail(-EINVAL, "ticket %llu was never handed out", (unsigned long long)ticket);
     const Clock::time_point spin_end = Clock::now() + spin_time();
     for (int i = 0;; ++i) {
-        if (ticket < q->done_upto.load(std::memory_order_acquire)) return q->error;
+        if (ticket < q->done_upto.load(std::memory_order_acquire)) return ticket_error(q, ticket);
         if ((i & 63) == 63 && Clock::now() >= spin_end) break;
         if ((i & 7) == 7)
             std::this_thread::yield();
@@ -364,7 +402,7 @@ int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
         q->cv.wait(lock, [&] { return ticket < q->done_upto.load(std::memory_order_seq_cst); });
     }
     q->sleepers.fetch_sub(1, std::memory_order_relaxed);
-    return q->error;
+    return ticket_error(q, ticket);
 }
 
 int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out) {
@@ -380,9 +418,17 @@ int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blo
     return 0;
 }
 
+int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n) {
+    if (!q) return fail(-EINVAL, "queue == NULL");
+    q->inject_fail.store(n, std::memory_order_relaxed);
+    return 0;
+}
+
 int crc32c_blocks_destroy(crc32c_blocks *q) {
     if (!q) return 0;
-    // (the worker launches what is queued, completes everything, returns)
+    // (no ticket is handed out from here; the worker launches what is
+    // queued, completes everything, returns)
+    q->next_ticket.fetch_or(kStopBit, std::memory_order_seq_cst);
     q->stop.store(true, std::memory_order_seq_cst);
     {
         std::lock_guard<std::mutex> lock(q->mu);

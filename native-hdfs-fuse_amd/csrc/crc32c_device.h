@@ -347,13 +347,31 @@ __device__ __forceinline__ void verify_init(const KParams &p) {
 // therefore empty: round 2's sharded tickets (every workgroup one returning
 // atomic, the last of each shard a second, the last of those the publish)
 // cost a small batch ~1.4 us (config 3: 5.05 vs 3.58 us).
+//
+// The wait is bounded (kVerifyKeyPolls polls, ~0.1-0.3 s): if another verify
+// launch of the same plan overlaps this one (a graph replay beside a direct
+// verify on another stream: the library cannot order those) its key may
+// replace this launch's before this workgroup sees it.  The workgroup then
+// gives up waiting, adds its count anyway and sets bit 31 of result[0]
+// (kVerifyOverlapBit): "indeterminate -- overlapping verify launches of one
+// plan".  The kernel always finishes.
+constexpr uint32_t kVerifyKeyPolls = 1u << 17;
+constexpr uint32_t kVerifyOverlapBit = 0x80000000u;
+
 __device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
     const uint32_t cnt = vacc[0];
     if (!cnt) return;
     const unsigned long long key = launch_key();
     unsigned long long *ep = reinterpret_cast<unsigned long long *>(p.sched + kEpochWord);
-    while (__hip_atomic_fetch_add(ep, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key)
+    uint32_t polls = 0;
+    while (__hip_atomic_fetch_add(ep, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key) {
+        if (++polls == kVerifyKeyPolls) {
+            uint32_t o = __hip_atomic_fetch_or(p.result, kVerifyOverlapBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("" : "+v"(o));
+            break;
+        }
         __builtin_amdgcn_s_sleep(8);
+    }
     uint32_t a = __hip_atomic_fetch_add(p.result, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t b = __hip_atomic_fetch_min(p.result + 1, vacc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("" : "+v"(a), "+v"(b));

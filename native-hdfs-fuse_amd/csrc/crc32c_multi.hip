@@ -8,11 +8,13 @@
 // are the path's only exchange; no payload byte crosses GPUs.
 //
 // Rank 0 checksums its own groups straight into their final places; every
-// other rank checksums its groups into one local array and sends it with ONE
-// ncclSend; rank 0 receives each peer's array into a staging slot and one
-// copy kernel scatters the groups into file order.  (So a one-GPU
-// communicator needs no transfer; CRC32C_MULTI_SELF_SEND routes rank 0's
-// own array through RCCL as well, to exercise the transport on one GPU.)
+// other rank checksums its groups into one local array and sends each group's
+// checksum range (merged where consecutive groups stay consecutive in file
+// order) with an ncclSend; rank 0 posts the matching ncclRecvs straight into
+// the groups' file-order places in its output -- no staging area, no copy
+// kernel.  (So a one-GPU communicator needs no transfer;
+// CRC32C_MULTI_SELF_SEND routes rank 0's own checksums through RCCL as well,
+// to exercise the transport on one GPU.)
 //
 // Two ways to build the communicator: one process driving every device
 // (crc32c_multi_create, ncclCommInitAll) or one process per device
@@ -186,35 +188,35 @@ void shard_packets(const crc32c_packet *pkts, size_t npkts, uint32_t gp, const s
     }
 }
 
-// The gather step of a plan: what each rank's local array holds, where
-// rank 0's staging area receives it, and the scatter items that move every
-// received group into file order.  Rank 0's own groups are computed in place
-// (no transfer) unless self_send.  crc32c_multi_plan_create builds its
-// device plan from exactly this; crc32c_multi_gather_plan exports it.
-struct Gather {
-    std::vector<uint64_t> staging_off;  // per rank
-    std::vector<uint64_t> items;        // 3 per received group: {staging index, file index, count}
-    uint64_t staging_total = 0;
+// The gather step of a plan: the point-to-point transfers, in the order they
+// are posted -- {sending rank, index in its local array, file index on rank
+// 0, count}.  One per received group, merged with the previous one when both
+// come from the same rank and stay contiguous on both sides (a one-rank
+// self-send is then one transfer).  Every sender posts its ncclSends and rank
+// 0 its ncclRecvs (straight into the file-order output) in this order, so
+// each (sender, rank 0) pair matches in order.  Rank 0's own groups are
+// computed in place (no transfer) unless self_send.  crc32c_multi_plan_create
+// builds its exec from exactly this; crc32c_multi_transfers exports it.
+struct Xfer {
+    int rank;
+    uint64_t local, file, count;
 };
 
 bool sends(int rank, bool self_send) { return rank != 0 || self_send; }
 
-void build_gather(const std::vector<Group> &groups, const std::vector<uint64_t> &local_nout, int nranks,
-                  bool self_send, Gather *g) {
-    g->staging_off.assign(size_t(nranks), 0);
-    g->items.clear();
-    uint64_t total = 0;
-    for (int r = 0; r < nranks; ++r) {
-        g->staging_off[size_t(r)] = total;
-        if (sends(r, self_send)) total += local_nout[size_t(r)];
-    }
-    g->staging_total = total;
-    for (const Group &G : groups)
-        if (G.n && sends(G.rank, self_send)) {
-            g->items.push_back(g->staging_off[size_t(G.rank)] + G.local_out);
-            g->items.push_back(G.omin);
-            g->items.push_back(G.n);
+void build_transfers(const std::vector<Group> &groups, bool self_send, std::vector<Xfer> *xs) {
+    xs->clear();
+    for (const Group &G : groups) {
+        if (!G.n || !sends(G.rank, self_send)) continue;
+        if (!xs->empty()) {
+            Xfer &b = xs->back();
+            if (b.rank == G.rank && b.local + b.count == G.local_out && b.file + b.count == G.omin) {
+                b.count += G.n;
+                continue;
+            }
         }
+        xs->push_back(Xfer{G.rank, G.local_out, G.omin, G.n});
+    }
 }
 
 // The packets rank r's plan computes: payload offsets in its shard; out
@@ -253,16 +255,12 @@ struct crc32c_multi_plan {
     std::vector<uint32_t *> d_local;     // per local device: its local array (none for rank 0 in place)
     uint64_t nchecksums = 0;
     bool self_send = false;
-    // rank 0's process: the peers' arrays land in d_staging (staging_off[r]
-    // for rank r), then scatter_groups() moves every group into place.
-    uint32_t *d_staging = nullptr;
-    std::vector<uint64_t> staging_off;
-    uint4 *d_scatter = nullptr;  // {src index in staging, dst index in root_out, count, 0}
-    uint32_t nscatter = 0;
+    std::vector<Xfer> xfers;  // the gather's transfers, in posting order
     int root_local = -1;  // local device index of rank 0 (-1: not in this process)
-    // Successive execs reuse d_local / d_staging: per local device, the
-    // stream of the previous exec and an event after its last step, so an
-    // exec on another stream first waits for it.
+    // Successive execs reuse d_local (an exec's sends read it while the next
+    // exec's kernel rewrites it): per local device, the stream of the
+    // previous exec; an exec on another stream first waits for an event
+    // recorded on that one at the switch (same stream: stream order, no call).
     std::vector<hipStream_t> last_stream;
     std::vector<hipEvent_t> last_done;
     std::vector<char> launched;
@@ -270,26 +268,25 @@ struct crc32c_multi_plan {
 
 namespace {
 
-// One workgroup per received group: its checksums from the staging area to
-// their place in rank 0's output (u32 copies, coalesced).
-__global__ __launch_bounds__(256) void scatter_groups(const uint32_t *staging, const uint4 *items, uint32_t *out) {
-    const uint4 it = items[blockIdx.x];
-    for (uint32_t k = threadIdx.x; k < it.z; k += blockDim.x) out[it.y + k] = staging[it.x + k];
-}
-
-// Records where this exec ended on every local device (outside a capture:
-// a captured exec is ordered by its graph's own stream).
-int mark_execs(crc32c_multi_plan *mp, void *const *streams) {
+// Before an exec on `s` (local device i): when the previous exec of the plan
+// went on another stream, an event recorded on that stream now (it follows
+// everything issued there so far, the previous exec's sends included) is
+// waited on -- by `s`, or by the host while `s` is being captured (a capture
+// cannot wait on work outside it).  A previous exec captured into a graph
+// needs nothing: its replays are ordered by the caller's graph launches.
+int order_exec(crc32c_multi_plan *mp, size_t i, hipStream_t s) {
+    if (!mp->launched[i] || mp->last_stream[i] == s) return 0;
     crc32c_multi *m = mp->m;
-    for (size_t i = 0; i < m->ctxs.size(); ++i) {
-        const hipStream_t s = local_stream(m, i, streams);
-        DeviceGuard guard(m->ctxs[i]->device);
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        HIP_TRY(hipStreamIsCapturing(s, &cs));
-        if (cs == hipStreamCaptureStatusNone) HIP_TRY(hipEventRecord(mp->last_done[i], s));
-        mp->last_stream[i] = s;
-        mp->launched[i] = 1;
-    }
+    DeviceGuard guard(m->ctxs[i]->device);
+    hipStreamCaptureStatus prev = hipStreamCaptureStatusNone, cur = hipStreamCaptureStatusNone;
+    HIP_TRY(hipStreamIsCapturing(mp->last_stream[i], &prev));
+    if (prev != hipStreamCaptureStatusNone) return 0;
+    HIP_TRY(hipEventRecord(mp->last_done[i], mp->last_stream[i]));
+    HIP_TRY(hipStreamIsCapturing(s, &cur));
+    if (cur != hipStreamCaptureStatusNone)
+        HIP_TRY(hipEventSynchronize(mp->last_done[i]));
+    else
+        HIP_TRY(hipStreamWaitEvent(s, mp->last_done[i], 0));
     return 0;
 }
 
@@ -412,22 +409,22 @@ int64_t crc32c_multi_rank_packets(const crc32c_packet *pkts, size_t npkts, uint3
     return int64_t(v.size());
 }
 
-int64_t crc32c_multi_gather_plan(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
-                                 uint32_t flags, uint64_t *local_nout, uint64_t *staging_off, uint64_t *items,
-                                 size_t cap) {
+int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                               uint32_t flags, uint64_t *local_nout, uint64_t *xfers, size_t cap) {
     std::vector<Group> groups;
     std::vector<uint64_t> sb, ln;
     if (int rc = build_layout(pkts, npkts, group_packets, nranks, &groups, &sb, &ln)) return rc;
     const bool self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
-    Gather ga;
-    build_gather(groups, ln, nranks, self_send, &ga);
-    for (int r = 0; r < nranks; ++r) {
-        if (local_nout) local_nout[r] = sends(r, self_send) ? ln[size_t(r)] : 0;
-        if (staging_off) staging_off[r] = ga.staging_off[size_t(r)];
+    std::vector<Xfer> xs;
+    build_transfers(groups, self_send, &xs);
+    for (int r = 0; local_nout && r < nranks; ++r) local_nout[r] = sends(r, self_send) ? ln[size_t(r)] : 0;
+    for (size_t k = 0; xfers && k < std::min(cap, xs.size()); ++k) {
+        xfers[4 * k] = uint64_t(xs[k].rank);
+        xfers[4 * k + 1] = xs[k].local;
+        xfers[4 * k + 2] = xs[k].file;
+        xfers[4 * k + 3] = xs[k].count;
     }
-    const size_t n = ga.items.size() / 3;
-    if (items) std::copy(ga.items.begin(), ga.items.begin() + 3 * std::min(cap, n), items);
-    return int64_t(n);
+    return int64_t(xs.size());
 }
 
 int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
@@ -476,23 +473,8 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
         }
         mp->d_local.push_back(d);
     }
-    if (mp->root_local >= 0) {  // staging slots and scatter list for the arrays rank 0 receives
-        Gather ga;
-        build_gather(mp->groups, mp->local_nout, m->nranks, mp->self_send, &ga);
-        mp->staging_off = ga.staging_off;
-        const uint64_t total = ga.staging_total;
-        if (total > UINT32_MAX || mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
-        std::vector<uint4> items;
-        for (size_t k = 0; k + 2 < ga.items.size(); k += 3)
-            items.push_back(make_uint4(uint32_t(ga.items[k]), uint32_t(ga.items[k + 1]), uint32_t(ga.items[k + 2]), 0u));
-        DeviceGuard guard(m->ctxs[size_t(mp->root_local)]->device);
-        if (total) HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_staging), total * sizeof(uint32_t)));
-        if (!items.empty()) {
-            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_scatter), items.size() * sizeof(uint4)));
-            HIP_TRY(hipMemcpy(mp->d_scatter, items.data(), items.size() * sizeof(uint4), hipMemcpyHostToDevice));
-        }
-        mp->nscatter = uint32_t(items.size());
-    }
+    build_transfers(mp->groups, mp->self_send, &mp->xfers);
+    if (mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
     *out = mp.release();
     return 0;
 }
@@ -513,19 +495,13 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
         if (mp->local_nout[size_t(m->ranks[i])] && (!dev_shards || !dev_shards[i]))
             return fail(-EINVAL, "local device %zu: shard payload == NULL", i);
     if (mp->root_local >= 0 && mp->nchecksums && !root_out) return fail(-EINVAL, "root_out == NULL on rank 0");
-    // 0. after the previous exec when it ran on another stream (its sends and
-    //    scatter may still read the buffers this one overwrites)
+    // 0. after the previous exec when it ran on another stream (its sends may
+    //    still read the local arrays this one overwrites)
+    for (size_t i = 0; i < m->ctxs.size(); ++i)
+        if (int rc = order_exec(mp, i, local_stream(m, i, streams))) return rc;
     for (size_t i = 0; i < m->ctxs.size(); ++i) {
-        const hipStream_t s = local_stream(m, i, streams);
-        if (mp->launched[i] && mp->last_stream[i] != s) {
-            DeviceGuard guard(m->ctxs[i]->device);
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            HIP_TRY(hipStreamIsCapturing(s, &cs));
-            if (cs != hipStreamCaptureStatusNone)  // (a capture cannot wait on work outside it)
-                HIP_TRY(hipEventSynchronize(mp->last_done[i]));
-            else
-                HIP_TRY(hipStreamWaitEvent(s, mp->last_done[i], 0));
-        }
+        mp->last_stream[i] = local_stream(m, i, streams);
+        mp->launched[i] = 1;
     }
     // 1. every local device checksums its shard: rank 0 into place, the
     //    others into their local arrays
@@ -534,37 +510,26 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
         uint32_t *dst = mp->d_local[i] ? mp->d_local[i] : root_out;
         if (int rc = crc32c_plan_exec(mp->plans[i], dev_shards[i], dst, local_stream(m, i, streams))) return rc;
     }
-    // 2. one group of point-to-point transfers: each sending rank's whole
-    //    local array to rank 0's staging slot for it
-    bool any = false;
-    for (int r = 0; r < m->nranks; ++r)
-        if (sends(r, mp->self_send) && mp->local_nout[size_t(r)]) any = true;
-    if (!any) return mark_execs(mp, streams);
+    // 2. one group of point-to-point transfers: every sender's group ranges
+    //    from its local array, rank 0's receives straight into file order
+    if (mp->xfers.empty()) return 0;
     if (int rc = ensure_comms(m)) return rc;
     NCCL_TRY(rccl().GroupStart());
     ncclResult_t r = ncclSuccess;
     for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
         const hipStream_t s = local_stream(m, i, streams);
         const int me = m->ranks[i];
-        if (mp->d_local[i]) r = rccl().Send(mp->d_local[i], mp->local_nout[size_t(me)], ncclUint32, 0, m->comms[i], s);
-        if (me != 0) continue;
-        for (int peer = 0; peer < m->nranks && r == ncclSuccess; ++peer)
-            if (sends(peer, mp->self_send) && mp->local_nout[size_t(peer)])
-                r = rccl().Recv(mp->d_staging + mp->staging_off[size_t(peer)], mp->local_nout[size_t(peer)], ncclUint32,
-                             peer, m->comms[i], s);
+        for (const Xfer &x : mp->xfers) {
+            if (r != ncclSuccess) break;
+            if (x.rank == me) r = rccl().Send(mp->d_local[i] + x.local, x.count, ncclUint32, 0, m->comms[i], s);
+            if (me == 0 && r == ncclSuccess)
+                r = rccl().Recv(root_out + x.file, x.count, ncclUint32, x.rank, m->comms[i], s);
+        }
     }
     const ncclResult_t e = rccl().GroupEnd();
     NCCL_TRY(r);
     NCCL_TRY(e);
-    // 3. rank 0: the received groups into file order
-    if (mp->root_local >= 0 && mp->nscatter) {
-        const size_t i = size_t(mp->root_local);
-        DeviceGuard guard(m->ctxs[i]->device);
-        hipLaunchKernelGGL(scatter_groups, dim3(mp->nscatter), dim3(256), 0, local_stream(m, i, streams),
-                           mp->d_staging, mp->d_scatter, root_out);
-        HIP_TRY(hipGetLastError());
-    }
-    return mark_execs(mp, streams);
+    return 0;
 }
 
 int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
@@ -580,11 +545,6 @@ int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
             DeviceGuard guard(mp->m->ctxs[i]->device);
             (void)hipFree(mp->d_local[i]);
         }
-    }
-    if (mp->root_local >= 0) {
-        DeviceGuard guard(mp->m->ctxs[size_t(mp->root_local)]->device);
-        if (mp->d_staging) (void)hipFree(mp->d_staging);
-        if (mp->d_scatter) (void)hipFree(mp->d_scatter);
     }
     delete mp;
     return 0;

@@ -582,20 +582,24 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
             stage_bytes = 0;
             for (const auto &r : runs) stage_bytes += size_t(r.second - (r.first & ~uint64_t(15))) + 16;
         }
-        rc = grow_device(&s.d_payload, &s.payload_cap, stage_bytes + 16);
-        if (!rc && !(pinned && (ranged || by_runs))) rc = grow_pinned(&s.h_payload, &s.staging_cap, stage_bytes + 16);
-        if (rc) return rc;
         // 1. The payload copy goes first: it needs no plan, and the copy
         //    stream runs the slices' copies back to back.  (This stage's
         //    previous kernel is done: drain_stage waited for it.)
         //    A small batch (one slice) is not copied: the kernel reads it in
-        //    host memory (zero copy).
-        local.assign(pkts + i, pkts + j);
-        const uint8_t *kpayload = s.d_payload;
+        //    host memory (zero copy), and no device or pinned staging is
+        //    grown for it.
         // (pinned input: only small batches -- a CPU copy of 1 MiB already
         // costs what the copy command saves; 64 KiB: 22 vs 40 us per call)
         const bool zero_copy = ranged && i == 0 && j == npkts &&
                                (hi - lo) <= (pinned ? zero_copy_bytes() / 4 : zero_copy_bytes());
+        if (!zero_copy) {
+            rc = grow_device(&s.d_payload, &s.payload_cap, stage_bytes + 16);
+            if (!rc && !(pinned && (ranged || by_runs)))
+                rc = grow_pinned(&s.h_payload, &s.staging_cap, stage_bytes + 16);
+            if (rc) return rc;
+        }
+        local.assign(pkts + i, pkts + j);
+        const uint8_t *kpayload = s.d_payload;
         if (zero_copy) {  // (into mapped staging, which the kernel reads in place)
             rc = grow_mapped(&s.h_zc, &s.d_zc, &s.zc_cap, stage_bytes + 16);
             if (rc) return rc;

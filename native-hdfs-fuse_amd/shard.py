@@ -57,49 +57,41 @@ def plan_packets(pkts, group_packets: int, world: int, rank: int, flags: int = 0
     return _pkg().multi_rank_packets(pkts, group_packets, world, rank, flags)
 
 
-def gather_plan(pkts, group_packets: int, world: int, flags: int = 0):
-    """(local_nout, staging_off, scatter items {staging index, file index, count}) -- crc32c_multi_gather_plan."""
-    return _pkg().multi_gather_plan(pkts, group_packets, world, flags)
+def transfers(pkts, group_packets: int, world: int, flags: int = 0):
+    """(local_nout, transfers {sending rank, local index, file index, count}) -- crc32c_multi_transfers."""
+    return _pkg().multi_transfers(pkts, group_packets, world, flags)
 
 
 def gather_checksums(local, pkts, group_packets: int, world: int, rank: int, flags: int = 0):
     """The exchange of crc32c_multi_plan_exec, over torch.distributed: `local`
     is the u32 array this rank's plan wrote (a torch int32 tensor laid out by
     plan_packets -- rank 0's in place, indexed by global out index, unless
-    CRC32C_MULTI_SELF_SEND); every sending rank sends it whole in ONE send,
-    rank 0 receives each into its staging slot and applies the library's
-    scatter items to move every received group into file order -- the same
-    sends, receives and copies the library issues through RCCL and its scatter
-    kernel, driven by the library's own gather plan.  Returns the file's
+    CRC32C_MULTI_SELF_SEND).  The library's transfer list drives it exactly as
+    it drives the RCCL group: every sender sends each of its transfers' local
+    ranges, in list order, and rank 0 receives each straight into its
+    file-order place (no staging area, no copy).  Returns the file's
     checksums (np.uint32) on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
 
-    ln, so, items = gather_plan(pkts, group_packets, world, flags)
+    ln, xs = transfers(pkts, group_packets, world, flags)
     total = int(_pkg().total_checksums(pkts))
     ops = []
-    staging = None
+    full = None
     if rank == 0:
         full = torch.zeros(max(total, 1), dtype=torch.int32, device=local.device)
         if not ln[0]:  # rank 0 in place: its own groups are already at their file indices
             full[:min(total, local.numel())] = local[:total]
-        staging = torch.zeros(max(int((so + ln).max()) if world else 0, 1), dtype=torch.int32, device=local.device)
-        for r in range(world):
-            n = int(ln[r])
-            if not n:
-                continue
-            dst = staging[int(so[r]):int(so[r]) + n]
-            if r == 0:  # self-send: RCCL copies rank 0's array to its own staging slot
-                dst.copy_(local[:n])
-            else:
-                ops.append(dist.P2POp(dist.irecv, dst, r))
-    elif int(ln[rank]):
-        ops.append(dist.P2POp(dist.isend, local[:int(ln[rank])].contiguous(), 0))
+    for r, lo, fo, n in xs.astype(np.int64):
+        if r == rank and rank == 0:  # self-send: RCCL copies rank 0's range into its own output
+            full[fo:fo + n] = local[lo:lo + n]
+        elif r == rank:
+            ops.append(dist.P2POp(dist.isend, local[lo:lo + n].contiguous(), 0))
+        elif rank == 0:
+            ops.append(dist.P2POp(dist.irecv, full[fo:fo + n], int(r)))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     if rank != 0:
         return None
-    for src, dst, n in items.astype(np.int64):  # the scatter kernel, one group per item
-        full[dst:dst + n] = staging[src:src + n]
     return full[:total].cpu().numpy().view(np.uint32)

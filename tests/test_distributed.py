@@ -2,15 +2,14 @@
 
 The multi-GPU plan deals a file's blocks (groups of
 consecutive packets) round-robin over the ranks; each rank checksums its
-shard into one local u32 array, sends it to rank 0 in ONE send, and rank 0
-receives every array into a staging slot and scatters the groups into file
-order -- the path's only exchange.  Every part of that exchange that only
-N > 1 reaches is the library's own code here: each rank's shard and the
-packets its plan computes (payload offsets into the shard, out indices into
-its local array) come from crc32c_multi_layout / crc32c_multi_rank_packets,
-and the staging offsets and scatter items rank 0 applies from
-crc32c_multi_gather_plan -- the same host code crc32c_multi_plan_create
-builds its device plan from.  The checksums themselves come from the oracle
+shard into one local u32 array and sends each group's range, and rank 0
+receives every range straight into its file-order place -- the path's only
+exchange.  Every part of that exchange that only N > 1 reaches is the
+library's own code here: each rank's shard and the packets its plan
+computes (payload offsets into the shard, out indices into its local array)
+come from crc32c_multi_layout / crc32c_multi_rank_packets, and the transfer
+list both sides post from crc32c_multi_transfers -- the same host code
+crc32c_multi_plan_create builds its exec from.  The checksums themselves come from the oracle
 (the GPU ranks run the HIP kernel); the transfers are gloo send / receive in
 place of RCCL's.  Rank 0's assembled array must equal the reference's golden
 digest of config 4's 128 MiB file, or the oracle over the whole file, bit for
@@ -84,7 +83,7 @@ def _worker(rank: int, world: int, port: int, case: tuple, flags: int, result_pa
         lay, sb = shard.layout(pk, gp, world)
         assert set(int(x) for x in lay[:, 0]) <= set(range(world))
         payload = shard.rank_payload(file_bytes, lay, sb, rank)
-        ln, so, items = shard.gather_plan(pk, gp, world, flags)
+        ln, xs = shard.transfers(pk, gp, world, flags)
         mine = shard.plan_packets(pk, gp, world, rank, flags)
         in_place = rank == 0 and not ln[0]
         nlocal = total if in_place else int(ln[rank])
@@ -103,9 +102,9 @@ def _worker(rank: int, world: int, port: int, case: tuple, flags: int, result_pa
                 ok = hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"]
             else:
                 ok = bool(np.array_equal(got, oracle.Oracle().batch(file_bytes, pk, total)))
-            # every received group is one scatter item, every checksum covered exactly once
+            # the transfers and rank 0's in-place groups cover every checksum exactly once
             seen = np.zeros(total, np.int32)
-            for src, dst, n in items.astype(np.int64):
+            for _, _, dst, n in xs.astype(np.int64):
                 seen[dst:dst + n] += 1
             if in_place:
                 for p in mine:
@@ -123,7 +122,7 @@ def _worker(rank: int, world: int, port: int, case: tuple, flags: int, result_pa
     (2, ("f", 7, 512, False), 0), (2, ("f", 2, 4096, True), SELF_SEND), (3, ("f", 8, 512, True), 0),
     (2, ("f", 1, 512, False), 0), (3, ("f", 5, 1536, True), 0), (3, ("f", 5, 1536, True), SELF_SEND),
     (8, ("f", 11, 512, True), 0)])
-def test_library_gather_plan_matches_reference(tmp_path, world, case, flags):
+def test_library_transfers_match_reference(tmp_path, world, case, flags):
     import oracle
 
     oracle.build()
@@ -134,29 +133,39 @@ def test_library_gather_plan_matches_reference(tmp_path, world, case, flags):
         assert f.read() == "ok"
 
 
-def test_gather_plan_shape():
-    """crc32c_multi_gather_plan on config 4 at 8 ranks: 7 sending ranks of 4
-    blocks (32 768 checksums = 128 KiB each), staged back to back, 28 scatter
-    items of 8192 checksums; rank 0 in place sends nothing (with
-    CRC32C_MULTI_SELF_SEND it sends too: 32 items)."""
+def test_transfers_shape():
+    """crc32c_multi_transfers on config 4 at 8 ranks: 7 sending ranks of 4
+    blocks (32 768 checksums = 128 KiB local arrays), one transfer of 8192
+    checksums per block (28), each straight to its block's file index; rank 0
+    in place sends nothing.  With CRC32C_MULTI_SELF_SEND rank 0 sends too (32
+    transfers); on a one-rank communicator the self-send is ONE transfer
+    (consecutive groups merge)."""
     hdfs = load_package()
     hdfs.lib()
     import oracle
     from hdfs_crc32c_amd import shard
 
     pk = oracle.uniform_packets(2048, 65536, 512)
-    ln, so, items = shard.gather_plan(pk, 64, 8)
-    assert list(ln) == [0] + [32768] * 7 and list(so) == [0, 0] + [32768 * k for k in range(1, 7)]
-    assert items.shape == (28, 3) and set(items[:, 2]) == {8192}
-    # block g (on rank g % 8 > 0) lands at file index 8192 g from its rank's slot
-    for src, dst, n in items.astype(np.int64):
-        g = dst // 8192
-        assert g % 8 and src == so[g % 8] + (g // 8) * 8192
-    ln, so, items = shard.gather_plan(pk, 64, 8, SELF_SEND)
-    assert list(ln) == [32768] * 8 and items.shape == (32, 3)
+    ln, xs = shard.transfers(pk, 64, 8)
+    assert list(ln) == [0] + [32768] * 7
+    assert xs.shape == (28, 4) and set(xs[:, 3]) == {8192}
+    # block g (on rank g % 8 > 0) lands at file index 8192 g from local index (g // 8) * 8192
+    for r, lo, fo, n in xs.astype(np.int64):
+        g = fo // 8192
+        assert g % 8 == r and r > 0 and lo == (g // 8) * 8192
+    # posting order: for every sender, its transfers in file order
+    for r in range(1, 8):
+        mine = xs[xs[:, 0] == r]
+        assert np.all(np.diff(mine[:, 2].astype(np.int64)) > 0)
+    ln, xs = shard.transfers(pk, 64, 8, SELF_SEND)
+    assert list(ln) == [32768] * 8 and xs.shape == (32, 4)
     p0 = shard.plan_packets(pk, 64, 8, 0, SELF_SEND)
     assert p0.size == 256 and int(p0["out_idx"].max()) == 32768 - 128  # local indices when self-sending
     assert int(shard.plan_packets(pk, 64, 8, 0)["out_idx"].max()) == 2048 * 128 - 128 - 7 * 64 * 128  # global
+    ln, xs = shard.transfers(pk, 64, 1, SELF_SEND)
+    assert list(ln) == [262144] and xs.tolist() == [[0, 0, 0, 262144]]
+    ln, xs = shard.transfers(pk, 64, 1)
+    assert list(ln) == [0] and xs.shape == (0, 4)
 
 
 def test_layout_helpers():

@@ -327,10 +327,12 @@ def test_multi_plan_config4_rccl_gather(hdfs, golden, orc, self_send):
     """Config 4 through crc32c_multi_plan_*: a 128 MiB file as 32 x 4 MiB
     blocks dealt round-robin over the communicator's ranks (here every
     visible device, one process; the box has one), each rank checksumming
-    its shard device-resident, the u32 arrays gathered into file order on
-    rank 0 by RCCL send/recv + the scatter kernel: the golden c4 digest from
-    the reference.  With CRC32C_MULTI_SELF_SEND rank 0's own array travels
-    through RCCL too (a send to itself), so the transport runs on one GPU."""
+    its shard device-resident, every group's checksum range received by RCCL
+    straight into its file-order place on rank 0: the golden c4 digest from
+    the reference.  With CRC32C_MULTI_SELF_SEND rank 0's own checksums travel
+    through RCCL too (a send to itself), so the transport runs on one GPU.
+    Then the whole step (kernels + RCCL group) captured into a HIP graph and
+    replayed twice, as the bench's config-4 steps are."""
     torch = _torch()
     spec = [b for b in golden["batches"] if b["name"] == "c4_file_128MiB"][0]
     pk = golden_batch_packets(spec)
@@ -363,6 +365,21 @@ def test_multi_plan_config4_rccl_gather(hdfs, golden, orc, self_send):
     for s in streams:
         s.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), got)
+    if ndev == 1:
+        cs = torch.cuda.Stream()
+        mp.exec([t.data_ptr() for t in shards], out.data_ptr(), [cs.cuda_stream])  # (stream switch outside the capture)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=cs, capture_error_mode="thread_local"):
+            for _ in range(3):
+                mp.exec([t.data_ptr() for t in shards], out.data_ptr(), [cs.cuda_stream])
+        for _ in range(2):
+            out.zero_()
+            torch.cuda.synchronize()
+            graph.replay()
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), got)
+        del graph
     mp.close()
     m.close()
 
@@ -393,8 +410,8 @@ def test_multi_rank_mode_single_rank(hdfs, orc):
     mp.exec([shard.data_ptr()], out.data_ptr())
     m.sync()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, mp.nchecksums, big_endian=True))
-    # successive execs on alternating streams (they reuse the plan's staging
-    # buffers: each waits for the previous one), two different shards
+    # successive execs on alternating streams (they reuse the plan's local
+    # array: each waits for the previous one), two different shards
     torch_streams = [torch.cuda.Stream(), torch.cuda.Stream()]
     host2 = host.copy()
     host2[:host2.size - 16] ^= 0x5C
@@ -788,6 +805,43 @@ def test_block_queue_threads(hdfs, gpu_ctx, orc):
     plan.close()
 
 
+def test_block_queue_failed_flush_is_its_own(hdfs, gpu_ctx, orc):
+    """A flush whose issue fails (crc32c_debug_blocks_fail_flushes) fails
+    exactly its own tickets: the flush before it and every flush after it
+    succeed, bit-exact (one sticky queue error failed every later
+    write); and a submit after destroy began is refused, never queued."""
+    torch = _torch()
+    pk = _block_shape("full")
+    n = oracle.total_checksums(pk)
+    hosts = [oracle.xorshift64_bytes(64 * 65536, 9500 + k) for k in range(10)]
+    want = [orc.batch(h, pk, n) for h in hosts]
+    devs = [torch.from_numpy(h).cuda() for h in hosts]
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in hosts]
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    q = plan.blocks(max_blocks=4, window_us=10**6)
+    first = [q.submit(devs[i].data_ptr(), outs[i].data_ptr()) for i in range(4)]  # one full flush
+    for t in first:
+        q.wait(t)
+    q.debug_fail_flushes(1)
+    bad = [q.submit(devs[i].data_ptr(), outs[i].data_ptr()) for i in (4, 5)]
+    q.flush()
+    for t in bad:
+        with pytest.raises(hdfs.Crc32cError) as ei:
+            q.wait(t)
+        assert ei.value.rc == -5  # -EIO
+    later = [q.submit(devs[i].data_ptr(), outs[i].data_ptr()) for i in range(6, 10)]
+    for t in later + first:
+        q.wait(t)
+    for i in list(range(4)) + list(range(6, 10)):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), want[i]), i
+    for i in (4, 5):  # nothing was launched for the failed flush
+        assert not outs[i].cpu().numpy().any()
+    assert q.stats() == (3, 10)
+    q.close()
+    plan.close()
+
+
 def test_block_queue_ring_reuse_two_in_flight(hdfs, gpu_ctx, orc):
     """crc32c_blocks with more tickets than its ring has slots (1024): 16
     threads keep two blocks in flight each (submit the next, then wait for
@@ -843,6 +897,58 @@ def test_block_queue_ring_reuse_two_in_flight(hdfs, gpu_ctx, orc):
     flushes, blocks = q.stats()
     assert blocks == nthreads * per and flushes <= blocks, (flushes, blocks)
     q.close()
+    plan.close()
+
+
+def test_verify_overlapping_launches_terminate(hdfs, gpu_ctx, orc):
+    """The one verify overlap the library cannot order: a graph of captured
+    verify launches replayed on one stream while the same plan is verified
+    directly on another (a mismatching workgroup then waited for
+    its launch's key forever).  With mismatches in every launch, both streams
+    must finish (the key wait is bounded); every result is either exact or
+    flagged CRC32C_VERIFY_OVERLAP; a verify after both is exact again."""
+    torch = _torch()
+    pk = oracle.uniform_packets(1024)
+    n = oracle.total_checksums(pk)
+    payload = oracle.xorshift64_bytes(int(pk["payload_off"][-1] + pk["len"][-1]) + 16, 4242)
+    want = orc.batch(payload, pk, n)
+    dpay = torch.from_numpy(payload).cuda()
+    bad_idx = np.arange(5, n, n // 97)  # mismatches spread over most workgroups
+    badv = want.copy()
+    badv[bad_idx] ^= 0x0F0F
+    bad = torch.from_numpy(badv.view(np.int32)).cuda()
+    expect = (len(bad_idx), int(bad_idx.min()))
+    plan = gpu_ctx.plan(pk)
+    cap, direct = torch.cuda.Stream(), torch.cuda.Stream()
+    nl = 6
+    gres = [torch.zeros(2, dtype=torch.int32, device="cuda") for _ in range(nl)]
+    dres = [torch.zeros(2, dtype=torch.int32, device="cuda") for _ in range(nl)]
+    plan.verify(dpay.data_ptr(), bad.data_ptr(), gres[0].data_ptr(), cap.cuda_stream)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        for r in gres:
+            plan.verify(dpay.data_ptr(), bad.data_ptr(), r.data_ptr(), cap.cuda_stream)
+    torch.cuda.synchronize()
+    replay = torch.cuda.Stream()
+    with torch.cuda.stream(replay):
+        g.replay()  # (not on the capture stream: the plan's ordering cannot see it)
+    for r in dres:
+        plan.verify(dpay.data_ptr(), bad.data_ptr(), r.data_ptr(), direct.cuda_stream)
+    torch.cuda.synchronize()
+    flagged = 0
+    for r in gres + dres:
+        c, first = (int(x) for x in r.cpu().numpy().view(np.uint32))
+        if c & hdfs.CRC32C_VERIFY_OVERLAP:
+            flagged += 1
+        else:
+            assert (c, first) == expect
+    print("overlap-flagged results: %d of %d" % (flagged, 2 * nl))
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    plan.verify(dpay.data_ptr(), bad.data_ptr(), res.data_ptr(), direct.cuda_stream)
+    torch.cuda.synchronize()
+    assert tuple(int(x) for x in res.cpu().numpy().view(np.uint32)) == expect
+    del g
     plan.close()
 
 

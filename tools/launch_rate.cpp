@@ -10,12 +10,24 @@
 //   tools/launch_rate [packets=64] [launches=4000]
 //   tools/launch_rate write [iterations=2000]
 //   tools/launch_rate raw [launches=4000]   (an empty kernel: HIP's own launch cost)
-// prints one JSON line.  `write`: one FUSE-shaped 4 MiB block write per
+//   tools/launch_rate calls [packets=64] [launches=4000]
+// prints one JSON line.  `calls`: per call kind on the same plan, host issue
+// time and GPU time per launch -- exec, verify (crc32c_plan_verify), verify
+// with a mismatch bitmap (crc32c_plan_verify_bitmap), exec followed by a
+// hipEventRecord of a timing-disabled event (the price of a completion record
+// per launch), exec + hipStreamIsCapturing.
+//   tools/launch_rate multi [packets=256] [steps=2000]
+// config 4's per-rank step at N = 8 on one GPU (a 16 MiB shard = 4 blocks of
+// 64 packets): crc32c_plan_exec of the shard, crc32c_multi_plan_exec in place
+// (no RCCL call) and with CRC32C_MULTI_SELF_SEND (the shard's checksums
+// through one RCCL send/recv group, as a peer's gather), each host-issued and
+// replayed from a HIP graph of 100 steps (kernels + RCCL group captured).  `write`: one FUSE-shaped 4 MiB block write per
 // iteration (TRUNCATE / NULLPADDING / THEDATA / TRAILINGDATA buffers,
 // src/fuse.c:1348-1354) through crc32c_plan_create_buffers -> exec ->
 // stream sync -> destroy: the per-write host cost of the buffer-list path.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -131,9 +143,185 @@ static int write_mode(int iters) {
     return 0;
 }
 
+// One call kind timed like main's exec loop: warm-up, then n calls between
+// two events; host issue time and GPU time per call.
+template <class F>
+static int time_calls(const char *name, hipStream_t s, int n, F call, bool first) {
+    for (int i = 0; i < 300; ++i)
+        if (call(i)) return 1;
+    if (hipStreamSynchronize(s) != hipSuccess) return 1;
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess);
+    CHECK(hipEventRecord(e0, s) == hipSuccess);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; ++i)
+        if (call(i)) return 1;
+    const auto t1 = std::chrono::steady_clock::now();
+    CHECK(hipEventRecord(e1, s) == hipSuccess);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess);
+    std::printf("%s\"%s\": {\"host_issue_us\": %.3f, \"gpu_us_per_launch\": %.3f}", first ? "" : ", ", name,
+                std::chrono::duration<double, std::micro>(t1 - t0).count() / n, ms * 1e3 / n);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+static int calls_mode(size_t npk, int n) {
+    const uint32_t len = 65536, bpc = 512;
+    std::vector<crc32c_packet> pk(npk);
+    for (size_t i = 0; i < npk; ++i) pk[i] = crc32c_packet{uint64_t(i) * len, uint64_t(i) * (len / bpc), len, bpc};
+    crc32c_ctx *ctx = nullptr;
+    CHECK(crc32c_ctx_create(0, &ctx) == 0);
+    crc32c_plan *plan = nullptr;
+    CHECK(crc32c_plan_create(ctx, pk.data(), npk, 0, &plan) == 0);
+    const size_t bytes = npk * len, nsums = npk * (len / bpc);
+    void *src = nullptr;
+    uint32_t *dst = nullptr, *res = nullptr, *bits = nullptr;
+    CHECK(hipMalloc(&src, bytes) == hipSuccess);
+    CHECK(hipMemset(src, 0x5a, bytes) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&dst), nsums * 4) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&res), 64) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&bits), (nsums + 31) / 32 * 4) == hipSuccess);
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    CHECK(crc32c_plan_exec(plan, src, dst, s) == 0);  // expected values for the verifies
+    hipEvent_t ev;
+    CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess);
+    std::printf("{\"mode\": \"calls\", \"packets\": %zu, \"launches\": %d, ", npk, n);
+    int rc = time_calls("exec", s, n, [&](int) { return crc32c_plan_exec(plan, src, dst + 0, s); }, true);
+    rc = rc || time_calls("verify", s, n, [&](int) { return crc32c_plan_verify(plan, src, dst, res, s); }, false);
+    rc = rc || time_calls("verify_bitmap", s, n,
+                          [&](int) { return crc32c_plan_verify_bitmap(plan, src, dst, res, bits, s); }, false);
+    rc = rc || time_calls("exec_event_record", s, n, [&](int) {
+             return crc32c_plan_exec(plan, src, dst, s) || hipEventRecord(ev, s) != hipSuccess;
+         }, false);
+    rc = rc || time_calls("exec_is_capturing", s, n, [&](int) {
+             hipStreamCaptureStatus cs;
+             return crc32c_plan_exec(plan, src, dst, s) || hipStreamIsCapturing(s, &cs) != hipSuccess;
+         }, false);
+    uint32_t host_res[2] = {1, 1};
+    CHECK(hipMemcpy(host_res, res, 8, hipMemcpyDeviceToHost) == hipSuccess);
+    std::printf(", \"verify_clean\": %s}\n", (host_res[0] == 0 && host_res[1] == 0xFFFFFFFFu) ? "true" : "false");
+    (void)hipEventDestroy(ev);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    (void)hipFree(res);
+    (void)hipFree(bits);
+    crc32c_plan_destroy(plan);
+    crc32c_ctx_destroy(ctx);
+    return rc;
+}
+
+// Host-issued and graph-replayed time per step of `step` on stream s.
+template <class F>
+static int time_step(const char *name, hipStream_t s, int n, F step) {
+    for (int i = 0; i < 200; ++i)
+        if (step()) return 1;
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess);
+    CHECK(hipEventRecord(e0, s) == hipSuccess);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n; ++i)
+        if (step()) return 1;
+    const auto t1 = std::chrono::steady_clock::now();
+    CHECK(hipEventRecord(e1, s) == hipSuccess);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess);
+    const double issue = std::chrono::duration<double, std::micro>(t1 - t0).count() / n, eager = ms * 1e3 / n;
+    // the same steps captured into one graph (100 steps) and replayed
+    const int per = 100, reps = std::max(1, n / per);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess);
+    int rc = 0;
+    for (int i = 0; i < per && !rc; ++i) rc = step();
+    const hipError_t ce = hipStreamEndCapture(s, &g);
+    if (rc || ce != hipSuccess || hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) {
+        std::printf("\"%s\": {\"host_issue_us\": %.3f, \"eager_us\": %.3f, \"graph\": \"capture failed (rc %d, %d)\"}, ",
+                    name, issue, eager, rc, int(ce));
+        (void)hipGetLastError();
+        return 0;
+    }
+    CHECK(hipGraphLaunch(ge, s) == hipSuccess);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    CHECK(hipEventRecord(e0, s) == hipSuccess);
+    for (int r = 0; r < reps; ++r) CHECK(hipGraphLaunch(ge, s) == hipSuccess);
+    CHECK(hipEventRecord(e1, s) == hipSuccess);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    CHECK(hipEventElapsedTime(&ms, e0, e1) == hipSuccess);
+    std::printf("\"%s\": {\"host_issue_us\": %.3f, \"eager_us\": %.3f, \"graph_us\": %.3f}, ", name, issue, eager,
+                ms * 1e3 / (reps * per));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}
+
+static int multi_mode(size_t npk, int n) {
+    const uint32_t len = 65536, bpc = 512;
+    std::vector<crc32c_packet> pk(npk);
+    for (size_t i = 0; i < npk; ++i) pk[i] = crc32c_packet{uint64_t(i) * len, uint64_t(i) * (len / bpc), len, bpc};
+    const size_t bytes = npk * len, nsums = npk * (len / bpc);
+    void *src = nullptr;
+    uint32_t *out = nullptr;
+    CHECK(hipMalloc(&src, bytes + 64) == hipSuccess);
+    CHECK(hipMemset(src, 0x3c, bytes + 64) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&out), nsums * 4) == hipSuccess);
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    std::printf("{\"mode\": \"multi\", \"packets\": %zu, \"steps\": %d, ", npk, n);
+    crc32c_ctx *ctx = nullptr;
+    CHECK(crc32c_ctx_create(0, &ctx) == 0);
+    crc32c_plan *plan = nullptr;
+    CHECK(crc32c_plan_create(ctx, pk.data(), npk, 0, &plan) == 0);
+    CHECK(crc32c_plan_exec(plan, src, out, s) == 0);
+    if (time_step("shard_plan_exec", s, n, [&] { return crc32c_plan_exec(plan, src, out, s); })) return 1;
+    std::vector<uint32_t> want(nsums), got(nsums);
+    CHECK(hipStreamSynchronize(s) == hipSuccess);
+    CHECK(hipMemcpy(want.data(), out, nsums * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    crc32c_plan_destroy(plan);
+    crc32c_ctx_destroy(ctx);
+    bool exact = true;
+    for (uint32_t flags : {0u, CRC32C_MULTI_SELF_SEND}) {
+        crc32c_multi *m = nullptr;
+        const int dev = 0;
+        CHECK(crc32c_multi_create(&dev, 1, &m) == 0);
+        crc32c_multi_plan *mp = nullptr;
+        CHECK(crc32c_multi_plan_create(m, pk.data(), npk, 64, flags, &mp) == 0);
+        const void *shards[1] = {src};
+        void *streams[1] = {s};
+        CHECK(hipMemset(out, 0, nsums * 4) == hipSuccess);
+        CHECK(crc32c_multi_plan_exec(mp, shards, out, streams) == 0);  // (creates the communicator)
+        CHECK(hipStreamSynchronize(s) == hipSuccess);
+        CHECK(hipMemcpy(got.data(), out, nsums * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        exact = exact && got == want;
+        if (time_step(flags ? "multi_self_send" : "multi_in_place", s, n,
+                      [&] { return crc32c_multi_plan_exec(mp, shards, out, streams); }))
+            return 1;
+        CHECK(hipStreamSynchronize(s) == hipSuccess);
+        CHECK(hipMemcpy(got.data(), out, nsums * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        exact = exact && got == want;
+        crc32c_multi_plan_destroy(mp);
+        crc32c_multi_destroy(m);
+    }
+    std::printf("\"exact\": %s}\n", exact ? "true" : "false");
+    (void)hipFree(src);
+    (void)hipFree(out);
+    return exact ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "write") return write_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
     if (argc > 1 && std::string(argv[1]) == "raw") return raw_mode(argc > 2 ? std::atoi(argv[2]) : 4000);
+    if (argc > 1 && std::string(argv[1]) == "multi")
+        return multi_mode(argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 256, argc > 3 ? std::atoi(argv[3]) : 2000);
+    if (argc > 1 && std::string(argv[1]) == "calls")
+        return calls_mode(argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 64, argc > 3 ? std::atoi(argv[3]) : 4000);
     const size_t npk = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 64;
     const int n = argc > 2 ? std::atoi(argv[2]) : 4000;
     const uint32_t len = 65536, bpc = 512;

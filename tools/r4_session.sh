@@ -1,0 +1,32 @@
+#!/usr/bin/env bash
+# Round-4 GPU session steps (each step under its own time limit; a crash,
+# timeout or signal ends the session).  STEPS selects them.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-r4}
+mkdir -p $OUT
+export TMPDIR=/tmp
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -4 $OUT/$name.log
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-calls multi}; do
+  case $s in
+    calls) run calls 120 tools/launch_rate calls 64 4000 ;;
+    multi) run multi 180 tools/launch_rate multi 256 2000 ;;
+    multiprof) run multiprof 300 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/multiprof -o run --output-format csv -- tools/launch_rate multi 256 1000 ;;
+    tmulti) run tmulti 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "multi" ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    bench20) run bench20 600 python bench.py --steps 20 --warmup 5 ;;
+    c4model) run c4model 300 python tools/c4_model.py ;;
+  esac
+done
+echo "session done"
