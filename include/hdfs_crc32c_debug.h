@@ -81,6 +81,20 @@ const char *crc32c_debug_variant_name(int variant, int *exact);
 int crc32c_debug_stream_probe(const void *dev_src, uint64_t bytes, uint32_t *dev_out, uint32_t grid, int shape,
                               void *stream);
 
+/* A/B experiment: a RESIDENT kernel for concurrent block writes (see
+ * debug/resident.hip).  The kernel stays on the GPU (all CUs, tables staged
+ * once) and takes blocks from a ring the submitting threads fill; it exits on
+ * destroy, after idle_us (0: 2000) with nothing queued, or when stuck, and
+ * submit / wait relaunch it on demand.  The plan must be aligned
+ * power-of-two tiles only (one block's shape); payloads 16-byte aligned.
+ * While it runs it holds every CU's LDS: other kernels wait. */
+typedef struct crc32c_resident crc32c_resident;
+int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_resident **out);
+int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket);
+int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket);
+int crc32c_debug_resident_stats(const crc32c_resident *r, uint64_t *launches);
+int crc32c_debug_resident_destroy(crc32c_resident *r);
+
 #ifdef __cplusplus
 }
 #endif

@@ -137,10 +137,11 @@ extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev
     p.stamps = dev_stamps;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lock(plan->mu);
-    if (int rc = prepare_launch(plan, s)) return rc;
+    bool capturing = false;
+    if (int rc = prepare_launch(plan, s, &capturing)) return rc;
     HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
                          : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));
-    return 0;
+    return capturing ? 0 : mark_launch(plan, s);
 }
 
 extern "C" const char *crc32c_debug_variant_name(int variant, int *exact) {

@@ -1,0 +1,429 @@
+// resident.hip -- A/B experiment (libhdfs_crc32c_debug.so only): a
+// bounded-lifetime RESIDENT checksum kernel for concurrent block writes.
+//
+// libfuse writes one 4 MiB block per hadoop_fuse_write_block call on many
+// worker threads (src/fuse.c:336-449, fuse.c:1771).  One launch per block
+// costs ~4.3 us of fixed work per launch (kernel boundary, table staging,
+// tail: DESIGN.md section 5), which caps 16 writers with one block each at
+// 1.8 us per block through the group-commit queue (crc32c_blocks).  Here the
+// kernel stays on the GPU instead: tables staged ONCE per launch, blocks
+// pulled from a ring the submitting threads fill, completion written to
+// host memory -- no launch per block at all.
+//
+// Protocol (all host words in pinned, device-mapped, coherent memory):
+//  * submit (host): ticket t = an atomic counter; slot t % kRing is reused
+//    only once block t - kRing is complete; payload / out pointers, then
+//    hseq[slot] = t + 1.
+//  * forwarder (workgroup 0's last wave): reads 64 slots' hseq per poll
+//    (one PCIe round trip per poll, not per block), copies the ready
+//    blocks' pointers into a device ring and publishes dseq[slot] = t + 1
+//    (agent scope).  It also collects: block t is complete when all
+//    workgroups' flags for its slot hold t + 1 (one 1 KiB load per check),
+//    then hdone[slot] = t + 1 (system scope).
+//  * workers (waves 0-10 of every workgroup): block t is run by phase t % 5
+//    (5 blocks in flight); within a phase two waves per workgroup take one
+//    8 KiB tile each (a 4 MiB block is 512 tiles = 2 per CU); a workgroup's
+//    phase workers count themselves in LDS and the last one stores the
+//    workgroup's flag.  Checksums are stored write-through (system scope),
+//    and every store has completed before the flag.
+//  * lifetime: the forwarder exits on the host's stop word, after idle_us
+//    with nothing queued, or after kStuckMs without progress while blocks are
+//    outstanding (a workgroup that never got a CU); on exit it raises the
+//    device stop word that every worker polls, and records where it stopped
+//    (exit_col) so a relaunch resumes there.  The host relaunches the kernel
+//    on demand (submit, or a waiter that waits long), never while one runs.
+//    Workers have their own bound (kWorkerMs without a block).  Every wave
+//    therefore exits, whatever the host does.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <thread>
+
+#include "../crc32c_device.h"
+#include "../runtime_internal.h"
+#include "hdfs_crc32c_debug.h"
+
+namespace {
+
+using namespace hdfs_crc_dev;
+
+constexpr uint32_t kRing = 64;       // tickets in flight at most
+constexpr uint32_t kPhases = 5;      // blocks processed concurrently
+constexpr uint32_t kWaves = 12;      // 768 threads, one workgroup per CU (152 KiB LDS)
+constexpr uint32_t kWorkers = kWaves - 1;
+constexpr uint32_t kMaxWg = 256;     // one flag lane-dword per workgroup (64 lanes x 4)
+constexpr uint64_t kTicksPerUs = 100;  // s_memrealtime: 100 MHz
+constexpr uint64_t kStuckMs = 50;
+constexpr uint64_t kWorkerMs = 200;
+
+struct HostRing {
+    uint64_t seq[kRing];      // host: ticket + 1 once payload / out hold the ticket's block
+    uint64_t payload[kRing];
+    uint64_t out[kRing];
+    uint64_t done[kRing];     // kernel: ticket + 1 once the block's checksums are stored
+    uint32_t stop;            // host: exit now
+    uint32_t pad0[15];
+    uint64_t exit_col;        // kernel (at exit): tickets below this are complete
+    uint64_t exits;           // kernel: launches that have exited
+};
+
+struct DevRing {
+    uint64_t seq[kRing];
+    uint64_t payload[kRing];
+    uint64_t out[kRing];
+    uint32_t flag[kRing][kMaxWg];  // per slot and workgroup: ticket + 1 once its workers are done
+    uint32_t stop;
+};
+
+struct RParams {
+    HostRing *h;
+    DevRing *d;
+    const FastTile *tiles;
+    const uint8_t *table_s4;
+    uint32_t ntiles;
+    uint32_t flags;
+    uint32_t c_lg[5];
+    uint64_t first;       // first ticket this launch forwards
+    uint64_t idle_ticks;  // forwarder: exit after this long with nothing queued
+};
+
+template <typename T>
+__device__ __forceinline__ T ld_sys(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ T ld_dev(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sys(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void st_dev(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// One power-of-two tile of a block (the plan's block shape; offsets relative
+// to the block's payload / checksum array): the production tile's loads,
+// lookups and reduce, stores write-through.
+__device__ __forceinline__ void run_tile(const RParams &p, const uint8_t *lds, const uint8_t *payload,
+                                         uint32_t *out, uint32_t idx, int lane) {
+    typedef const __attribute__((address_space(4))) FastTile *CT;
+    const CT tp = (CT)(p.tiles) + idx;
+    const FastTile t{tp->src, tp->out, tp->meta};
+    const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu;
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(payload + t.src, nb * 512u);
+    uint4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16u * uint32_t(lane) + 1024u * i, 0, 2);
+        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t pc[8];
+    tile_pieces<0, true, kImgFull>(lds, v, pc, lane, NoPrep{});
+    uint32_t x = block_lin(pc, lane);
+    const uint32_t blk = rep_block(lane);
+    if (lg) {
+        const uint32_t nbc = 1u << lg;
+        const uint32_t s = nbc - 1u - (blk & (nbc - 1u));
+        if (s) x = zshift<true, kImgFull>(lds, s, x);
+        x ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), 32));
+        if (lg >= 2) x ^= dpp<kDppXor8>(x);
+        if (lg >= 3) x ^= dpp<kDppXor2>(x);
+        if (lg >= 4) x ^= dpp<kDppXor1>(x);
+    }
+    if (rep_lane(lane, blk, nb, lg)) {
+        typedef __attribute__((address_space(1))) uint32_t *GU32;  // (a global store, not a flat one)
+        __hip_atomic_store((GU32)(out + t.out + (blk >> lg)), out_order(x ^ p.c_lg[lg], p.flags), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__device__ void forwarder(const RParams &p, int lane) {
+    HostRing *h = p.h;
+    DevRing *d = p.d;
+    uint64_t fwd = p.first, col = p.first;
+    uint64_t last = now();
+    const uint32_t ng = gridDim.x;
+    for (;;) {
+        bool progress = false;
+        // forward: the next 64 tickets' slots, one load per lane (ring reuse:
+        // ticket t only once t - kRing is complete)
+        const uint64_t cand = fwd + uint64_t(lane);
+        const bool room = cand < col + kRing;
+        const uint64_t s = room ? ld_sys(&h->seq[cand % kRing]) : 0;
+        const uint64_t ready = __ballot(room && s == cand + 1);
+        const uint32_t n = ~ready ? uint32_t(__builtin_ctzll(~ready)) : 64u;  // consecutive ready tickets from fwd
+        if (n) {
+            if (uint32_t(lane) < n) {
+                const uint32_t sl = uint32_t(cand % kRing);
+                const uint64_t pay = ld_sys(&h->payload[sl]), o = ld_sys(&h->out[sl]);
+                st_dev(&d->payload[sl], pay);
+                st_dev(&d->out[sl], o);
+                wait_vmem();  // (the pointers have landed before the sequence word)
+                st_dev(&d->seq[sl], cand + 1);
+            }
+            fwd += n;
+            progress = true;
+        }
+        // collect: the (up to 8) oldest outstanding blocks' workgroup flags,
+        // loaded together; completed in ticket order
+        {
+            constexpr uint32_t kCheck = 8;
+            const uint64_t nout = fwd - col;
+            uint32_t f[kCheck][4];
+#pragma unroll
+            for (uint32_t c = 0; c < kCheck; ++c)
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k) {
+                    const uint32_t wg = 4u * uint32_t(lane) + k;
+                    f[c][k] = (c < nout && wg < ng) ? ld_dev(&d->flag[(col + c) % kRing][wg]) : 0u;
+                }
+#pragma unroll
+            for (uint32_t c = 0; c < kCheck; ++c) {
+                if (c >= nout) break;
+                const uint32_t want = uint32_t(col + 1);
+                bool ok = true;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k)
+                    if (4u * uint32_t(lane) + k < ng && f[c][k] != want) ok = false;
+                if (__ballot(!ok)) break;
+                if (lane == 0) st_sys(&h->done[col % kRing], col + 1);
+                ++col;
+                progress = true;
+            }
+        }
+        const uint64_t t = now();
+        if (progress) {
+            last = t;
+            continue;
+        }
+        if (ld_sys(&h->stop)) break;
+        if (col == fwd && t - last > p.idle_ticks) break;          // idle
+        if (col < fwd && t - last > kStuckMs * 1000 * kTicksPerUs) break;  // no progress: give up
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+        st_dev(&d->stop, 1u);
+        st_sys(&h->exit_col, col);
+        wait_vmem();
+        st_sys(&h->exits, ld_sys(&h->exits) + 1);
+    }
+}
+
+__global__ __launch_bounds__(kWaves * 64, 3) void resident_kernel(RParams p) {
+    constexpr uint32_t kStage = kS4StageBytes;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 4 * kRing];
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(lds + kStage);  // per slot: this workgroup's workers done
+    const int lane = int(threadIdx.x & 63u);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    constexpr uint32_t kChunks = kStage / 1024u;
+    const uint32_t rot = (blockIdx.x * 37u) % kChunks;
+    for (uint32_t i = wv; i < kChunks; i += kWaves) {
+        const uint32_t c = i + rot < kChunks ? i + rot : i + rot - kChunks;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)(p.table_s4 + c * 1024u + 16u * uint32_t(lane)),
+            (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
+    }
+    if (threadIdx.x < kRing) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+    if (wv == kWaves - 1) {
+        if (blockIdx.x == 0) forwarder(p, lane);
+        return;
+    }
+    // Worker: phase (b + w) % 5; the workgroup's waves of a phase (2 or 3)
+    // rank in wave order; the first two take tiles 2b, 2b + 1 (+ 2G, ...).
+    const uint32_t b = blockIdx.x, G = gridDim.x;
+    const uint32_t phase = (b + wv) % kPhases;
+    uint32_t rank = 0, expect = 0;
+    for (uint32_t w = 0; w < kWorkers; ++w)
+        if ((b + w) % kPhases == phase) {
+            if (w < wv) ++rank;
+            ++expect;
+        }
+    DevRing *d = p.d;
+    uint64_t j = p.first + (phase + kPhases - uint32_t(p.first % kPhases)) % kPhases;  // first block of the phase
+    uint64_t last = now();
+    for (;;) {
+        const uint32_t sl = uint32_t(j % kRing);
+        bool stop = false;
+        for (uint32_t polls = 0;; ++polls) {
+            if (ld_dev(&d->seq[sl]) == j + 1) break;
+            if ((polls & 15u) == 15u && (ld_dev(&d->stop) || now() - last > kWorkerMs * 1000 * kTicksPerUs)) {
+                stop = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (stop) break;
+        const uint8_t *payload = reinterpret_cast<const uint8_t *>(ld_dev(&d->payload[sl]));
+        uint32_t *out = reinterpret_cast<uint32_t *>(ld_dev(&d->out[sl]));
+        if (rank < 2)
+            for (uint32_t idx = 2u * b + rank; idx < p.ntiles; idx += 2u * G) run_tile(p, lds, payload, out, idx, lane);
+        wait_vmem();  // (this wave's checksum stores have completed)
+        if (lane == 0) {
+            const uint32_t old = atomicAdd(&lcnt[sl], 1u);
+            if (old + 1u == expect) {
+                lcnt[sl] = 0;
+                st_dev(&d->flag[sl][b], uint32_t(j + 1));
+            }
+        }
+        j += kPhases;
+        last = now();
+    }
+}
+
+}  // namespace
+
+struct crc32c_resident {
+    crc32c_plan *plan = nullptr;
+    int device = 0;
+    uint32_t grid = 0;
+    uint64_t idle_ticks = 0;
+    HostRing *h = nullptr;    // host view
+    HostRing *h_dev = nullptr;  // the same memory, device view
+    DevRing *d = nullptr;
+    hipStream_t stream = nullptr;
+    std::atomic<uint64_t> next{0};
+    std::mutex mu;           // launches
+    bool running = false;    // a launch may be on the GPU (under mu)
+    uint64_t launches = 0;
+};
+
+namespace {
+
+// Launches the kernel unless one is running (caller holds r->mu).  A launch
+// that has exited shows as an idle stream.
+int ensure_running(crc32c_resident *r) {
+    if (r->running) {
+        const hipError_t q = hipStreamQuery(r->stream);
+        if (q == hipErrorNotReady) return 0;
+        if (q != hipSuccess) return hdfs_crc::fail(-EIO, "resident kernel: %s", hipGetErrorString(q));
+        r->running = false;
+    }
+    const uint64_t col = __atomic_load_n(&r->h->exit_col, __ATOMIC_ACQUIRE);
+    if (col >= r->next.load(std::memory_order_acquire)) return 0;  // nothing queued
+    hdfs_crc::KParams kp = hdfs_crc::plan_params(r->plan, nullptr, nullptr);
+    RParams p{};
+    p.h = r->h_dev;
+    p.d = r->d;
+    p.tiles = kp.tiles;
+    p.table_s4 = kp.table_s4;
+    p.ntiles = kp.ntiles;
+    p.flags = kp.flags;
+    for (int i = 0; i < 5; ++i) p.c_lg[i] = kp.c_lg[i];
+    p.first = col;
+    p.idle_ticks = r->idle_ticks;
+    hdfs_crc::DeviceGuard guard(r->device);
+    HIP_TRY(hipMemsetAsync(&r->d->stop, 0, sizeof(uint32_t), r->stream));
+    hipLaunchKernelGGL(resident_kernel, dim3(r->grid), dim3(kWaves * 64), 0, r->stream, p);
+    HIP_TRY(hipGetLastError());
+    r->running = true;
+    ++r->launches;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_resident **out) {
+    using namespace hdfs_crc;
+    if (!plan || !out) return fail(-EINVAL, "plan/out == NULL");
+    *out = nullptr;
+    const DevicePlan &dp = plan->dp;
+    if (dp.ngen || dp.nseg || dp.nconst || dp.general || dp.misaligned || !dp.ntiles || plan->absolute)
+        return fail(-EINVAL, "the resident kernel runs plans of aligned power-of-two tiles only");
+    std::unique_ptr<crc32c_resident, int (*)(crc32c_resident *)> r(new crc32c_resident, crc32c_debug_resident_destroy);
+    r->plan = plan;
+    r->device = plan->ctx->device;
+    r->grid = uint32_t(std::min(plan->ctx->num_cu, int(kMaxWg)));
+    r->idle_ticks = uint64_t(idle_us ? idle_us : 2000) * kTicksPerUs;
+    hdfs_crc::DeviceGuard guard(r->device);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&r->h), sizeof(HostRing), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(static_cast<void *>(r->h), 0, sizeof(HostRing));
+    void *hd = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&hd, r->h, 0));
+    r->h_dev = static_cast<HostRing *>(hd);
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&r->d), sizeof(DevRing)));
+    HIP_TRY(hipMemset(r->d, 0, sizeof(DevRing)));
+    HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    // (the plan's descriptors are uploaded on the context's upload stream)
+    if (plan->dp.uploaded) HIP_TRY(hipStreamWaitEvent(r->stream, plan->dp.uploaded, 0));
+    *out = r.release();
+    return 0;
+}
+
+int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
+    using namespace hdfs_crc;
+    if (!r || !dev_payload || !dev_out) return fail(-EINVAL, "bad arguments");
+    if (reinterpret_cast<uintptr_t>(dev_payload) & 15u) return fail(-EINVAL, "payload must be 16-byte aligned");
+    const uint64_t t = r->next.fetch_add(1, std::memory_order_acq_rel);
+    const uint32_t sl = uint32_t(t % kRing);
+    // the slot's previous block (t - kRing) must be complete
+    if (t >= kRing)
+        while (__atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE) < t - kRing + 1) {
+            if (int rc = crc32c_debug_resident_wait(r, t - kRing)) return rc;
+        }
+    r->h->payload[sl] = reinterpret_cast<uint64_t>(dev_payload);
+    r->h->out[sl] = reinterpret_cast<uint64_t>(dev_out);
+    __atomic_store_n(&r->h->seq[sl], t + 1, __ATOMIC_RELEASE);
+    if (ticket) *ticket = t;
+    std::lock_guard<std::mutex> lock(r->mu);
+    return ensure_running(r);
+}
+
+int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket) {
+    using namespace hdfs_crc;
+    if (!r) return fail(-EINVAL, "resident == NULL");
+    if (ticket >= r->next.load(std::memory_order_acquire)) return fail(-EINVAL, "ticket never handed out");
+    const uint32_t sl = uint32_t(ticket % kRing);
+    auto t0 = std::chrono::steady_clock::now();
+    const auto deadline = t0 + std::chrono::seconds(5);
+    for (uint32_t i = 0;; ++i) {
+        const uint64_t v = __atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE);
+        if (v >= ticket + 1) return 0;  // (a later ticket in the slot implies this one completed)
+        if ((i & 255u) == 255u) {
+            const auto t = std::chrono::steady_clock::now();
+            if (t > deadline) return fail(-ETIMEDOUT, "resident kernel: block %llu not done", (unsigned long long)ticket);
+            if (t - t0 > std::chrono::microseconds(100)) {  // the kernel may have exited: relaunch it
+                std::lock_guard<std::mutex> lock(r->mu);
+                if (int rc = ensure_running(r)) return rc;
+                t0 = t;
+            }
+            std::this_thread::yield();
+        } else {
+            __builtin_ia32_pause();
+        }
+    }
+}
+
+int crc32c_debug_resident_stats(const crc32c_resident *r, uint64_t *launches) {
+    if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
+    if (launches) *launches = r->launches;
+    return 0;
+}
+
+int crc32c_debug_resident_destroy(crc32c_resident *r) {
+    if (!r) return 0;
+    if (r->h) __atomic_store_n(&r->h->stop, 1u, __ATOMIC_RELEASE);
+    hdfs_crc::DeviceGuard guard(r->device);
+    if (r->stream) {
+        (void)hipStreamSynchronize(r->stream);  // (the kernel exits on the stop word)
+        (void)hipStreamDestroy(r->stream);
+    }
+    if (r->d) (void)hipFree(r->d);
+    if (r->h) (void)hipHostFree(r->h);
+    delete r;
+    return 0;
+}
+
+}  // extern "C"

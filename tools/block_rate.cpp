@@ -13,6 +13,12 @@
 //              then wait for the previous)
 //   kernel  -- one thread issuing crc32c_plan_exec_blocks of B blocks back to
 //              back: the GPU's time per block in a multi-block launch (events)
+//   resident, resident2 -- the debug library's resident kernel
+//              (crc32c_debug_resident_*: no launch per block), one / two
+//              blocks in flight per thread, every block checked against the
+//              queue's checksums of the same buffer
+// Every line has cpu_us_per_block: the process's CPU time (getrusage) per
+// block -- the submitting threads' and the queue worker's spinning included.
 //
 //   tools/block_rate [threads=16] [iterations=400] [max_blocks=16] [window_us=30]
 //                    [max_depth=2] [queue_modes_only=0]
@@ -29,6 +35,7 @@
 #include <vector>
 
 #include "hdfs_crc32c.h"
+#include "hdfs_crc32c_debug.h"
 
 #define CHECK(x)                                                                      \
     do {                                                                              \
@@ -115,9 +122,9 @@ int main(int argc, char **argv) {
         const long long th1 = throttled_usec();
         const double blocks = double(nthreads) * iters;
         std::printf("{\"mode\": \"%s\", \"threads\": %d, \"blocks\": %.0f, \"us_per_block\": %.3f, \"gib_s\": %.1f, "
-                    "\"cpus_busy\": %.2f, \"throttled_us\": %lld",
+                    "\"cpus_busy\": %.2f, \"cpu_us_per_block\": %.3f, \"throttled_us\": %lld",
                     mode, nthreads, blocks, s / blocks * 1e6, blocks * kBlock / s / double(1 << 30), cpus,
-                    th0 < 0 || th1 < 0 ? -1ll : th1 - th0);
+                    cpus * s / blocks * 1e6, th0 < 0 || th1 < 0 ? -1ll : th1 - th0);
     };
 
     // single: one launch per block
@@ -163,6 +170,46 @@ int main(int argc, char **argv) {
                         w);
             CHECK(crc32c_blocks_destroy(q) == 0);
         }
+    // resident kernel (A/B, debug library): depth 1 and 2; the outputs are
+    // compared with the queue's (the last queue run wrote every buffer's)
+    {
+        std::vector<std::vector<uint32_t>> want(nbuf, std::vector<uint32_t>(nout));
+        CHECK(hipDeviceSynchronize() == hipSuccess);
+        for (int i = 0; i < nbuf; ++i) CHECK(hipMemcpy(want[i].data(), outs[i], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        for (int depth = 1; depth <= std::min(maxdepth, 2); ++depth)
+            for (int w = 0; w < 2; ++w) {
+                for (int i = 0; i < nbuf; ++i) CHECK(hipMemset(outs[i], 0, nout * 4) == hipSuccess);
+                CHECK(hipDeviceSynchronize() == hipSuccess);
+                crc32c_resident *r = nullptr;
+                CHECK(crc32c_debug_resident_create(plan, 2000, &r) == 0);
+                run(depth == 1 ? "resident" : "resident2", [&](int k) {
+                    std::vector<uint64_t> ring(depth);
+                    for (int i = 0; i < iters; ++i) {
+                        const int slot = i % depth;
+                        if (i >= depth) CHECK(crc32c_debug_resident_wait(r, ring[slot]) == 0);
+                        const int b = depth * k + slot;
+                        CHECK(crc32c_debug_resident_submit(r, bufs[b], outs[b], &ring[slot]) == 0);
+                        if (depth == 1) CHECK(crc32c_debug_resident_wait(r, ring[slot]) == 0);
+                    }
+                    if (depth > 1)
+                        for (int i = std::max(0, iters - depth); i < iters; ++i)
+                            CHECK(crc32c_debug_resident_wait(r, ring[i % depth]) == 0);
+                });
+                uint64_t launches = 0;
+                CHECK(crc32c_debug_resident_stats(r, &launches) == 0);
+                CHECK(crc32c_debug_resident_destroy(r) == 0);
+                int bad = 0;
+                std::vector<uint32_t> got(nout);
+                for (int k = 0; k < nthreads; ++k)
+                    for (int slot = 0; slot < depth; ++slot) {
+                        const int b = depth * k + slot;
+                        CHECK(hipMemcpy(got.data(), outs[b], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
+                        bad += got != want[b];
+                    }
+                std::printf(", \"launches\": %llu, \"blocks_wrong\": %d, \"pass\": %d}\n", (unsigned long long)launches,
+                            bad, w);
+            }
+    }
     if (sweep_only) {
         crc32c_plan_destroy(plan);
         for (auto &s : streams) (void)hipStreamDestroy(s);

@@ -17,8 +17,12 @@ per step (HIP events on the launch stream, 1000 steps after 200 warm-up):
                                scatter kernel -- a lower bound for one peer's
                                gather at N = 8.
 
+Each multi step is also captured (kernel + RCCL group) into a graph of 100
+steps and replayed (*_graph_us), as bench.py replays config 4's steps.
+
 Prints one JSON line.  The model: step(N = 8) ~= shard time + gather time,
-with the gather at least (multi_self_send - multi_in_place)."""
+with the gather at least (multi_self_send - multi_in_place); graph-replayed,
+step(N = 8) ~= multi_self_send_graph (the shard plus one RCCL group)."""
 from __future__ import annotations
 
 import json
@@ -65,7 +69,7 @@ def main():
     plan = ctx.plan(pk)
     res["shard_eager_us"] = round(timed(lambda: plan.exec(payload.data_ptr(), out.data_ptr(), stream.cuda_stream)), 3)
     g = torch.cuda.CUDAGraph()
-    cs = torch.cuda.Stream(device=dev)
+    cs = torch.cuda.Stream(device=dev)  # (capture stream)
     plan.exec(payload.data_ptr(), out.data_ptr(), cs.cuda_stream)
     torch.cuda.synchronize()
     with torch.cuda.graph(g, stream=cs, capture_error_mode="thread_local"):
@@ -75,15 +79,37 @@ def main():
     torch.cuda.synchronize()
     res["shard_graph_us"] = round(timed(lambda: g.replay(), n=50, warm=5) / 100, 3)
     plan.close()
-    for name, flags in (("multi_in_place_us", 0), ("multi_self_send_us", hdfs.CRC32C_MULTI_SELF_SEND)):
+    for name, flags in (("multi_in_place", 0), ("multi_self_send", hdfs.CRC32C_MULTI_SELF_SEND)):
         m = hdfs.Multi([0])
         mp = m.plan(pk, 64, flags)
-        res[name] = round(timed(lambda: mp.exec([payload.data_ptr()], out.data_ptr(), [stream.cuda_stream])), 3)
+        res[name + "_us"] = round(timed(lambda: mp.exec([payload.data_ptr()], out.data_ptr(), [stream.cuda_stream])), 3)
+        # the whole step (kernel + RCCL group) captured 100 times into one graph
+        mp.exec([payload.data_ptr()], out.data_ptr(), [cs.cuda_stream])
+        torch.cuda.synchronize()
+        try:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, stream=cs, capture_error_mode="thread_local"):
+                for _ in range(100):
+                    mp.exec([payload.data_ptr()], out.data_ptr(), [cs.cuda_stream])
+            gm.replay()
+            torch.cuda.synchronize()
+            res[name + "_graph_us"] = round(timed(lambda: gm.replay(), n=50, warm=5) / 100, 3)
+            del gm
+        except RuntimeError as e:
+            res[name + "_graph_error"] = str(e)[:200]
+            torch.cuda.synchronize()
         mp.close()
         m.close()
+    # One rank of config 4 at N = 8 checksums 4 of the 32 blocks (this shard)
+    # and, at rank 0, receives 7 peers' 4 x 32 KiB; a peer's transfer costs at
+    # least what the self-send adds to the in-place step (one RCCL group).
     res["gather_lower_bound_us"] = round(res["multi_self_send_us"] - res["multi_in_place_us"], 3)
     res["model_step_n8_us"] = round(res["shard_eager_us"] + res["gather_lower_bound_us"], 3)
     res["model_value_n8_gib_s"] = round(32 * (4 << 20) / (res["model_step_n8_us"] * 1e-6) / 2**30, 1)
+    if "multi_self_send_graph_us" in res:  # the bench's config-4 steps are graph-replayed
+        res["gather_lower_bound_graph_us"] = round(res["multi_self_send_graph_us"] - res["shard_graph_us"], 3)
+        res["model_step_n8_graph_us"] = res["multi_self_send_graph_us"]
+        res["model_value_n8_graph_gib_s"] = round(32 * (4 << 20) / (res["multi_self_send_graph_us"] * 1e-6) / 2**30, 1)
     print(json.dumps(res), flush=True)
     ctx.close()
 

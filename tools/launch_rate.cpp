@@ -36,6 +36,15 @@
 
 #include "hdfs_crc32c.h"
 
+// (internal, exported by the library: a multi-block launch whose last kernel
+// completes `stop` -- hipExtLaunchKernel's stop event; diagnostic use only)
+struct ihipStream_t;
+struct ihipEvent_t;
+namespace hdfs_crc {
+int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs, size_t nblocks,
+                hipStream_t stream, hipEvent_t stop);
+}
+
 #define CHECK(x)                                                           \
     do {                                                                   \
         if (!(x)) {                                                        \
@@ -197,6 +206,12 @@ static int calls_mode(size_t npk, int n) {
     rc = rc || time_calls("exec_event_record", s, n, [&](int) {
              return crc32c_plan_exec(plan, src, dst, s) || hipEventRecord(ev, s) != hipSuccess;
          }, false);
+    const void *pays[1] = {src};
+    uint32_t *os[1] = {dst};
+    rc = rc || time_calls("exec_blocks1", s, n, [&](int) { return hdfs_crc::exec_blocks(plan, pays, os, 1, s, nullptr); },
+                          false);
+    rc = rc || time_calls("exec_blocks1_stop_event", s, n,
+                          [&](int) { return hdfs_crc::exec_blocks(plan, pays, os, 1, s, ev); }, false);
     rc = rc || time_calls("exec_is_capturing", s, n, [&](int) {
              hipStreamCaptureStatus cs;
              return crc32c_plan_exec(plan, src, dst, s) || hipStreamIsCapturing(s, &cs) != hipSuccess;

@@ -19,6 +19,8 @@ run() {  # name timeout cmd...
 for s in ${STEPS:-calls multi}; do
   case $s in
     calls) run calls 120 tools/launch_rate calls 64 4000 ;;
+    brate) run brate 240 tools/block_rate ${BR_ARGS:-16 400 16 30 2 1} ;;
+    brate1) run brate1 120 tools/block_rate 1 2000 16 0 1 1 ;;
     multi) run multi 180 tools/launch_rate multi 256 2000 ;;
     multiprof) run multiprof 300 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/multiprof -o run --output-format csv -- tools/launch_rate multi 256 1000 ;;
     tmulti) run tmulti 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "multi" ;;
@@ -27,6 +29,11 @@ for s in ${STEPS:-calls multi}; do
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench20) run bench20 600 python bench.py --steps 20 --warmup 5 ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
+    tgen) run tgen 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or unaligned or shifted or verify or write_plan or fsx or edge or small" ;;
+    tqueue) run tqueue 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "block_queue or overlapping or per_launch or destroyed or across_streams or recycled" ;;
+    ab) for c in ${ABCFGS:-c2b1000 c2b1536 c2t c2u c5}; do
+          run ab_base_$c 300 bash -c "cd abwt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
+          run ab_cand_$c 300 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-} || exit 1; done ;;
   esac
 done
 echo "session done"
