@@ -107,8 +107,55 @@ def debug_lib():
         L.crc32c_debug_stream_probe.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint32, i32, vp]
         L.crc32c_debug_variant_name.restype = ctypes.c_char_p
         L.crc32c_debug_variant_name.argtypes = [i32, ctypes.POINTER(i32)]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        for name, args in (("crc32c_debug_resident_create", [vp, ctypes.c_uint32, ctypes.POINTER(vp)]),
+                           ("crc32c_debug_resident_submit", [vp, vp, vp, u64p]),
+                           ("crc32c_debug_resident_wait", [vp, ctypes.c_uint64]),
+                           ("crc32c_debug_resident_stats", [vp, u64p]),
+                           ("crc32c_debug_resident_destroy", [vp])):
+            f = getattr(L, name)
+            f.restype = i32
+            f.argtypes = args
         _DEBUG_LIB = L
     return _DEBUG_LIB
+
+
+class Resident:
+    """crc32c_debug_resident_* (debug library, A/B experiment): a resident
+    kernel taking one block's plan over blocks submitted by any thread."""
+
+    def __init__(self, plan: "Plan", idle_us: int = 0):
+        h = ctypes.c_void_p()
+        L = debug_lib()
+        _check(L.crc32c_debug_resident_create(plan.handle, idle_us, ctypes.byref(h)), "crc32c_debug_resident_create")
+        self.plan = plan  # (outlives the resident kernel)
+        self.handle = h
+
+    def submit(self, dev_payload: int, dev_out: int) -> int:
+        t = ctypes.c_uint64(0)
+        _check(debug_lib().crc32c_debug_resident_submit(self.handle, ctypes.c_void_p(dev_payload),
+                                                        ctypes.c_void_p(dev_out), ctypes.byref(t)),
+               "crc32c_debug_resident_submit")
+        return int(t.value)
+
+    def wait(self, ticket: int) -> None:
+        _check(debug_lib().crc32c_debug_resident_wait(self.handle, ticket), "crc32c_debug_resident_wait")
+
+    def launches(self) -> int:
+        n = ctypes.c_uint64(0)
+        _check(debug_lib().crc32c_debug_resident_stats(self.handle, ctypes.byref(n)), "crc32c_debug_resident_stats")
+        return int(n.value)
+
+    def close(self) -> None:
+        if self.handle:
+            debug_lib().crc32c_debug_resident_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def variant_info(v: int):

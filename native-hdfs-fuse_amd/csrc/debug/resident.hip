@@ -72,12 +72,20 @@ struct HostRing {
     uint64_t exits;           // kernel: launches that have exited
 };
 
+// A device slot is two 64-bit words, payload and out pointer (48-bit GPU
+// addresses), each tagged in bits 48-63 with the low 16 bits of ticket + 1:
+// a worker that reads both with matching tags has the block's pointers (no
+// separate sequence word to wait for first).
+constexpr int kTagShift = 48;
+constexpr uint64_t kAddrMask = (1ull << kTagShift) - 1;
+__host__ __device__ constexpr uint64_t tag_of(uint64_t ticket) { return ((ticket + 1) & 0xffffull) << kTagShift; }
+
 struct DevRing {
-    uint64_t seq[kRing];
-    uint64_t payload[kRing];
-    uint64_t out[kRing];
+    uint64_t slot[kRing][2];
     uint32_t flag[kRing][kMaxWg];  // per slot and workgroup: ticket + 1 once its workers are done
-    uint32_t stop;
+    uint64_t fwd;                  // forwarder: tickets below this are forwarded
+    uint64_t col;                  // collector: tickets below this are complete
+    uint32_t stop;                 // forwarder: every wave exits
 };
 
 struct RParams {
@@ -147,59 +155,39 @@ __device__ __forceinline__ void run_tile(const RParams &p, const uint8_t *lds, c
     }
 }
 
+// Forwarder (workgroup 0's last wave): the host ring -> the device ring.
+// One PCIe round trip per poll covers the next 64 tickets.  Decides the
+// launch's end: the host's stop word, idle_ticks with nothing outstanding,
+// or kStuckMs without the collector advancing while blocks are outstanding.
 __device__ void forwarder(const RParams &p, int lane) {
     HostRing *h = p.h;
     DevRing *d = p.d;
     uint64_t fwd = p.first, col = p.first;
     uint64_t last = now();
-    const uint32_t ng = gridDim.x;
     for (;;) {
         bool progress = false;
-        // forward: the next 64 tickets' slots, one load per lane (ring reuse:
+        const uint64_t c = ld_dev(&d->col);
+        if (c != col) {
+            col = c;
+            progress = true;
+        }
+        // the next 64 tickets' host slots, one load per lane (ring reuse:
         // ticket t only once t - kRing is complete)
         const uint64_t cand = fwd + uint64_t(lane);
         const bool room = cand < col + kRing;
-        const uint64_t s = room ? ld_sys(&h->seq[cand % kRing]) : 0;
-        const uint64_t ready = __ballot(room && s == cand + 1);
+        const uint64_t sq = room ? ld_sys(&h->seq[cand % kRing]) : 0;
+        const uint64_t ready = __ballot(room && sq == cand + 1);
         const uint32_t n = ~ready ? uint32_t(__builtin_ctzll(~ready)) : 64u;  // consecutive ready tickets from fwd
         if (n) {
             if (uint32_t(lane) < n) {
                 const uint32_t sl = uint32_t(cand % kRing);
                 const uint64_t pay = ld_sys(&h->payload[sl]), o = ld_sys(&h->out[sl]);
-                st_dev(&d->payload[sl], pay);
-                st_dev(&d->out[sl], o);
-                wait_vmem();  // (the pointers have landed before the sequence word)
-                st_dev(&d->seq[sl], cand + 1);
+                st_dev(&d->slot[sl][0], (pay & kAddrMask) | tag_of(cand));
+                st_dev(&d->slot[sl][1], (o & kAddrMask) | tag_of(cand));
             }
             fwd += n;
+            if (lane == 0) st_dev(&d->fwd, fwd);
             progress = true;
-        }
-        // collect: the (up to 8) oldest outstanding blocks' workgroup flags,
-        // loaded together; completed in ticket order
-        {
-            constexpr uint32_t kCheck = 8;
-            const uint64_t nout = fwd - col;
-            uint32_t f[kCheck][4];
-#pragma unroll
-            for (uint32_t c = 0; c < kCheck; ++c)
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k) {
-                    const uint32_t wg = 4u * uint32_t(lane) + k;
-                    f[c][k] = (c < nout && wg < ng) ? ld_dev(&d->flag[(col + c) % kRing][wg]) : 0u;
-                }
-#pragma unroll
-            for (uint32_t c = 0; c < kCheck; ++c) {
-                if (c >= nout) break;
-                const uint32_t want = uint32_t(col + 1);
-                bool ok = true;
-#pragma unroll
-                for (uint32_t k = 0; k < 4; ++k)
-                    if (4u * uint32_t(lane) + k < ng && f[c][k] != want) ok = false;
-                if (__ballot(!ok)) break;
-                if (lane == 0) st_sys(&h->done[col % kRing], col + 1);
-                ++col;
-                progress = true;
-            }
         }
         const uint64_t t = now();
         if (progress) {
@@ -207,12 +195,63 @@ __device__ void forwarder(const RParams &p, int lane) {
             continue;
         }
         if (ld_sys(&h->stop)) break;
-        if (col == fwd && t - last > p.idle_ticks) break;          // idle
+        if (col == fwd && t - last > p.idle_ticks) break;                  // idle
         if (col < fwd && t - last > kStuckMs * 1000 * kTicksPerUs) break;  // no progress: give up
         __builtin_amdgcn_s_sleep(2);
     }
+    if (lane == 0) st_dev(&d->stop, 1u);
+}
+
+// Collector (workgroup 1's last wave): block t is complete when every
+// workgroup's flag for its slot holds t + 1; the (up to 8) oldest
+// outstanding blocks' flags are loaded together and completed in ticket
+// order (hdone[slot] = t + 1 in host memory).  Ends once the forwarder has
+// stopped and nothing it forwarded is outstanding (or kStuckMs later), then
+// records where it stopped for the next launch.
+__device__ void collector(const RParams &p, int lane) {
+    HostRing *h = p.h;
+    DevRing *d = p.d;
+    uint64_t col = p.first;
+    uint64_t last = now();
+    const uint32_t ng = gridDim.x;
+    for (;;) {
+        const uint32_t stop = ld_dev(&d->stop);
+        const uint64_t fwd = ld_dev(&d->fwd);
+        bool progress = false;
+        constexpr uint32_t kCheck = 8;
+        const uint64_t nout = fwd > col ? fwd - col : 0;
+        uint32_t f[kCheck][4];
+#pragma unroll
+        for (uint32_t c = 0; c < kCheck; ++c)
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t wg = 4u * uint32_t(lane) + k;
+                f[c][k] = (c < nout && wg < ng) ? ld_dev(&d->flag[(col + c) % kRing][wg]) : 0u;
+            }
+#pragma unroll
+        for (uint32_t c = 0; c < kCheck; ++c) {
+            if (c >= nout) break;
+            const uint32_t want = uint32_t(col + 1);
+            bool ok = true;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+                if (4u * uint32_t(lane) + k < ng && f[c][k] != want) ok = false;
+            if (__ballot(!ok)) break;
+            if (lane == 0) st_sys(&h->done[col % kRing], col + 1);
+            ++col;
+            progress = true;
+        }
+        if (progress) {
+            if (lane == 0) st_dev(&d->col, col);
+            last = now();
+            continue;
+        }
+        if (stop && col >= fwd) break;
+        if (stop && now() - last > kStuckMs * 1000 * kTicksPerUs) break;
+        if (now() - last > kWorkerMs * 1000 * kTicksPerUs) break;  // (the forwarder is gone)
+        __builtin_amdgcn_s_sleep(1);
+    }
     if (lane == 0) {
-        st_dev(&d->stop, 1u);
         st_sys(&h->exit_col, col);
         wait_vmem();
         st_sys(&h->exits, ld_sys(&h->exits) + 1);
@@ -237,6 +276,7 @@ __global__ __launch_bounds__(kWaves * 64, 3) void resident_kernel(RParams p) {
     __syncthreads();
     if (wv == kWaves - 1) {
         if (blockIdx.x == 0) forwarder(p, lane);
+        if (blockIdx.x == 1) collector(p, lane);
         return;
     }
     // Worker: phase (b + w) % 5; the workgroup's waves of a phase (2 or 3)
@@ -255,8 +295,11 @@ __global__ __launch_bounds__(kWaves * 64, 3) void resident_kernel(RParams p) {
     for (;;) {
         const uint32_t sl = uint32_t(j % kRing);
         bool stop = false;
+        uint64_t w0 = 0, w1 = 0;
         for (uint32_t polls = 0;; ++polls) {
-            if (ld_dev(&d->seq[sl]) == j + 1) break;
+            w0 = ld_dev(&d->slot[sl][0]);
+            w1 = ld_dev(&d->slot[sl][1]);
+            if ((w0 & ~kAddrMask) == tag_of(j) && (w1 & ~kAddrMask) == tag_of(j)) break;
             if ((polls & 15u) == 15u && (ld_dev(&d->stop) || now() - last > kWorkerMs * 1000 * kTicksPerUs)) {
                 stop = true;
                 break;
@@ -264,8 +307,8 @@ __global__ __launch_bounds__(kWaves * 64, 3) void resident_kernel(RParams p) {
             __builtin_amdgcn_s_sleep(1);
         }
         if (stop) break;
-        const uint8_t *payload = reinterpret_cast<const uint8_t *>(ld_dev(&d->payload[sl]));
-        uint32_t *out = reinterpret_cast<uint32_t *>(ld_dev(&d->out[sl]));
+        const uint8_t *payload = reinterpret_cast<const uint8_t *>(w0 & kAddrMask);
+        uint32_t *out = reinterpret_cast<uint32_t *>(w1 & kAddrMask);
         if (rank < 2)
             for (uint32_t idx = 2u * b + rank; idx < p.ntiles; idx += 2u * G) run_tile(p, lds, payload, out, idx, lane);
         wait_vmem();  // (this wave's checksum stores have completed)
@@ -295,7 +338,7 @@ struct crc32c_resident {
     std::atomic<uint64_t> next{0};
     std::mutex mu;           // launches
     bool running = false;    // a launch may be on the GPU (under mu)
-    uint64_t launches = 0;
+    std::atomic<uint64_t> launches{0};
 };
 
 namespace {
@@ -323,11 +366,14 @@ int ensure_running(crc32c_resident *r) {
     p.first = col;
     p.idle_ticks = r->idle_ticks;
     hdfs_crc::DeviceGuard guard(r->device);
-    HIP_TRY(hipMemsetAsync(&r->d->stop, 0, sizeof(uint32_t), r->stream));
+    // (fresh control words; the device slots keep their tags: a tag names its ticket)
+    const uint64_t ctl[3] = {col, col, 0};
+    HIP_TRY(hipMemcpyAsync(&r->d->fwd, ctl, sizeof ctl, hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));  // (ctl is on this stack)
     hipLaunchKernelGGL(resident_kernel, dim3(r->grid), dim3(kWaves * 64), 0, r->stream, p);
     HIP_TRY(hipGetLastError());
     r->running = true;
-    ++r->launches;
+    r->launches.fetch_add(1, std::memory_order_release);
     return 0;
 }
 
@@ -377,8 +423,14 @@ int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, ui
     r->h->out[sl] = reinterpret_cast<uint64_t>(dev_out);
     __atomic_store_n(&r->h->seq[sl], t + 1, __ATOMIC_RELEASE);
     if (ticket) *ticket = t;
-    std::lock_guard<std::mutex> lock(r->mu);
-    return ensure_running(r);
+    // every launch so far has exited (or is exiting): start one (a launch
+    // still running forwards this ticket; one that exits before seeing it is
+    // relaunched by the waiter)
+    if (__atomic_load_n(&r->h->exits, __ATOMIC_ACQUIRE) >= r->launches.load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> lock(r->mu);
+        return ensure_running(r);
+    }
+    return 0;
 }
 
 int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket) {
@@ -408,7 +460,7 @@ int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket) {
 
 int crc32c_debug_resident_stats(const crc32c_resident *r, uint64_t *launches) {
     if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
-    if (launches) *launches = r->launches;
+    if (launches) *launches = r->launches.load();
     return 0;
 }
 

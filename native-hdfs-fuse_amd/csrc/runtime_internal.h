@@ -160,8 +160,8 @@ struct crc32c_plan {
     hipStream_t last_stream = nullptr;
     bool launched = false;
     // Per stream the plan was launched on (outside a graph capture): an event
-    // re-recorded after every launch of the plan there, so it completes after
-    // the plan's last launch on that stream.  Destroy gates the block's reuse
+    // every launch of the plan there completes as its dispatch's stop event,
+    // so it completes after the plan's last launch on that stream.  Destroy gates the block's reuse
     // on these events and touches no stream (the caller may have destroyed
     // it already); a verify launch on another stream than the previous one
     // waits on the previous stream's event.  captured: a launch went into a
@@ -194,9 +194,10 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
 // Before a launch of `plan` on `stream` (caller holds plan->mu): orders it
 // after the plan's upload; *capturing: the stream is being captured.
 int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing);
-// After a launch of `plan` on `stream` outside a capture (caller holds
-// plan->mu): re-records the stream's mark (crc32c_plan::marks).
-int mark_launch(crc32c_plan *plan, hipStream_t stream);
+// The (plan, stream) mark event (crc32c_plan::marks), created on first use
+// (caller holds plan->mu): a launch outside a capture passes it as its stop
+// event, so it completes after the plan's last launch on that stream.
+int stream_mark(crc32c_plan *plan, hipStream_t stream, hipEvent_t *out);
 // crc32c_plan_exec_blocks; `stop` (optional) is completed by the last launch.
 int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs, size_t nblocks,
                 hipStream_t stream, hipEvent_t stop);

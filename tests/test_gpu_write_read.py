@@ -842,6 +842,70 @@ def test_block_queue_failed_flush_is_its_own(hdfs, gpu_ctx, orc):
     plan.close()
 
 
+def test_resident_kernel_blocks(hdfs, gpu_ctx, orc):
+    """The debug library's resident kernel (A/B experiment, DESIGN.md section
+    6): blocks submitted from 8 threads, 2 in flight each, bit-exact; the
+    kernel exits after idle_us with nothing queued and a later submit
+    relaunches it; destroy with blocks still queued returns (the kernel
+    exits on the stop word) and a plain launch runs after it.  Every wave of
+    the kernel has its own bounded wait, so nothing here can hang the GPU."""
+    import threading
+    import time
+
+    torch = _torch()
+    pk = _block_shape("full")
+    n = oracle.total_checksums(pk)
+    hosts = [oracle.xorshift64_bytes(64 * 65536, 8800 + k) for k in range(16)]
+    want = [orc.batch(h, pk, n) for h in hosts]
+    devs = [torch.from_numpy(h).cuda() for h in hosts]
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in hosts]
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    r = hdfs.Resident(plan, idle_us=500)
+    errs = []
+
+    def worker(k):
+        try:
+            ring = []
+            for i in range(20):
+                b = 2 * k + (i % 2)
+                if len(ring) == 2:
+                    t, bb = ring.pop(0)
+                    r.wait(t)
+                    got = outs[bb].cpu().numpy().view(np.uint32)
+                    assert np.array_equal(got, want[bb]), (k, i)
+                    outs[bb].zero_()
+                    torch.cuda.synchronize()
+                ring.append((r.submit(devs[b].data_ptr(), outs[b].data_ptr()), b))
+            for t, bb in ring:
+                r.wait(t)
+                assert np.array_equal(outs[bb].cpu().numpy().view(np.uint32), want[bb]), k
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    first = r.launches()
+    time.sleep(0.05)  # past idle_us: the kernel has exited
+    outs[0].zero_()
+    torch.cuda.synchronize()
+    r.wait(r.submit(devs[0].data_ptr(), outs[0].data_ptr()))
+    assert np.array_equal(outs[0].cpu().numpy().view(np.uint32), want[0])
+    assert r.launches() > first
+    for i in range(10):  # destroy with blocks queued
+        r.submit(devs[i].data_ptr(), outs[i].data_ptr())
+    r.close()
+    outs[1].zero_()
+    plan.exec(devs[1].data_ptr(), outs[1].data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(outs[1].cpu().numpy().view(np.uint32), want[1])
+    plan.close()
+
+
 def test_block_queue_ring_reuse_two_in_flight(hdfs, gpu_ctx, orc):
     """crc32c_blocks with more tickets than its ring has slots (1024): 16
     threads keep two blocks in flight each (submit the next, then wait for

@@ -16,6 +16,11 @@
 // with a mismatch bitmap (crc32c_plan_verify_bitmap), exec followed by a
 // hipEventRecord of a timing-disabled event (the price of a completion record
 // per launch), exec + hipStreamIsCapturing.
+//   tools/launch_rate rtt [launches=2000]
+// one launch then a wait for it, back to back (submit -> complete latency of
+// a single writer): an empty kernel with hipStreamSynchronize, the plan of
+// one 4 MiB block with hipStreamSynchronize, and the same with a spin on
+// hipEventQuery of a stop event instead of the blocking synchronise.
 //   tools/launch_rate multi [packets=256] [steps=2000]
 // config 4's per-rank step at N = 8 on one GPU (a 16 MiB shard = 4 blocks of
 // 64 packets): crc32c_plan_exec of the shard, crc32c_multi_plan_exec in place
@@ -330,9 +335,63 @@ static int multi_mode(size_t npk, int n) {
     return exact ? 0 : 1;
 }
 
+static int rtt_mode(int n) {
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    BigArg a{};
+    auto per = [&](auto fn) {
+        for (int i = 0; i < 100; ++i)
+            if (fn()) return -1.0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < n; ++i)
+            if (fn()) return -1.0;
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / n;
+    };
+    const double empty = per([&] {
+        hipLaunchKernelGGL(empty_kernel, dim3(256), dim3(768), 0, s, a);
+        return hipStreamSynchronize(s) != hipSuccess;
+    });
+    const uint32_t len = 65536, bpc = 512;
+    std::vector<crc32c_packet> pk(64);
+    for (size_t i = 0; i < 64; ++i) pk[i] = crc32c_packet{uint64_t(i) * len, uint64_t(i) * (len / bpc), len, bpc};
+    crc32c_ctx *ctx = nullptr;
+    CHECK(crc32c_ctx_create(0, &ctx) == 0);
+    crc32c_plan *plan = nullptr;
+    CHECK(crc32c_plan_create(ctx, pk.data(), 64, 0, &plan) == 0);
+    void *src = nullptr;
+    uint32_t *dst = nullptr;
+    CHECK(hipMalloc(&src, 64 * len) == hipSuccess);
+    CHECK(hipMemset(src, 0x11, 64 * len) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&dst), 64 * 128 * 4) == hipSuccess);
+    const double block_sync = per([&] {
+        return crc32c_plan_exec(plan, src, dst, s) || hipStreamSynchronize(s) != hipSuccess;
+    });
+    hipEvent_t ev;
+    CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess);
+    const void *pays[1] = {src};
+    uint32_t *os[1] = {dst};
+    const double block_spin = per([&] {
+        if (hdfs_crc::exec_blocks(plan, pays, os, 1, s, ev)) return true;
+        hipError_t q;
+        while ((q = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
+        return q != hipSuccess;
+    });
+    std::printf("{\"mode\": \"rtt\", \"launches\": %d, \"empty_kernel_sync_us\": %.3f, \"block_exec_sync_us\": %.3f, "
+                "\"block_exec_event_spin_us\": %.3f}\n",
+                n, empty, block_sync, block_spin);
+    (void)hipEventDestroy(ev);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    crc32c_plan_destroy(plan);
+    crc32c_ctx_destroy(ctx);
+    (void)hipStreamDestroy(s);
+    return 0;
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "write") return write_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
     if (argc > 1 && std::string(argv[1]) == "raw") return raw_mode(argc > 2 ? std::atoi(argv[2]) : 4000);
+    if (argc > 1 && std::string(argv[1]) == "rtt") return rtt_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
     if (argc > 1 && std::string(argv[1]) == "multi")
         return multi_mode(argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 256, argc > 3 ? std::atoi(argv[3]) : 2000);
     if (argc > 1 && std::string(argv[1]) == "calls")
