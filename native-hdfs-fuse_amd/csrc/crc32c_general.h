@@ -382,15 +382,20 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         for (int i = 0; i < 8; ++i) ld(i);
         __builtin_amdgcn_sched_barrier(0);
     }
+    const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
     for (uint32_t s = 0; s < nsub; ++s) {
         uint32_t pc[8];
+        // (without ROLL, unpadded items' loads need no block facts: issue them
+        // before the subtile's pattern-table fetches, two dependent scalar loads)
+        if (!kRoll && contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
+        // (subtile s's facts; subtile 0's were derived before the loop)
+        if (s) gs = gsub(g, s, st);
         GState st1 = st;
         gstate_next(g, gs, st1);
         if (kRoll) {
             // what the wave loads next: subtile s + 1 (its facts are derived
             // again at the top of the next iteration: cheaper than keeping them
             // live through the lookups), or the next work item
-            if (s) gs = gsub(g, s, st);
             const bool last = s + 1u == nsub;
             const Roll r = !last     ? roll_general(p, g, gsub(g, s + 1u, st1), s + 1u)
                            : has_next ? roll_item(p, nft)
@@ -402,11 +407,6 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
                 v[8] = make_uint4(x[0], x[1], x[2], x[3]);
             }
         } else {
-            // Unpadded items' loads need no block facts: issue them before the
-            // subtile's pattern-table fetches (two dependent scalar loads).
-            const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
-            if (contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
-            if (s) gs = gsub(g, s, st);
             if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
             gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
         }

@@ -734,6 +734,7 @@ int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute
               crc32c_plan **out) {
     std::unique_ptr<crc32c_plan, int (*)(crc32c_plan *)> p(new crc32c_plan, crc32c_plan_destroy);
     p->ctx = ctx;
+    ctx->refs.fetch_add(1, std::memory_order_relaxed);  // (released by crc32c_plan_destroy)
     p->nchecksums = hp.nchecksums;
     p->payload_bytes = hp.payload_bytes;
     p->flags = flags & (CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32);
@@ -796,8 +797,12 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     return 0;
 }
 
-int crc32c_ctx_destroy(crc32c_ctx *ctx) {
-    if (!ctx) return 0;
+}  // extern "C"
+
+namespace {
+
+// The context's teardown, when its last reference goes.
+void ctx_teardown(crc32c_ctx *ctx) {
     {
         DeviceGuard guard(ctx->device);
         for (Stage &s : ctx->stage) free_stage(s);
@@ -815,6 +820,19 @@ int crc32c_ctx_destroy(crc32c_ctx *ctx) {
         }
     }
     delete ctx;
+}
+
+void ctx_release(crc32c_ctx *ctx) {
+    if (ctx->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) ctx_teardown(ctx);
+}
+
+}  // namespace
+
+extern "C" {
+
+int crc32c_ctx_destroy(crc32c_ctx *ctx) {
+    if (!ctx) return 0;
+    ctx_release(ctx);
     return 0;
 }
 
@@ -997,11 +1015,13 @@ int64_t crc32c_verify_host(crc32c_ctx *ctx, const void *payload, const crc32c_pa
 
 int crc32c_plan_destroy(crc32c_plan *plan) {
     if (!plan) return 0;
+    crc32c_ctx *ctx = plan->ctx;
     {
-        DeviceGuard guard(plan->ctx->device);
+        DeviceGuard guard(ctx->device);
         release_plan_blocks(plan);  // (the verify slots live in the same block)
     }
     delete plan;
+    ctx_release(ctx);
     return 0;
 }
 

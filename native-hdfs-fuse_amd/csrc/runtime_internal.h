@@ -125,6 +125,11 @@ struct RelaxedCapture {
 struct crc32c_ctx {
     int device = 0;
     int num_cu = 0;
+    // The context handle and every live plan hold one reference; the
+    // context is torn down when the last goes (a plan destroyed after
+    // crc32c_ctx_destroy -- e.g. one a garbage collector frees late -- still
+    // returns its block to a live pool instead of a freed one).
+    std::atomic<int> refs{1};
     // per checksum type (0 = CRC32C, 1 = CRC32 / CRC32C_TYPE_CRC32)
     uint8_t *d_table[2] = {nullptr, nullptr};
     uint8_t *d_table_s4[2] = {nullptr, nullptr};

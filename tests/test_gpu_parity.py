@@ -745,6 +745,31 @@ def _hip_runtime():
     raise RuntimeError("libamdhip64 is not loaded")
 
 
+def test_plan_destroyed_after_its_context(hdfs, orc):
+    """A plan outliving crc32c_ctx_destroy (a garbage collector freeing a
+    plan late, e.g. one a failed test's traceback held): the context is
+    reference-counted by its plans, so the late destroy returns the plan's
+    block to a still-live pool and the context goes with its last plan."""
+    torch = _torch()
+    pk = oracle.uniform_packets(8)
+    n = hdfs.total_checksums(pk)
+    payload = oracle.xorshift64_bytes(8 * 65536, 31337)
+    dev = torch.from_numpy(payload).cuda()
+    out = torch.zeros(n, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        ctx = hdfs.Context(0)
+        plans = [hdfs.Plan(ctx, pk) for _ in range(3)]
+        for p in plans:
+            p.exec(dev.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        ctx.close()  # (the plans still hold it)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, n))
+        plans[0].exec(dev.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        for p in plans:
+            p.close()
+        torch.cuda.synchronize()
+
+
 def test_stream_destroyed_before_plan(hdfs, orc):
     """A caller's stream destroyed BEFORE the plan that ran on it (a FUSE
     worker thread tearing down its stream, then the plan): the

@@ -28,7 +28,7 @@ for s in ${STEPS:-calls multi}; do
     multi) run multi 180 tools/launch_rate multi 256 2000 ;;
     multiprof) run multiprof 300 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/multiprof -o run --output-format csv -- tools/launch_rate multi 256 1000 ;;
     tmulti) run tmulti 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "multi" ;;
-    tests) run tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
+    tests) run tests 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench20) run bench20 600 python bench.py --steps 20 --warmup 5 ;;
