@@ -447,21 +447,14 @@ __device__ __forceinline__ void load_tile(const KParams &p, FastTile t, int lane
 // lin() of a tile's 8 pieces (instruction i's 16 bytes per lane), each
 // piece first passed through prep(i, piece) (general tiles: the chunk-start
 // masks), so that piece i's lookups start as soon as its own load is back.
-struct NoPost {
-    __device__ __forceinline__ void operator()(int) const {}
-};
-// post(i) runs once piece i has consumed v[i] (general builds: the next
-// subtile's or work item's load i goes into v[i] there, crc32c_general.h).
-template <int DIAG, bool S4, int IMG, typename Prep, int NP = 8, typename Post = NoPost>
-__device__ __forceinline__ void tile_pieces(const uint8_t *lds, uint4 v[8], uint32_t pc[8], int lane, Prep prep,
-                                            Post post = Post{}) {
+template <int DIAG, bool S4, int IMG, typename Prep, int NP = 8>
+__device__ __forceinline__ void tile_pieces(const uint8_t *lds, uint4 v[8], uint32_t pc[8], int lane, Prep prep) {
     const LaneCols cols = lane_cols<IMG>(uint32_t(lane & 31));
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
         prep(i, v[i]);
         pc[i] = piece<S4, DIAG, IMG>(lds, v[i], cols);
         opaque(pc[i]);
-        post(i);
         // One piece at a time (nibble tables: 32 independent reads each), or
         // two (S4: a piece is a chain of 4 dependent steps, so two chains
         // interleave to keep 8 reads in flight): keeps the scheduler from
@@ -842,28 +835,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     };
 
     if (!EARLY && t < tend) load_next(t);
-    // General builds (not the quarter-unit one): a general item grabs the
-    // wave's next work item BEFORE its lookups and rolls that item's first
-    // loads in behind them (finish_gtile ROLL, crc32c_general.h), so the next
-    // item's load latency overlaps this item's compute; pre0 tells the next
-    // general item that its first subtile is loaded already.
-    constexpr bool ROLL = GENERAL && !QUARTER && !COMPDIAG;
-    bool pre0 = false;
     while (t < tend) {
-        if (ROLL && (ft.meta & kGeneralTile)) {
-            const uint32_t tn = pool_grab(pool_ctr, lane);
-            const bool has = tn < tend;
-            const FastTile nft = has ? tile_at(p, tn) : ft;
-            uint32_t evn = 0;
-            if (VERIFY && has) evn = expect_of(p, nft, lane);
-            finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, true>(p, lds, vacc, ft, v, ev, lane, pre0, nft, has);
-            if (!has) break;
-            t = tn;
-            ft = nft;
-            ev = evn;
-            pre0 = (nft.meta & kGeneralTile) != 0;
-            continue;
-        }
         if (!QUARTER || kind == 1)
             finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GENERAL>(p, lds, vacc, ft, v, ev, lane);
         else if (kind == 2)
@@ -871,7 +843,6 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         t = pool_grab(pool_ctr, lane);
         if (t >= tend) break;
         load_next(t);
-        pre0 = false;
     }
     items();
     if (VERIFY) {

@@ -166,95 +166,6 @@ __device__ __forceinline__ void load_gtile(const KParams &p, FastTile t, int lan
     if (VERIFY && uint32_t(lane) < g.nch + (g.kt ? 1u : 0u)) ev = p.expect[t.out + uint32_t(lane)];
 }
 
-// ---- rolling loads (general builds) ---------------------------------------
-// A wave runs a general item's subtiles one after another, and each
-// subtile's lookups can only start once its loads are back; with the loads
-// issued after the previous subtile (or item) was done, a general item's
-// load latency and its compute did not overlap within the wave (bpc 1000:
-// 64.9 us against max(memory only 46.4, compute only 49.9), DESIGN.md
-// section 10).  Instead, the loads of whatever the wave runs next -- the
-// next subtile of its item, or the first loads of its next work item (a
-// general item's first subtile or a power-of-two tile) -- are issued piece
-// by piece DURING the current subtile's lookups: load i goes into v[i] as
-// soon as piece i has consumed it (tile_pieces' post hook), so no extra
-// registers hold them.  Every load is one buffer_load whose per-lane offset
-// is 16 * lane plus a wave-uniform value per (half-wave, load), computed on
-// the scalar unit beforehand.
-struct Roll {
-    __amdgpu_buffer_rsrc_t rsrc;
-    // offset of load i, half-wave h, lane q: base + 512 h + 1024 i + 16 q - D,
-    // D = pad x (before + full chunks started in blocks 0 .. 2i + h) + (padt
-    // in the tail); blocks not in `valid` read nothing.  All wave-uniform
-    // (SGPRs); the per-load offsets are derived on the scalar unit as the
-    // loads go out, so no table of them stays live through the lookups.
-    uint32_t base, pad, padt, before, sfull, tailm, valid;
-    uint32_t v8;  // a shifted power-of-two tile's last 16 bytes: lane 0's offset (kRollNone: none)
-};
-constexpr uint32_t kRollNone = 0x80000000u;
-
-// Subtile s of general item g, facts gs: the descriptor starts 16 bytes
-// before the item (its 16-byte shift), as load_gsub's.  (load_gsub also
-// skips lanes wholly inside a chunk's zero prefix; here they read the bytes
-// before the chunk, which the chunk-start keep masks zero.)
-__device__ __forceinline__ Roll roll_general(const KParams &p, const GShape &g, const GSub &gs, uint32_t s) {
-    return Roll{uniform_rsrc(p.payload + g.src - 16u, 16u + g.nch * g.bpc + g.tl), 16u + 8192u * s, g.pad, g.padt,
-                gs.before, gs.sfull, gs.tailm, gs.valid, kRollNone};
-}
-
-// A power-of-two tile (meta: nb | lg << 8), shifted when off 16-byte
-// alignment (load_tile / load_tile_shifted with a 16-byte descriptor shift;
-// blocks past nb fall outside the descriptor).
-__device__ __forceinline__ Roll roll_pow2(const KParams &p, FastTile t) {
-    const uint32_t nb = t.meta & 0xffu;
-    const uint32_t m = uint32_t(reinterpret_cast<uintptr_t>(p.payload + t.src)) & 15u;
-    return Roll{uniform_rsrc(p.payload + t.src - m - 16u, 16u + m + nb * 512u), 16u, 0u, 0u, 0u, 0u, 0u, 0xffffu,
-                m ? m + nb * 512u : kRollNone};
-}
-
-__device__ __forceinline__ Roll roll_none(const KParams &p) {
-    return Roll{uniform_rsrc(p.payload, 0u), 16u, 0u, 0u, 0u, 0u, 0u, 0u, kRollNone};
-}
-
-// The first loads of work item t: a general item's subtile 0, or a tile.
-__device__ __forceinline__ Roll roll_item(const KParams &p, FastTile t) {
-    if (t.meta & kGeneralTile) {
-        const GShape g = gshape(t);
-        return roll_general(p, g, gsub(g, 0, GState{}), 0);
-    }
-    return roll_pow2(p, t);
-}
-
-// tile_pieces' post hook: load i of the roll into v[i] (just consumed).
-template <int AUX>
-struct RollPost {
-    const Roll &r;
-    uint4 *v;
-    uint32_t lane16;  // 16 * (lane & 31)
-    bool hi;          // lane >= 32
-    __device__ __forceinline__ uint32_t delta(uint32_t i, uint32_t h) const {  // (scalar)
-        const uint32_t b = 2u * i + h;
-        const uint32_t d = r.pad * (r.before + __builtin_popcount(r.sfull & ((2u << b) - 1u))) +
-                           (((r.tailm >> b) & 1u) ? r.padt : 0u);
-        return ((r.valid >> b) & 1u) ? r.base + 512u * h + 1024u * i - d : kRollNone;
-    }
-    __device__ __forceinline__ void operator()(int i) const {
-        const uint32_t x0 = delta(uint32_t(i), 0u), x1 = delta(uint32_t(i), 1u);
-        const uint32_t off = lane16 + (hi ? x1 : x0);
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(r.rsrc, off, 0, AUX);
-        v[i] = make_uint4(x[0], x[1], x[2], x[3]);
-    }
-};
-
-// VERIFY: the expected checksums lane `lane` compares for work item t.
-__device__ __forceinline__ uint32_t expect_of(const KParams &p, FastTile t, int lane) {
-    if (t.meta & kGeneralTile) {
-        const GShape g = gshape(t);
-        return uint32_t(lane) < g.nch + (g.kt ? 1u : 0u) ? p.expect[t.out + uint32_t(lane)] : 0u;
-    }
-    const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
-    return rep_lane(lane, blk, nb, lg) ? p.expect[t.out + (blk >> lg)] : 0u;
-}
-
 // Bytes of a dword with index < n (n clamped to 0..4).
 __device__ __forceinline__ uint32_t bytes_mask(int64_t n) {
     return n >= 4 ? 0xffffffffu : (n <= 0 ? 0u : ((1u << (8 * uint32_t(n))) - 1u));
@@ -306,11 +217,11 @@ __device__ __forceinline__ void apply_keep(uint4 &x, const uint4 &k, uint32_t f)
 // tail chunk (at most one start per item) takes its own masks in the piece
 // row that holds its first block (a wave-uniform branch).  Unpadded items
 // (bpc = 512 k, tail a multiple of 512) need nothing.
-template <int DIAG, bool S4, int IMG, typename Post = NoPost>
+template <int DIAG, bool S4, int IMG>
 __device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g, const GSub &gs, const uint4 &kp,
-                                            uint4 v[8], uint32_t pc[8], int lane, Post post = Post{}) {
+                                            uint4 v[8], uint32_t pc[8], int lane) {
     if (DIAG & 4) {  // DIAGNOSTIC (debug variants only, wrong results): no chunk-start masks
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{}, post);
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
         return;
     }
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
@@ -323,14 +234,14 @@ __device__ __forceinline__ void gsub_pieces(const uint8_t *lds, const GShape &g,
             apply_keep(x, kp, 0u - ((sfh >> (2 * i)) & 1u));
             if ((tst >> (2 * i)) & 3u)  // (uniform)
                 apply_keep(x, keep_masks(mt), 0u - ((tsh >> (2 * i)) & 1u));
-        }, post);
+        });
     } else if (g.padt) {
         // Only the tail chunk is padded (a power-of-two or 512 k packet with a short tail).
         tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, [&](int i, uint4 &x) {
             if ((tst >> (2 * i)) & 3u) apply_keep(x, keep_masks(mt), 0u - ((tsh >> (2 * i)) & 1u));
-        }, post);
+        });
     } else {
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{}, post);
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
     }
 }
 
@@ -344,19 +255,11 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
 // order and prefix-XORed along 16-lane rows (DPP row_shr), and lane c adds
 // the XOR of its chunk's blocks in the subtile as P[hi - 1] ^ P[lo - 1].
 // After the last subtile lane c holds chunk c's lin, and crc = lin ^
-// crc(0, zeros(n)) for its n bytes.
-//
-// ROLL (general builds, not the diagnostic compute-only build): subtile s +
-// 1's loads are issued during subtile s's lookups, and during the last
-// subtile's the first loads of the wave's next work item `nft` (when
-// has_next; its loads then sit in v[] on return, a shifted tile's extra 16
-// bytes in v[8]); pre0: this item's subtile 0 was loaded that way by the
-// previous item.  Without ROLL each subtile's loads are issued after the
-// previous one's lookups.
-template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, bool ROLL = false>
+// crc(0, zeros(n)) for its n bytes.  Each subtile's loads are issued after
+// the previous one's lookups.
+template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
-                                             uint4 v[9], uint32_t ev, int lane, bool pre0 = false,
-                                             FastTile nft = FastTile{0, 0, 0}, bool has_next = false) {
+                                             uint4 v[8], uint32_t ev, int lane) {
     const GShape g = gshape(t);
     const uint32_t c = uint32_t(lane);
     const uint32_t nout = g.nch + (g.kt ? 1u : 0u);
@@ -373,62 +276,35 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     const uint4 kp = keep_masks(int(g.pad) - int(16u * (uint32_t(lane) & 31u)));
     GState st;
     uint32_t acc = 0;
-    constexpr bool kRoll = ROLL && !COMPDIAG;
-    GSub gs = gsub(g, 0, st);
-    if (kRoll && !pre0) {
-        const Roll r0 = roll_general(p, g, gs, 0);
-        const RollPost<AUX> ld{r0, v, 16u * (uint32_t(lane) & 31u), lane >= 32};
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ld(i);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
     for (uint32_t s = 0; s < nsub; ++s) {
+        // Unpadded items' loads need no block facts: issue them before the
+        // subtile's pattern-table fetches (two dependent scalar loads).
+        const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
+        if (contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
+        const GSub gs = gsub(g, s, st);
+        if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
         uint32_t pc[8];
-        // (without ROLL, unpadded items' loads need no block facts: issue them
-        // before the subtile's pattern-table fetches, two dependent scalar loads)
-        if (!kRoll && contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
-        // (subtile s's facts; subtile 0's were derived before the loop)
-        if (s) gs = gsub(g, s, st);
-        GState st1 = st;
-        gstate_next(g, gs, st1);
-        if (kRoll) {
-            // what the wave loads next: subtile s + 1 (its facts are derived
-            // again at the top of the next iteration: cheaper than keeping them
-            // live through the lookups), or the next work item
-            const bool last = s + 1u == nsub;
-            const Roll r = !last     ? roll_general(p, g, gsub(g, s + 1u, st1), s + 1u)
-                           : has_next ? roll_item(p, nft)
-                                      : roll_none(p);
-            gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane,
-                                       RollPost<AUX>{r, v, 16u * (uint32_t(lane) & 31u), lane >= 32});
-            if (last && r.v8 != kRollNone) {  // (uniform) a shifted tile's last 16 bytes, lane 0
-                const auto x = __builtin_amdgcn_raw_buffer_load_b128(r.rsrc, lane == 0 ? r.v8 : kRollNone, 0, AUX);
-                v[8] = make_uint4(x[0], x[1], x[2], x[3]);
-            }
-        } else {
-            if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
-            gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
-        }
+        gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
         uint32_t x = block_lin(pc, lane);
         if (DIAG & 2) {  // DIAGNOSTIC (debug variants only, wrong results): no per-subtile gather
             acc ^= x;
-        } else {
-            const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
-            const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
-            if (sh) x = zshift<S4, IMG>(lds, sh, x);
-            uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(x)));  // lane l: block l & 15
-            y ^= dpp_zero<0x111>(y);  // row_shr:1
-            y ^= dpp_zero<0x112>(y);  // row_shr:2
-            y ^= dpp_zero<0x114>(y);  // row_shr:4
-            y ^= dpp_zero<0x118>(y);  // row_shr:8: lane l holds blocks 0 .. l & 15
-            const int base = int(16u * s);
-            const int l1 = min(max(int(lo) - base, 0), 16), h1 = min(max(int(hi) - base, 0), 16);
-            const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(y)));
-            const uint32_t pl = uint32_t(__builtin_amdgcn_ds_bpermute((max(l1, 1) - 1) << 2, int(y)));
-            if (h1 > l1) acc ^= ph ^ (l1 ? pl : 0u);
+            gstate_next(g, gs, st);
+            continue;
         }
-        st = st1;
+        const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
+        const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
+        if (sh) x = zshift<S4, IMG>(lds, sh, x);
+        uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(x)));  // lane l: block l & 15
+        y ^= dpp_zero<0x111>(y);  // row_shr:1
+        y ^= dpp_zero<0x112>(y);  // row_shr:2
+        y ^= dpp_zero<0x114>(y);  // row_shr:4
+        y ^= dpp_zero<0x118>(y);  // row_shr:8: lane l holds blocks 0 .. l & 15
+        const int base = int(16u * s);
+        const int l1 = min(max(int(lo) - base, 0), 16), h1 = min(max(int(hi) - base, 0), 16);
+        const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(y)));
+        const uint32_t pl = uint32_t(__builtin_amdgcn_ds_bpermute((max(l1, 1) - 1) << 2, int(y)));
+        if (h1 > l1) acc ^= ph ^ (l1 ? pl : 0u);
+        gstate_next(g, gs, st);
     }
     if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ (c < g.nch ? cf : ct), ev);
 }

@@ -182,6 +182,53 @@ static int time_calls(const char *name, hipStream_t s, int n, F call, bool first
     return 0;
 }
 
+// Does a stop event per launch cost more the longer it runs?  exec (the
+// plan's mark as the stop event), verify, exec again, then multi-block
+// launches of one block with no stop event the library sees... (every
+// plan launch now completes the plan's mark), with one reused stop event,
+// and with a ring of 8 stop events.
+static int stopev_mode(size_t npk, int n) {
+    const uint32_t len = 65536, bpc = 512;
+    std::vector<crc32c_packet> pk(npk);
+    for (size_t i = 0; i < npk; ++i) pk[i] = crc32c_packet{uint64_t(i) * len, uint64_t(i) * (len / bpc), len, bpc};
+    crc32c_ctx *ctx = nullptr;
+    CHECK(crc32c_ctx_create(0, &ctx) == 0);
+    crc32c_plan *plan = nullptr;
+    CHECK(crc32c_plan_create(ctx, pk.data(), npk, 0, &plan) == 0);
+    const size_t bytes = npk * len, nsums = npk * (len / bpc);
+    void *src = nullptr;
+    uint32_t *dst = nullptr, *res = nullptr;
+    CHECK(hipMalloc(&src, bytes) == hipSuccess);
+    CHECK(hipMemset(src, 0x5a, bytes) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&dst), nsums * 4) == hipSuccess);
+    CHECK(hipMalloc(reinterpret_cast<void **>(&res), 64) == hipSuccess);
+    hipStream_t s;
+    CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+    CHECK(crc32c_plan_exec(plan, src, dst, s) == 0);
+    hipEvent_t ring[8];
+    for (auto &e : ring) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess);
+    const void *pays[1] = {src};
+    uint32_t *os[1] = {dst};
+    std::printf("{\"mode\": \"stopev\", \"packets\": %zu, \"launches\": %d, ", npk, n);
+    int rc = time_calls("exec_1", s, n, [&](int) { return crc32c_plan_exec(plan, src, dst, s); }, true);
+    rc = rc || time_calls("verify", s, n, [&](int) { return crc32c_plan_verify(plan, src, dst, res, s); }, false);
+    rc = rc || time_calls("exec_2", s, n, [&](int) { return crc32c_plan_exec(plan, src, dst, s); }, false);
+    rc = rc || time_calls("blocks_stop_one", s, n, [&](int) { return hdfs_crc::exec_blocks(plan, pays, os, 1, s, ring[0]); },
+                          false);
+    rc = rc || time_calls("blocks_stop_ring8", s, n,
+                          [&](int i) { return hdfs_crc::exec_blocks(plan, pays, os, 1, s, ring[i & 7]); }, false);
+    rc = rc || time_calls("exec_3", s, n, [&](int) { return crc32c_plan_exec(plan, src, dst, s); }, false);
+    std::printf("}\n");
+    for (auto &e : ring) (void)hipEventDestroy(e);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    (void)hipFree(res);
+    crc32c_plan_destroy(plan);
+    crc32c_ctx_destroy(ctx);
+    (void)hipStreamDestroy(s);
+    return rc;
+}
+
 static int calls_mode(size_t npk, int n) {
     const uint32_t len = 65536, bpc = 512;
     std::vector<crc32c_packet> pk(npk);
@@ -391,6 +438,8 @@ static int rtt_mode(int n) {
 int main(int argc, char **argv) {
     if (argc > 1 && std::string(argv[1]) == "write") return write_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
     if (argc > 1 && std::string(argv[1]) == "raw") return raw_mode(argc > 2 ? std::atoi(argv[2]) : 4000);
+    if (argc > 1 && std::string(argv[1]) == "stopev")
+        return stopev_mode(argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 64, argc > 3 ? std::atoi(argv[3]) : 4000);
     if (argc > 1 && std::string(argv[1]) == "rtt") return rtt_mode(argc > 2 ? std::atoi(argv[2]) : 2000);
     if (argc > 1 && std::string(argv[1]) == "multi")
         return multi_mode(argc > 2 ? std::strtoul(argv[2], nullptr, 10) : 256, argc > 3 ? std::atoi(argv[3]) : 2000);

@@ -24,6 +24,8 @@ for s in ${STEPS:-calls multi}; do
     brate) run brate 240 tools/block_rate ${BR_ARGS:-16 400 16 30 2 1} ;;
     brate1) run brate1 120 tools/block_rate 1 2000 16 0 1 1 ;;
     rtt) run rtt 120 tools/launch_rate rtt 2000 ;;
+    stopev) run stopev_base 120 abwt/tools/launch_rate calls 64 4000 && run stopev 120 tools/launch_rate stopev 64 4000 &&
+            run stopev_base2 120 abwt/tools/launch_rate calls 64 4000 && run stopev2 120 tools/launch_rate stopev 64 4000 ;;
     tres) run tres 200 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "resident or destroyed" ;;
     multi) run multi 180 tools/launch_rate multi 256 2000 ;;
     multiprof) run multiprof 300 rocprofv3 --kernel-trace --hip-trace --stats -d $OUT/multiprof -o run --output-format csv -- tools/launch_rate multi 256 1000 ;;
