@@ -249,13 +249,15 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
 // Orders a launch on `stream` after the plan's upload: nothing once the
 // upload is known complete; else a stream wait on its event (or, while the
 // stream is being captured into a graph, a host wait: a capture cannot wait
-// on work outside it).
-int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing) {
+// on work outside it).  Notes the stream for the plan's release.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream) {
     RelaxedCapture relaxed;  // (the queries below while another thread captures a graph)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(stream, &cs));
-    *capturing = cs != hipStreamCaptureStatusNone;
-    if (*capturing) plan->captured = true;
+    const bool capturing = cs != hipStreamCaptureStatusNone;
+    if (capturing) plan->captured = true;
+    if (std::find(plan->launch_streams.begin(), plan->launch_streams.end(), stream) == plan->launch_streams.end())
+        plan->launch_streams.push_back(stream);
     DevicePlan *dp = &plan->dp;
     if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
         const hipError_t q = hipEventQuery(dp->uploaded);
@@ -263,7 +265,7 @@ int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing) {
             dp->ready.store(true, std::memory_order_release);
         } else {
             if (q != hipErrorNotReady) HIP_TRY(q);
-            if (*capturing) {
+            if (capturing) {
                 HIP_TRY(hipEventSynchronize(dp->uploaded));
                 dp->ready.store(true, std::memory_order_release);
             } else {
@@ -274,40 +276,61 @@ int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing) {
     return 0;
 }
 
-int stream_mark(crc32c_plan *plan, hipStream_t stream, hipEvent_t *out) {
-    RelaxedCapture relaxed;
-    for (const auto &x : plan->marks)
-        if (x.stream == stream) {
-            *out = x.done;
-            return 0;
-        }
-    hipEvent_t e = nullptr;
-    {
-        std::lock_guard<std::mutex> lock(plan->ctx->pool_mu);
-        e = take_event(plan->ctx);
-    }
-    if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    plan->marks.push_back({stream, e});
-    *out = e;
-    return 0;
+void plan_forget_stream(crc32c_plan *plan, hipStream_t stream) {
+    std::lock_guard<std::mutex> lock(plan->mu);
+    auto &v = plan->launch_streams;
+    v.erase(std::remove(v.begin(), v.end(), stream), v.end());
 }
 
-// The plan's block goes back to the pool once the marks (each recorded after
-// the plan's last launch on its stream) and the upload have completed; no
-// stream is touched, so the caller may already have destroyed them.
 void release_plan_blocks(crc32c_plan *plan) {
     crc32c_ctx *ctx = plan->ctx;
     DevicePlan *dp = &plan->dp;
+    RelaxedCapture relaxed;
     Release r;
     r.d = dp->d;
     r.dcap = dp->cap;
     r.h = dp->h;
     r.hcap = dp->hcap;
-    for (const auto &m : plan->marks) r.events.push_back(m.done);
-    plan->marks.clear();
+    bool held = plan->captured;
+    // Per launch stream: nothing when it is idle (its launches of the plan
+    // are done -- the usual case: exec, synchronise, destroy), else an event
+    // recorded now (it completes after them).  The streams must still exist:
+    // a plan is destroyed before the streams it was launched on.
+    for (hipStream_t s : plan->launch_streams) {
+        if (held) break;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            (void)hipGetLastError();
+            held = true;  // (a capture in progress on it may hold the plan's launches)
+            break;
+        }
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) continue;
+        if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            held = true;
+            break;
+        }
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> lock(ctx->pool_mu);
+            e = take_event(ctx);
+        }
+        if ((!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) || hipEventRecord(e, s) != hipSuccess) {
+            (void)hipGetLastError();
+            if (e) {
+                std::lock_guard<std::mutex> lock(ctx->pool_mu);
+                ctx->spare_events.push_back(e);
+            }
+            held = true;
+            break;
+        }
+        r.events.push_back(e);
+    }
+    plan->launch_streams.clear();
     if (dp->uploaded) r.events.push_back(dp->uploaded);
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
-    if (plan->captured && r.d) {  // (a graph may replay its launches at any time)
+    if (held && r.d) {
         ctx->held.emplace_back(r.d, r.dcap);
         drop_block(ctx->dev_pool, r.d);
         r.d = nullptr;
@@ -372,27 +395,23 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
 }
 
 // Orders the plan's next verify launch on `stream` after its previous ones:
-// when the stream changes, the previous stream's mark (recorded after the
-// plan's last launch there) is waited on.  Same stream: nothing to do
-// (stream order).  A previous launch that was captured has no mark: graph
-// replays are ordered by the caller.  Caller holds plan->mu.
+// when the stream changes, an event recorded on the previous stream now (it
+// covers that stream's launches so far) is waited on.  Same stream: nothing
+// to do (stream order).  Caller holds plan->mu.
 int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
-    if (plan->launched && plan->last_stream != stream)
-        for (const auto &m : plan->marks)
-            if (m.stream == plan->last_stream) HIP_TRY(hipStreamWaitEvent(stream, m.done, 0));
+    if (plan->launched && plan->last_stream != stream) {
+        if (!plan->last_done) HIP_TRY(hipEventCreateWithFlags(&plan->last_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(plan->last_done, plan->last_stream));
+        HIP_TRY(hipStreamWaitEvent(stream, plan->last_done, 0));
+    }
     plan->last_stream = stream;
     plan->launched = true;
     return 0;
 }
 
-// `stop` (optional): an event the launch completes itself (the block queue's
-// flushes, on the queue's own stream, which it drains before the plan can be
-// destroyed) -- such a launch leaves no mark; any other launch outside a
-// capture completes its stream's mark.
 int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream, hipEvent_t stop = nullptr) {
     std::lock_guard<std::mutex> lock(plan->mu);
-    bool capturing = false;
-    if (int rc = prepare_launch(plan, stream, &capturing)) return rc;
+    if (int rc = prepare_launch(plan, stream)) return rc;
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
@@ -402,12 +421,6 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream, hipEven
             HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.bad_bits), 0,
                                       size_t((plan->nchecksums + 31) / 32), stream));
     }
-    // outside a capture, the launch completes the stream's mark itself (its
-    // dispatch's stop event: no extra command on the stream -- an
-    // hipEventRecord after the launch cost ~3 us of GPU time per small launch
-    // and ~1 us of host time, tools/launch_rate calls)
-    if (!capturing && !stop)
-        if (int rc = stream_mark(plan, stream, &stop)) return rc;
     return launch(plan->ctx, p, plan->sched, stream, stop);
 }
 
@@ -1019,6 +1032,7 @@ int crc32c_plan_destroy(crc32c_plan *plan) {
     {
         DeviceGuard guard(ctx->device);
         release_plan_blocks(plan);  // (the verify slots live in the same block)
+        if (plan->last_done) (void)hipEventDestroy(plan->last_done);
     }
     delete plan;
     ctx_release(ctx);

@@ -7,8 +7,6 @@
 // Variant numbers are those of DESIGN.md (round 1 measured 37; the ones
 // still built are listed below, the others were within noise of variant 0
 // and were removed).
-#include <hip/hip_ext.h>
-
 #include "../crc32c_device.h"
 #include "../runtime_internal.h"
 #include "hdfs_crc32c_debug.h"
@@ -71,16 +69,9 @@ const Variant *find(int v) {
     return nullptr;
 }
 
-#define HDFS_LAUNCH(T, W, M)                                                                 \
-    do {                                                                                     \
-        if (stop)                                                                            \
-            hipExtLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, nullptr, stop, 0u, p); \
-        else                                                                                 \
-            hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p);     \
-    } while (0)
+#define HDFS_LAUNCH(T, W, M) hipLaunchKernelGGL((hdfs_crc32c_plan_kernel<T, W, M>), g, b, 0, stream, p)
 
-hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream,
-                          hipEvent_t stop) {
+hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
     const uint32_t units = (v.id >= 51 && v.id <= 55) ? 4u : (v.id == 60 || v.id == 61) ? 2u : 1u;
@@ -146,13 +137,9 @@ extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev
     p.stamps = dev_stamps;
     const hipStream_t s = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lock(plan->mu);
-    bool capturing = false;
-    if (int rc = prepare_launch(plan, s, &capturing)) return rc;
-    hipEvent_t mark = nullptr;
-    if (!capturing)
-        if (int rc = stream_mark(plan, s, &mark)) return rc;
-    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s, mark)
-                         : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s, mark));
+    if (int rc = prepare_launch(plan, s)) return rc;
+    HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
+                         : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));
     return 0;
 }
 

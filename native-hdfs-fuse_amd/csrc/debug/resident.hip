@@ -40,6 +40,7 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -53,9 +54,10 @@ namespace {
 using namespace hdfs_crc_dev;
 
 constexpr uint32_t kRing = 64;       // tickets in flight at most
-constexpr uint32_t kPhases = 5;      // blocks processed concurrently
-constexpr uint32_t kWaves = 12;      // 768 threads, one workgroup per CU (152 KiB LDS)
-constexpr uint32_t kWorkers = kWaves - 1;
+// (the kernel is a template on WAVES per workgroup -- one workgroup per CU,
+// 152 KiB of LDS -- and PHASES, the blocks processed at once: two worker
+// waves per workgroup and phase; HDFS_CRC32C_RESIDENT_WAVES=16 selects 16
+// waves / 7 phases instead of 12 / 5, an A/B of this debug-only experiment)
 constexpr uint32_t kMaxWg = 256;     // one flag lane-dword per workgroup (64 lanes x 4)
 constexpr uint64_t kTicksPerUs = 100;  // s_memrealtime: 100 MHz
 constexpr uint64_t kStuckMs = 50;
@@ -166,16 +168,17 @@ __device__ void forwarder(const RParams &p, int lane) {
     uint64_t last = now();
     for (;;) {
         bool progress = false;
+        // the next 64 tickets' host slots, one load per lane (ring reuse:
+        // ticket t only once t - kRing is complete; `col` from the previous
+        // pass, so the collector's word and the host slots load together)
+        const uint64_t cand = fwd + uint64_t(lane);
+        const bool room = cand < col + kRing;
+        const uint64_t sq = room ? ld_sys(&h->seq[cand % kRing]) : 0;
         const uint64_t c = ld_dev(&d->col);
         if (c != col) {
             col = c;
             progress = true;
         }
-        // the next 64 tickets' host slots, one load per lane (ring reuse:
-        // ticket t only once t - kRing is complete)
-        const uint64_t cand = fwd + uint64_t(lane);
-        const bool room = cand < col + kRing;
-        const uint64_t sq = room ? ld_sys(&h->seq[cand % kRing]) : 0;
         const uint64_t ready = __ballot(room && sq == cand + 1);
         const uint32_t n = ~ready ? uint32_t(__builtin_ctzll(~ready)) : 64u;  // consecutive ready tickets from fwd
         if (n) {
@@ -258,7 +261,9 @@ __device__ void collector(const RParams &p, int lane) {
     }
 }
 
-__global__ __launch_bounds__(kWaves * 64, 3) void resident_kernel(RParams p) {
+template <uint32_t kWaves, uint32_t kPhases>
+__global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RParams p) {
+    constexpr uint32_t kWorkers = kWaves - 1;
     constexpr uint32_t kStage = kS4StageBytes;
     __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 4 * kRing];
     uint32_t *lcnt = reinterpret_cast<uint32_t *>(lds + kStage);  // per slot: this workgroup's workers done
@@ -336,6 +341,7 @@ struct crc32c_resident {
     DevRing *d = nullptr;
     hipStream_t stream = nullptr;
     std::atomic<uint64_t> next{0};
+    uint32_t waves = 12;     // A/B: HDFS_CRC32C_RESIDENT_WAVES
     std::mutex mu;           // launches
     bool running = false;    // a launch may be on the GPU (under mu)
     std::atomic<uint64_t> launches{0};
@@ -370,7 +376,10 @@ int ensure_running(crc32c_resident *r) {
     const uint64_t ctl[3] = {col, col, 0};
     HIP_TRY(hipMemcpyAsync(&r->d->fwd, ctl, sizeof ctl, hipMemcpyHostToDevice, r->stream));
     HIP_TRY(hipStreamSynchronize(r->stream));  // (ctl is on this stack)
-    hipLaunchKernelGGL(resident_kernel, dim3(r->grid), dim3(kWaves * 64), 0, r->stream, p);
+    if (r->waves == 16)
+        hipLaunchKernelGGL((resident_kernel<16, 7>), dim3(r->grid), dim3(16 * 64), 0, r->stream, p);
+    else
+        hipLaunchKernelGGL((resident_kernel<12, 5>), dim3(r->grid), dim3(12 * 64), 0, r->stream, p);
     HIP_TRY(hipGetLastError());
     r->running = true;
     r->launches.fetch_add(1, std::memory_order_release);
@@ -393,6 +402,7 @@ int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_res
     r->device = plan->ctx->device;
     r->grid = uint32_t(std::min(plan->ctx->num_cu, int(kMaxWg)));
     r->idle_ticks = uint64_t(idle_us ? idle_us : 2000) * kTicksPerUs;
+    if (const char *w = std::getenv("HDFS_CRC32C_RESIDENT_WAVES")) r->waves = std::atoi(w) == 16 ? 16u : 12u;
     hdfs_crc::DeviceGuard guard(r->device);
     HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&r->h), sizeof(HostRing), hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(static_cast<void *>(r->h), 0, sizeof(HostRing));

@@ -159,25 +159,18 @@ struct crc32c_plan {
     crc32c_ctx *ctx = nullptr;
     // Verify launches of a plan share its scheduler slots, so they are kept
     // in GPU order: one on another stream than the previous one first waits
-    // for that stream's mark.  Exec launches are not ordered.
+    // for it (last_done).  Exec launches are not ordered.
     std::mutex mu;
     hdfs_crc::SchedSlots sched;
     hipStream_t last_stream = nullptr;
+    hipEvent_t last_done = nullptr;
     bool launched = false;
-    // Per stream the plan was launched on (outside a graph capture): an event
-    // every launch of the plan there completes as its dispatch's stop event,
-    // so it completes after the plan's last launch on that stream.  Destroy gates the block's reuse
-    // on these events and touches no stream (the caller may have destroyed
-    // it already); a verify launch on another stream than the previous one
-    // waits on the previous stream's event.  captured: a launch went into a
-    // graph capture (then the block is never reused).  (Round 3 queried and
-    // recorded on every launch stream at destroy time, which crashed on a
-    // stream destroyed first.)
-    struct StreamMark {
-        hipStream_t stream;
-        hipEvent_t done;
-    };
-    std::vector<StreamMark> marks;
+    // Every stream a launch of the plan went on (at destroy time: nothing to
+    // do for an idle one, else an event recorded on it gates the block's
+    // reuse), and whether a launch went into a graph capture (then the block
+    // is never reused).  (Round 3 first gave every launch a stop event to
+    // complete instead; that cost every launch)
+    std::vector<hipStream_t> launch_streams;
     bool captured = false;
     hdfs_crc::DevicePlan dp;
     uint64_t nchecksums = 0, payload_bytes = 0;
@@ -197,12 +190,11 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
 // device (into *dp), asynchronously; plan_ready orders a launch after it.
 int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
 // Before a launch of `plan` on `stream` (caller holds plan->mu): orders it
-// after the plan's upload; *capturing: the stream is being captured.
-int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing);
-// The (plan, stream) mark event (crc32c_plan::marks), created on first use
-// (caller holds plan->mu): a launch outside a capture passes it as its stop
-// event, so it completes after the plan's last launch on that stream.
-int stream_mark(crc32c_plan *plan, hipStream_t stream, hipEvent_t *out);
+// after the plan's upload and notes the stream for the plan's release.
+int prepare_launch(crc32c_plan *plan, hipStream_t stream);
+// `stream` (idle, about to be destroyed by the library itself: a block
+// queue's) no longer needs an event at the plan's release.
+void plan_forget_stream(crc32c_plan *plan, hipStream_t stream);
 // crc32c_plan_exec_blocks; `stop` (optional) is completed by the last launch.
 int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs, size_t nblocks,
                 hipStream_t stream, hipEvent_t stop);

@@ -734,17 +734,6 @@ def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
         ctx.close()
 
 
-def _hip_runtime():
-    """The process's one HIP runtime (torch's, which the library binds to too)."""
-    import ctypes
-
-    with open("/proc/self/maps") as f:
-        for line in f:
-            if "libamdhip64" in line:
-                return ctypes.CDLL(line.split()[-1])
-    raise RuntimeError("libamdhip64 is not loaded")
-
-
 def test_plan_destroyed_after_its_context(hdfs, orc):
     """A plan outliving crc32c_ctx_destroy (a garbage collector freeing a
     plan late, e.g. one a failed test's traceback held): the context is
@@ -768,51 +757,6 @@ def test_plan_destroyed_after_its_context(hdfs, orc):
         for p in plans:
             p.close()
         torch.cuda.synchronize()
-
-
-def test_stream_destroyed_before_plan(hdfs, orc):
-    """A caller's stream destroyed BEFORE the plan that ran on it (a FUSE
-    worker thread tearing down its stream, then the plan): the
-    plan's launches leave one event per (plan, stream), so destroy touches
-    no stream.  Launches in flight on a raw HIP stream, the stream destroyed,
-    then the plan; its pooled block is recycled into new plans of the same
-    size on another stream.  Every output exact, no crash."""
-    import ctypes
-
-    torch = _torch()
-    hip = _hip_runtime()
-    ctx = hdfs.Context(0)
-    try:
-        pk = oracle.uniform_packets(512)
-        n = hdfs.total_checksums(pk)
-        payload = oracle.xorshift64_bytes(512 * 65536, 4711)
-        want = orc.batch(payload, pk, n)
-        dev = torch.from_numpy(payload).cuda()
-        outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(4)]
-        torch.cuda.synchronize()
-        for rnd in range(3):
-            s = ctypes.c_void_p()
-            assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0  # hipStreamNonBlocking
-            plan = hdfs.Plan(ctx, pk)
-            for o in outs:
-                plan.exec(dev.data_ptr(), o.data_ptr(), s.value)
-            assert hip.hipStreamDestroy(s) == 0  # (launches may still be in flight)
-            plan.close()
-            torch.cuda.synchronize()
-            for o in outs:
-                assert np.array_equal(o.cpu().numpy().view(np.uint32), want), rnd
-                o.zero_()
-            # the block comes back to the pool: a new plan of the same size on a torch stream
-            p2 = hdfs.Plan(ctx, pk)
-            ts = torch.cuda.Stream()
-            p2.exec(dev.data_ptr(), outs[0].data_ptr(), ts.cuda_stream)
-            ts.synchronize()
-            assert np.array_equal(outs[0].cpu().numpy().view(np.uint32), want), rnd
-            p2.close()
-            outs[0].zero_()
-            torch.cuda.synchronize()
-    finally:
-        ctx.close()
 
 
 @pytest.mark.parametrize("bpc", [512, 2048, 4096])
