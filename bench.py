@@ -226,6 +226,52 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def _hip_runtime():
+    """The process's one HIP runtime (torch's; the library binds to it too)."""
+    import ctypes
+
+    with open("/proc/self/maps") as f:
+        for line in f:
+            if "libamdhip64" in line:
+                return ctypes.CDLL(line.split()[-1])
+    return None
+
+
+def record_in_graph(ev, stream) -> None:
+    """hipEventRecordWithFlags(ev, stream, hipEventRecordExternal): inside a
+    capture, an event record node of the graph."""
+    import ctypes
+
+    rc = _hip_runtime().hipEventRecordWithFlags(ctypes.c_void_p(ev.cuda_event), ctypes.c_void_p(stream.cuda_stream), 1)
+    if rc != 0:
+        raise RuntimeError("hipEventRecordWithFlags(external) rc %d" % rc)
+
+
+def graph_timing_events(torch, dev, one_step):
+    """Two timing events that can be recorded INSIDE a captured graph, or None
+    when this stack cannot: a one-step trial graph [record, step, record] is
+    captured, replayed and timed first."""
+    try:
+        if _hip_runtime() is None:
+            return None
+        evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        trial = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(trial, capture_error_mode="thread_local"):
+            cap = torch.cuda.current_stream(dev)
+            record_in_graph(evs[0], cap)
+            one_step(cap.cuda_stream)
+            record_in_graph(evs[1], cap)
+        trial.replay()
+        torch.cuda.synchronize()
+        ok = evs[0].elapsed_time(evs[1]) > 0
+        del trial
+        torch.cuda.synchronize()
+        return evs if ok else None
+    except Exception:  # noqa: BLE001 -- any failure: time the window instead
+        torch.cuda.synchronize()
+        return None
+
+
 def timed_calls(fn, budget_s: float = 0.25, min_reps: int = 5, max_reps: int = 2000) -> float:
     """Median wall seconds of one call of fn(), over about budget_s of calls."""
     fn()
@@ -470,20 +516,25 @@ def main():
     # recorded on the stream around graph.replay() also hold the graph's
     # launch latency, which a short window (the driver's 20 steps) would
     # spread over its launches (~1 us per step at K = 20).
+    # (torch refuses external events on ROCm; HIP's own hipEventRecordWithFlags
+    # with hipEventRecordExternal records one as a graph node -- tried on a
+    # one-step trial graph first, and left out if anything about it fails)
     gev = None
+    if use_graph:
+        gev = graph_timing_events(torch, dev, lambda cap: step(0, cap))
     if use_graph:
         try:
             graph = torch.cuda.CUDAGraph()
-            gev = (torch.cuda.Event(enable_timing=True, external=True),
-                   torch.cuda.Event(enable_timing=True, external=True))
             # (thread_local: other threads of the process -- e.g. the process
             # group's watchdog -- may make CUDA calls while this thread captures)
             with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                 cap = torch.cuda.current_stream(dev)
-                gev[0].record(cap)
+                if gev is not None:
+                    record_in_graph(gev[0], cap)
                 for i in range(args.steps):
                     step(i, cap.cuda_stream)
-                gev[1].record(cap)
+                if gev is not None:
+                    record_in_graph(gev[1], cap)
             graph.replay()  # (first replay uploads the graph)
             torch.cuda.synchronize()
         except RuntimeError as e:  # no graph on this stack: time host-issued launches instead

@@ -23,7 +23,12 @@ for s in ${STEPS:-calls multi}; do
              run calls_base2 120 abwt/tools/launch_rate calls 64 4000 && run calls_cand2 120 tools/launch_rate calls 64 4000 ;;
     brate) run brate 240 tools/block_rate ${BR_ARGS:-16 400 16 30 2 1} ;;
     brate1) run brate1 120 tools/block_rate 1 2000 16 0 1 1 ;;
+    bres) run bres12 240 tools/block_rate 16 400 16 30 2 1 && run bres16 240 env HDFS_CRC32C_RESIDENT_WAVES=16 tools/block_rate 16 400 16 30 2 1 &&
+          run bres1_16 120 env HDFS_CRC32C_RESIDENT_WAVES=16 tools/block_rate 1 2000 16 0 1 1 ;;
     rtt) run rtt 120 tools/launch_rate rtt 2000 ;;
+    brlong) run brlong 300 tools/block_rate 16 4000 16 30 2 1 ;;
+    bspin) for sp in 50 10 0; do run bspin$sp 200 env HDFS_CRC32C_QUEUE_SPIN_US=$sp tools/block_rate 16 400 16 30 2 1 || exit 1; done ;;
+    b4) run bench_c4 300 python bench.py --config c4 --no-cpu --no-host --steps 200 --warmup 20 ;;
     stopev) run stopev_base 120 abwt/tools/launch_rate calls 64 4000 && run stopev 120 tools/launch_rate stopev 64 4000 &&
             run stopev_base2 120 abwt/tools/launch_rate calls 64 4000 && run stopev2 120 tools/launch_rate stopev 64 4000 ;;
     tres) run tres 200 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "resident or destroyed" ;;
