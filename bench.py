@@ -239,7 +239,8 @@ def _hip_runtime():
 
 def record_in_graph(ev, stream) -> None:
     """hipEventRecordWithFlags(ev, stream, hipEventRecordExternal): inside a
-    capture, an event record node of the graph."""
+    capture, an event record node of the graph.  `ev` must already exist (a
+    torch event is created by its first record)."""
     import ctypes
 
     rc = _hip_runtime().hipEventRecordWithFlags(ctypes.c_void_p(ev.cuda_event), ctypes.c_void_p(stream.cuda_stream), 1)
@@ -247,29 +248,39 @@ def record_in_graph(ev, stream) -> None:
         raise RuntimeError("hipEventRecordWithFlags(external) rc %d" % rc)
 
 
+_trial_graphs = []  # (kept: torch aborts destroying a graph whose capture failed)
+
+
 def graph_timing_events(torch, dev, one_step):
     """Two timing events that can be recorded INSIDE a captured graph, or None
     when this stack cannot: a one-step trial graph [record, step, record] is
-    captured, replayed and timed first."""
-    try:
-        if _hip_runtime() is None:
-            return None
-        evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        trial = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(trial, capture_error_mode="thread_local"):
-            cap = torch.cuda.current_stream(dev)
-            record_in_graph(evs[0], cap)
-            one_step(cap.cuda_stream)
-            record_in_graph(evs[1], cap)
-        trial.replay()
-        torch.cuda.synchronize()
-        ok = evs[0].elapsed_time(evs[1]) > 0
-        del trial
-        torch.cuda.synchronize()
-        return evs if ok else None
-    except Exception:  # noqa: BLE001 -- any failure: time the window instead
-        torch.cuda.synchronize()
+    captured, replayed and timed first.  Nothing inside the capture may raise
+    (torch cannot destroy a graph whose capture ended in an exception), so
+    the events and the entry point are checked before it."""
+    hip = _hip_runtime()
+    if hip is None or not hasattr(hip, "hipEventRecordWithFlags"):
         return None
+    evs = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    for e in evs:
+        e.record()  # creates the HIP event
+    torch.cuda.synchronize()
+    if not all(e.cuda_event for e in evs):
+        return None
+    trial = torch.cuda.CUDAGraph()
+    _trial_graphs.append(trial)
+    rcs = []
+    with torch.cuda.graph(trial, capture_error_mode="thread_local"):
+        cap = torch.cuda.current_stream(dev)
+        import ctypes
+
+        rcs.append(hip.hipEventRecordWithFlags(ctypes.c_void_p(evs[0].cuda_event), ctypes.c_void_p(cap.cuda_stream), 1))
+        one_step(cap.cuda_stream)
+        rcs.append(hip.hipEventRecordWithFlags(ctypes.c_void_p(evs[1].cuda_event), ctypes.c_void_p(cap.cuda_stream), 1))
+    if any(rcs):
+        return None
+    trial.replay()
+    torch.cuda.synchronize()
+    return evs if evs[0].elapsed_time(evs[1]) > 0 else None
 
 
 def timed_calls(fn, budget_s: float = 0.25, min_reps: int = 5, max_reps: int = 2000) -> float:

@@ -368,7 +368,13 @@ class Context:
 
 
 class Plan:
-    """Device-resident batch plan (crc32c_plan): build once, execute many."""
+    """Device-resident batch plan (crc32c_plan): build once, execute many.
+
+    ``stream`` is a raw HIP stream handle or an object with a ``cuda_stream`` attribute (a
+    ``torch.cuda.Stream``). The C library touches every stream a plan ran on when the plan is
+    destroyed (include/hdfs_crc32c.h, crc32c_plan_destroy), so a plan must be destroyed before
+    its launch streams; a stream object passed here is kept alive by the plan until ``close()``.
+    """
 
     def __init__(self, ctx: Context, pkts, flags: int = 0, write=None):
         h = ctypes.c_void_p()
@@ -384,18 +390,28 @@ class Plan:
                    "crc32c_plan_create_buffers")
         self.ctx = ctx  # keeps the context alive
         self.handle = h
+        self._streams = {}  # stream objects launched on, kept alive until close()
         self.nchecksums = int(lib().crc32c_plan_nchecksums(h))
         self.payload_bytes = int(lib().crc32c_plan_payload_bytes(h))
 
-    def exec(self, dev_payload: int, dev_out: int, stream: int = 0) -> None:
+    def _stream(self, stream) -> int:
+        if isinstance(stream, int):
+            return stream
+        h = int(stream.cuda_stream)
+        self._streams.setdefault(h, stream)
+        return h
+
+    def exec(self, dev_payload: int, dev_out: int, stream=0) -> None:
+        stream = self._stream(stream)
         _check(lib().crc32c_plan_exec(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
                                       ctypes.c_void_p(stream)), "crc32c_plan_exec")
 
-    def verify(self, dev_payload: int, dev_expected: int, dev_result: int, stream: int = 0,
+    def verify(self, dev_payload: int, dev_expected: int, dev_result: int, stream=0,
                dev_bad_bits: int = 0) -> None:
         """Compare instead of store: dev_result[0] = mismatches, [1] = lowest bad index (async); with
         dev_bad_bits (ceil(nchecksums / 32) u32s) also the bitmap of mismatching checksums
         (crc32c_plan_verify_bitmap)."""
+        stream = self._stream(stream)
         if dev_bad_bits:
             _check(lib().crc32c_plan_verify_bitmap(self.handle, ctypes.c_void_p(dev_payload),
                                                    ctypes.c_void_p(dev_expected), ctypes.c_void_p(dev_result),
@@ -405,8 +421,9 @@ class Plan:
         _check(lib().crc32c_plan_verify(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_expected),
                                         ctypes.c_void_p(dev_result), ctypes.c_void_p(stream)), "crc32c_plan_verify")
 
-    def exec_blocks(self, dev_payloads, dev_outs, stream: int = 0) -> None:
+    def exec_blocks(self, dev_payloads, dev_outs, stream=0) -> None:
         """crc32c_plan_exec_blocks: this plan (one block's shape) on every block, one launch per <= 32."""
+        stream = self._stream(stream)
         n = len(dev_payloads)
         pays = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(x) for x in dev_payloads])
         outs = (ctypes.c_void_p * max(n, 1))(*[ctypes.c_void_p(x) for x in dev_outs])
@@ -427,6 +444,7 @@ class Plan:
         if self.handle:
             lib().crc32c_plan_destroy(self.handle)
             self.handle = None
+        self._streams = {}
 
     def __del__(self):
         try:

@@ -528,3 +528,22 @@ def test_kernel_buffer_resources_not_sign_extended(tmp_path):
         if "buffer_load_dwordx4" in line:
             window = lines[max(0, i - 12):i + 4]
             assert not (any("v_readfirstlane" in w for w in window) and any("s_cbranch_execnz" in w for w in window)), i
+
+
+def test_plan_keeps_stream_objects_alive():
+    """Plan.exec/verify accept a stream object and hold it until close() (destroy touches
+    the plan's launch streams, crc32c_plan_destroy in include/hdfs_crc32c.h)."""
+    import importlib
+    pkg = importlib.import_module("native-hdfs-fuse_amd")
+
+    class FakeStream:
+        cuda_stream = 0x1234
+
+    p = pkg.Plan.__new__(pkg.Plan)
+    p.handle = None
+    p._streams = {}
+    s = FakeStream()
+    assert p._stream(s) == 0x1234 and p._stream(7) == 7
+    assert p._streams == {0x1234: s}
+    p.close()
+    assert p._streams == {}

@@ -42,6 +42,10 @@ for s in ${STEPS:-calls multi}; do
     c4model) run c4model 300 python tools/c4_model.py ;;
     tgen) run tgen 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or unaligned or shifted or verify or write_plan or fsx or edge or small" ;;
     tqueue) run tqueue 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "block_queue or overlapping or per_launch or destroyed or across_streams or recycled" ;;
+    prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py ;;
+    prof3) run prof3 300 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run --output-format csv -- python3 bench.py --config c3 --no-cpu --no-host ;;
+    pmc3) run pmc3 900 env PMC_CONFIG=c3 PMC_OUT=$OUT/pmc_c3 bash tools/pmc_session.sh ;;
+    pmc2) run pmc2 900 env PMC_CONFIG=c2 PMC_OUT=$OUT/pmc_c2 bash tools/pmc_session.sh ;;
     ab) for c in ${ABCFGS:-c2b1000 c2b1536 c2t c2u c5}; do
           run ab_base_$c 300 bash -c "cd abwt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
           run ab_cand_$c 300 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-} || exit 1; done ;;
