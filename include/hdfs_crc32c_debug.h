@@ -57,6 +57,10 @@ void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_
  * return the error. */
 int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n);
 
+/* CPU time the queue's worker thread has used so far (its thread CPU clock),
+ * in ns: what the queue itself costs beside the submitting threads. */
+int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns);
+
 /* ---- 2. libhdfs_crc32c_debug.so only ---- */
 
 /* Launch of a plan with an explicit kernel variant (0 = production; see

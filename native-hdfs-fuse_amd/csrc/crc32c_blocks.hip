@@ -38,6 +38,8 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <pthread.h>
+#include <time.h>
 #include <thread>
 #include <vector>
 
@@ -93,6 +95,11 @@ struct crc32c_blocks {
     std::atomic<uint32_t> inject_fail{0};  // crc32c_debug_blocks_fail_flushes
     bool record_events = false;  // A/B (HDFS_CRC32C_QUEUE_RECORD=1): an hipEventRecord after each flush
     unsigned event_flags = hipEventDisableTiming;  // A/B (HDFS_CRC32C_QUEUE_TIMING=1: timing events)
+    // A/B (HDFS_CRC32C_QUEUE_BLOCKING=1): with max_inflight() flushes in
+    // flight (nothing more may be launched), the worker sleeps in
+    // hipEventSynchronize on the oldest one's blocking-sync event instead of
+    // polling it.
+    bool blocking = false;
     std::thread worker;
     // Diagnostic (HDFS_CRC32C_QUEUE_TRACE=<file>): per flush, steady-clock
     // ns of its first block seen by the worker, issue start / end,
@@ -284,6 +291,8 @@ void worker_loop(crc32c_blocks *q) {
             if (complete_front(q)) {
                 wake = true;
                 idle_since = Clock::now();
+            } else if (q->blocking && q->inflight.size() >= max_inflight() && q->inflight.front().ev) {
+                (void)hipEventSynchronize(q->inflight.front().ev);  // (its status: complete_front's query)
             } else {
                 relax();
             }
@@ -343,6 +352,11 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
     q->record_events = rec && rec[0] == '1';
     const char *tim = std::getenv("HDFS_CRC32C_QUEUE_TIMING");
     if (tim && tim[0] == '1') q->event_flags = hipEventDefault;
+    const char *blk = std::getenv("HDFS_CRC32C_QUEUE_BLOCKING");
+    if (blk && blk[0] == '1') {
+        q->blocking = true;
+        q->event_flags |= hipEventBlockingSync;
+    }
     DeviceGuard guard(q->device);
     HIP_TRY(hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking));
     try {
@@ -421,6 +435,16 @@ int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blo
 int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n) {
     if (!q) return fail(-EINVAL, "queue == NULL");
     q->inject_fail.store(n, std::memory_order_relaxed);
+    return 0;
+}
+
+int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns) {
+    if (!q || !ns) return fail(-EINVAL, "queue/ns == NULL");
+    clockid_t cid;
+    timespec ts{};
+    if (pthread_getcpuclockid(q->worker.native_handle(), &cid) != 0 || clock_gettime(cid, &ts) != 0)
+        return fail(-EIO, "worker thread CPU clock unavailable");
+    *ns = uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
     return 0;
 }
 

@@ -842,7 +842,8 @@ def test_block_queue_failed_flush_is_its_own(hdfs, gpu_ctx, orc):
     plan.close()
 
 
-def test_resident_kernel_blocks(hdfs, gpu_ctx, orc):
+@pytest.mark.parametrize("shape", ["12", "16x15"])
+def test_resident_kernel_blocks(hdfs, gpu_ctx, orc, shape, monkeypatch):
     """The debug library's resident kernel (A/B experiment, DESIGN.md section
     6): blocks submitted from 8 threads, 2 in flight each, bit-exact; the
     kernel exits after idle_us with nothing queued and a later submit
@@ -861,6 +862,7 @@ def test_resident_kernel_blocks(hdfs, gpu_ctx, orc):
     outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in hosts]
     torch.cuda.synchronize()
     plan = gpu_ctx.plan(pk)
+    monkeypatch.setenv("HDFS_CRC32C_RESIDENT_WAVES", shape)  # (read at create: the kernel's shape)
     r = hdfs.Resident(plan, idle_us=500)
     errs = []
 

@@ -18,7 +18,9 @@
 //              blocks in flight per thread, every block checked against the
 //              queue's checksums of the same buffer
 // Every line has cpu_us_per_block: the process's CPU time (getrusage) per
-// block -- the submitting threads' and the queue worker's spinning included.
+// block -- the submitting threads' and the queue worker's spinning included;
+// queue lines also the worker thread's own (worker_cpu_us_per_block, and
+// worker_busy = its CPU seconds per wall second).
 //
 //   tools/block_rate [threads=16] [iterations=400] [max_blocks=16] [window_us=30]
 //                    [max_depth=2] [queue_modes_only=0]
@@ -148,6 +150,9 @@ int main(int argc, char **argv) {
             CHECK(crc32c_blocks_create(plan, max_blocks, window_us, &q) == 0);
             char name[32];
             std::snprintf(name, sizeof name, depth == 1 ? "queue" : "queue%d", depth);
+            uint64_t wc0 = 0, wc1 = 0;
+            CHECK(crc32c_debug_blocks_worker_cpu_ns(q, &wc0) == 0);
+            const Clock::time_point q0 = Clock::now();
             run(name, [&](int k) {
                 if (depth == 1) {
                     for (int i = 0; i < iters; ++i) CHECK(crc32c_block_checksums(q, bufs[k], outs[k]) == 0);
@@ -162,12 +167,14 @@ int main(int argc, char **argv) {
                 }
                 for (int i = std::max(0, iters - depth); i < iters; ++i) CHECK(crc32c_block_wait(q, ring[i % depth]) == 0);
             });
+            CHECK(crc32c_debug_blocks_worker_cpu_ns(q, &wc1) == 0);
+            const double qs = seconds(q0, Clock::now());
             uint64_t flushes = 0, blocks = 0;
             CHECK(crc32c_blocks_stats(q, &flushes, &blocks) == 0);
             std::printf(", \"max_blocks\": %u, \"window_us\": %u, \"launches\": %llu, \"blocks_per_launch\": %.2f, "
-                        "\"pass\": %d}\n",
+                        "\"worker_cpu_us_per_block\": %.3f, \"worker_busy\": %.2f, \"pass\": %d}\n",
                         max_blocks, window_us, (unsigned long long)flushes, double(blocks) / double(flushes ? flushes : 1),
-                        w);
+                        double(wc1 - wc0) * 1e-3 / (double(nthreads) * iters), double(wc1 - wc0) * 1e-9 / qs, w);
             CHECK(crc32c_blocks_destroy(q) == 0);
         }
     // resident kernel (A/B, debug library): depth 1 and 2; the outputs are

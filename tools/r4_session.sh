@@ -25,6 +25,10 @@ for s in ${STEPS:-calls multi}; do
     brate1) run brate1 120 tools/block_rate 1 2000 16 0 1 1 ;;
     bres) run bres12 240 tools/block_rate 16 400 16 30 2 1 && run bres16 240 env HDFS_CRC32C_RESIDENT_WAVES=16 tools/block_rate 16 400 16 30 2 1 &&
           run bres1_16 120 env HDFS_CRC32C_RESIDENT_WAVES=16 tools/block_rate 1 2000 16 0 1 1 ;;
+    bresall) for w in 12 16 12x11 16x15; do run bres_$w 240 env HDFS_CRC32C_RESIDENT_WAVES=$w tools/block_rate 16 400 16 30 2 1 &&
+               run bres1_$w 120 env HDFS_CRC32C_RESIDENT_WAVES=$w tools/block_rate 1 2000 16 0 1 1 || exit 1; done ;;
+    bqblock) run bq_spin 240 tools/block_rate 16 400 16 30 2 1 && run bq_block 240 env HDFS_CRC32C_QUEUE_BLOCKING=1 tools/block_rate 16 400 16 30 2 1 &&
+             run bq_spin32 240 tools/block_rate 32 200 32 30 1 1 && run bq_block32 240 env HDFS_CRC32C_QUEUE_BLOCKING=1 tools/block_rate 32 200 32 30 1 1 ;;
     rtt) run rtt 120 tools/launch_rate rtt 2000 ;;
     brlong) run brlong 300 tools/block_rate 16 4000 16 30 2 1 ;;
     bspin) for sp in 50 10 0; do run bspin$sp 200 env HDFS_CRC32C_QUEUE_SPIN_US=$sp tools/block_rate 16 400 16 30 2 1 || exit 1; done ;;
