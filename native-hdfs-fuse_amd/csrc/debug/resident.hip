@@ -12,32 +12,28 @@
 //
 // Protocol (all host words in pinned, device-mapped, coherent memory):
 //  * submit (host): ticket t = an atomic counter; slot t % kRing is reused
-//    only once every ticket up to t - kRing is complete; the slot's two
-//    words (payload and out pointer) each carry t's tag, so one read of the
-//    slot tells a complete entry from a stale or half-written one.
-//  * forwarder (workgroup 0's last wave): reads 64 host slots (and the
-//    host's completion counter) per poll -- one PCIe round trip per poll, not
-//    per block -- and copies the ready slots into a device ring, tags and
-//    all (agent scope).
-//  * workers (the other waves of every workgroup): block t is run by phase
-//    t % P (P blocks in flight); within a phase PER waves per workgroup take
-//    its tiles (a 4 MiB block is 512 tiles = 2 per CU); a workgroup's phase
-//    workers count themselves in LDS and the last one writes the
-//    workgroup's flag for the slot into HOST memory (system scope) after all
-//    its checksum stores have completed.
-//  * completion (host): block t is complete when all workgroups' flags for
-//    its slot hold t + 1 (1 KiB of host memory); a waiter that sees it
-//    advances the host's completion counter `col` past every complete
-//    ticket in order.  No GPU wave collects.
+//    only once block t - kRing is complete; the slot's two words (payload
+//    and out pointer) each carry t's tag, so one read of the slot tells a
+//    complete entry from a stale or half-written one.
+//  * forwarder (workgroup 0's last wave): reads 64 host slots per poll (one
+//    PCIe round trip per poll, not per block) and copies the ready ones into
+//    a device ring, tags and all (agent scope).  It also collects: block t is complete when all
+//    workgroups' flags for its slot hold t + 1 (one 1 KiB load per check),
+//    then hdone[slot] = t + 1 (system scope).
+//  * workers (waves 0-10 of every workgroup): block t is run by phase t % 5
+//    (5 blocks in flight); within a phase two waves per workgroup take one
+//    8 KiB tile each (a 4 MiB block is 512 tiles = 2 per CU); a workgroup's
+//    phase workers count themselves in LDS and the last one stores the
+//    workgroup's flag.  Checksums are stored write-through (system scope),
+//    and every store has completed before the flag.
 //  * lifetime: the forwarder exits on the host's stop word, after idle_us
-//    with nothing outstanding, or after kStuckMs without `col` advancing
-//    while blocks are outstanding (a workgroup that never got a CU); on exit
-//    it raises the device stop word that every worker polls.  A relaunch
-//    resumes at `col` (re-running a complete block past it is harmless: the
-//    same checksums).  The host relaunches the kernel on demand (submit, or
-//    a waiter that waits long), never while one runs.  Workers have their
-//    own bound (kWorkerMs without a block).  Every wave therefore exits,
-//    whatever the host does.
+//    with nothing queued, or after kStuckMs without progress while blocks are
+//    outstanding (a workgroup that never got a CU); on exit it raises the
+//    device stop word that every worker polls, and records where it stopped
+//    (exit_col) so a relaunch resumes there.  The host relaunches the kernel
+//    on demand (submit, or a waiter that waits long), never while one runs.
+//    Workers have their own bound (kWorkerMs without a block).  Every wave
+//    therefore exits, whatever the host does.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -62,36 +58,38 @@ constexpr uint32_t kRing = 64;       // tickets in flight at most
 // (the kernel is a template on WAVES per workgroup -- one workgroup per CU,
 // 152 KiB of LDS --, PHASES, the blocks processed at once, and PER, the
 // worker waves per workgroup and phase that take tiles (2: one 8 KiB tile
-// each; 1: both tiles of the workgroup, one after the other, so twice the
-// phases fit); HDFS_CRC32C_RESIDENT_WAVES selects 12 (12 / 5 / 2, default),
-// 16 (16 / 7 / 2), 12x11 (12 / 11 / 1) or 16x15 (16 / 15 / 1): an A/B of
-// this debug-only experiment)
+// each; 1: both tiles of the workgroup, both loaded before the first one's
+// lookups, so twice the phases fit); HDFS_CRC32C_RESIDENT_WAVES selects 12
+// (12 / 5 / 2, default), 16 (16 / 7 / 2), 12x11 (12 / 11 / 1) or 16x15
+// (16 / 15 / 1): an A/B of this debug-only experiment)
 constexpr uint32_t kMaxWg = 256;     // one flag lane-dword per workgroup (64 lanes x 4)
 constexpr uint64_t kTicksPerUs = 100;  // s_memrealtime: 100 MHz
 constexpr uint64_t kStuckMs = 50;
 constexpr uint64_t kWorkerMs = 200;
 
-// A slot is two 64-bit words, payload and out pointer (48-bit GPU
-// addresses), each tagged in bits 48-63 with the low 16 bits of ticket + 1:
-// a reader that sees both with matching tags has the block's pointers (no
-// separate sequence word, and no ordering between the two stores needed).
+// A slot (host ring and device ring alike) is two 64-bit words, payload and
+// out pointer (48-bit GPU addresses), each tagged in bits 48-63 with the low
+// 16 bits of ticket + 1: a reader that sees both with matching tags has the
+// block's pointers (no separate sequence word, no order between the stores).
 constexpr int kTagShift = 48;
 constexpr uint64_t kAddrMask = (1ull << kTagShift) - 1;
 __host__ __device__ constexpr uint64_t tag_of(uint64_t ticket) { return ((ticket + 1) & 0xffffull) << kTagShift; }
 
 struct HostRing {
-    uint64_t slot[kRing][2];       // host: the ticket's tagged payload / out pointers
-    uint64_t col;                  // host: tickets below this are complete
-    uint32_t stop;                 // host: exit now
-    uint32_t pad0[13];
-    uint64_t exits;                // kernel: launches whose forwarder has exited
-    uint64_t pad1[7];
-    uint32_t flag[kRing][kMaxWg];  // workers: per slot and workgroup, ticket + 1 once its tiles are stored
+    uint64_t slot[kRing][2];  // host: the ticket's tagged payload / out pointers (the device slot format)
+    uint64_t done[kRing];     // kernel: ticket + 1 once the block's checksums are stored
+    uint32_t stop;            // host: exit now
+    uint32_t pad0[15];
+    uint64_t exit_col;        // kernel (at exit): tickets below this are complete
+    uint64_t exits;           // kernel: launches that have exited
 };
 
 struct DevRing {
-    uint64_t slot[kRing][2];  // forwarded copies of the host slots
-    uint32_t stop;            // forwarder: every wave exits
+    uint64_t slot[kRing][2];
+    uint32_t flag[kRing][kMaxWg];  // per slot and workgroup: ticket + 1 once its workers are done
+    uint64_t fwd;                  // forwarder: tickets below this are forwarded
+    uint64_t col;                  // collector: tickets below this are complete
+    uint32_t stop;                 // forwarder: every wave exits
 };
 
 struct RParams {
@@ -185,10 +183,9 @@ __device__ __forceinline__ void run_tile_pair(const RParams &p, const uint8_t *l
 }
 
 // Forwarder (workgroup 0's last wave): the host ring -> the device ring.
-// One PCIe round trip per poll covers the next 64 tickets and the host's
-// completion counter.  Decides the launch's end: the host's stop word,
-// idle_ticks with nothing outstanding, or kStuckMs without the completion
-// counter advancing while blocks are outstanding.
+// One PCIe round trip per poll covers the next 64 tickets.  Decides the
+// launch's end: the host's stop word, idle_ticks with nothing outstanding,
+// or kStuckMs without the collector advancing while blocks are outstanding.
 __device__ void forwarder(const RParams &p, int lane) {
     HostRing *h = p.h;
     DevRing *d = p.d;
@@ -196,14 +193,14 @@ __device__ void forwarder(const RParams &p, int lane) {
     uint64_t last = now();
     for (;;) {
         bool progress = false;
-        // the next 64 tickets' host slots, two loads per lane (ring reuse:
+        // the next 64 tickets' host slots, one load per lane (ring reuse:
         // ticket t only once t - kRing is complete; `col` from the previous
-        // pass, so the counter and the slots load together)
+        // pass, so the collector's word and the host slots load together)
         const uint64_t cand = fwd + uint64_t(lane);
         const bool room = cand < col + kRing;
         const uint32_t sl = uint32_t(cand % kRing);
         const uint64_t w0 = room ? ld_sys(&h->slot[sl][0]) : 0, w1 = room ? ld_sys(&h->slot[sl][1]) : 0;
-        const uint64_t c = ld_sys(&h->col);
+        const uint64_t c = ld_dev(&d->col);
         if (c != col) {
             col = c;
             progress = true;
@@ -217,6 +214,7 @@ __device__ void forwarder(const RParams &p, int lane) {
                 st_dev(&d->slot[sl][1], w1);
             }
             fwd += n;
+            if (lane == 0) st_dev(&d->fwd, fwd);
             progress = true;
         }
         const uint64_t t = now();
@@ -225,12 +223,65 @@ __device__ void forwarder(const RParams &p, int lane) {
             continue;
         }
         if (ld_sys(&h->stop)) break;
-        if (col >= fwd && t - last > p.idle_ticks) break;                  // idle
+        if (col == fwd && t - last > p.idle_ticks) break;                  // idle
         if (col < fwd && t - last > kStuckMs * 1000 * kTicksPerUs) break;  // no progress: give up
         __builtin_amdgcn_s_sleep(2);
     }
+    if (lane == 0) st_dev(&d->stop, 1u);
+}
+
+// Collector (workgroup 1's last wave): block t is complete when every
+// workgroup's flag for its slot holds t + 1; the (up to 8) oldest
+// outstanding blocks' flags are loaded together and completed in ticket
+// order (hdone[slot] = t + 1 in host memory).  Ends once the forwarder has
+// stopped and nothing it forwarded is outstanding (or kStuckMs later), then
+// records where it stopped for the next launch.
+__device__ void collector(const RParams &p, int lane) {
+    HostRing *h = p.h;
+    DevRing *d = p.d;
+    uint64_t col = p.first;
+    uint64_t last = now();
+    const uint32_t ng = gridDim.x;
+    for (;;) {
+        const uint32_t stop = ld_dev(&d->stop);
+        const uint64_t fwd = ld_dev(&d->fwd);
+        bool progress = false;
+        constexpr uint32_t kCheck = 8;
+        const uint64_t nout = fwd > col ? fwd - col : 0;
+        uint32_t f[kCheck][4];
+#pragma unroll
+        for (uint32_t c = 0; c < kCheck; ++c)
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                const uint32_t wg = 4u * uint32_t(lane) + k;
+                f[c][k] = (c < nout && wg < ng) ? ld_dev(&d->flag[(col + c) % kRing][wg]) : 0u;
+            }
+#pragma unroll
+        for (uint32_t c = 0; c < kCheck; ++c) {
+            if (c >= nout) break;
+            const uint32_t want = uint32_t(col + 1);
+            bool ok = true;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k)
+                if (4u * uint32_t(lane) + k < ng && f[c][k] != want) ok = false;
+            if (__ballot(!ok)) break;
+            if (lane == 0) st_sys(&h->done[col % kRing], col + 1);
+            ++col;
+            progress = true;
+        }
+        if (progress) {
+            if (lane == 0) st_dev(&d->col, col);
+            last = now();
+            continue;
+        }
+        if (stop && col >= fwd) break;
+        if (stop && now() - last > kStuckMs * 1000 * kTicksPerUs) break;
+        if (now() - last > kWorkerMs * 1000 * kTicksPerUs) break;  // (the forwarder is gone)
+        __builtin_amdgcn_s_sleep(1);
+    }
     if (lane == 0) {
-        st_dev(&d->stop, 1u);
+        st_sys(&h->exit_col, col);
+        wait_vmem();
         st_sys(&h->exits, ld_sys(&h->exits) + 1);
     }
 }
@@ -253,8 +304,9 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
     }
     if (threadIdx.x < kRing) lcnt[threadIdx.x] = 0;
     __syncthreads();
-    if (wv == kWaves - 1) {  // (idle outside workgroup 0)
+    if (wv == kWaves - 1) {
         if (blockIdx.x == 0) forwarder(p, lane);
+        if (blockIdx.x == 1) collector(p, lane);
         return;
     }
     // Worker: phase (b + w) % P; the workgroup's waves of a phase rank in
@@ -303,7 +355,7 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
             const uint32_t old = atomicAdd(&lcnt[sl], 1u);
             if (old + 1u == expect) {
                 lcnt[sl] = 0;
-                st_sys(&p.h->flag[sl][b], uint32_t(j + 1));
+                st_dev(&d->flag[sl][b], uint32_t(j + 1));
             }
         }
         j += kPhases;
@@ -331,26 +383,6 @@ struct crc32c_resident {
 
 namespace {
 
-// Block t is complete: every workgroup's flag for its slot holds t + 1.
-bool slot_complete(const crc32c_resident *r, uint64_t t) {
-    const uint32_t *f = r->h->flag[t % kRing];
-    const uint32_t want = uint32_t(t + 1);
-    uint32_t bad = 0;
-    for (uint32_t wg = 0; wg < r->grid; ++wg) bad |= __atomic_load_n(&f[wg], __ATOMIC_RELAXED) ^ want;
-    std::atomic_thread_fence(std::memory_order_acquire);
-    return bad == 0;
-}
-
-// Moves the host's completion counter past every complete ticket, in order;
-// returns it.
-uint64_t advance_col(crc32c_resident *r) {
-    uint64_t c = __atomic_load_n(&r->h->col, __ATOMIC_ACQUIRE);
-    while (c < r->next.load(std::memory_order_acquire) && slot_complete(r, c)) {
-        if (__atomic_compare_exchange_n(&r->h->col, &c, c + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) ++c;
-    }
-    return c;
-}
-
 // Launches the kernel unless one is running (caller holds r->mu).  A launch
 // that has exited shows as an idle stream.
 int ensure_running(crc32c_resident *r) {
@@ -360,7 +392,7 @@ int ensure_running(crc32c_resident *r) {
         if (q != hipSuccess) return hdfs_crc::fail(-EIO, "resident kernel: %s", hipGetErrorString(q));
         r->running = false;
     }
-    const uint64_t col = advance_col(r);
+    const uint64_t col = __atomic_load_n(&r->h->exit_col, __ATOMIC_ACQUIRE);
     if (col >= r->next.load(std::memory_order_acquire)) return 0;  // nothing queued
     hdfs_crc::KParams kp = hdfs_crc::plan_params(r->plan, nullptr, nullptr);
     RParams p{};
@@ -374,8 +406,10 @@ int ensure_running(crc32c_resident *r) {
     p.first = col;
     p.idle_ticks = r->idle_ticks;
     hdfs_crc::DeviceGuard guard(r->device);
-    // (a fresh stop word; the device slots keep their tags: a tag names its ticket)
-    HIP_TRY(hipMemsetAsync(&r->d->stop, 0, sizeof r->d->stop, r->stream));
+    // (fresh control words; the device slots keep their tags: a tag names its ticket)
+    const uint64_t ctl[3] = {col, col, 0};
+    HIP_TRY(hipMemcpyAsync(&r->d->fwd, ctl, sizeof ctl, hipMemcpyHostToDevice, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));  // (ctl is on this stack)
     switch (r->shape) {
         case 1: hipLaunchKernelGGL((resident_kernel<16, 7, 2>), dim3(r->grid), dim3(16 * 64), 0, r->stream, p); break;
         case 2: hipLaunchKernelGGL((resident_kernel<12, 11, 1>), dim3(r->grid), dim3(12 * 64), 0, r->stream, p); break;
@@ -429,12 +463,10 @@ int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, ui
     if (reinterpret_cast<uintptr_t>(dev_payload) & 15u) return fail(-EINVAL, "payload must be 16-byte aligned");
     const uint64_t t = r->next.fetch_add(1, std::memory_order_acq_rel);
     const uint32_t sl = uint32_t(t % kRing);
-    // the slot is reused once every ticket up to t - kRing is complete
+    // the slot's previous block (t - kRing) must be complete
     if (t >= kRing)
-        for (;;) {
-            const uint64_t c = advance_col(r);
-            if (c > t - kRing) break;
-            if (int rc = crc32c_debug_resident_wait(r, c)) return rc;
+        while (__atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE) < t - kRing + 1) {
+            if (int rc = crc32c_debug_resident_wait(r, t - kRing)) return rc;
         }
     __atomic_store_n(&r->h->slot[sl][0], (reinterpret_cast<uint64_t>(dev_payload) & kAddrMask) | tag_of(t),
                      __ATOMIC_RELAXED);
@@ -455,15 +487,13 @@ int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket) {
     using namespace hdfs_crc;
     if (!r) return fail(-EINVAL, "resident == NULL");
     if (ticket >= r->next.load(std::memory_order_acquire)) return fail(-EINVAL, "ticket never handed out");
+    const uint32_t sl = uint32_t(ticket % kRing);
     auto t0 = std::chrono::steady_clock::now();
     const auto deadline = t0 + std::chrono::seconds(5);
     for (uint32_t i = 0;; ++i) {
-        if (__atomic_load_n(&r->h->col, __ATOMIC_ACQUIRE) > ticket) return 0;
-        if (slot_complete(r, ticket)) {
-            advance_col(r);
-            return 0;
-        }
-        if ((i & 63u) == 63u) {
+        const uint64_t v = __atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE);
+        if (v >= ticket + 1) return 0;  // (a later ticket in the slot implies this one completed)
+        if ((i & 255u) == 255u) {
             const auto t = std::chrono::steady_clock::now();
             if (t > deadline) return fail(-ETIMEDOUT, "resident kernel: block %llu not done", (unsigned long long)ticket);
             if (t - t0 > std::chrono::microseconds(100)) {  // the kernel may have exited: relaunch it
