@@ -97,6 +97,13 @@ int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_res
 int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket);
 int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket);
 int crc32c_debug_resident_stats(const crc32c_resident *r, uint64_t *launches);
+/* Trace of a resident runner created with HDFS_CRC32C_RESIDENT_STAMPS=1:
+ * ends the running launch (a later submit relaunches), then copies 4 x u64
+ * s_memrealtime stamps (100 MHz) per ticket t at [4 (t % 4096)]: forwarded,
+ * seen by workgroup 0's worker, that worker's tiles stored, completed by the
+ * collector; and the sum / count of the forwarder's host-slot poll round
+ * trips (ticks). -EINVAL without the trace. */
+int crc32c_debug_resident_trace(crc32c_resident *r, uint64_t *stamps, uint64_t *rtt_ticks, uint64_t *rtt_polls);
 int crc32c_debug_resident_destroy(crc32c_resident *r);
 
 #ifdef __cplusplus

@@ -65,6 +65,11 @@ constexpr uint32_t kRing = 64;       // tickets in flight at most
 constexpr uint32_t kMaxWg = 256;     // one flag lane-dword per workgroup (64 lanes x 4)
 constexpr uint64_t kTicksPerUs = 100;  // s_memrealtime: 100 MHz
 constexpr uint64_t kStuckMs = 50;
+// Trace (HDFS_CRC32C_RESIDENT_STAMPS=1 at create): per ticket t % kStampRing,
+// s_memrealtime when the forwarder forwarded it, when workgroup 0's worker
+// of its phase saw it, when that worker's tiles were stored, and when the
+// collector completed it; plus the forwarder's host-slot poll round trips.
+constexpr uint32_t kStampRing = 4096;
 constexpr uint64_t kWorkerMs = 200;
 
 // A slot (host ring and device ring alike) is two 64-bit words, payload and
@@ -90,6 +95,7 @@ struct DevRing {
     uint64_t fwd;                  // forwarder: tickets below this are forwarded
     uint64_t col;                  // collector: tickets below this are complete
     uint32_t stop;                 // forwarder: every wave exits
+    uint64_t rtt_sum, rtt_n;       // trace: forwarder poll round trips (ticks), count
 };
 
 struct RParams {
@@ -102,6 +108,7 @@ struct RParams {
     uint32_t c_lg[5];
     uint64_t first;       // first ticket this launch forwards
     uint64_t idle_ticks;  // forwarder: exit after this long with nothing queued
+    uint64_t *stamps;     // trace (nullptr: off), 4 per ticket % kStampRing
 };
 
 template <typename T>
@@ -191,8 +198,10 @@ __device__ void forwarder(const RParams &p, int lane) {
     DevRing *d = p.d;
     uint64_t fwd = p.first, col = p.first;
     uint64_t last = now();
+    uint64_t rtt_sum = 0, rtt_n = 0;
     for (;;) {
         bool progress = false;
+        const uint64_t t_poll = p.stamps ? now() : 0;
         // the next 64 tickets' host slots, one load per lane (ring reuse:
         // ticket t only once t - kRing is complete; `col` from the previous
         // pass, so the collector's word and the host slots load together)
@@ -207,11 +216,16 @@ __device__ void forwarder(const RParams &p, int lane) {
         }
         const bool ok = room && (w0 & ~kAddrMask) == tag_of(cand) && (w1 & ~kAddrMask) == tag_of(cand);
         const uint64_t ready = __ballot(ok);
+        if (p.stamps) {  // (the ballot waited for the host loads)
+            rtt_sum += now() - t_poll;
+            ++rtt_n;
+        }
         const uint32_t n = ~ready ? uint32_t(__builtin_ctzll(~ready)) : 64u;  // consecutive ready tickets from fwd
         if (n) {
             if (uint32_t(lane) < n) {
                 st_dev(&d->slot[sl][0], w0);
                 st_dev(&d->slot[sl][1], w1);
+                if (p.stamps) st_dev(&p.stamps[4 * (cand % kStampRing)], now());
             }
             fwd += n;
             if (lane == 0) st_dev(&d->fwd, fwd);
@@ -227,7 +241,13 @@ __device__ void forwarder(const RParams &p, int lane) {
         if (col < fwd && t - last > kStuckMs * 1000 * kTicksPerUs) break;  // no progress: give up
         __builtin_amdgcn_s_sleep(2);
     }
-    if (lane == 0) st_dev(&d->stop, 1u);
+    if (lane == 0) {
+        st_dev(&d->stop, 1u);
+        if (p.stamps) {
+            st_dev(&d->rtt_sum, ld_dev(&d->rtt_sum) + rtt_sum);
+            st_dev(&d->rtt_n, ld_dev(&d->rtt_n) + rtt_n);
+        }
+    }
 }
 
 // Collector (workgroup 1's last wave): block t is complete when every
@@ -265,7 +285,10 @@ __device__ void collector(const RParams &p, int lane) {
             for (uint32_t k = 0; k < 4; ++k)
                 if (4u * uint32_t(lane) + k < ng && f[c][k] != want) ok = false;
             if (__ballot(!ok)) break;
-            if (lane == 0) st_sys(&h->done[col % kRing], col + 1);
+            if (lane == 0) {
+                st_sys(&h->done[col % kRing], col + 1);
+                if (p.stamps) st_dev(&p.stamps[4 * (col % kStampRing) + 3], now());
+            }
             ++col;
             progress = true;
         }
@@ -337,6 +360,8 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
             __builtin_amdgcn_s_sleep(1);
         }
         if (stop) break;
+        const bool stamp = p.stamps && b == 0 && lane == 0;
+        if (stamp) st_dev(&p.stamps[4 * (j % kStampRing) + 1], now());
         const uint8_t *payload = reinterpret_cast<const uint8_t *>(w0 & kAddrMask);
         uint32_t *out = reinterpret_cast<uint32_t *>(w1 & kAddrMask);
         if (kPer == 1) {  // (rank 0: this workgroup's tiles b, b + G, ..., two at a time)
@@ -351,6 +376,7 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
                 run_tile(p, lds, payload, out, idx, lane);
         }
         wait_vmem();  // (this wave's checksum stores have completed)
+        if (stamp && rank == 0) st_dev(&p.stamps[4 * (j % kStampRing) + 2], now());
         if (lane == 0) {
             const uint32_t old = atomicAdd(&lcnt[sl], 1u);
             if (old + 1u == expect) {
@@ -379,6 +405,7 @@ struct crc32c_resident {
     std::mutex mu;           // launches
     bool running = false;    // a launch may be on the GPU (under mu)
     std::atomic<uint64_t> launches{0};
+    uint64_t *stamps = nullptr;  // trace (HDFS_CRC32C_RESIDENT_STAMPS=1)
 };
 
 namespace {
@@ -405,6 +432,7 @@ int ensure_running(crc32c_resident *r) {
     for (int i = 0; i < 5; ++i) p.c_lg[i] = kp.c_lg[i];
     p.first = col;
     p.idle_ticks = r->idle_ticks;
+    p.stamps = r->stamps;
     hdfs_crc::DeviceGuard guard(r->device);
     // (fresh control words; the device slots keep their tags: a tag names its ticket)
     const uint64_t ctl[3] = {col, col, 0};
@@ -451,6 +479,10 @@ int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_res
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&r->d), sizeof(DevRing)));
     HIP_TRY(hipMemset(r->d, 0, sizeof(DevRing)));
     HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
+    if (const char *st = std::getenv("HDFS_CRC32C_RESIDENT_STAMPS"); st && st[0] == '1') {
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&r->stamps), sizeof(uint64_t) * 4 * kStampRing));
+        HIP_TRY(hipMemset(r->stamps, 0, sizeof(uint64_t) * 4 * kStampRing));
+    }
     // (the plan's descriptors are uploaded on the context's upload stream)
     if (plan->dp.uploaded) HIP_TRY(hipStreamWaitEvent(r->stream, plan->dp.uploaded, 0));
     *out = r.release();
@@ -514,6 +546,23 @@ int crc32c_debug_resident_stats(const crc32c_resident *r, uint64_t *launches) {
     return 0;
 }
 
+int crc32c_debug_resident_trace(crc32c_resident *r, uint64_t *stamps, uint64_t *rtt_ticks, uint64_t *rtt_polls) {
+    using namespace hdfs_crc;
+    if (!r || !stamps || !rtt_ticks || !rtt_polls) return fail(-EINVAL, "bad arguments");
+    if (!r->stamps) return fail(-EINVAL, "no trace: create with HDFS_CRC32C_RESIDENT_STAMPS=1");
+    DeviceGuard guard(r->device);
+    std::lock_guard<std::mutex> lock(r->mu);
+    // (the launch ends first: the forwarder's round-trip sums are written at its exit)
+    __atomic_store_n(&r->h->stop, 1u, __ATOMIC_RELEASE);
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    __atomic_store_n(&r->h->stop, 0u, __ATOMIC_RELEASE);
+    r->running = false;
+    HIP_TRY(hipMemcpy(stamps, r->stamps, sizeof(uint64_t) * 4 * kStampRing, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rtt_ticks, &r->d->rtt_sum, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(rtt_polls, &r->d->rtt_n, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int crc32c_debug_resident_destroy(crc32c_resident *r) {
     if (!r) return 0;
     if (r->h) __atomic_store_n(&r->h->stop, 1u, __ATOMIC_RELEASE);
@@ -523,6 +572,7 @@ int crc32c_debug_resident_destroy(crc32c_resident *r) {
         (void)hipStreamDestroy(r->stream);
     }
     if (r->d) (void)hipFree(r->d);
+    if (r->stamps) (void)hipFree(r->stamps);
     if (r->h) (void)hipHostFree(r->h);
     delete r;
     return 0;

@@ -43,7 +43,7 @@ def test_exports_every_declared_symbol(hdfs):
     dbg = _declared_functions(debug_only=True)
     assert dbg == {"crc32c_debug_plan_exec_variant", "crc32c_debug_variant_name", "crc32c_debug_stream_probe",
                    "crc32c_debug_resident_create", "crc32c_debug_resident_submit", "crc32c_debug_resident_wait",
-                   "crc32c_debug_resident_stats", "crc32c_debug_resident_destroy"}
+                   "crc32c_debug_resident_stats", "crc32c_debug_resident_trace", "crc32c_debug_resident_destroy"}
     dlib = hdfs.debug_lib()
     for n in sorted(dbg):
         assert hasattr(dlib, n), n

@@ -34,6 +34,7 @@
 #include <cstring>
 #include <sys/resource.h>
 #include <thread>
+#include <string>
 #include <vector>
 
 #include "hdfs_crc32c.h"
@@ -204,6 +205,36 @@ int main(int argc, char **argv) {
                 });
                 uint64_t launches = 0;
                 CHECK(crc32c_debug_resident_stats(r, &launches) == 0);
+                std::string trace;
+                if (const char *st = std::getenv("HDFS_CRC32C_RESIDENT_STAMPS"); st && st[0] == '1') {
+                    // medians over the run's last tickets (ring of 4096), us (stamps: 100 MHz)
+                    std::vector<uint64_t> stm(4 * 4096);
+                    uint64_t rtt = 0, polls = 0;
+                    CHECK(crc32c_debug_resident_trace(r, stm.data(), &rtt, &polls) == 0);
+                    const uint64_t nt = uint64_t(nthreads) * iters, n = std::min<uint64_t>(nt, 4096);
+                    std::vector<double> d[4];
+                    for (uint64_t t = nt - n; t < nt; ++t) {
+                        const uint64_t *x = &stm[4 * (t % 4096)];
+                        if (!x[0] || !x[1] || !x[2] || !x[3]) continue;
+                        d[0].push_back((double(x[1]) - double(x[0])) / 100.0);  // forwarded -> seen by a worker
+                        d[1].push_back((double(x[2]) - double(x[1])) / 100.0);  // seen -> its tiles stored
+                        d[2].push_back((double(x[3]) - double(x[2])) / 100.0);  // stored -> collected
+                        d[3].push_back((double(x[3]) - double(x[0])) / 100.0);  // forwarded -> collected
+                    }
+                    auto med = [](std::vector<double> &v) {
+                        if (v.empty()) return -1.0;
+                        std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+                        return v[v.size() / 2];
+                    };
+                    char buf[512];
+                    std::snprintf(buf, sizeof buf,
+                                  ", \"trace_us\": {\"fwd_to_seen\": %.2f, \"seen_to_stored\": %.2f, "
+                                  "\"stored_to_collected\": %.2f, \"fwd_to_collected\": %.2f, \"host_poll_rtt\": %.2f, "
+                                  "\"tickets\": %zu}",
+                                  med(d[0]), med(d[1]), med(d[2]), med(d[3]), polls ? double(rtt) / double(polls) / 100.0 : -1.0,
+                                  d[3].size());
+                    trace = buf;
+                }
                 CHECK(crc32c_debug_resident_destroy(r) == 0);
                 int bad = 0;
                 std::vector<uint32_t> got(nout);
@@ -213,8 +244,8 @@ int main(int argc, char **argv) {
                         CHECK(hipMemcpy(got.data(), outs[b], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
                         bad += got != want[b];
                     }
-                std::printf(", \"launches\": %llu, \"blocks_wrong\": %d, \"pass\": %d}\n", (unsigned long long)launches,
-                            bad, w);
+                std::printf(", \"launches\": %llu, \"blocks_wrong\": %d%s, \"pass\": %d}\n", (unsigned long long)launches,
+                            bad, trace.c_str(), w);
             }
     }
     if (sweep_only) {

@@ -29,6 +29,8 @@ for s in ${STEPS:-calls multi}; do
                run bres1_$w 120 env HDFS_CRC32C_RESIDENT_WAVES=$w tools/block_rate 1 2000 16 0 1 1 || exit 1; done ;;
     bqblock) run bq_spin 240 tools/block_rate 16 400 16 30 2 1 && run bq_block 240 env HDFS_CRC32C_QUEUE_BLOCKING=1 tools/block_rate 16 400 16 30 2 1 &&
              run bq_spin32 240 tools/block_rate 32 200 32 30 1 1 && run bq_block32 240 env HDFS_CRC32C_QUEUE_BLOCKING=1 tools/block_rate 32 200 32 30 1 1 ;;
+    btrace) run btrace1 120 env HDFS_CRC32C_RESIDENT_STAMPS=1 HDFS_CRC32C_RESIDENT_WAVES=16 tools/block_rate 1 2000 16 0 1 1 &&
+            run btrace16 240 env HDFS_CRC32C_RESIDENT_STAMPS=1 HDFS_CRC32C_RESIDENT_WAVES=16 tools/block_rate 16 400 16 30 2 1 ;;
     rtt) run rtt 120 tools/launch_rate rtt 2000 ;;
     brlong) run brlong 300 tools/block_rate 16 4000 16 30 2 1 ;;
     bspin) for sp in 50 10 0; do run bspin$sp 200 env HDFS_CRC32C_QUEUE_SPIN_US=$sp tools/block_rate 16 400 16 30 2 1 || exit 1; done ;;
@@ -46,6 +48,7 @@ for s in ${STEPS:-calls multi}; do
     c4model) run c4model 300 python tools/c4_model.py ;;
     tgen) run tgen 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or unaligned or shifted or verify or write_plan or fsx or edge or small" ;;
     tqueue) run tqueue 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "block_queue or overlapping or per_launch or destroyed or across_streams or recycled" ;;
+    configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py ;;
     prof3) run prof3 300 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run --output-format csv -- python3 bench.py --config c3 --no-cpu --no-host ;;
     pmc3) run pmc3 900 env PMC_CONFIG=c3 PMC_OUT=$OUT/pmc_c3 bash tools/pmc_session.sh ;;
