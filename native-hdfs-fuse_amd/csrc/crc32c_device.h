@@ -101,6 +101,13 @@ constexpr int kModeGDiagNoGather = 128;  // DIAGNOSTIC, wrong results: general i
 constexpr int kModeGDiagNoMask = 8192;   // DIAGNOSTIC, wrong results: general items skip the chunk-start masks
 constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan without them runs the kernel without
                                     // their code: the power-of-two tile loop stays as compact as round 1's)
+// (with kModeGeneral) the batch has no shifted tiles / no general tiles: the
+// build leaves that code out, so the other path gets the registers and the
+// schedule to itself
+constexpr int kModeNoShift = 32768;
+constexpr int kModeNoGItems = 65536;
+// GEN bits of the tile helpers below: general tiles, shifted (unaligned) tiles
+constexpr int kGenItems = 1, kGenShift = 2;
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -612,15 +619,15 @@ struct ShiftPrep {
     }
 };
 
-template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, bool GENERAL>
+template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, int GEN>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             uint4 v[9], uint32_t ev, int lane) {
     uint32_t pc[8];
-    if (GENERAL && (t.meta & kGeneralTile)) {
+    if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG>(p, lds, vacc, t, v, ev, lane);
         return;
     }
-    const uint32_t r = GENERAL && !COMPDIAG ? tile_misalign(p, t) : 0u;
+    const uint32_t r = (GEN & kGenShift) && !COMPDIAG ? tile_misalign(p, t) : 0u;
     if (r) {
         const uint32_t b = r & 3u, li = ((t.meta & 0xffu) - 1u) >> 1;
         const int ll = int(((t.meta & 0xffu) - 1u) & 1u) * 32 + 31;
@@ -636,11 +643,11 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane);
 }
 
-template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL>
+template <int AUX, bool COMPDIAG, bool VERIFY, int GEN>
 __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[9], uint32_t &ev) {
-    if (GENERAL && (t.meta & kGeneralTile)) {
+    if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         load_gtile<VERIFY>(p, t, lane, ev);
-    } else if (GENERAL && !COMPDIAG && tile_misalign(p, t)) {
+    } else if ((GEN & kGenShift) && !COMPDIAG && tile_misalign(p, t)) {
         load_tile_shifted<AUX, VERIFY>(p, t, tile_misalign(p, t), lane, v, ev);
     } else {
         load_tile<AUX, COMPDIAG, VERIFY>(p, t, lane, v, ev);
@@ -657,7 +664,7 @@ __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane,
 // unit 0 of their tile (units 1-3 are empty).
 // SPLIT 2 (A/B, debug library): halves of 8 blocks instead (chunks <= 4 KiB).
 // Returns 0 (empty unit), 1 (a whole tile / item in ft) or 2 (a unit in ft).
-template <int AUX, bool COMPDIAG, bool VERIFY, bool GENERAL, int SPLIT = 4>
+template <int AUX, bool COMPDIAG, bool VERIFY, int GEN, int SPLIT = 4>
 __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane, FastTile &ft, uint4 v[9],
                                          uint32_t &ev) {
     constexpr uint32_t kUB = 16 / SPLIT;  // blocks per unit
@@ -665,10 +672,10 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     const FastTile x = tile_at(p, j / SPLIT);
     const uint32_t u = j % SPLIT;
     const uint32_t lg = (x.meta >> 8) & 0xffu;
-    if ((GENERAL && (x.meta & kGeneralTile)) || (1u << lg) > kUB) {
+    if (((GEN & kGenItems) && (x.meta & kGeneralTile)) || (1u << lg) > kUB) {
         if (u) return 0;
         ft = x;
-        load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+        load_any<AUX, COMPDIAG, VERIFY, GEN>(p, ft, lane, v, ev);
         return 1;
     }
     const uint32_t nb = x.meta & 0xffu;
@@ -736,6 +743,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool C = S4 && (MODE & kModeS4C) != 0;
     constexpr int IMG = C ? kImgCompact : kImgFull;
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
+    constexpr int GEN = !GENERAL ? 0
+                                 : ((MODE & kModeNoGItems) ? 0 : kGenItems) | ((MODE & kModeNoShift) ? 0 : kGenShift);
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
     constexpr bool XCDMAP = (MODE & kModeXcdMap) != 0;
@@ -782,10 +791,10 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     int kind = 1;     // QUARTER: what load_unit found (0 empty, 1 tile / item, 2 quarter)
     auto load_next = [&](uint32_t j) {
         if (QUARTER) {
-            kind = load_unit<AUX, COMPDIAG, VERIFY, GENERAL, SPLIT>(p, j, lane, ft, v, ev);
+            kind = load_unit<AUX, COMPDIAG, VERIFY, GEN, SPLIT>(p, j, lane, ft, v, ev);
         } else {
             ft = tile_at(p, j);
-            load_any<AUX, COMPDIAG, VERIFY, GENERAL>(p, ft, lane, v, ev);
+            load_any<AUX, COMPDIAG, VERIFY, GEN>(p, ft, lane, v, ev);
         }
     };
     // EARLY: the first tile's loads go out before the staging (their latency
@@ -837,7 +846,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     if (!EARLY && t < tend) load_next(t);
     while (t < tend) {
         if (!QUARTER || kind == 1)
-            finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GENERAL>(p, lds, vacc, ft, v, ev, lane);
+            finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GEN>(p, lds, vacc, ft, v, ev, lane);
         else if (kind == 2)
             finish_quarter<DIAG, S4, VERIFY, IMG, SPLIT>(p, lds, vacc, ft, v, ev, lane);
         t = pool_grab(pool_ctr, lane);

@@ -6,7 +6,11 @@
 // three builds, each storing checksums (crc32c_plan_exec) or comparing them
 // (crc32c_plan_verify):
 //   * full image, power-of-two tiles only: the bulk path (config 2);
-//   * full image with the general-tile code (bpc outside 512 * 2^k);
+//   * full image with the general-tile code (bpc outside 512 * 2^k, packet
+//     tails) and the shifted loads of tiles off 16-byte alignment, in three
+//     forms: both paths, general tiles only, shifted tiles only (a build
+//     without the path a batch does not need has its registers and schedule
+//     to the other path);
 //   * compact image (28 KiB staged instead of 152 KiB, with the general-tile
 //     code): batches of at most kSmallBatchItemsPerCu work items per CU,
 //     where the table staging is most of a launch (one 4 MiB block: 5.8 ->
@@ -60,6 +64,10 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>));
         else if (small)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>));
+        else if (p.general == kGeneralItems)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeVerify>));
+        else if (p.general == kGeneralShift)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoGItems | kModeVerify>));
         else if (p.general)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeVerify>));
         else
@@ -69,6 +77,10 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>));
         else if (small)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>));
+        else if (p.general == kGeneralItems)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift>));
+        else if (p.general == kGeneralShift)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoGItems>));
         else if (p.general)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen>));
         else

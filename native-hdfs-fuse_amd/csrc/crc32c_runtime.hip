@@ -113,8 +113,9 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     p.ngen = dp.ngen;
     p.nseg = dp.nseg;
     p.nconst = dp.nconst;
-    // the general build also carries the shifted loads of tiles off 16-byte alignment
-    p.general = (dp.general || dp.misaligned || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? 1u : 0u;
+    // the general builds: general tiles (bit 0), shifted loads of tiles off 16-byte alignment (bit 1)
+    p.general = (dp.general ? kGeneralItems : 0u) |
+                ((dp.misaligned || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
     return p;
 }
 
@@ -690,7 +691,7 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         p.ngen = uint32_t(plan.gen.size());
         // (the staged slices keep every packet's 16-byte phase: tiles off
         // alignment take the general build's shifted loads, as in plans)
-        p.general = (has_general(plan) || has_misaligned(plan)) ? 1u : 0u;
+        p.general = (has_general(plan) ? kGeneralItems : 0u) | (has_misaligned(plan) ? kGeneralShift : 0u);
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));
@@ -954,7 +955,7 @@ int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *co
             b.payload_delta = uint64_t(uintptr_t(dev_payloads[k]) - plo);
             b.out_delta = uint32_t((uintptr_t(dev_outs[k]) - olo) / 4);
             b.reserved = 0;
-            if (b.payload_delta & 15u) p.general = 1u;  // (shifted loads for blocks off 16-byte alignment)
+            if (b.payload_delta & 15u) p.general |= kGeneralShift;  // (shifted loads for blocks off 16-byte alignment)
         }
         if (int rc = launch_plan(plan, p, s, j == nblocks ? stop : nullptr)) return rc;
         i = j;

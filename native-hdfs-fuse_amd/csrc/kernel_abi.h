@@ -34,6 +34,8 @@ struct BlockRef {
 // Blocks one launch carries (in the kernel arguments: 16 B each).
 constexpr uint32_t kMaxLaunchBlocks = 32;
 
+constexpr uint32_t kGeneralItems = 1u, kGeneralShift = 2u;  // KParams::general bits
+
 struct KParams {
     const FastTile *tiles;  // power-of-two and general tiles
     const GenItem *gen;
@@ -48,7 +50,8 @@ struct KParams {
     uint32_t ngen;
     uint32_t nseg;
     uint32_t nconst;
-    uint32_t general;  // nonzero when tiles[] holds general tiles (selects the kernel that has their code)
+    uint32_t general;  // kGeneralItems: tiles[] holds general tiles; kGeneralShift: some tile is off 16-byte
+                       // alignment (each selects a build that has that code)
     uint32_t flags;
     uint32_t c_lg[5];
     uint32_t c_small[4];

@@ -53,9 +53,9 @@ for s in ${STEPS:-calls multi}; do
     prof3) run prof3 300 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run --output-format csv -- python3 bench.py --config c3 --no-cpu --no-host ;;
     pmc3) run pmc3 900 env PMC_CONFIG=c3 PMC_OUT=$OUT/pmc_c3 bash tools/pmc_session.sh ;;
     pmc2) run pmc2 900 env PMC_CONFIG=c2 PMC_OUT=$OUT/pmc_c2 bash tools/pmc_session.sh ;;
-    ab) for c in ${ABCFGS:-c2b1000 c2b1536 c2t c2u c5}; do
-          run ab_base_$c 300 bash -c "cd abwt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
-          run ab_cand_$c 300 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-} || exit 1; done ;;
+    ab) for r in $(seq 1 ${ABROUNDS:-1}); do for c in ${ABCFGS:-c2b1000 c2b1536 c2t c2u c5}; do
+          run ab_base_${c}_$r 300 bash -c "cd abwt && python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-}" &&
+          run ab_cand_${c}_$r 300 python bench.py --config $c --no-cpu --no-host ${AB_ARGS:-} || exit 1; done; done ;;
   esac
 done
 echo "session done"
