@@ -93,6 +93,17 @@ static bool has_general(const HostPlan &hp) {
     return false;
 }
 
+// Some general tile's full chunks are padded (bpc not a multiple of 512).
+// Such batches run the general build with both paths even without shifted
+// tiles: the general-tiles-only build, which helps unpadded general tiles
+// (412-byte tails: 48.2 -> 46.2 us), measured slower for padded ones (bpc
+// 1000: 62.8 -> 64.3 us, same box, 3 rounds).
+static bool has_padded_general(const HostPlan &hp) {
+    for (const FastTile &t : hp.tiles)
+        if ((t.meta & kGeneralTile) && ((t.meta >> 18) & 511u)) return true;
+    return false;
+}
+
 // Some power-of-two tile starts off 16-byte alignment (the general build's
 // shifted loads read it from the aligned address below).
 static bool has_misaligned(const HostPlan &hp) {
@@ -115,7 +126,7 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     p.nconst = dp.nconst;
     // the general builds: general tiles (bit 0), shifted loads of tiles off 16-byte alignment (bit 1)
     p.general = (dp.general ? kGeneralItems : 0u) |
-                ((dp.misaligned || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
+                ((dp.misaligned || dp.padded || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
     return p;
 }
 
@@ -218,6 +229,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->nconst = uint32_t(hp.consts.size());
     dp->general = has_general(hp);
     dp->misaligned = has_misaligned(hp);
+    dp->padded = has_padded_general(hp);
     dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
     dp->tiles_off = (kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
@@ -691,7 +703,8 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         p.ngen = uint32_t(plan.gen.size());
         // (the staged slices keep every packet's 16-byte phase: tiles off
         // alignment take the general build's shifted loads, as in plans)
-        p.general = (has_general(plan) ? kGeneralItems : 0u) | (has_misaligned(plan) ? kGeneralShift : 0u);
+        p.general = (has_general(plan) ? kGeneralItems : 0u) |
+                    ((has_misaligned(plan) || has_padded_general(plan)) ? kGeneralShift : 0u);
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));

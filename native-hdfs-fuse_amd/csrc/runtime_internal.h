@@ -85,6 +85,7 @@ struct DevicePlan {
     uint32_t ntiles = 0, ngen = 0, nseg = 0, nconst = 0;
     bool general = false;     // some tile is a general tile
     bool misaligned = false;  // some power-of-two tile's offset is not a multiple of 16
+    bool padded = false;      // some general tile's full chunks are padded (bpc not 512 k)
     size_t tiles_off = 0, gen_off = 0, seg_off = 0, pieces_off = 0, consts_off = 0, slots_off = 0;
 };
 
