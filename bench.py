@@ -469,8 +469,9 @@ def main():
     # over the second part only: its launches are queued while the first
     # part's run, so it holds neither the host's first issue nor a graph's
     # launch latency (~20 us on this stack: spread over a 20-step window that
-    # is ~1 us per step).  n_lead covers >= 40 us of kernel time
-    # (at most half the steps).  Both parts are timed steps: the wall clock
+    # is ~1 us per step).  n_lead covers >= 150 us of kernel time
+    # (at most half the steps): a graph of 19 launches measured up to ~50 us
+    # from replay to its first kernel.  Both parts are timed steps: the wall clock
     # holds all K of them.
     step_us = 0.0
     if args.steps > 1:
@@ -482,7 +483,7 @@ def main():
         e1.record(stream)
         torch.cuda.synchronize()
         step_us = e0.elapsed_time(e1) * 1e3 / 10
-    n_lead = 0 if args.steps < 2 else min(args.steps // 2, max(1, -(-40 // max(int(step_us), 1))))
+    n_lead = 0 if args.steps < 2 else min(args.steps // 2, max(1, -(-150 // max(int(step_us), 1))))
     if world > 1:  # (one split on every rank)
         nl = torch.tensor([n_lead], dtype=torch.int64, device=dev if backend == "nccl" else torch.device("cpu"))
         dist.all_reduce(nl, op=dist.ReduceOp.MAX)

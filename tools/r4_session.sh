@@ -45,6 +45,8 @@ for s in ${STEPS:-calls multi}; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench20) run bench20 600 python bench.py --steps 20 --warmup 5 ;;
+    b20x3) for r in 1 2 3; do run bench20_$r 300 python bench.py --steps 20 --warmup 5 --no-cpu --no-host || exit 1; done ;;
+    c3x20) run c3_20 300 python bench.py --config c3 --steps 20 --warmup 5 --no-cpu --no-host && run c3_2000 300 python bench.py --config c3 --no-cpu --no-host ;;
     c4model) run c4model 300 python tools/c4_model.py ;;
     tgen) run tgen 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or unaligned or shifted or verify or write_plan or fsx or edge or small" ;;
     tqueue) run tqueue 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "block_queue or overlapping or per_launch or destroyed or across_streams or recycled" ;;
