@@ -250,14 +250,22 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
     return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xF, 0xF, true));
 }
 
-// A general item: for every subtile, block b's lin (block_lin) is shifted
-// by Z^(512 dist_b) to its chunk's end; the blocks are permuted into block
-// order and prefix-XORed along 16-lane rows (DPP row_shr), and lane c adds
-// the XOR of its chunk's blocks in the subtile as P[hi - 1] ^ P[lo - 1].
-// After the last subtile lane c holds chunk c's lin, and crc = lin ^
-// crc(0, zeros(n)) for its n bytes.  Each subtile's loads are issued after
-// the previous one's lookups.
-template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG>
+// A general item: for every subtile the power-of-two reduce-scatter gives
+// each block's lin (block_lin); the blocks are permuted into block order
+// (one ds_bpermute) and gathered, subtile s into 16-lane row s mod GROUP, so
+// with GROUP = 4 one 64-lane vector holds up to 4 subtiles' 64 blocks.  Per
+// group of GROUP subtiles (or the item's last, partial group): block b is shifted by
+// Z^(512 dist_b) to its chunk's end (one nibble-table application for all
+// 64 blocks), prefix-XORed over the 64 lanes (DPP row_shr within rows, then
+// row_bcast across them), and lane c adds the XOR of its chunk's blocks in
+// the group as P[hi - 1] ^ P[lo - 1].  After the last group lane c holds
+// chunk c's lin, and crc = lin ^ crc(0, zeros(n)) for its n bytes.  GROUP
+// = 1 is round 3's per-subtile gather (every row holds the subtile; no
+// cross-row step): the general-tiles-only build takes GROUP = 4 (bpc 1536:
+// 49.6 -> 48.1 us), the builds with both paths keep GROUP = 1 (padded bpc
+// 1000's verify ran 61.8 -> 63.5 us with 4).  Each
+// subtile's loads are issued after the previous one's lookups.
+template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, uint32_t GROUP = 1>
 __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                              uint4 v[8], uint32_t ev, int lane) {
     const GShape g = gshape(t);
@@ -266,8 +274,8 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     // lane c's chunk: virtual blocks [lo, hi)
     const uint32_t lo = c < g.nch ? c * g.k : g.nfb;
     const uint32_t hi = c < g.nch ? lo + g.k : (c < nout ? g.nb : lo);
-    const uint32_t blk = rep_block(lane);
     const uint32_t from = block_lane(uint32_t(lane) & 15u) << 2;
+    const uint32_t row = uint32_t(lane) >> 4, col = uint32_t(lane) & 15u;
     const uint32_t nsub = (g.nb + 15u) >> 4;
     // lane c's affine constant crc(0, zeros(n)), n = bpc or tl (scalar loads)
     typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
@@ -276,6 +284,8 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     const uint4 kp = keep_masks(int(g.pad) - int(16u * (uint32_t(lane) & 31u)));
     GState st;
     uint32_t acc = 0;
+    uint32_t comb = 0;  // row r: subtile 4 q + r's blocks, in block order
+    uint32_t shv = 0;   // ... and each block's distance to its chunk's end
     for (uint32_t s = 0; s < nsub; ++s) {
         // Unpadded items' loads need no block facts: issue them before the
         // subtile's pattern-table fetches (two dependent scalar loads).
@@ -285,26 +295,39 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
         uint32_t pc[8];
         gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
-        uint32_t x = block_lin(pc, lane);
+        const uint32_t x = block_lin(pc, lane);
+        gstate_next(g, gs, st);
         if (DIAG & 2) {  // DIAGNOSTIC (debug variants only, wrong results): no per-subtile gather
             acc ^= x;
-            gstate_next(g, gs, st);
             continue;
         }
-        const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
-        const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
-        if (sh) x = zshift<S4, IMG>(lds, sh, x);
-        uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(x)));  // lane l: block l & 15
-        y ^= dpp_zero<0x111>(y);  // row_shr:1
-        y ^= dpp_zero<0x112>(y);  // row_shr:2
-        y ^= dpp_zero<0x114>(y);  // row_shr:4
-        y ^= dpp_zero<0x118>(y);  // row_shr:8: lane l holds blocks 0 .. l & 15
-        const int base = int(16u * s);
-        const int l1 = min(max(int(lo) - base, 0), 16), h1 = min(max(int(hi) - base, 0), 16);
-        const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(y)));
-        const uint32_t pl = uint32_t(__builtin_amdgcn_ds_bpermute((max(l1, 1) - 1) << 2, int(y)));
+        const uint32_t r = s % GROUP;  // (uniform)
+        const uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(x)));  // lane l: block l & 15
+        if (GROUP == 1 || row == r) {
+            comb = y;
+            shv = __builtin_amdgcn_ubfe(col < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32), 4u * (col & 7u), 4u);
+        }
+        if (r != GROUP - 1u && s + 1u != nsub) continue;
+        // the group: subtiles 4 q .. s, blocks [64 q, 64 q + 16 (r + 1)); rows past r hold zeros
+        uint32_t z = comb;
+        if (shv) z = zshift<S4, IMG>(lds, shv, z);
+        z ^= dpp_zero<0x111>(z);  // row_shr:1
+        z ^= dpp_zero<0x112>(z);  // row_shr:2
+        z ^= dpp_zero<0x114>(z);  // row_shr:4
+        z ^= dpp_zero<0x118>(z);  // row_shr:8: lane l holds its row's blocks 0 .. l & 15
+        if (GROUP > 1) {
+            // row_bcast:15 -- rows 1 and 3 add the last lane of rows 0 and 2;
+            // row_bcast:31 -- rows 2 and 3 add lane 31 (rows 0 and 1 in all)
+            z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x142, 0xA, 0xF, false));
+            z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x143, 0xC, 0xF, false));
+        }
+        const int base = int(16u * GROUP * (s / GROUP)), span = int(16u * GROUP);
+        const int l1 = min(max(int(lo) - base, 0), span), h1 = min(max(int(hi) - base, 0), span);
+        const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(z)));
+        const uint32_t pl = uint32_t(__builtin_amdgcn_ds_bpermute((max(l1, 1) - 1) << 2, int(z)));
         if (h1 > l1) acc ^= ph ^ (l1 ? pl : 0u);
-        gstate_next(g, gs, st);
+        comb = 0;
+        shv = 0;
     }
     if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ (c < g.nch ? cf : ct), ev);
 }
