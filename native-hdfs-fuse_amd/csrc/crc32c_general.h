@@ -260,8 +260,8 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
 // row_bcast across them), and lane c adds the XOR of its chunk's blocks in
 // the group as P[hi - 1] ^ P[lo - 1].  After the last group lane c holds
 // chunk c's lin, and crc = lin ^ crc(0, zeros(n)) for its n bytes.  GROUP
-// = 1 is round 3's per-subtile gather (every row holds the subtile; no
-// cross-row step): the general-tiles-only build takes GROUP = 4 (bpc 1536:
+// = 1 is round 3's per-subtile gather (each block shifted before the
+// permute, a prefix per 16-lane row): the general-tiles-only build takes GROUP = 4 (bpc 1536:
 // 49.6 -> 48.1 us), the builds with both paths keep GROUP = 1 (padded bpc
 // 1000's verify ran 61.8 -> 63.5 us with 4).  Each
 // subtile's loads are issued after the previous one's lookups.
@@ -301,9 +301,27 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
             acc ^= x;
             continue;
         }
+        if constexpr (GROUP == 1) {  // round 3's form: shift, then permute, per subtile
+            const uint32_t blk = rep_block(lane);
+            const uint32_t half = blk < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32);
+            const uint32_t sh = __builtin_amdgcn_ubfe(half, 4u * (blk & 7u), 4u);
+            uint32_t xs = x;
+            if (sh) xs = zshift<S4, IMG>(lds, sh, xs);
+            uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(xs)));  // lane l: block l & 15
+            y ^= dpp_zero<0x111>(y);  // row_shr:1
+            y ^= dpp_zero<0x112>(y);  // row_shr:2
+            y ^= dpp_zero<0x114>(y);  // row_shr:4
+            y ^= dpp_zero<0x118>(y);  // row_shr:8: lane l holds blocks 0 .. l & 15
+            const int base = int(16u * s);
+            const int l1 = min(max(int(lo) - base, 0), 16), h1 = min(max(int(hi) - base, 0), 16);
+            const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(y)));
+            const uint32_t pl = uint32_t(__builtin_amdgcn_ds_bpermute((max(l1, 1) - 1) << 2, int(y)));
+            if (h1 > l1) acc ^= ph ^ (l1 ? pl : 0u);
+            continue;
+        }
         const uint32_t r = s % GROUP;  // (uniform)
         const uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(from), int(x)));  // lane l: block l & 15
-        if (GROUP == 1 || row == r) {
+        if (row == r) {
             comb = y;
             shv = __builtin_amdgcn_ubfe(col < 8u ? uint32_t(gs.dist) : uint32_t(gs.dist >> 32), 4u * (col & 7u), 4u);
         }
@@ -315,12 +333,10 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         z ^= dpp_zero<0x112>(z);  // row_shr:2
         z ^= dpp_zero<0x114>(z);  // row_shr:4
         z ^= dpp_zero<0x118>(z);  // row_shr:8: lane l holds its row's blocks 0 .. l & 15
-        if (GROUP > 1) {
-            // row_bcast:15 -- rows 1 and 3 add the last lane of rows 0 and 2;
-            // row_bcast:31 -- rows 2 and 3 add lane 31 (rows 0 and 1 in all)
-            z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x142, 0xA, 0xF, false));
-            z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x143, 0xC, 0xF, false));
-        }
+        // row_bcast:15 -- rows 1 and 3 add the last lane of rows 0 and 2;
+        // row_bcast:31 -- rows 2 and 3 add lane 31 (rows 0 and 1 in all)
+        z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x142, 0xA, 0xF, false));
+        z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x143, 0xC, 0xF, false));
         const int base = int(16u * GROUP * (s / GROUP)), span = int(16u * GROUP);
         const int l1 = min(max(int(lo) - base, 0), span), h1 = min(max(int(hi) - base, 0), span);
         const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(z)));
