@@ -80,18 +80,22 @@ def baseline_metric() -> str:
         return "GiB/s CRC32C, device-resident 64 KiB packets \u00d7 512 B chunks, 1/2/4/8 GPU"
 
 
-def latest_pmc(profile_dir: str):
-    """HBM bytes per launch of the kernel from the committed rocprofv3 PMC
-    summary (profiles/*pmc*.json written by tools/pmc_summary.py)."""
-    files = sorted(glob.glob(os.path.join(profile_dir, "*pmc_c*.json")))
-    if not files:
-        return None
-    try:
-        with open(files[-1]) as f:
-            d = json.load(f)
-        return d
-    except Exception:
-        return None
+def latest_pmc(profile_dir: str, config: str):
+    """HBM bytes per launch of the kernel from the newest committed rocprofv3
+    PMC summary of this config (profiles/[rNN/]rNN_pmc_<config>.json, written
+    by tools/pmc_summary.py)."""
+    files = glob.glob(os.path.join(profile_dir, "*pmc_c*.json")) + \
+        glob.glob(os.path.join(profile_dir, "r*", "*pmc_c*.json"))
+    best = None
+    for fn in sorted(files, key=os.path.basename):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("config") == config:
+            best = d
+    return best
 
 
 def cpu_quota():
@@ -835,7 +839,7 @@ def main():
                               "gpu_pinned_beats_reference_1t_from_bytes": min(cross) if cross else None}
 
     if rank == 0:
-        pmc = latest_pmc(os.path.join(ROOT, "profiles"))
+        pmc = latest_pmc(os.path.join(ROOT, "profiles"), args.config)
         traffic = traffic_commit = None
         if (pmc and pmc.get("config") == args.config
                 and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
