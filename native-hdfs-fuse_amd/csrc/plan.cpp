@@ -1,4 +1,5 @@
 // plan.cpp -- see plan.h.
+#include <cstdlib>
 #include "plan.h"
 #include "hdfs_crc32c.h"
 
@@ -36,6 +37,18 @@ static void push_gen(HostPlan *plan, uint64_t src, uint64_t out, uint32_t len) {
     g.out = uint32_t(out);
     g.len = len;
     plan->gen.push_back(g);
+}
+
+
+// Full chunks per general item when k does not divide 16 (A/B:
+// HDFS_CRC32C_GCHUNKS, 1..31; default kGeneralChunks).
+static uint64_t general_chunks() {
+    static const uint64_t n = [] {
+        const char *e = std::getenv("HDFS_CRC32C_GCHUNKS");
+        const long v = e ? std::atol(e) : 0;
+        return uint64_t(v >= 1 && v <= 31 ? v : kGeneralChunks);
+    }();
+    return n;
 }
 
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
@@ -81,7 +94,7 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         const uint32_t pad = k * kBlockBytes - p.bpc;
         // (k dividing 16: whole chunks fill subtiles exactly, and one subtile
         // per item keeps the item loop out of the way)
-        const uint64_t per = kTileBlocks % k == 0 ? kTileBlocks / k : kGeneralChunks;
+        const uint64_t per = kTileBlocks % k == 0 ? kTileBlocks / k : general_chunks();
         for (uint64_t c = 0; c < nfull;) {
             const uint64_t src = p.payload_off + c * p.bpc;
             if (pad && !(absolute ? (src & 4095u) >= 16 : src >= 16)) {

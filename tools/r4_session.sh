@@ -50,6 +50,8 @@ for s in ${STEPS:-calls multi}; do
     c4model) run c4model 300 python tools/c4_model.py ;;
     tgen) run tgen 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or unaligned or shifted or verify or write_plan or fsx or edge or small" ;;
     tqueue) run tqueue 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "block_queue or overlapping or per_launch or destroyed or across_streams or recycled" ;;
+    tgench) for n in 5 21 31; do run tgen_gch$n 600 env HDFS_CRC32C_GCHUNKS=$n python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or edge" || exit 1; done ;;
+    gch) for n in ${GCH:-16 5 10 21 16}; do run gch_${n} 300 env HDFS_CRC32C_GCHUNKS=$n python bench.py --config ${GCFG:-c2b1536} --no-cpu --no-host || exit 1; done ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py ;;
     prof3) run prof3 300 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run --output-format csv -- python3 bench.py --config c3 --no-cpu --no-host ;;
