@@ -99,6 +99,11 @@ static bool has_general(const HostPlan &hp) {
 // (412-byte tails: 48.2 -> 46.2 us), measured slower for padded ones (bpc
 // 1000: 62.8 -> 64.3 us, same box, 3 rounds).
 static bool has_padded_general(const HostPlan &hp) {
+    static const bool off = [] {  // (A/B: HDFS_CRC32C_PADDED_FULL=0 sends them to the general-tiles-only build)
+        const char *e = std::getenv("HDFS_CRC32C_PADDED_FULL");
+        return e && e[0] == '0';
+    }();
+    if (off) return false;
     for (const FastTile &t : hp.tiles)
         if ((t.meta & kGeneralTile) && ((t.meta >> 18) & 511u)) return true;
     return false;

@@ -50,6 +50,16 @@ static uint64_t general_chunks() {
     }();
     return n;
 }
+// ... when k divides 16 (A/B: HDFS_CRC32C_GCHUNKS_DIV, a multiple of 16 / k
+// up to 31; default one subtile, 16 / k).
+static uint64_t general_chunks_div(uint32_t k) {
+    static const long v = [] {
+        const char *e = std::getenv("HDFS_CRC32C_GCHUNKS_DIV");
+        return e ? std::atol(e) : 0L;
+    }();
+    const uint64_t one = kTileBlocks / k;
+    return v >= 1 && v <= 31 && uint64_t(v) % one == 0 ? uint64_t(v) : one;
+}
 
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
     // A zero-length packet (the block's last-packet marker, hadooprpc.c:644,
@@ -94,7 +104,7 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         const uint32_t pad = k * kBlockBytes - p.bpc;
         // (k dividing 16: whole chunks fill subtiles exactly, and one subtile
         // per item keeps the item loop out of the way)
-        const uint64_t per = kTileBlocks % k == 0 ? kTileBlocks / k : general_chunks();
+        const uint64_t per = kTileBlocks % k == 0 ? general_chunks_div(k) : general_chunks();
         for (uint64_t c = 0; c < nfull;) {
             const uint64_t src = p.payload_off + c * p.bpc;
             if (pad && !(absolute ? (src & 4095u) >= 16 : src >= 16)) {

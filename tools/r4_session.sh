@@ -51,6 +51,13 @@ for s in ${STEPS:-calls multi}; do
     tgen) run tgen 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or unaligned or shifted or verify or write_plan or fsx or edge or small" ;;
     tqueue) run tqueue 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "block_queue or overlapping or per_launch or destroyed or across_streams or recycled" ;;
     tgench) for n in 5 21 31; do run tgen_gch$n 600 env HDFS_CRC32C_GCHUNKS=$n python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or edge" || exit 1; done ;;
+    g1000) run g1000_base 300 python bench.py --config c2b1000 --no-cpu --no-host &&
+           run g1000_16 300 env HDFS_CRC32C_GCHUNKS_DIV=16 python bench.py --config c2b1000 --no-cpu --no-host &&
+           run g1000_32 300 env HDFS_CRC32C_GCHUNKS_DIV=24 python bench.py --config c2b1000 --no-cpu --no-host &&
+           run g1000_16io 300 env HDFS_CRC32C_GCHUNKS_DIV=16 HDFS_CRC32C_PADDED_FULL=0 python bench.py --config c2b1000 --no-cpu --no-host &&
+           run g1000_24io 300 env HDFS_CRC32C_GCHUNKS_DIV=24 HDFS_CRC32C_PADDED_FULL=0 python bench.py --config c2b1000 --no-cpu --no-host &&
+           run g1000_base2 300 python bench.py --config c2b1000 --no-cpu --no-host ;;
+    tg1000) run tg1000 600 env HDFS_CRC32C_GCHUNKS_DIV=24 HDFS_CRC32C_PADDED_FULL=0 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or edge" ;;
     gch) for n in ${GCH:-16 5 10 21 16}; do run gch_${n} 300 env HDFS_CRC32C_GCHUNKS=$n python bench.py --config ${GCFG:-c2b1536} --no-cpu --no-host || exit 1; done ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py ;;
