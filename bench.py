@@ -98,6 +98,14 @@ def latest_pmc(profile_dir: str, config: str):
     return best
 
 
+def config_name(name: str) -> str:
+    """--config: a BASELINE.json config or one of its variants (c2b<bpc>: config 2 with that bytesPerChecksum)."""
+    if name in ("c2", "c3", "c4", "c5", "c2u", "c2t", "c3u") or (name.startswith("c2b") and name[3:].isdigit()
+                                                                    and 4 <= int(name[3:]) <= 65536):
+        return name
+    raise argparse.ArgumentTypeError("unknown config %r" % name)
+
+
 def cpu_quota():
     """(CPUs this process may run on, CPU bandwidth quota in CPUs or None):
     sched_getaffinity and the cgroup v2 cpu.max / v1 cfs quota -- a container
@@ -296,7 +304,8 @@ def main():
     # the 1.4 kW package cap).  2500 launches take ~0.1 s.
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "c2b1536", "c2b1000", "c2u", "c2t", "c3u"])
+    ap.add_argument("--config", default="c2", type=config_name,
+                    help="c2 | c3 | c4 | c5 | c2b1536 | c2b1000 | c2b<bpc> | c2u | c2t | c3u")
     ap.add_argument("--nbuf", type=int, default=4, help="rotating payload buffers (defeat the 256 MiB L3)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-cpu", action="store_true")

@@ -40,25 +40,28 @@ static void push_gen(HostPlan *plan, uint64_t src, uint64_t out, uint32_t len) {
 }
 
 
-// Full chunks per general item when k does not divide 16 (A/B:
-// HDFS_CRC32C_GCHUNKS, 1..31; default kGeneralChunks).
-static uint64_t general_chunks() {
-    static const uint64_t n = [] {
-        const char *e = std::getenv("HDFS_CRC32C_GCHUNKS");
-        const long v = e ? std::atol(e) : 0;
-        return uint64_t(v >= 1 && v <= 31 ? v : kGeneralChunks);
-    }();
-    return n;
+// Full chunks per general item of k blocks per chunk.  A/B knobs:
+// HDFS_CRC32C_GBLOCKS (about that many blocks per item; 0: round 3's sizes,
+// one subtile when k divides 16, else kGeneralChunks),
+// HDFS_CRC32C_GCHUNKS (k not dividing 16) and HDFS_CRC32C_GCHUNKS_DIV (k
+// dividing 16, a multiple of 16 / k) override it.  At most 31 (the
+// descriptor's field).
+static long env_long(const char *name) {
+    const char *e = std::getenv(name);
+    return e ? std::atol(e) : -1L;
 }
-// ... when k divides 16 (A/B: HDFS_CRC32C_GCHUNKS_DIV, a multiple of 16 / k
-// up to 31; default one subtile, 16 / k).
-static uint64_t general_chunks_div(uint32_t k) {
-    static const long v = [] {
-        const char *e = std::getenv("HDFS_CRC32C_GCHUNKS_DIV");
-        return e ? std::atol(e) : 0L;
-    }();
-    const uint64_t one = kTileBlocks / k;
-    return v >= 1 && v <= 31 && uint64_t(v) % one == 0 ? uint64_t(v) : one;
+static uint64_t item_chunks(uint32_t k) {
+    static const long blocks = env_long("HDFS_CRC32C_GBLOCKS"), ch = env_long("HDFS_CRC32C_GCHUNKS"),
+                      div = env_long("HDFS_CRC32C_GCHUNKS_DIV");
+    const uint64_t one = kTileBlocks % k == 0 ? kTileBlocks / k : 1;  // chunks that fill whole subtiles
+    if (kTileBlocks % k == 0 && div >= 1 && div <= 31 && uint64_t(div) % one == 0) return uint64_t(div);
+    if (kTileBlocks % k != 0 && ch >= 1 && ch <= 31) return uint64_t(ch);
+    const uint64_t target = blocks >= 0 ? uint64_t(blocks) : kItemBlocks;
+    if (target == 0) return kTileBlocks % k == 0 ? one : kGeneralChunks;
+    uint64_t n = std::max<uint64_t>(target / k, 1);
+    n = std::max<uint64_t>(n / one, 1) * one;  // whole subtiles when k divides 16
+    while (n > 31) n -= one;
+    return n;
 }
 
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
@@ -104,7 +107,7 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         const uint32_t pad = k * kBlockBytes - p.bpc;
         // (k dividing 16: whole chunks fill subtiles exactly, and one subtile
         // per item keeps the item loop out of the way)
-        const uint64_t per = kTileBlocks % k == 0 ? general_chunks_div(k) : general_chunks();
+        const uint64_t per = item_chunks(k);
         for (uint64_t c = 0; c < nfull;) {
             const uint64_t src = p.payload_off + c * p.bpc;
             if (pad && !(absolute ? (src & 4095u) >= 16 : src >= 16)) {

@@ -63,6 +63,9 @@ def config_packets(name: str):
         return uniform_packets(4096, bpc=1536), "4096 x 64KiB packets, 1536B chunks (general path)"
     if name == "c2b1000":  # config 2 with bytesPerChecksum 1000 (padded general tiles)
         return uniform_packets(4096, bpc=1000), "4096 x 64KiB packets, 1000B chunks (padded general tiles)"
+    if name.startswith("c2b") and name[3:].isdigit():  # config 2 with any other bytesPerChecksum
+        bpc = int(name[3:])
+        return uniform_packets(4096, bpc=bpc), "4096 x 64KiB packets, %dB chunks (general path)" % bpc
     if name == "c2t":  # config 2 with a 412-byte tail chunk in every packet (4096 general-path items)
         return (uniform_packets(4096, pkt_len=PACKET_BYTES - 100, stride=PACKET_BYTES),
                 "4096 x (64KiB - 100 B) packets, 512B chunks + a 412 B tail each")

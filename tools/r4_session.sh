@@ -58,6 +58,9 @@ for s in ${STEPS:-calls multi}; do
            run g1000_24io 300 env HDFS_CRC32C_GCHUNKS_DIV=24 HDFS_CRC32C_PADDED_FULL=0 python bench.py --config c2b1000 --no-cpu --no-host &&
            run g1000_base2 300 python bench.py --config c2b1000 --no-cpu --no-host ;;
     tg1000) run tg1000 600 env HDFS_CRC32C_GCHUNKS_DIV=24 HDFS_CRC32C_PADDED_FULL=0 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or edge" ;;
+    gblk) for c in ${GBCFGS:-c2b1000 c2b700 c2b2560 c2b3000 c2b4000 c2b1536}; do for gb in ${GBS:-0 48}; do
+             run gb_${c}_$gb 300 env HDFS_CRC32C_GBLOCKS=$gb python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
+    tgblk) run tgblk 600 env HDFS_CRC32C_GBLOCKS=48 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "general or golden or random or fuzz or mixed or edge" ;;
     gch) for n in ${GCH:-16 5 10 21 16}; do run gch_${n} 300 env HDFS_CRC32C_GCHUNKS=$n python bench.py --config ${GCFG:-c2b1536} --no-cpu --no-host || exit 1; done ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py ;;
