@@ -40,9 +40,12 @@ static void push_gen(HostPlan *plan, uint64_t src, uint64_t out, uint32_t len) {
 }
 
 
-// Full chunks per general item of k blocks per chunk.  A/B knobs:
-// HDFS_CRC32C_GBLOCKS (about that many blocks per item; 0: round 3's sizes,
-// one subtile when k divides 16, else kGeneralChunks),
+// Full chunks per general item of k blocks per chunk: when k divides 16,
+// whole chunks filling two subtiles (round 3: one; measured, same box:
+// bpc 1000 60.3 -> 58.5 us, bpc 700 73.6 -> 70.2, bpc 4000 62.3 -> 59.8),
+// else kGeneralChunks = 16 (bpc 1536: 3 subtiles, the best of 5-31 chunks;
+// bpc 2560 / 3000 slower or equal with fewer).  A/B knobs:
+// HDFS_CRC32C_GBLOCKS (about that many blocks per item; 0: round 3's sizes),
 // HDFS_CRC32C_GCHUNKS (k not dividing 16) and HDFS_CRC32C_GCHUNKS_DIV (k
 // dividing 16, a multiple of 16 / k) override it.  At most 31 (the
 // descriptor's field).
@@ -56,8 +59,10 @@ static uint64_t item_chunks(uint32_t k) {
     const uint64_t one = kTileBlocks % k == 0 ? kTileBlocks / k : 1;  // chunks that fill whole subtiles
     if (kTileBlocks % k == 0 && div >= 1 && div <= 31 && uint64_t(div) % one == 0) return uint64_t(div);
     if (kTileBlocks % k != 0 && ch >= 1 && ch <= 31) return uint64_t(ch);
-    const uint64_t target = blocks >= 0 ? uint64_t(blocks) : kItemBlocks;
-    if (target == 0) return kTileBlocks % k == 0 ? one : kGeneralChunks;
+    if (blocks < 0)  // the default: two subtiles of whole chunks when k divides 16, else 16 chunks
+        return kTileBlocks % k == 0 ? (2 * one <= 31 ? 2 * one : one) : kGeneralChunks;
+    const uint64_t target = uint64_t(blocks);
+    if (target == 0) return kTileBlocks % k == 0 ? one : kGeneralChunks;  // round 3's sizes
     uint64_t n = std::max<uint64_t>(target / k, 1);
     n = std::max<uint64_t>(n / one, 1) * one;  // whole subtiles when k divides 16
     while (n > 31) n -= one;

@@ -53,8 +53,6 @@ struct FastTile {
 static_assert(sizeof(FastTile) == 16, "FastTile is 16 bytes");
 constexpr uint64_t kSrcMask = (1ull << 48) - 1;
 constexpr uint32_t kGeneralChunks = 16;  // full chunks per general item
-// (plan.cpp item_chunks, A/B default 0 = round 3's sizes until measured)
-constexpr uint32_t kItemBlocks = 0;
 
 inline uint32_t general_meta(uint32_t nch, uint32_t k, uint32_t pad, uint32_t kt = 0) {
     return kGeneralTile | ((nch * k + kt + kTileBlocks - 1) / kTileBlocks) | (k << 8) | (nch << 13) | (pad << 18);
