@@ -261,10 +261,12 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
 // the group as P[hi - 1] ^ P[lo - 1].  After the last group lane c holds
 // chunk c's lin, and crc = lin ^ crc(0, zeros(n)) for its n bytes.  GROUP
 // = 1 is round 3's per-subtile gather (each block shifted before the
-// permute, a prefix per 16-lane row): the general-tiles-only build takes GROUP = 4 (bpc 1536:
-// 49.6 -> 48.1 us), the builds with both paths keep GROUP = 1 (padded bpc
-// 1000's verify ran 61.8 -> 63.5 us with 4).  Each
-// subtile's loads are issued after the previous one's lookups.
+// permute, a prefix per 16-lane row).  The general-tiles-only build takes
+// GROUP = 4 (bpc 1536: 49.6 -> 48.1 us), the builds with both paths GROUP =
+// 2 (padded chunks, two subtiles per item when k divides 16: bpc 700 72.1
+// -> 69.7 us, bpc 1000 58.1 -> 57.3; with 4, bpc 1000's verify had run
+// 61.8 -> 63.5).  Each subtile's loads are issued
+// after the previous one's lookups.
 template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, uint32_t GROUP = 1>
 __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                              uint4 v[8], uint32_t ev, int lane) {
@@ -336,7 +338,8 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         // row_bcast:15 -- rows 1 and 3 add the last lane of rows 0 and 2;
         // row_bcast:31 -- rows 2 and 3 add lane 31 (rows 0 and 1 in all)
         z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x142, 0xA, 0xF, false));
-        z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x143, 0xC, 0xF, false));
+        if (GROUP > 2)
+            z ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(z), 0x143, 0xC, 0xF, false));
         const int base = int(16u * GROUP * (s / GROUP)), span = int(16u * GROUP);
         const int l1 = min(max(int(lo) - base, 0), span), h1 = min(max(int(hi) - base, 0), span);
         const uint32_t ph = uint32_t(__builtin_amdgcn_ds_bpermute((max(h1, 1) - 1) << 2, int(z)));
