@@ -17,23 +17,25 @@
 //    complete entry from a stale or half-written one.
 //  * forwarder (workgroup 0's last wave): reads 64 host slots per poll (one
 //    PCIe round trip per poll, not per block) and copies the ready ones into
-//    a device ring, tags and all (agent scope).  It also collects: block t is complete when all
-//    workgroups' flags for its slot hold t + 1 (one 1 KiB load per check),
-//    then hdone[slot] = t + 1 (system scope).
-//  * workers (waves 0-10 of every workgroup): block t is run by phase t % 5
-//    (5 blocks in flight); within a phase two waves per workgroup take one
-//    8 KiB tile each (a 4 MiB block is 512 tiles = 2 per CU); a workgroup's
-//    phase workers count themselves in LDS and the last one stores the
-//    workgroup's flag.  Checksums are stored write-through (system scope),
-//    and every store has completed before the flag.
+//    a device ring, tags and all (agent scope).
+//  * collector (workgroup 1's last wave): block t is complete when all
+//    workgroups' flags for its slot hold t + 1 (one 1 KiB load per check);
+//    blocks complete in ticket order, hdone[slot] = t + 1 (system scope).
+//  * workers (every other wave): block t is run by phase t % P (P blocks in
+//    flight); within a phase PER waves per workgroup take its tiles (a 4 MiB
+//    block is 512 tiles = 2 per CU: one each, or both by one wave with both
+//    loaded first); a workgroup's phase workers count themselves in LDS and
+//    the last one stores the workgroup's flag.  Checksums are stored
+//    write-through (system scope), and every store has completed before the
+//    flag.
 //  * lifetime: the forwarder exits on the host's stop word, after idle_us
 //    with nothing queued, or after kStuckMs without progress while blocks are
 //    outstanding (a workgroup that never got a CU); on exit it raises the
-//    device stop word that every worker polls, and records where it stopped
-//    (exit_col) so a relaunch resumes there.  The host relaunches the kernel
-//    on demand (submit, or a waiter that waits long), never while one runs.
-//    Workers have their own bound (kWorkerMs without a block).  Every wave
-//    therefore exits, whatever the host does.
+//    device stop word that every worker polls; the collector records where
+//    it stopped (exit_col) so a relaunch resumes there.  The host relaunches
+//    the kernel on demand (submit, or a waiter that waits long), never while
+//    one runs.  Workers have their own bound (kWorkerMs without a block).
+//    Every wave therefore exits, whatever the host does.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
