@@ -705,6 +705,25 @@ def main():
             verify["graph_kernel_avg_us"] = round(e0.elapsed_time(e1) / nv * 1e3, 2)
             verify["graph_clean"] = bool(r[0] == 0 and r[1] == 0xFFFFFFFF)
             verify["clean"] = verify["clean"] and verify["graph_clean"]
+            # The same nv-launch graph form for exec, right after (into the
+            # scratch outputs): what the verify graph is read against, and a
+            # steady-state exec figure beside the timed window's.
+            try:
+                plan.exec(bufs[0].data_ptr(), scratch_outs[0].data_ptr(), cs.cuda_stream)
+                torch.cuda.synchronize()
+                egraph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(egraph, stream=cs, capture_error_mode="thread_local"):
+                    for i in range(nv):
+                        plan.exec(bufs[i % nbuf].data_ptr(), scratch_outs[i % nbuf].data_ptr(), cs.cuda_stream)
+                egraph.replay()
+                torch.cuda.synchronize()
+                e0.record(stream)
+                egraph.replay()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                verify["exec_graph_kernel_avg_us"] = round(e0.elapsed_time(e1) / nv * 1e3, 2)
+            except RuntimeError:
+                torch.cuda.synchronize()
 
     # The box's own streaming-read rate over the same rotating buffers, right
     # after the timed region (same power state): a plain grid-stride read
