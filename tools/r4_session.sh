@@ -64,6 +64,7 @@ for s in ${STEPS:-calls multi}; do
     gch) for n in ${GCH:-16 5 10 21 16}; do run gch_${n} 300 env HDFS_CRC32C_GCHUNKS=$n python bench.py --config ${GCFG:-c2b1536} --no-cpu --no-host || exit 1; done ;;
     soak) run soak $(( ${SOAK_S:-240} + 90 )) python -u tools/soak.py --seconds ${SOAK_S:-240} --out $OUT/soak.jsonl ;;
     syncp) run sync_default 120 python tools/sync_probe.py && run sync_spin 120 python tools/sync_probe.py --spin ;;
+    tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     prof2) run prof2 600 rocprofv3 --kernel-trace --stats -d $OUT/prof2 -o run --output-format csv -- python3 bench.py ;;
     prof3) run prof3 300 rocprofv3 --kernel-trace --stats -d $OUT/prof3 -o run --output-format csv -- python3 bench.py --config c3 --no-cpu --no-host ;;
