@@ -19,6 +19,22 @@ exits with its return code.  After the timed region the ranks' checksum
 arrays are gathered to rank 0 over RCCL (the only collective of configs 2/5;
 timed separately as "gather_ms"; config 4 gathers inside every step).
 Rank 0 prints ONE JSON line.
+
+The default line (config 2, weak scaling) also carries, at every N, the two
+other shapes BASELINE.json's 1/2/4/8-GPU curve is quoted on (each timed like
+the main steps: K steps, graph-replayed, max over ranks, bit-exact against
+the reference):
+  config4         -- config 4 (128 MiB file = 32 x 4 MiB blocks dealt
+                     round-robin over the ranks, src/fuse.c:580-647): every
+                     step is crc32c_multi_plan_exec, the shards' launches AND
+                     the RCCL gather of the checksums into file order on
+                     rank 0, captured into the step graph;
+  strong_scaling  -- the one config-2 batch (256 MiB) split over the ranks.
+Graph capture is rank-consistent (native-hdfs-fuse_amd/graphs.py): the
+ranks agree (MIN all-reduce) on a probe with no collective and then on the
+step capture; if any rank fails, every rank drops its graphs, the config-4
+communicator is rebuilt on every rank, and every rank issues its steps from
+the host.  BENCH_CAPTURE_FAIL_RANK=r injects a step-capture failure on rank r.
 """
 from __future__ import annotations
 
@@ -30,6 +46,7 @@ import math
 import os
 import sys
 import time
+from types import SimpleNamespace
 
 import numpy as np
 
@@ -43,6 +60,9 @@ KERNEL_NAME = "hdfs_crc32c_plan_kernel"
 # kVariants[0]: 768 threads, 3 waves/SIMD, kModeS4 | kModeNt); PMC traffic is
 # only reported from a summary of this exact kernel.
 PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<768, 3, 3>"
+C4_BLOCKS = 32        # config 4: 128 MiB file = 32 x 4 MiB blocks
+C4_GROUP_PACKETS = 64  # one 4 MiB block = 64 packets of 64 KiB
+MULTI_SELF_SEND = 0x10  # CRC32C_MULTI_SELF_SEND
 
 
 def load_package():
@@ -77,7 +97,7 @@ def baseline_metric() -> str:
         with open(os.path.join(ROOT, "BASELINE.json")) as f:
             return json.load(f)["metric"]
     except Exception:
-        return "GiB/s CRC32C, device-resident 64 KiB packets \u00d7 512 B chunks, 1/2/4/8 GPU"
+        return "GiB/s CRC32C, device-resident 64 KiB packets × 512 B chunks, 1/2/4/8 GPU"
 
 
 def latest_pmc(profile_dir: str, config: str):
@@ -296,6 +316,394 @@ def host_block_latency(hdfs, ctx, pk, payload: np.ndarray, want, ref_threads: in
     return res
 
 
+# ---- the timed region, shared by the main line and its sub-runs ------------
+def settle_for(env, ms: float, fn, collective: bool) -> int:
+    """Untimed back-to-back steps for ~ms; returns how many.  Steps that hold
+    collective calls run a fixed count (every rank makes the same calls)."""
+    import torch
+
+    n = 0
+    if ms <= 0:
+        return 0
+    if collective and env.world > 1:
+        for n in range(int(ms * 10)):
+            fn(n)
+        return n + 1
+    # (chunks of 20 launches; the host waits for the chunk before the last
+    # one, so the GPU always has one queued and never idles)
+    s0 = time.perf_counter()
+    prev = None
+    while (time.perf_counter() - s0) * 1e3 < ms:
+        for _ in range(20):
+            fn(n)
+            n += 1
+        ev = torch.cuda.Event()
+        ev.record(env.stream)
+        if prev is not None:
+            prev.synchronize()
+        prev = ev
+    return n
+
+
+def time_steps(env, args, step, warm_step, *, collective=False, use_graph=True, zero=None, probe=None,
+               on_abandon=None, settle_ms=None) -> dict:
+    """Capture, settle, warm up and time args.steps steps of `step(i, stream)`.
+
+    - The K timed steps are captured into HIP graphs and replayed: each step
+      is still one pass of the path over one batch (config 4: the shard
+      launch + the RCCL group), but the launches are issued by the GPU's
+      command processor instead of one Python -> ctypes -> hipLaunchKernel
+      call each (~4.1 us per launch on the host, which bounds one-block
+      batches: DESIGN.md section 5).  Capture is agreed over the ranks
+      (graphs.capture_agreed): all ranks replay or all issue from the host.
+    - The K steps are split in two: the first n_lead of them, then the rest,
+      with a timing event between.  The per-launch kernel time is taken over
+      the second part only: its launches are queued while the first part's
+      run, so it holds neither the host's first issue nor a graph's launch
+      latency (~20 us on this stack).  n_lead covers >= 150 us of kernel
+      time (at most half the steps).  Both parts are timed steps: the wall
+      clock holds all K of them.  A lead of steps of >= 25 us each is issued
+      from the host (its first launch starts within a few us, and the main
+      part's graph launch hides behind it).  BENCH_CAPTURE_FAIL_RANK=r makes
+      rank r's step capture fail (every rank then issues from the host).
+    - Outputs are zeroed (`zero`) BEFORE the power settle, so the GPU goes
+      from settle to warm-up to the timed steps with no idle gap; settle and
+      warm-up steps (`warm_step`) write scratch outputs.  Back-to-back
+      launches of this kernel push the package to its 1.4 kW cap; the first
+      few hundred ride a boost-then-clamp transient 5-12 % slower than the
+      steady state.
+    Returns the times, max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from hdfs_crc32c_amd.graphs import capture_agreed
+
+    K = args.steps
+    world, dev, stream = env.world, env.dev, env.stream
+    step_us = 0.0
+    if K > 1:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(10):
+            warm_step(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        step_us = e0.elapsed_time(e1) * 1e3 / 10
+    n_lead = 0 if K < 2 else min(K // 2, max(1, -(-150 // max(int(step_us), 1))))
+    if world > 1:  # (one split and one lead form on every rank)
+        t = torch.tensor([n_lead, step_us], dtype=torch.float64, device=env.cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n_lead, step_us = int(t[0].item()), float(t[1].item())
+    parts = [(0, n_lead), (n_lead, K)] if n_lead else [(0, K)]
+    lead_host = n_lead > 0 and step_us >= 25.0
+    graphs, graph_error = {}, None
+    if use_graph:
+        def capture():
+            gs = {}
+            try:
+                for k, (lo, hi) in enumerate(parts):
+                    if lead_host and k == 0:
+                        continue
+                    g_ = torch.cuda.CUDAGraph()
+                    # (thread_local: other threads of the process -- e.g. the process
+                    # group's watchdog -- may make HIP calls while this thread captures)
+                    with torch.cuda.graph(g_, capture_error_mode="thread_local"):
+                        cap = torch.cuda.current_stream(dev)
+                        for i in range(lo, hi):
+                            step(i, cap.cuda_stream)
+                    gs[k] = g_
+                for g_ in gs.values():
+                    g_.replay()  # (first replay uploads the graph)
+                torch.cuda.synchronize()
+            except RuntimeError:
+                torch.cuda.synchronize()
+                raise
+            return gs
+
+        inject = os.environ.get("BENCH_CAPTURE_FAIL_RANK", "") == str(env.rank)
+        got, graph_error = capture_agreed(capture, world, env.cdev, probe=probe, on_abandon=on_abandon,
+                                          inject_fail=inject)
+        graphs = got or {}
+        use_graph = bool(got)
+    if zero is not None:
+        zero()
+    torch.cuda.synchronize()
+    settle = settle_for(env, args.settle_ms if settle_ms is None else settle_ms, warm_step, collective)
+    for i in range(args.warmup):
+        warm_step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(parts) + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for k, (lo, hi) in enumerate(parts):
+        if k in graphs:
+            graphs[k].replay()
+        else:
+            for i in range(lo, hi):
+                step(i)
+        evs[k + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # avg per step, on the launch stream: over the steps after the lead (all
+    # K when there is no lead)
+    window_ms = evs[0].elapsed_time(evs[-1]) / max(K, 1)
+    lo_t, hi_t = parts[-1]
+    kernel_ms = evs[-2].elapsed_time(evs[-1]) / max(hi_t - lo_t, 1)
+    own = (elapsed, kernel_ms, window_ms)
+    if world > 1:
+        t = torch.tensor(own, dtype=torch.float64, device=env.cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms, window_ms = (float(x) for x in t.tolist())
+    return {"elapsed": elapsed, "kernel_ms": kernel_ms, "window_ms": window_ms, "parts": parts, "n_lead": n_lead,
+            "lead_host": lead_host, "graphs": graphs, "use_graph": use_graph, "graph_error": graph_error,
+            "settle": settle, "own_kernel_ms": own[1]}
+
+
+def launch_text(r) -> str:
+    if r["use_graph"]:
+        return "%s, replayed" % " + ".join(("%d host-issued" if k not in r["graphs"] else "hip graph of %d") % (hi - lo)
+                                           for k, (lo, hi) in enumerate(r["parts"]))
+    return "host-issued, one launch per step" + (
+        "" if r["graph_error"] is None else " (graph capture not agreed: %s)" % r["graph_error"])
+
+
+def agree_min(env, ok: bool) -> bool:
+    from hdfs_crc32c_amd.graphs import agree
+
+    return agree(ok, env.world, env.cdev)
+
+
+# ---- config 4: the multi-GPU file step (also the default line's sub-object) --
+def run_config4(hdfs, args, env) -> dict:
+    """Config 4 at this N: a 128 MiB file as 32 x 4 MiB blocks dealt
+    round-robin over the ranks (group g of 64 packets on rank g mod N,
+    src/fuse.c:580-647 writes a file block by block; hadooprpc.c:815-860
+    cuts each block into packets).  One step = crc32c_multi_plan_exec: every
+    rank checksums its shard from its own HBM (rank 0 straight into file
+    order) and ONE RCCL group lands every peer's block checksums in file
+    order on rank 0 (no staging, no copy kernel), captured into the step
+    graph.  Buffer b of every rank is its shard of the PCG64 file of seed
+    2024 + b, so rank 0 checks the array the LAST timed step gathered
+    against the reference over that step's file.  Ranks sharing GPUs over
+    gloo (BENCH_DIST_BACKEND=gloo, a rehearsal) run the same shard plans and
+    gather with shard.gather_checksums over gloo instead, host-issued."""
+    import torch
+    import torch.distributed as dist
+
+    from hdfs_crc32c_amd import shard
+    from hdfs_crc32c_amd.workloads import synthetic_bytes, uniform_packets
+
+    world, rank, dev = env.world, env.rank, env.dev
+    gp = C4_GROUP_PACKETS
+    file_pk = uniform_packets(C4_GROUP_PACKETS * C4_BLOCKS)
+    file_bytes_total = C4_BLOCKS * shard.BLOCK_BYTES
+    lay, shard_sizes = shard.layout(file_pk, gp, world)
+    rehearsal = world > 1 and env.backend != "nccl"
+    self_send = os.environ.get("BENCH_C4_SELF_SEND") == "1"  # (tests: rank 0's array through RCCL too)
+    flags = MULTI_SELF_SEND if self_send else 0
+    nbuf = max(1, args.nbuf)
+    file0 = synthetic_bytes(file_bytes_total, 2024)
+    bufs = []
+    for b in range(nbuf):
+        fb = file0 if b == 0 else synthetic_bytes(file_bytes_total, 2024 + b)
+        bufs.append(torch.from_numpy(shard.rank_payload(fb, lay, shard_sizes, rank)).to(dev))
+        del fb
+    # this rank's shard plan alone (what the multi plan launches on it): the
+    # probe capture with no collective in it, and the shard kernel's time
+    mine = shard.plan_packets(file_pk, gp, world, rank, flags)
+    ln, xs = shard.transfers(file_pk, gp, world, flags)
+    nchk = hdfs.total_checksums(file_pk)
+    in_place = rank == 0 and not int(ln[0])
+    nlocal = nchk if in_place else int(ln[rank])
+    sctx = hdfs.Context(env.local_rank)
+    splan = sctx.plan(mine) if mine.size else None
+    local_out = torch.zeros(max(nlocal, 1), dtype=torch.int32, device=dev)
+    root_out = torch.zeros(max(nchk, 1), dtype=torch.int32, device=dev)
+    scratch_root = torch.zeros_like(root_out)
+    sptr = env.sptr
+
+    state = {}
+
+    def make_multi():
+        if world == 1:
+            m = hdfs.Multi([env.local_rank])
+        else:
+            obj = [hdfs.multi_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            m = hdfs.Multi(device=env.local_rank, rank=rank, nranks=world, uid=obj[0])
+        state["multi"] = m
+        state["mplan"] = m.plan(file_pk, gp, flags)
+
+    def close_multi():
+        if state.get("mplan") is not None:
+            state["mplan"].close()
+        if state.get("multi") is not None:
+            state["multi"].close()
+        state["mplan"] = state["multi"] = None
+
+    rebuilt = [0]
+
+    def abandon():
+        # A rank whose capture failed inside the RCCL group may have left it
+        # half-posted: every rank drops its communicator and builds a new one
+        # (new id, new crc32c_multi), then issues its steps from the host.
+        torch.cuda.synchronize()
+        close_multi()
+        make_multi()
+        rebuilt[0] += 1
+
+    if not rehearsal:
+        make_multi()
+
+    def step_into(i, out_t, sp):
+        b = i % nbuf
+        if rehearsal:
+            if splan is not None:
+                splan.exec(bufs[b].data_ptr(), local_out.data_ptr(), sp)
+            torch.cuda.synchronize()
+            got = shard.gather_checksums(local_out.cpu(), file_pk, gp, world, rank, flags)
+            if rank == 0:
+                out_t[:nchk].copy_(torch.from_numpy(got.view(np.int32).copy()))
+        else:
+            state["mplan"].exec([bufs[b].data_ptr()], out_t.data_ptr() if rank == 0 else 0, [sp])
+
+    def step(i, sp=None):
+        step_into(i, root_out, sptr if sp is None else sp)
+
+    def warm_step(i):
+        step_into(i, scratch_root, sptr)
+
+    def probe():
+        if splan is None:
+            return
+        g_ = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g_, capture_error_mode="thread_local"):
+                splan.exec(bufs[0].data_ptr(), local_out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+            g_.replay()
+        finally:
+            torch.cuda.synchronize()
+
+    # correctness gate (outside the timed region): the whole file's checksums
+    # gathered on rank 0 against the reference
+    step(0)
+    torch.cuda.synchronize()
+    want0 = reference_checksums(file0, file_pk, nchk) if rank == 0 else None
+    gate = rank != 0 or bool(np.array_equal(root_out.cpu().numpy().view(np.uint32)[:nchk], want0))
+    r = time_steps(env, args, step, warm_step, collective=world > 1, use_graph=not (args.no_graph or rehearsal),
+                   zero=lambda: root_out.zero_(), probe=probe, on_abandon=abandon,
+                   settle_ms=0 if rehearsal else None)
+    timed = True
+    b_last = (args.steps - 1) % nbuf
+    if rank == 0 and args.steps > 0:
+        wb = want0 if b_last == 0 else reference_checksums(synthetic_bytes(file_bytes_total, 2024 + b_last),
+                                                           file_pk, nchk)
+        timed = bool(np.array_equal(root_out.cpu().numpy().view(np.uint32)[:nchk], wb))
+    # the shard's plan launch alone (no gather), same buffers, graph-replayed
+    # when the step was: what the gather adds to a step is the difference
+    # (every rank or none: the timing holds collectives)
+    shard_max = None
+    if not rehearsal and agree_min(env, splan is not None):
+        def sstep(i, sp=None):
+            splan.exec(bufs[i % nbuf].data_ptr(), local_out.data_ptr(), sptr if sp is None else sp)
+        rs = time_steps(env, args, sstep, sstep, use_graph=r["use_graph"], settle_ms=min(args.settle_ms, 50.0))
+        shard_max = rs["kernel_ms"] * 1e3  # (max over ranks)
+    exact = agree_min(env, gate and timed)
+    close_multi()
+    if splan is not None:
+        splan.close()
+    sctx.close()
+    per_rank_max = int(shard_sizes.max()) if len(shard_sizes) else 0
+    step_kernel_us = r["kernel_ms"] * 1e3
+    return {
+        "workload": "128MiB file as 32 x 4MiB blocks round-robin over %d ranks, %s gather of the checksums into "
+                    "file order on rank 0 inside every step (config 4)" % (world, "gloo rehearsal" if rehearsal
+                                                                           else "RCCL"),
+        "n_ranks": world, "steps": args.steps, "warmup": args.warmup,
+        "gib_s": round(file_bytes_total * args.steps / r["elapsed"] / GIB, 2),
+        "step_us": round(r["elapsed"] / max(args.steps, 1) * 1e6, 3),
+        "kernel_step_us": round(step_kernel_us, 3),
+        "kernel_step_gib_s": round(file_bytes_total / (step_kernel_us * 1e-6) / GIB, 2),
+        # the whole file's bytes per step over the chip's HBM peak x ranks
+        "frac_of_hbm_roofline": round(file_bytes_total / (step_kernel_us * 1e-6) / 1e9 / (PEAK_HBM_GBS * world), 4),
+        "shard_kernel_us": None if shard_max is None else round(shard_max, 3),
+        "shard_bytes_max": per_rank_max,
+        "shard_frac_of_hbm_roofline": None if not shard_max else
+        round(per_rank_max / (shard_max * 1e-6) / 1e9 / PEAK_HBM_GBS, 4),
+        "gather_us": None if shard_max is None else round(step_kernel_us - shard_max, 3),
+        "transfers": int(xs.shape[0]), "self_send": self_send,
+        "bit_exact": exact,
+        "bit_exact_checks": {"before_warmup_file0": gate, "timed_file_buf%d" % b_last: timed} if rank == 0 else None,
+        "launch": launch_text(r), "lead_steps": "host-issued" if (r["lead_host"] or not r["use_graph"]) else "graph",
+        "communicator_rebuilt": rebuilt[0], "settle_launches": r["settle"],
+        "mode": "gloo rehearsal (ranks share GPUs; not a measurement)" if rehearsal else "rccl",
+    }
+
+
+def run_strong(hdfs, args, env, ctx) -> dict:
+    """The one config-2 batch (4096 x 64 KiB packets, 256 MiB) split over the
+    ranks (strong scaling): rank r checksums packets
+    [r N/W, (r+1) N/W) from its own HBM, no data-path collective; value =
+    256 MiB per step / the slowest rank's time."""
+    import torch
+
+    from hdfs_crc32c_amd.workloads import synthetic_bytes, uniform_packets
+
+    world, rank, dev = env.world, env.rank, env.dev
+    full = uniform_packets(4096)
+    lo, hi = rank * full.size // world, (rank + 1) * full.size // world
+    pk = full[lo:hi].copy()
+    pk["payload_off"] -= pk["payload_off"][0]
+    pk["out_idx"] -= pk["out_idx"][0]
+    nbytes = int(pk["len"].astype(np.int64).sum())
+    total_bytes = int(full["len"].astype(np.int64).sum())
+    nout = hdfs.total_checksums(pk)
+    plan = ctx.plan(pk)
+    nbuf = max(1, args.nbuf)
+    payload0 = synthetic_bytes(nbytes, 3030 + rank)
+    bufs = [torch.from_numpy(payload0).to(dev)]
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    for _ in range(1, nbuf):
+        bufs.append(torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device=dev, generator=g))
+    outs = [torch.zeros(max(nout, 1), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+    scratch = [torch.zeros_like(o) for o in outs]
+    sptr = env.sptr
+
+    def step(i, sp=None):
+        plan.exec(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), sptr if sp is None else sp)
+
+    def warm(i):
+        plan.exec(bufs[i % nbuf].data_ptr(), scratch[i % nbuf].data_ptr(), sptr)
+
+    def zero():
+        for o in outs:
+            o.zero_()
+
+    r = time_steps(env, args, step, warm, use_graph=not args.no_graph, zero=zero)
+    want = reference_checksums(payload0, pk, nout)
+    exact = args.steps < nbuf or bool(np.array_equal(outs[0].cpu().numpy().view(np.uint32)[:nout], want))
+    exact = agree_min(env, exact)
+    plan.close()
+    kernel_us = r["kernel_ms"] * 1e3
+    return {
+        "workload": "the config-2 batch (4096 x 64KiB packets, 256 MiB) split over %d ranks" % world,
+        "n_ranks": world, "packets_per_rank": int(pk.size), "steps": args.steps,
+        "gib_s": round(total_bytes * args.steps / r["elapsed"] / GIB, 2),
+        "step_us": round(r["elapsed"] / max(args.steps, 1) * 1e6, 3),
+        "kernel_us_max_rank": round(kernel_us, 3),
+        "frac_of_hbm_roofline_per_gpu": round(nbytes / (kernel_us * 1e-6) / 1e9 / PEAK_HBM_GBS, 4),
+        "bit_exact": exact, "launch": launch_text(r), "settle_launches": r["settle"],
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -310,6 +718,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=4.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--no-config4", action="store_true", help="skip the config4 sub-object of the c2 line")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong_scaling sub-object of the c2 line")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak (default): every rank checksums its own config batch; strong: the config-2/5 batch's "
                          "packets are split evenly over the ranks (SURVEY.md section 8e)")
@@ -364,249 +774,106 @@ def main():
     hdfs.lib()
 
     from hdfs_crc32c_amd import shard
-    from hdfs_crc32c_amd.workloads import config_packets, synthetic_bytes, uniform_packets
+    from hdfs_crc32c_amd.workloads import config_packets, synthetic_bytes
 
-    c4 = args.config == "c4"
-    if c4:
-        # 128 MiB file = 32 x 4 MiB blocks, block b on rank b mod world, through
-        # the C ABI's multi-GPU plan: every rank checksums its shard and one
-        # RCCL send/recv group lands the checksums in file order on rank 0.
-        # One step = shard checksums + the gather (the whole config-4 job).
-        file_pk = uniform_packets(64 * 32)
-        file_bytes = synthetic_bytes(32 * shard.BLOCK_BYTES, 2024)
-        if world == 1:
-            multi = hdfs.Multi([local_rank])
-        else:
-            obj = [hdfs.multi_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            multi = hdfs.Multi(device=local_rank, rank=rank, nranks=world, uid=obj[0])
-        mplan = multi.plan(file_pk, 64)
-        lay, shard_sizes = shard.layout(file_pk, 64, world)
-        pk = shard.rank_packets(file_pk, 64, world, rank)
-        workload = "128MiB file as 32 x 4MiB blocks round-robin over %d ranks, RCCL gather to rank 0 (config 4)" % world
-        nbuf = args.nbuf
-    else:
-        pk, workload = config_packets(args.config)
-        if args.scaling == "strong" and world > 1:
-            if args.config not in ("c2", "c5") or pk.size % world:
-                raise SystemExit("--scaling strong needs config c2/c5 and a rank count dividing %d" % pk.size)
-            per = pk.size // world
-            pk = pk[rank * per:(rank + 1) * per].copy()  # this rank's packets, rebased
-            pk["payload_off"] -= pk["payload_off"][0]
-            pk["out_idx"] -= pk["out_idx"][0]
-            workload += ", strong scaling: packets split over %d ranks" % world
-        nbuf = args.nbuf if args.config not in ("c3", "c3u") else 1
+    dev = torch.device("cuda", local_rank)
+    stream = torch.cuda.current_stream(dev)
+    env = SimpleNamespace(world=world, rank=rank, local_rank=local_rank, backend=backend, dev=dev, stream=stream,
+                          sptr=stream.cuda_stream,
+                          cdev=dev if backend == "nccl" else torch.device("cpu"))  # where collectives run
+    cdev = env.cdev
+
+    if args.config == "c4":  # config 4 as the main line (builder's runs): its sub-run, reported flat
+        c4 = run_config4(hdfs, args, env)
+        if rank == 0:
+            kus = c4["kernel_step_us"]
+            line = {
+                "metric": baseline_metric(), "value": c4["gib_s"], "unit": "GiB/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(c4["step_us"] * 1e-3, 5),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+                "data": "synthetic (PCG64 file bytes, %d rotating files)" % max(1, args.nbuf),
+                "config": {"workload": c4["workload"], "config": "c4",
+                           "parallelism": "dp%d (block shards, crc32c_multi_plan: RCCL send/recv gather of the "
+                                          "checksums to rank 0 inside every step)" % world},
+                "roofline": {"bound": "hbm", "achieved": round(C4_BLOCKS * shard.BLOCK_BYTES / (kus * 1e-6) / 1e9, 1),
+                             "peak": PEAK_HBM_GBS * world, "unit": "GB/s", "frac": c4["frac_of_hbm_roofline"],
+                             "traffic": None, "kernel": KERNEL_NAME, "kernel_avg_us": kus,
+                             "algorithmic_bytes_per_launch": C4_BLOCKS * shard.BLOCK_BYTES},
+                "cpu_baseline": None, "bit_exact_vs_reference": c4["bit_exact"], "config4": c4,
+            }
+            if not args.no_cpu and world == 1:
+                from hdfs_crc32c_amd.workloads import uniform_packets
+
+                line["cpu_baseline"] = cpu_baseline(uniform_packets(C4_GROUP_PACKETS * C4_BLOCKS),
+                                                    synthetic_bytes(C4_BLOCKS * shard.BLOCK_BYTES, 2024),
+                                                    args.cpu_seconds)
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    pk, workload = config_packets(args.config)
+    if args.scaling == "strong" and world > 1:
+        if args.config not in ("c2", "c5") or pk.size % world:
+            raise SystemExit("--scaling strong needs config c2/c5 and a rank count dividing %d" % pk.size)
+        per = pk.size // world
+        pk = pk[rank * per:(rank + 1) * per].copy()  # this rank's packets, rebased
+        pk["payload_off"] -= pk["payload_off"][0]
+        pk["out_idx"] -= pk["out_idx"][0]
+        workload += ", strong scaling: packets split over %d ranks" % world
+    nbuf = args.nbuf if args.config not in ("c3", "c3u") else 1
     nbytes = int(pk["len"].astype(np.int64).sum())
     extent = int((pk["payload_off"] + pk["len"]).max())
     nout = hdfs.total_checksums(pk)
 
-    ctx = plan = None
-    if not c4:
-        ctx = hdfs.Context(local_rank)
-        plan = ctx.plan(pk)
-    dev = torch.device("cuda", local_rank)
-    # buffer 0: PCG64 host bytes (checked against the CPU
-    # path below); the rest: device-generated random bytes.  Config 4:
-    # buffer b is this rank's shard of the PCG64 file of seed 2024 + b, so
-    # rank 0 can rebuild whichever file a timed step checksummed.
-    if c4:
-        payload0 = shard.rank_payload(file_bytes, lay, shard_sizes, rank)
-        extent = payload0.size
-        root_out = torch.zeros(max(mplan.nchecksums, 1), dtype=torch.int32, device=dev)
-    else:
-        payload0 = synthetic_bytes(extent, 2024 + rank)
+    ctx = hdfs.Context(local_rank)
+    plan = ctx.plan(pk)
+    # buffer 0: PCG64 host bytes (checked against the CPU path below); the
+    # rest: device-generated random bytes
+    payload0 = synthetic_bytes(extent, 2024 + rank)
     bufs = [torch.from_numpy(payload0).to(dev)]
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     for b in range(1, nbuf):
-        if c4:
-            fb = synthetic_bytes(32 * shard.BLOCK_BYTES, 2024 + b)
-            bufs.append(torch.from_numpy(shard.rank_payload(fb, lay, shard_sizes, rank)).to(dev))
-            del fb
-        else:
-            bufs.append(torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g))
+        bufs.append(torch.randint(0, 256, (extent,), dtype=torch.uint8, device=dev, generator=g))
     outs = [torch.zeros(max(nout, 1), dtype=torch.int32, device=dev) for _ in range(nbuf)]
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+    sptr = env.sptr
 
     def step(i, sp=None):
         b = i % nbuf
-        sp = sptr if sp is None else sp
-        if c4:
-            mplan.exec([bufs[b].data_ptr()], root_out.data_ptr() if rank == 0 else 0, [sp])
-        else:
-            plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sp)
+        plan.exec(bufs[b].data_ptr(), outs[b].data_ptr(), sptr if sp is None else sp)
 
     # correctness gate (outside the timed region): every buffer-0 checksum
-    # (config 4: the whole file's, gathered on rank 0)
     step(0)
     torch.cuda.synchronize()
-    if c4:
-        want = reference_checksums(file_bytes, file_pk, mplan.nchecksums) if rank == 0 else None
-        bit_exact = rank != 0 or bool(np.array_equal(root_out.cpu().numpy().view(np.uint32), want))
-    else:
-        want = reference_checksums(payload0, pk, nout)
-        got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
-        bit_exact = bool(np.array_equal(got0, want))
+    want = reference_checksums(payload0, pk, nout)
+    got0 = outs[0].cpu().numpy().view(np.uint32)[:nout]
+    bit_exact = bool(np.array_equal(got0, want))
     gate_exact = bit_exact
 
-    # Settle and warm-up steps write a scratch copy of the outputs (same
-    # payloads, same plan), so the outputs the timed steps write are zeroed
-    # BEFORE the settle phase and the checks after the timed region still see
-    # only what the timed launches wrote -- and the GPU goes from settle to
-    # warm-up to the timed steps with no idle gap beyond one synchronise
-    # (round 3 captured and zeroed between settle and timing: the GPU idled
-    # there and a 20-step window ran slower than the verify window after it).
-    scratch_outs = [torch.zeros_like(o) for o in ([root_out] if c4 else outs)]
+    # settle and warm-up steps write a scratch copy of the outputs (same
+    # payloads, same plan), so the checks after the timed region see only
+    # what the timed launches wrote
+    scratch_outs = [torch.zeros_like(o) for o in outs]
 
     def warm_step(i):
         b = i % nbuf
-        if c4:
-            mplan.exec([bufs[b].data_ptr()], scratch_outs[0].data_ptr() if rank == 0 else 0, [sptr])
-        else:
-            plan.exec(bufs[b].data_ptr(), scratch_outs[b].data_ptr(), sptr)
+        plan.exec(bufs[b].data_ptr(), scratch_outs[b].data_ptr(), sptr)
 
-    # The K timed steps are captured once into a HIP graph and replayed:
-    # each step is still one launch of the plan over one batch (config 4:
-    # the shard launch + the RCCL group), but the launches are issued by the
-    # GPU's command processor instead of one Python -> ctypes -> hipLaunchKernel
-    # call each (~4.1 us per launch on the host, which bounds one-block
-    # batches: DESIGN.md section 5).  The host-issued rate is reported beside
-    # it (eager_ms_per_step).  Config 4 at N > 1 captures the RCCL group too
-    # (the communicator exists: the gate step above created it); if this
-    # stack cannot capture, the steps are host-issued instead.
-    use_graph = not args.no_graph
-    graph_error = None
-    # The K timed steps are split in two: the first n_lead of them, then the
-    # rest, with a timing event between.  The per-launch kernel time is taken
-    # over the second part only: its launches are queued while the first
-    # part's run, so it holds neither the host's first issue nor a graph's
-    # launch latency (~20 us on this stack: spread over a 20-step window that
-    # is ~1 us per step).  n_lead covers >= 150 us of kernel time
-    # (at most half the steps): a graph of 19 launches measured up to ~50 us
-    # from replay to its first kernel.  Both parts are timed steps: the wall clock
-    # holds all K of them.
-    step_us = 0.0
-    if args.steps > 1:
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for i in range(10):
-            warm_step(i)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        step_us = e0.elapsed_time(e1) * 1e3 / 10
-    n_lead = 0 if args.steps < 2 else min(args.steps // 2, max(1, -(-150 // max(int(step_us), 1))))
-    if world > 1:  # (one split on every rank)
-        nl = torch.tensor([n_lead], dtype=torch.int64, device=dev if backend == "nccl" else torch.device("cpu"))
-        dist.all_reduce(nl, op=dist.ReduceOp.MAX)
-        n_lead = int(nl.item())
-    parts = [(0, n_lead), (n_lead, args.steps)] if n_lead else [(0, args.steps)]
-    # A lead of steps of >= 25 us each is issued from the host: its first
-    # launch starts within a few us where a graph replay takes ~20 us to
-    # start, and the main part's graph launch hides behind it.  Shorter steps
-    # (config 3) cannot hide a graph launch behind host issues, so their lead
-    # is a graph too.
-    lead_host = n_lead > 0 and step_us >= 25.0
-    graphs = {}
-    if use_graph:
-        try:
-            for k, (lo, hi) in enumerate(parts):
-                if lead_host and k == 0:
-                    continue
-                g_ = torch.cuda.CUDAGraph()
-                # (thread_local: other threads of the process -- e.g. the process
-                # group's watchdog -- may make CUDA calls while this thread captures)
-                with torch.cuda.graph(g_, capture_error_mode="thread_local"):
-                    cap = torch.cuda.current_stream(dev)
-                    for i in range(lo, hi):
-                        step(i, cap.cuda_stream)
-                graphs[k] = g_
-            for g_ in graphs.values():
-                g_.replay()  # (first replay uploads the graph)
-            torch.cuda.synchronize()
-        except RuntimeError as e:  # no graph on this stack: time host-issued launches instead
-            graphs, use_graph, graph_error = {}, False, str(e)[:200]
-            torch.cuda.synchronize()
-    # Outputs cleared before the settle phase (untimed): the checks after the
-    # timed region see only what the timed launches wrote.
-    for o in ([root_out] if c4 else outs):
-        o.zero_()
-    torch.cuda.synchronize()
+    def zero_outs():
+        for o in outs:
+            o.zero_()
 
-    # Power settle (untimed, before the W warm-up steps): back-to-back
-    # launches of this kernel push the package to its 1.4 kW cap; the first
-    # few hundred ride a boost-then-clamp transient 5-12 % slower than the
-    # steady state, so a short timed window (the
-    # driver's 20 steps after 5) would measure the transient.  ~settle_ms of
-    # the same step first, reported in the line; --settle-ms 0 disables it.
-    def settle_for(ms, fn=warm_step):  # untimed steps for ~ms; returns how many
-        n = 0
-        if ms > 0 and c4 and world > 1:
-            # (config 4's steps hold RCCL calls: every rank makes the same count)
-            for n in range(int(ms * 10)):
-                fn(n)
-            n += 1
-        elif ms > 0:
-            # (chunks of 20 launches; the host waits for the chunk before the
-            # last one, so the GPU always has one queued and never idles)
-            s0 = time.perf_counter()
-            prev = None
-            while (time.perf_counter() - s0) * 1e3 < ms:
-                for _ in range(20):
-                    fn(n)
-                    n += 1
-                ev = torch.cuda.Event()
-                ev.record(stream)
-                if prev is not None:
-                    prev.synchronize()
-                prev = ev
-        return n
-
-    settle = settle_for(args.settle_ms)
-    for i in range(args.warmup):
-        warm_step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(len(parts) + 1)]
-    t0 = time.perf_counter()
-    evs[0].record(stream)
-    for k, (lo, hi) in enumerate(parts):
-        if k in graphs:
-            graphs[k].replay()
-        else:
-            for i in range(lo, hi):
-                step(i)
-        evs[k + 1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    # avg per launch, on the launch stream: over the steps after the lead
-    # (all K when there is no lead)
-    window_ms = evs[0].elapsed_time(evs[-1]) / max(args.steps, 1)
-    lo_t, hi_t = parts[-1]
-    kernel_ms = evs[-2].elapsed_time(evs[-1]) / max(hi_t - lo_t, 1)
+    r = time_steps(env, args, step, warm_step, use_graph=not args.no_graph, zero=zero_outs)
+    elapsed, kernel_ms, window_ms = r["elapsed"], r["kernel_ms"], r["window_ms"]
+    use_graph, graphs, parts = r["use_graph"], r["graphs"], r["parts"]
 
     # Correctness of the timed launches themselves (outside the timed region):
-    # configs 2/3/5 -- the checksums the last timed launch on buffer 0 (PCG64
-    # host bytes) and on buffer 1 (device random bytes, copied back) wrote,
-    # against the reference's crc32c.c; config 4 -- the file-order array the
-    # last timed step gathered on rank 0, against the reference over the file
-    # that step checksummed.
+    # the checksums the last timed launch on buffer 0 (PCG64 host bytes) and
+    # on buffer 1 (device random bytes, copied back) wrote, against the
+    # reference's crc32c.c.
     timed_checks = {}
-    b_last = (args.steps - 1) % nbuf
-    if c4:
-        if rank == 0 and args.steps > 0:
-            fb = file_bytes if b_last == 0 else synthetic_bytes(32 * shard.BLOCK_BYTES, 2024 + b_last)
-            wb = want if b_last == 0 else reference_checksums(fb, file_pk, mplan.nchecksums)
-            timed_checks["timed_file_buf%d" % b_last] = bool(
-                np.array_equal(root_out.cpu().numpy().view(np.uint32)[:mplan.nchecksums], wb))
-    elif args.steps > 0:
+    if args.steps > 0:
         timed_checks["timed_buf0"] = bool(np.array_equal(outs[0].cpu().numpy().view(np.uint32)[:nout], want))
         if nbuf > 1 and args.steps > 1:
             w1 = reference_checksums(bufs[1].cpu().numpy(), pk, nout)
@@ -617,7 +884,7 @@ def main():
     if use_graph:  # the same steps issued one by one from the host, for comparison
         # (after the checks above the GPU sat idle for a while: settle again,
         # or the host-issued launches ride the power transient)
-        settle_for(args.settle_ms)
+        settle_for(env, args.settle_ms, warm_step, False)
         ne = min(args.steps, 500)
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
@@ -628,19 +895,15 @@ def main():
         torch.cuda.synchronize()
         eager_ms = e0.elapsed_time(e1) / ne
 
-    cdev = dev if backend == "nccl" else torch.device("cpu")  # where collectives run
     if world > 1:
-        tt = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(tt[0]), float(tt[1])
         ok = torch.tensor([1 if bit_exact and timed_exact else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         bit_exact = bool(ok.item())
     # Configs 2/5 (weak scaling, independent batches): RCCL gather of every
     # rank's checksum array to rank 0 after the timed region, timed on its
-    # own.  (Config 4's gather is inside every step.)
+    # own.  (Config 4's gather is inside every step: the config4 sub-object.)
     gather_ms = None
-    if world > 1 and not c4:
+    if world > 1:
         torch.cuda.synchronize()
         g0 = time.perf_counter()
         send = outs[0].to(cdev)
@@ -649,8 +912,7 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) * 1e3
 
-    # config 4: every rank's shard is part of one 128 MiB file
-    total_bytes = (32 * shard.BLOCK_BYTES if c4 else nbytes * world) * args.steps
+    total_bytes = nbytes * world * args.steps
     value = total_bytes / elapsed / GIB
     achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
 
@@ -658,7 +920,7 @@ def main():
     # against their checksums (outs[b] now holds buffer b's), timed the same
     # way (rank 0, reported beside the main line).
     verify = None
-    if rank == 0 and plan is not None:
+    if rank == 0:
         res = torch.zeros(2, dtype=torch.int32, device=dev)
         for i in range(200):
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
@@ -672,10 +934,10 @@ def main():
             plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), sptr)
         e1.record(stream)
         torch.cuda.synchronize()
-        r = res.cpu().numpy().view(np.uint32)
+        rr = res.cpu().numpy().view(np.uint32)
         verify = {"gib_s": round(nbytes * nv / (e0.elapsed_time(e1) * 1e-3) / GIB, 1),
                   "kernel_avg_us": round(e0.elapsed_time(e1) / nv * 1e3, 2),
-                  "mismatches": int(r[0]), "clean": bool(r[0] == 0 and r[1] == 0xFFFFFFFF),
+                  "mismatches": int(rr[0]), "clean": bool(rr[0] == 0 and rr[1] == 0xFFFFFFFF),
                   "launch": "host-issued"}
         vgraph = None
         if use_graph:  # also replayed from a graph like the timed exec steps
@@ -684,14 +946,13 @@ def main():
             # first keeps that wait out of the capture.
             cs = torch.cuda.Stream(device=dev)
             torch.cuda.synchronize()
-            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), cs.cuda_stream)
+            plan.verify(bufs[0].data_ptr(), outs[0].data_ptr(), res.data_ptr(), cs)
             torch.cuda.synchronize()
             try:
                 vgraph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(vgraph, stream=cs, capture_error_mode="thread_local"):
                     for i in range(nv):
-                        plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(),
-                                    cs.cuda_stream)
+                        plan.verify(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), res.data_ptr(), cs)
                 vgraph.replay()
             except RuntimeError:
                 vgraph = None
@@ -701,20 +962,20 @@ def main():
             vgraph.replay()
             e1.record(stream)
             torch.cuda.synchronize()
-            r = res.cpu().numpy().view(np.uint32)
+            rr = res.cpu().numpy().view(np.uint32)
             verify["graph_kernel_avg_us"] = round(e0.elapsed_time(e1) / nv * 1e3, 2)
-            verify["graph_clean"] = bool(r[0] == 0 and r[1] == 0xFFFFFFFF)
+            verify["graph_clean"] = bool(rr[0] == 0 and rr[1] == 0xFFFFFFFF)
             verify["clean"] = verify["clean"] and verify["graph_clean"]
             # The same nv-launch graph form for exec, right after (into the
             # scratch outputs): what the verify graph is read against, and a
             # steady-state exec figure beside the timed window's.
             try:
-                plan.exec(bufs[0].data_ptr(), scratch_outs[0].data_ptr(), cs.cuda_stream)
+                plan.exec(bufs[0].data_ptr(), scratch_outs[0].data_ptr(), cs)
                 torch.cuda.synchronize()
                 egraph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(egraph, stream=cs, capture_error_mode="thread_local"):
                     for i in range(nv):
-                        plan.exec(bufs[i % nbuf].data_ptr(), scratch_outs[i % nbuf].data_ptr(), cs.cuda_stream)
+                        plan.exec(bufs[i % nbuf].data_ptr(), scratch_outs[i % nbuf].data_ptr(), cs)
                 egraph.replay()
                 torch.cuda.synchronize()
                 e0.record(stream)
@@ -732,7 +993,7 @@ def main():
     # prices the kernel against what this chip actually streams, beside the
     # 8 TB/s datasheet peak.  Rank 0, N = 1 only.
     read_probe = None
-    if rank == 0 and world == 1 and nbuf > 1 and not c4:
+    if rank == 0 and world == 1 and nbuf > 1:
         probe_out = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
         L = hdfs.debug_lib()  # the read probe lives in the debug library, not the product
 
@@ -761,7 +1022,7 @@ def main():
     # line, which stays one stream so that one step = one launch): the next
     # launch's workgroups start on the CUs the previous one has released.
     two_streams = None
-    if args.two_streams and rank == 0 and world == 1 and nbuf > 1 and not c4:
+    if args.two_streams and rank == 0 and world == 1 and nbuf > 1:
         ss = [torch.cuda.Stream(device=dev) for _ in range(2)]
 
         def two(n):
@@ -771,7 +1032,7 @@ def main():
             for s in ss:
                 s.wait_event(e0)
             for i in range(n):
-                plan.exec(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), ss[i % 2].cuda_stream)
+                plan.exec(bufs[i % nbuf].data_ptr(), outs[i % nbuf].data_ptr(), ss[i % 2])
             for s in ss:
                 ej = torch.cuda.Event()
                 ej.record(s)
@@ -791,7 +1052,7 @@ def main():
     # link; the node-level rate is all ranks' bytes / the slowest rank's time.
     # Beside it, the link's ceiling: a plain pinned H2D copy of the same bytes.
     host = h2d = host_multi = host_latency = host_sweep = None
-    if not args.no_host and args.config != "c4":
+    if not args.no_host:
         pinned = torch.from_numpy(payload0).pin_memory()
         hp = pinned.numpy()
         hout = np.zeros(max(nout, 1), np.uint32)  # caller-owned output, as hadooprpc.c's packet buffer
@@ -831,8 +1092,8 @@ def main():
         # node that shows eight; at N > 1 every rank's own link is measured
         # above instead).
         if world == 1 and args.host_multi_devices > 0:
-            ndev = min(args.host_multi_devices, torch.cuda.device_count())
-            devs = [(local_rank + k) % torch.cuda.device_count() for k in range(ndev)]
+            ndv = min(args.host_multi_devices, torch.cuda.device_count())
+            devs = [(local_rank + k) % torch.cuda.device_count() for k in range(ndv)]
             m = hdfs.Multi(devs)
             try:
                 mout = m.batch_host(hp, pk, group_packets=64)
@@ -841,7 +1102,7 @@ def main():
                 for _ in range(reps):
                     m.batch_host(hp, pk, group_packets=64)
                 host_multi = {"gib_s": round(nbytes * reps / (time.perf_counter() - h0) / GIB, 2),
-                              "devices": ndev, "bit_exact": exact_multi, "entry": "crc32c_multi_batch_host"}
+                              "devices": ndv, "bit_exact": exact_multi, "entry": "crc32c_multi_batch_host"}
                 timed_checks["host_resident_multi"] = exact_multi
                 bit_exact = bit_exact and exact_multi
             finally:
@@ -854,17 +1115,30 @@ def main():
             host_latency = host_block_latency(hdfs, ctx, pk, payload0, want, qthreads, not args.no_cpu)
             timed_checks["host_latency"] = host_latency["bit_exact"]
             if args.host_sweep:
+                from hdfs_crc32c_amd.workloads import uniform_packets
+
                 host_sweep = []
                 for npk in (1, 4, 16, 64, 256, 1024, 4096):
                     spk = uniform_packets(npk)
                     sp = synthetic_bytes(npk * 65536, 77 + npk)
                     sw = reference_checksums(sp, spk, hdfs.total_checksums(spk))
-                    r = host_block_latency(hdfs, ctx, spk, sp, sw, qthreads, not args.no_cpu)
-                    host_sweep.append(r)
-                    timed_checks["host_sweep_%d" % npk] = r["bit_exact"]
-                cross = [r["bytes"] for r in host_sweep if "reference_1t_us" in r and r["gpu_pinned_us"] < r["reference_1t_us"]]
+                    rr = host_block_latency(hdfs, ctx, spk, sp, sw, qthreads, not args.no_cpu)
+                    host_sweep.append(rr)
+                    timed_checks["host_sweep_%d" % npk] = rr["bit_exact"]
+                cross = [x["bytes"] for x in host_sweep
+                         if "reference_1t_us" in x and x["gpu_pinned_us"] < x["reference_1t_us"]]
                 host_sweep = {"sizes": host_sweep,
                               "gpu_pinned_beats_reference_1t_from_bytes": min(cross) if cross else None}
+
+    # The other two shapes of the 1/2/4/8-GPU curve, on the default line at
+    # every N (the driver only runs the default command): config 4's file
+    # step with its in-step RCCL gather, and config 2 split over the ranks.
+    config4 = strong = None
+    if args.config == "c2" and args.scaling == "weak":
+        if not args.no_config4:
+            config4 = run_config4(hdfs, args, env)
+        if not args.no_strong:
+            strong = run_strong(hdfs, args, env, ctx)
 
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"), args.config)
@@ -874,24 +1148,21 @@ def main():
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_commit = pmc.get("commit")
         # the CPU baseline is an N = 1 figure (timed on rank 0's host cores)
-        cpu = None if args.no_cpu or world > 1 else (
-            cpu_baseline(file_pk, file_bytes, args.cpu_seconds) if c4 else cpu_baseline(pk, payload0, args.cpu_seconds))
+        cpu = None if args.no_cpu or world > 1 else cpu_baseline(pk, payload0, args.cpu_seconds)
         line = {
             "metric": baseline_metric(),
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "settle_launches": settle,
+            "warmup": args.warmup, "settle_launches": r["settle"],
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True, "scaling": "strong" if args.config == "c4" or (args.scaling == "strong" and world > 1) else "weak",
+            "higher_is_better": True, "scaling": "strong" if (args.scaling == "strong" and world > 1) else "weak",
             "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (PCG64 host bytes + device random bytes, %d rotating %d MiB buffers per rank)"
                     % (nbuf, extent >> 20),
             "config": {"workload": workload, "config": args.config, "packets_per_rank": int(pk.size),
                        "packet_bytes": int(pk["len"][0]), "bytes_per_checksum": sorted(set(int(x) for x in pk["bpc"])),
                        "payload_bytes_per_rank": nbytes, "checksums_per_rank": nout,
-                       "parallelism": ("dp%d (block shards, crc32c_multi_plan: RCCL send/recv gather of the "
-                                       "checksums to rank 0 inside every step)" % world) if c4 else
-                                      ("dp%d (independent shards, %s gather of checksums after timing)"
-                                       % (world, "RCCL" if backend == "nccl" else backend + " rehearsal"))},
+                       "parallelism": "dp%d (independent shards, %s gather of checksums after timing)"
+                                      % (world, "RCCL" if backend == "nccl" else backend + " rehearsal")},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "traffic_source": None if traffic is None else
@@ -899,10 +1170,10 @@ def main():
                          % traffic_commit,
                          "kernel": KERNEL_NAME, "kernel_avg_us": round(kernel_ms * 1e3, 2),
                          "kernel_timing": "HIP events on the launch stream around timed steps %d..%d (the first %d "
-                                          "timed steps, launched first, cover the %s latency)"
-                                          % (parts[-1][0] + 1, parts[-1][1], n_lead,
+                                          "timed steps, launched first, cover the %s latency); max over ranks"
+                                          % (parts[-1][0] + 1, parts[-1][1], r["n_lead"],
                                              "graph launch" if use_graph else "first host issue"),
-                         "lead_steps": "host-issued" if (lead_host or not use_graph) else "graph",
+                         "lead_steps": "host-issued" if (r["lead_host"] or not use_graph) else "graph",
                          "window_avg_us_all_steps": round(window_ms * 1e3, 2),
                          "algorithmic_bytes_per_launch": nbytes},
             "cpu_baseline": cpu,
@@ -918,20 +1189,14 @@ def main():
             "two_streams": two_streams,
             "box_read_probe": read_probe,
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
-            "launch": ("%s, replayed" % " + ".join(
-                ("%d host-issued" if k not in graphs else "hip graph of %d") % (hi - lo)
-                for k, (lo, hi) in enumerate(parts))) if use_graph else
-                      ("host-issued, one launch per step" +
-                       ("" if graph_error is None else " (graph capture failed: %s)" % graph_error)),
+            "launch": launch_text(r),
             "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 5),
+            "config4": config4,
+            "strong_scaling": strong,
         }
         print(json.dumps(line), flush=True)
-    if c4:
-        mplan.close()
-        multi.close()
-    else:
-        plan.close()
-        ctx.close()
+    plan.close()
+    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

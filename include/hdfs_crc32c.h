@@ -208,7 +208,8 @@ int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_
  * "compute + compare, emit a mismatch bitmap"): dev_bad_bits holds
  * ceil(crc32c_plan_nchecksums(plan) / 32) device u32s; bit i % 32 of word
  * i / 32 is set for every mismatching checksum i and cleared for every
- * other one (the library zeroes the bitmap on `stream` before the launch).
+ * other one (the launch itself zeroes the bitmap before any bit is set: no
+ * separate memset on `stream`).
  * A reader that must report every corrupt chunk of a replica, not only the
  * first (the ChecksumException of hadooprpc.c:497-584's caller), takes it
  * from here; NULL = crc32c_plan_verify. */
@@ -274,6 +275,24 @@ int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, ui
  * crc32c_block_checksums is submit + wait.  Thread-safe.  Destroy the queue
  * (it launches what is queued and waits) before its plan.
  * crc32c_blocks_stats: launches (flushes) made and blocks they carried.
+ *
+ * crc32c_blocks_create_resident: the same queue calls served by a RESIDENT
+ * kernel (opt-in; replaces fuse.c:336's one-checksum-pass-per-call for many
+ * concurrent writers, fuse.c:1771): one launch stays on the GPU and takes
+ * each block as it is submitted from a ring in pinned host memory, so there
+ * is no launch (nor launch boundary, table staging, tail) per block; a
+ * waiter polls a completion word the kernel writes into host memory.
+ * CU policy: while it runs the kernel holds one 16-wave workgroup with the
+ * whole LDS on EVERY CU -- other kernels on the device (plan execs, other
+ * queues) wait for CUs until it exits.  It exits idle_us after the last
+ * block completes (0 = 2000 us), 50 ms after it stops making progress, or
+ * at destroy; the next submit relaunches it.  Plans of whole power-of-two
+ * tiles only (bpc 512 << k, chunks not split by a packet end: -EINVAL
+ * otherwise); payloads 16-byte aligned (submit returns -EINVAL otherwise).
+ * crc32c_block_flush does nothing (every block is taken at once);
+ * crc32c_blocks_stats reports the kernel's launches and the blocks
+ * submitted; destroy lets every submitted block complete, then stops the
+ * kernel.  A wait gives up with -ETIMEDOUT after 5 s without its block.
  * ------------------------------------------------------------------------- */
 int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
                             size_t nblocks, void *stream);
@@ -286,6 +305,7 @@ int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket);
 int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out);
 int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blocks);
 int crc32c_blocks_destroy(crc32c_blocks *q);
+int crc32c_blocks_create_resident(crc32c_plan *plan, uint32_t idle_us, crc32c_blocks **out);
 
 /* One-shot device batch: builds a plan, runs it on `stream` and waits for it. */
 int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,

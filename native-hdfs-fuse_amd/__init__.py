@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import ctypes
 import errno
+import numbers
 import os
 import subprocess
 
@@ -223,6 +224,7 @@ def _bind(L):
         "crc32c_block_checksums": (i32, [vp, vp, vp]),
         "crc32c_blocks_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_blocks_destroy": (i32, [vp]),
+        "crc32c_blocks_create_resident": (i32, [vp, u32, pp]),
         "crc32c_debug_blocks_fail_flushes": (i32, [vp, u32]),
         "crc32c_verify_frames_host": (i32, [vp, vp, sz, u32, u64, u32, ctypes.POINTER(FramesResult)]),
     }
@@ -240,6 +242,20 @@ def _check(rc: int, what: str) -> None:
 
 def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def _stream_handle(stream, keep: dict) -> int:
+    """A raw hipStream_t handle from a handle (int, numpy integer, None = the
+    default stream) or a stream object (``.cuda_stream``, e.g. a
+    ``torch.cuda.Stream``); a stream object is kept alive in ``keep`` (the
+    library touches a plan's launch streams until the plan is destroyed)."""
+    if stream is None:
+        return 0
+    if isinstance(stream, numbers.Integral):
+        return int(stream)
+    h = int(stream.cuda_stream)
+    keep.setdefault(h, stream)
+    return h
 
 
 def as_packets(pkts) -> np.ndarray:
@@ -395,11 +411,7 @@ class Plan:
         self.payload_bytes = int(lib().crc32c_plan_payload_bytes(h))
 
     def _stream(self, stream) -> int:
-        if isinstance(stream, int):
-            return stream
-        h = int(stream.cuda_stream)
-        self._streams.setdefault(h, stream)
-        return h
+        return _stream_handle(stream, self._streams)
 
     def exec(self, dev_payload: int, dev_out: int, stream=0) -> None:
         stream = self._stream(stream)
@@ -430,8 +442,11 @@ class Plan:
         _check(lib().crc32c_plan_exec_blocks(self.handle, pays, outs, n, ctypes.c_void_p(stream)),
                "crc32c_plan_exec_blocks")
 
-    def blocks(self, max_blocks: int = 16, window_us: int = 20) -> "Blocks":
-        return Blocks(self, max_blocks, window_us)
+    def blocks(self, max_blocks: int = 16, window_us: int = 20, resident: bool = False,
+               idle_us: int = 0) -> "Blocks":
+        """The block queue (crc32c_blocks_create), or its resident-kernel mode
+        (crc32c_blocks_create_resident) with ``resident=True``."""
+        return Blocks(self, max_blocks, window_us, resident=resident, idle_us=idle_us)
 
     def exec_variant(self, dev_payload: int, dev_out: int, variant: int, dev_stamps: int = 0, stream: int = 0) -> None:
         """Diagnostic (debug library): run an explicit kernel variant (5/6/36 write per-wave timestamps)."""
@@ -456,9 +471,15 @@ class Plan:
 class Blocks:
     """crc32c_blocks: block writes from several threads coalesced into one launch (group commit)."""
 
-    def __init__(self, plan: Plan, max_blocks: int = 16, window_us: int = 20):
+    def __init__(self, plan: Plan, max_blocks: int = 16, window_us: int = 20, resident: bool = False,
+                 idle_us: int = 0):
         h = ctypes.c_void_p()
-        _check(lib().crc32c_blocks_create(plan.handle, max_blocks, window_us, ctypes.byref(h)), "crc32c_blocks_create")
+        if resident:
+            _check(lib().crc32c_blocks_create_resident(plan.handle, idle_us, ctypes.byref(h)),
+                   "crc32c_blocks_create_resident")
+        else:
+            _check(lib().crc32c_blocks_create(plan.handle, max_blocks, window_us, ctypes.byref(h)),
+                   "crc32c_blocks_create")
         self.plan = plan  # the plan outlives the queue
         self.handle = h
 
@@ -562,15 +583,20 @@ class MultiPlan:
                                               ctypes.byref(h)), "crc32c_multi_plan_create")
         self.multi = multi
         self.handle = h
+        self._streams = {}  # stream objects launched on, kept alive until close()
         self.nchecksums = int(lib().crc32c_multi_plan_nchecksums(h))
 
     def shard_bytes(self, rank: int) -> int:
         return int(lib().crc32c_multi_plan_shard_bytes(self.handle, rank))
 
     def exec(self, dev_shards, root_out: int, streams=None) -> None:
+        """``streams``: one per local device, handles or stream objects (kept
+        alive until close(): the next exec on another stream records an event
+        on this one)."""
         n = len(dev_shards)
         shards = (ctypes.c_void_p * n)(*[ctypes.c_void_p(x) for x in dev_shards])
-        ss = None if streams is None else (ctypes.c_void_p * n)(*[ctypes.c_void_p(x) for x in streams])
+        ss = None if streams is None else (ctypes.c_void_p * n)(
+            *[ctypes.c_void_p(_stream_handle(x, self._streams)) for x in streams])
         _check(lib().crc32c_multi_plan_exec(self.handle, shards, ctypes.c_void_p(root_out), ss),
                "crc32c_multi_plan_exec")
 
@@ -578,6 +604,7 @@ class MultiPlan:
         if self.handle:
             lib().crc32c_multi_plan_destroy(self.handle)
             self.handle = None
+        self._streams = {}
 
     def __del__(self):
         try:

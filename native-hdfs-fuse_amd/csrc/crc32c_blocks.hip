@@ -26,6 +26,11 @@
 // after a flush queued on it (a futex hand-off each), and a batch took ~40
 // us to fill against ~15 us of GPU time per flush (HDFS_CRC32C_QUEUE_TRACE,
 // DESIGN.md section 5).
+//
+// Resident mode (crc32c_blocks_create_resident, opt-in): the same calls are
+// served by a resident kernel instead (crc32c_resident.hip /
+// resident_engine.h) -- no launch per flush, no worker thread; the kernel
+// holds every CU while it runs and exits idle_us after the last block.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -60,6 +65,7 @@ struct alignas(64) Slot {
 
 struct crc32c_blocks {
     crc32c_plan *plan = nullptr;
+    ResidentEngine *res = nullptr;  // resident mode: every call goes to it
     int device = 0;
     uint32_t max_blocks = 16;
     std::chrono::microseconds window{20};
@@ -76,7 +82,9 @@ struct crc32c_blocks {
     std::atomic<int> sleepers{0};  // waiters asleep on cv
     // Failed flushes (rare): each one's ticket range and error, so a wait
     // returns the error of its own flush only -- tickets before and after it
-    // succeed as their flushes do.
+    // succeed as their flushes do.  Flushes complete in ticket order, so the
+    // ranges are sorted; consecutive failed flushes with the same error are
+    // merged into one range (a device that keeps failing keeps one entry).
     std::mutex err_mu;
     std::vector<std::pair<std::pair<uint64_t, uint64_t>, int>> failed;
     std::atomic<int> nfailed{0};
@@ -125,17 +133,23 @@ uint64_t tickets_out(const crc32c_blocks *q, std::memory_order o = std::memory_o
 
 void record_failure(crc32c_blocks *q, uint64_t lo, uint64_t hi, int err) {
     std::lock_guard<std::mutex> lock(q->err_mu);
-    q->failed.push_back({{lo, hi}, err});
+    if (!q->failed.empty() && q->failed.back().first.second == lo && q->failed.back().second == err)
+        q->failed.back().first.second = hi;
+    else
+        q->failed.push_back({{lo, hi}, err});
     q->nfailed.store(int(q->failed.size()), std::memory_order_release);
 }
 
-// The error of the flush ticket t went out in (0 when it succeeded).
+// The error of the flush ticket t went out in (0 when it succeeded): a
+// binary search over the sorted failed ranges.
 int ticket_error(crc32c_blocks *q, uint64_t t) {
     if (!q->nfailed.load(std::memory_order_acquire)) return 0;
     std::lock_guard<std::mutex> lock(q->err_mu);
-    for (const auto &f : q->failed)
-        if (t >= f.first.first && t < f.first.second) return f.second;
-    return 0;
+    auto it = std::upper_bound(q->failed.begin(), q->failed.end(), t,
+                               [](uint64_t v, const auto &f) { return v < f.first.first; });
+    if (it == q->failed.begin()) return 0;
+    --it;
+    return t < it->first.second ? it->second : 0;
 }
 
 std::chrono::microseconds env_us(const char *name, int dflt) {
@@ -368,8 +382,20 @@ int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window
     return 0;
 }
 
+int crc32c_blocks_create_resident(crc32c_plan *plan, uint32_t idle_us, crc32c_blocks **out) {
+    if (!plan || !out) return fail(-EINVAL, "plan/out == NULL");
+    *out = nullptr;
+    std::unique_ptr<crc32c_blocks> q(new crc32c_blocks);
+    q->plan = plan;
+    q->device = plan->ctx->device;
+    if (int rc = resident_create(plan, idle_us, resident_launch_product, false, &q->res)) return rc;
+    *out = q.release();
+    return 0;
+}
+
 int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
     if (!q || !dev_out) return fail(-EINVAL, "queue/out == NULL");
+    if (q->res) return resident_submit(q->res, dev_payload, dev_out, ticket);
     // the stop check and the ticket are one atomic step (kStopBit)
     uint64_t t = q->next_ticket.load(std::memory_order_relaxed);
     do {
@@ -388,6 +414,7 @@ int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev
 
 int crc32c_block_flush(crc32c_blocks *q) {
     if (!q) return fail(-EINVAL, "queue == NULL");
+    if (q->res) return 0;  // (the resident kernel takes every block as it is submitted)
     const uint64_t hi = tickets_out(q);
     uint64_t cur = q->flush_upto.load(std::memory_order_relaxed);
     while (cur < hi && !q->flush_upto.compare_exchange_weak(cur, hi, std::memory_order_acq_rel)) {
@@ -398,6 +425,7 @@ int crc32c_block_flush(crc32c_blocks *q) {
 
 int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket) {
     if (!q) return fail(-EINVAL, "queue == NULL");
+    if (q->res) return resident_wait(q->res, ticket);
     if (ticket < q->done_upto.load(std::memory_order_acquire)) return ticket_error(q, ticket);
     if (ticket >= tickets_out(q))
         return fail(-EINVAL, "ticket %llu was never handed out", (unsigned long long)ticket);
@@ -427,6 +455,11 @@ int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *
 
 int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blocks) {
     if (!q) return fail(-EINVAL, "queue == NULL");
+    if (q->res) {  // (launches of the resident kernel; blocks handed to it)
+        if (flushes) *flushes = resident_launches(q->res);
+        if (blocks) *blocks = resident_tickets(q->res);
+        return 0;
+    }
     if (flushes) *flushes = q->flushes.load(std::memory_order_relaxed);
     if (blocks) *blocks = q->blocks.load(std::memory_order_relaxed);
     return 0;
@@ -434,12 +467,17 @@ int crc32c_blocks_stats(const crc32c_blocks *q, uint64_t *flushes, uint64_t *blo
 
 int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n) {
     if (!q) return fail(-EINVAL, "queue == NULL");
+    if (q->res) return fail(-EINVAL, "a resident queue has no flushes");
     q->inject_fail.store(n, std::memory_order_relaxed);
     return 0;
 }
 
 int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns) {
     if (!q || !ns) return fail(-EINVAL, "queue/ns == NULL");
+    if (q->res) {  // (no worker thread)
+        *ns = 0;
+        return 0;
+    }
     clockid_t cid;
     timespec ts{};
     if (pthread_getcpuclockid(q->worker.native_handle(), &cid) != 0 || clock_gettime(cid, &ts) != 0)
@@ -450,6 +488,11 @@ int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns) {
 
 int crc32c_blocks_destroy(crc32c_blocks *q) {
     if (!q) return 0;
+    if (q->res) {  // (every queued block completes, then the kernel stops)
+        const int rc = resident_destroy(q->res, true);
+        delete q;
+        return rc;
+    }
     // (no ticket is handed out from here; the worker launches what is
     // queued, completes everything, returns)
     q->next_ticket.fetch_or(kStopBit, std::memory_order_seq_cst);

@@ -296,28 +296,15 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
     return (flags & 1u) ? __builtin_bswap32(crc) : crc;  // htonl on the wire, hadooprpc.c:71-75
 }
 
-// A mismatch (VERIFY): bump the workgroup's LDS count and lower its LDS
-// first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish), and
-// set the checksum's bit in the caller's bitmap when there is one (rare path:
-// a clean launch executes none of this).
-__device__ __forceinline__ void mismatch(const KParams &p, uint32_t *vacc, uint32_t idx) {
-    atomicAdd(vacc, 1u);
-    atomicMin(vacc + 1, idx);
-    if (p.bad_bits) atomicOr(p.bad_bits + (idx >> 5), 1u << (idx & 31u));
-}
+// The workgroup's verification state in LDS (after the tables and the tile
+// counter): vacc[0] mismatches, vacc[1] lowest bad index, vacc[2] entries of
+// the bad-index list (vacc + kVaccList, kBadList of them), vacc[3] flags.
+constexpr uint32_t kBadList = 256;
+constexpr uint32_t kVaccList = 7;
+constexpr uint32_t kVaccTimedOut = 1u;  // vacc[3]: a key wait of this workgroup gave up
+constexpr uint32_t kVerifyKeyPolls = 1u << 17;
+constexpr uint32_t kVerifyOverlapBit = 0x80000000u;
 
-// Checksum `idx` of the batch: stored, or (VERIFY) compared with `expect`.
-template <bool VERIFY>
-__device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t expect) {
-    const uint32_t v = out_order(crc, p.flags);
-    if (VERIFY) {
-        if (v != expect) mismatch(p, vacc, idx);
-    } else {
-        p.out[idx] = v;
-    }
-}
-
-// ---- launch-wide verification result (kernel_abi.h slots) ----------------
 // Waits until every vector-memory operation of the wave has completed; for a
 // returning device-scope atomic that means it has been performed.
 __device__ __forceinline__ void wait_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -333,57 +320,148 @@ __device__ __forceinline__ uint64_t launch_key() {
     return ptr + llvm_amdgcn_dispatch_id() * 0x9E3779B97F4A7C15ull;
 }
 
-// Start of a verification launch, one lane of workgroup 0 (dispatched
-// first, so a workgroup waiting for the key below never waits for a
-// workgroup that has not been placed): the result becomes {0, ~0} (returning
-// device-scope atomics, performed at the memory side once the wait returns),
-// then the slot takes this launch's key.  No host-side reset of the result.
-__device__ __forceinline__ void verify_init(const KParams &p) {
-    uint32_t a = __hip_atomic_exchange(p.result, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t b = __hip_atomic_exchange(p.result + 1, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("" : "+v"(a), "+v"(b));  // (returning forms: the wait covers them)
-    wait_vmem();
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p.sched + kEpochWord),
-                       static_cast<unsigned long long>(launch_key()), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Waits (bounded: kVerifyKeyPolls polls, ~0.1-0.3 s) until the slot holds
+// this launch's key, i.e. workgroup 0 has initialised the result and cleared
+// the bitmap for this launch (polled with a returning atomic, performed where
+// the key was written; acquire: the clear is visible after it).  False when
+// it gave up.
+__device__ __forceinline__ bool wait_launch_key(const KParams &p) {
+    const unsigned long long key = launch_key();
+    unsigned long long *ep = reinterpret_cast<unsigned long long *>(p.sched + kEpochWord);
+    for (uint32_t polls = 0;; ++polls) {
+        if (__hip_atomic_fetch_add(ep, 0ull, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == key) return true;
+        if (polls == kVerifyKeyPolls) return false;
+        __builtin_amdgcn_s_sleep(8);
+    }
 }
 
-// End of a verification launch, thread 0 of every workgroup.  A clean
-// workgroup does nothing; one with mismatches waits until workgroup 0 has
-// initialised the result for this launch (the slot holds this launch's key:
-// polled with a returning atomic, performed where the key was written), then
-// adds its count and lowers the first bad index.  The clean launch's tail is
-// therefore empty: round 2's sharded tickets (every workgroup one returning
-// atomic, the last of each shard a second, the last of those the publish)
-// cost a small batch ~1.4 us (config 3: 5.05 vs 3.58 us).
+// A mismatch (VERIFY): bump the workgroup's LDS count and lower its LDS
+// first-bad index (vacc[0], vacc[1]; merged grid-wide by verify_finish), and,
+// when the caller passed a bitmap, note the index for it: the bitmap is
+// cleared by workgroup 0 of this same launch, so a bit may only be set after
+// this launch's key is published -- the first kBadList indices of the
+// workgroup wait in LDS for verify_finish, later ones wait for the key here
+// (rare path: a clean launch executes none of this).
+__device__ __forceinline__ void mismatch(const KParams &p, uint32_t *vacc, uint32_t idx) {
+    atomicAdd(vacc, 1u);
+    atomicMin(vacc + 1, idx);
+    if (!p.bad_bits) return;
+    const uint32_t slot = atomicAdd(vacc + 2, 1u);
+    if (slot < kBadList) {
+        vacc[kVaccList + slot] = idx;
+    } else {
+        if (!wait_launch_key(p)) atomicOr(vacc + 3, kVaccTimedOut);
+        atomicOr(p.bad_bits + (idx >> 5), 1u << (idx & 31u));
+    }
+}
+
+// Checksum `idx` of the batch: stored, or (VERIFY) compared with `expect`.
+template <bool VERIFY>
+__device__ __forceinline__ void emit(const KParams &p, uint32_t *vacc, uint32_t idx, uint32_t crc, uint32_t expect) {
+    const uint32_t v = out_order(crc, p.flags);
+    if (VERIFY) {
+        if (v != expect) mismatch(p, vacc, idx);
+    } else {
+        p.out[idx] = v;
+    }
+}
+
+// ---- launch-wide verification result (kernel_abi.h slots) ----------------
+// Start of a verification launch, the last wave of workgroup 0 (dispatched
+// first, so a workgroup waiting for the key never waits for a workgroup that
+// has not been placed): the caller's bitmap, when there is one, is cleared
+// with vector stores (1 KiB per store instruction; config 2's 64 KiB is 64 of
+// them), the result becomes {0, ~0} (returning device-scope atomics), and
+// once both are performed the slot takes this launch's key (a release
+// store).  No host-side memset of the bitmap or reset of the result precedes
+// a launch (round 4 cleared the bitmap with a hipMemsetD32Async before every
+// launch: 8.0 against 4.2 us per config-3 verify).
+__device__ __forceinline__ void verify_init(const KParams &p, int lane) {
+    if (p.bad_bits) {
+        uint32_t *b = p.bad_bits;
+        const uint32_t n = p.bad_words;
+        const uint32_t head = min(n, uint32_t(((16u - (uintptr_t(b) & 15u)) & 15u) >> 2));
+        if (uint32_t(lane) < head) b[lane] = 0;
+        uint4 *v = reinterpret_cast<uint4 *>(b + head);
+        const uint32_t nv = (n - head) >> 2;
+        for (uint32_t i = uint32_t(lane); i < nv; i += 64u) v[i] = make_uint4(0, 0, 0, 0);
+        const uint32_t tail = (n - head) & 3u;
+        if (uint32_t(lane) < tail) b[head + 4u * nv + uint32_t(lane)] = 0;
+    }
+    if (lane == 0) {
+        uint32_t a = __hip_atomic_exchange(p.result, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t c = __hip_atomic_exchange(p.result + 1, 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" : "+v"(a), "+v"(c));  // (returning forms: the wait covers them)
+    }
+    wait_vmem();  // (the whole wave's stores and atomics)
+    if (lane == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(p.sched + kEpochWord),
+                           static_cast<unsigned long long>(launch_key()), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The workgroup's listed bad indices into the caller's bitmap (every thread).
+template <uint32_t THREADS>
+__device__ __forceinline__ void set_listed_bits(const KParams &p, const uint32_t *vacc) {
+    if (!p.bad_bits) return;
+    const uint32_t n = min(vacc[2], kBadList);
+    for (uint32_t i = threadIdx.x; i < n; i += THREADS) {
+        const uint32_t idx = vacc[kVaccList + i];
+        atomicOr(p.bad_bits + (idx >> 5), 1u << (idx & 31u));
+    }
+}
+
+// Thread 0: this workgroup's count and lowest bad index into the result,
+// with the overlap bit when its key wait gave up.
+__device__ __forceinline__ void add_to_result(const KParams &p, const uint32_t *vacc, bool overlap) {
+    if (overlap) {
+        uint32_t o = __hip_atomic_fetch_or(p.result, kVerifyOverlapBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" : "+v"(o));
+    }
+    uint32_t a = __hip_atomic_fetch_add(p.result, vacc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t b = __hip_atomic_fetch_min(p.result + 1, vacc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" : "+v"(a), "+v"(b));
+    wait_vmem();
+}
+
+// End of a verification launch, every thread of every workgroup, after a
+// workgroup barrier.  A clean workgroup does nothing; one with mismatches
+// waits until workgroup 0 has initialised the result and cleared the bitmap
+// for this launch (the slot holds this launch's key), then adds its count,
+// lowers the first bad index and sets its listed bits.  The clean launch's
+// tail is therefore empty: round 2's sharded tickets (every workgroup one
+// returning atomic, the last of each shard a second, the last of those the
+// publish) cost a small batch ~1.4 us (config 3: 5.05 vs 3.58 us, DESIGN.md
+// section 5).
 //
 // The wait is bounded (kVerifyKeyPolls polls, ~0.1-0.3 s): if another verify
 // launch of the same plan overlaps this one (a graph replay beside a direct
 // verify on another stream: the library cannot order those) its key may
 // replace this launch's before this workgroup sees it.  The workgroup then
-// gives up waiting, adds its count anyway and sets bit 31 of result[0]
-// (kVerifyOverlapBit): "indeterminate -- overlapping verify launches of one
-// plan".  The kernel always finishes.
-constexpr uint32_t kVerifyKeyPolls = 1u << 17;
-constexpr uint32_t kVerifyOverlapBit = 0x80000000u;
-
-__device__ __forceinline__ void verify_finish(const KParams &p, const uint32_t *vacc) {
-    const uint32_t cnt = vacc[0];
-    if (!cnt) return;
-    const unsigned long long key = launch_key();
-    unsigned long long *ep = reinterpret_cast<unsigned long long *>(p.sched + kEpochWord);
-    uint32_t polls = 0;
-    while (__hip_atomic_fetch_add(ep, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key) {
-        if (++polls == kVerifyKeyPolls) {
-            uint32_t o = __hip_atomic_fetch_or(p.result, kVerifyOverlapBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("" : "+v"(o));
-            break;
-        }
-        __builtin_amdgcn_s_sleep(8);
+// gives up waiting, adds its count and bits anyway and sets bit 31 of
+// result[0] (kVerifyOverlapBit): "indeterminate -- overlapping verify
+// launches of one plan".  A wait can also give up because workgroup 0 of
+// this launch is merely late; its initialisation would then erase what this
+// workgroup added, so the workgroup waits a second time, and if the key does
+// appear it adds its count, the overlap bit and its bits again.  The kernel
+// always finishes.
+template <uint32_t THREADS>
+__device__ __forceinline__ void verify_finish(const KParams &p, uint32_t *vacc) {
+    if (!vacc[0]) return;  // (uniform: read after the barrier)
+    if (threadIdx.x == 0) {
+        if (!wait_launch_key(p)) vacc[3] |= kVaccTimedOut;
+        add_to_result(p, vacc, (vacc[3] & kVaccTimedOut) != 0);
     }
-    uint32_t a = __hip_atomic_fetch_add(p.result, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t b = __hip_atomic_fetch_min(p.result + 1, vacc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("" : "+v"(a), "+v"(b));
-    wait_vmem();
+    __syncthreads();
+    set_listed_bits<THREADS>(p, vacc);
+    if (!(vacc[3] & kVaccTimedOut)) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const bool late_init = wait_launch_key(p);
+        if (late_init) add_to_result(p, vacc, true);
+        vacc[3] = late_init ? 2u : 0u;
+    }
+    __syncthreads();
+    if (vacc[3] == 2u) set_listed_bits<THREADS>(p, vacc);
 }
 
 // ---- tiles: one wave, 16 blocks ------------------------------------------
@@ -756,8 +834,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr uint32_t kWaves = THREADS / 64;
     constexpr uint32_t kStage = !S4 ? kStageBytes : C ? kS4CStageBytes : kS4StageBytes;
     // One LDS array: the tables, then the workgroup's tile counter and (VERIFY)
-    // its mismatch count and first bad index.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 16];
+    // its mismatch count, first bad index and bad-index list (vacc).
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 32 + (VERIFY ? 4 * kBadList : 0)];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
     const uint8_t *table = !S4 ? p.table : C ? p.table_s4 + hdfs_crc::kS4COff : p.table_s4;
@@ -785,6 +863,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         if (VERIFY) {
             vacc[0] = 0;
             vacc[1] = 0xffffffffu;
+            vacc[2] = 0;
+            vacc[3] = 0;
         }
     }
     uint32_t t = tbeg + wv;
@@ -825,7 +905,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
     // (the last wave: idle in small batches; in large ones the workgroup's
     // tile pool absorbs its late start)
-    if (VERIFY && blockIdx.x == 0 && wv == kWaves - 1 && lane == 0) verify_init(p);
+    if (VERIFY && blockIdx.x == 0 && wv == kWaves - 1) verify_init(p, lane);
 
     // Gen pairs, seg pairs and constant runs, dealt over every wave of the
     // grid after the tiles.  (Before the tiles, so that their latency-bound
@@ -859,7 +939,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     items();
     if (VERIFY) {
         __syncthreads();
-        if (threadIdx.x == 0) verify_finish(p, vacc);
+        verify_finish<THREADS>(p, vacc);
     }
     if (STAMPS && lane == 0 && p.stamps) {  // (no buffer: a plan exec of a stamped variant)
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();

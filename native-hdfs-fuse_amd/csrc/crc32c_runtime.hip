@@ -433,11 +433,8 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream, hipEven
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
-        // the mismatch bitmap (one bit per checksum) is cleared after that
-        // wait, so a previous verify still setting bits in it has finished
-        if (p.bad_bits && plan->nchecksums)
-            HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p.bad_bits), 0,
-                                      size_t((plan->nchecksums + 31) / 32), stream));
+        // (the mismatch bitmap is cleared by the launch itself, after that
+        // wait: a previous verify still setting bits in it has finished)
     }
     return launch(plan->ctx, p, plan->sched, stream, stop);
 }
@@ -1014,6 +1011,7 @@ int crc32c_plan_verify_bitmap(crc32c_plan *plan, const void *dev_payload, const 
     p.expect = dev_expected;
     p.result = dev_result;
     p.bad_bits = dev_bad_bits;
+    p.bad_words = dev_bad_bits ? uint32_t((plan->nchecksums + 31) / 32) : 0;
     return launch_plan(plan, p, s);
 }
 

@@ -1,581 +1,88 @@
-// resident.hip -- A/B experiment (libhdfs_crc32c_debug.so only): a
-// bounded-lifetime RESIDENT checksum kernel for concurrent block writes.
-//
-// libfuse writes one 4 MiB block per hadoop_fuse_write_block call on many
-// worker threads (src/fuse.c:336-449, fuse.c:1771).  One launch per block
-// costs ~4.3 us of fixed work per launch (kernel boundary, table staging,
-// tail: DESIGN.md section 5), which caps 16 writers with one block each at
-// 1.8 us per block through the group-commit queue (crc32c_blocks).  Here the
-// kernel stays on the GPU instead: tables staged ONCE per launch, blocks
-// pulled from a ring the submitting threads fill, completion written to
-// host memory -- no launch per block at all.
-//
-// Protocol (all host words in pinned, device-mapped, coherent memory):
-//  * submit (host): ticket t = an atomic counter; slot t % kRing is reused
-//    only once block t - kRing is complete; the slot's two words (payload
-//    and out pointer) each carry t's tag, so one read of the slot tells a
-//    complete entry from a stale or half-written one.
-//  * forwarder (workgroup 0's last wave): reads 64 host slots per poll (one
-//    PCIe round trip per poll, not per block) and copies the ready ones into
-//    a device ring, tags and all (agent scope).
-//  * collector (workgroup 1's last wave): block t is complete when all
-//    workgroups' flags for its slot hold t + 1 (one 1 KiB load per check);
-//    blocks complete in ticket order, hdone[slot] = t + 1 (system scope).
-//  * workers (every other wave): block t is run by phase t % P (P blocks in
-//    flight); within a phase PER waves per workgroup take its tiles (a 4 MiB
-//    block is 512 tiles = 2 per CU: one each, or both by one wave with both
-//    loaded first); a workgroup's phase workers count themselves in LDS and
-//    the last one stores the workgroup's flag.  Checksums are stored
-//    write-through (system scope), and every store has completed before the
-//    flag.
-//  * lifetime: the forwarder exits on the host's stop word, after idle_us
-//    with nothing queued, or after kStuckMs without progress while blocks are
-//    outstanding (a workgroup that never got a CU); on exit it raises the
-//    device stop word that every worker polls; the collector records where
-//    it stopped (exit_col) so a relaunch resumes there.  The host relaunches
-//    the kernel on demand (submit, or a waiter that waits long), never while
-//    one runs.  Workers have their own bound (kWorkerMs without a block).
-//    Every wave therefore exits, whatever the host does.
+// resident.hip -- A/B shapes of the resident checksum kernel
+// (libhdfs_crc32c_debug.so only).  The kernel and its host side are the
+// product's (resident_engine.h, crc32c_resident.hip: the block queue's
+// resident mode runs the 16 / 7 / 2 shape); this file instantiates the other
+// shapes round 4 measured and selects one by environment, with an optional
+// per-ticket trace -- neither of which the product library reads:
+//   HDFS_CRC32C_RESIDENT_WAVES   12 (12 / 5 / 2, default here), 16 (16 / 7 / 2,
+//                                the product's), 12x11 (12 / 11 / 1) or 16x15
+//                                (16 / 15 / 1): waves per workgroup / blocks
+//                                in flight / worker waves per block
+//   HDFS_CRC32C_RESIDENT_STAMPS  1: s_memrealtime per ticket at each hop
+//                                (crc32c_debug_resident_trace)
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <atomic>
 #include <cerrno>
-#include <chrono>
 #include <cstdlib>
-#include <cstring>
-#include <mutex>
 #include <string>
-#include <thread>
 
-#include "../crc32c_device.h"
+#include "../resident_engine.h"
 #include "../runtime_internal.h"
 #include "hdfs_crc32c_debug.h"
 
+using namespace hdfs_crc_res;
+
 namespace {
 
-using namespace hdfs_crc_dev;
-
-constexpr uint32_t kRing = 64;       // tickets in flight at most
-// (the kernel is a template on WAVES per workgroup -- one workgroup per CU,
-// 152 KiB of LDS --, PHASES, the blocks processed at once, and PER, the
-// worker waves per workgroup and phase that take tiles (2: one 8 KiB tile
-// each; 1: both tiles of the workgroup, both loaded before the first one's
-// lookups, so twice the phases fit); HDFS_CRC32C_RESIDENT_WAVES selects 12
-// (12 / 5 / 2, default), 16 (16 / 7 / 2), 12x11 (12 / 11 / 1) or 16x15
-// (16 / 15 / 1): an A/B of this debug-only experiment)
-constexpr uint32_t kMaxWg = 256;     // one flag lane-dword per workgroup (64 lanes x 4)
-constexpr uint64_t kTicksPerUs = 100;  // s_memrealtime: 100 MHz
-constexpr uint64_t kStuckMs = 50;
-// Trace (HDFS_CRC32C_RESIDENT_STAMPS=1 at create): per ticket t % kStampRing,
-// s_memrealtime when the forwarder forwarded it, when workgroup 0's worker
-// of its phase saw it, when that worker's tiles were stored, and when the
-// collector completed it; plus the forwarder's host-slot poll round trips.
-constexpr uint32_t kStampRing = 4096;
-constexpr uint64_t kWorkerMs = 200;
-
-// A slot (host ring and device ring alike) is two 64-bit words, payload and
-// out pointer (48-bit GPU addresses), each tagged in bits 48-63 with the low
-// 16 bits of ticket + 1: a reader that sees both with matching tags has the
-// block's pointers (no separate sequence word, no order between the stores).
-constexpr int kTagShift = 48;
-constexpr uint64_t kAddrMask = (1ull << kTagShift) - 1;
-__host__ __device__ constexpr uint64_t tag_of(uint64_t ticket) { return ((ticket + 1) & 0xffffull) << kTagShift; }
-
-struct HostRing {
-    uint64_t slot[kRing][2];  // host: the ticket's tagged payload / out pointers (the device slot format)
-    uint64_t done[kRing];     // kernel: ticket + 1 once the block's checksums are stored
-    uint32_t stop;            // host: exit now
-    uint32_t pad0[15];
-    uint64_t exit_col;        // kernel (at exit): tickets below this are complete
-    uint64_t exits;           // kernel: launches that have exited
-};
-
-struct DevRing {
-    uint64_t slot[kRing][2];
-    uint32_t flag[kRing][kMaxWg];  // per slot and workgroup: ticket + 1 once its workers are done
-    uint64_t fwd;                  // forwarder: tickets below this are forwarded
-    uint64_t col;                  // collector: tickets below this are complete
-    uint32_t stop;                 // forwarder: every wave exits
-    uint64_t rtt_sum, rtt_n;       // trace: forwarder poll round trips (ticks), count
-};
-
-struct RParams {
-    HostRing *h;
-    DevRing *d;
-    const FastTile *tiles;
-    const uint8_t *table_s4;
-    uint32_t ntiles;
-    uint32_t flags;
-    uint32_t c_lg[5];
-    uint64_t first;       // first ticket this launch forwards
-    uint64_t idle_ticks;  // forwarder: exit after this long with nothing queued
-    uint64_t *stamps;     // trace (nullptr: off), 4 per ticket % kStampRing
-};
-
-template <typename T>
-__device__ __forceinline__ T ld_sys(const T *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-template <typename T>
-__device__ __forceinline__ T ld_dev(const T *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ void st_sys(T *p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-template <typename T>
-__device__ __forceinline__ void st_dev(T *p, T v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
-
-// One power-of-two tile of a block (the plan's block shape; offsets relative
-// to the block's payload / checksum array): the production tile's loads,
-// lookups and reduce, stores write-through.
-__device__ __forceinline__ FastTile rtile(const RParams &p, uint32_t idx) {
-    typedef const __attribute__((address_space(4))) FastTile *CT;
-    const CT tp = (CT)(p.tiles) + idx;
-    return FastTile{tp->src, tp->out, tp->meta};
-}
-__device__ __forceinline__ void rtile_load(const uint8_t *payload, const FastTile &t, int lane, uint4 v[8]) {
-    const uint32_t nb = t.meta & 0xffu;
-    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(payload + t.src, nb * 512u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16u * uint32_t(lane) + 1024u * i, 0, 2);
-        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
-    }
-}
-__device__ __forceinline__ void rtile_finish(const RParams &p, const uint8_t *lds, uint32_t *out, const FastTile &t,
-                                             uint4 v[8], int lane) {
-    const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu;
-    uint32_t pc[8];
-    tile_pieces<0, true, kImgFull>(lds, v, pc, lane, NoPrep{});
-    uint32_t x = block_lin(pc, lane);
-    const uint32_t blk = rep_block(lane);
-    if (lg) {
-        const uint32_t nbc = 1u << lg;
-        const uint32_t s = nbc - 1u - (blk & (nbc - 1u));
-        if (s) x = zshift<true, kImgFull>(lds, s, x);
-        x ^= static_cast<uint32_t>(__shfl_xor(static_cast<int>(x), 32));
-        if (lg >= 2) x ^= dpp<kDppXor8>(x);
-        if (lg >= 3) x ^= dpp<kDppXor2>(x);
-        if (lg >= 4) x ^= dpp<kDppXor1>(x);
-    }
-    if (rep_lane(lane, blk, nb, lg)) {
-        typedef __attribute__((address_space(1))) uint32_t *GU32;  // (a global store, not a flat one)
-        __hip_atomic_store((GU32)(out + t.out + (blk >> lg)), out_order(x ^ p.c_lg[lg], p.flags), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-__device__ __forceinline__ void run_tile(const RParams &p, const uint8_t *lds, const uint8_t *payload,
-                                         uint32_t *out, uint32_t idx, int lane) {
-    const FastTile t = rtile(p, idx);
-    uint4 v[8];
-    rtile_load(payload, t, lane, v);
-    __builtin_amdgcn_sched_barrier(0);
-    rtile_finish(p, lds, out, t, v, lane);
-}
-// Two tiles by one wave: both tiles' loads first, so the second one's
-// latency hides under the first one's lookups.
-__device__ __forceinline__ void run_tile_pair(const RParams &p, const uint8_t *lds, const uint8_t *payload,
-                                              uint32_t *out, uint32_t ia, uint32_t ib, int lane) {
-    const FastTile ta = rtile(p, ia), tb = rtile(p, ib);
-    uint4 va[8], vb[8];
-    rtile_load(payload, ta, lane, va);
-    rtile_load(payload, tb, lane, vb);
-    __builtin_amdgcn_sched_barrier(0);
-    rtile_finish(p, lds, out, ta, va, lane);
-    rtile_finish(p, lds, out, tb, vb, lane);
-}
-
-// Forwarder (workgroup 0's last wave): the host ring -> the device ring.
-// One PCIe round trip per poll covers the next 64 tickets.  Decides the
-// launch's end: the host's stop word, idle_ticks with nothing outstanding,
-// or kStuckMs without the collector advancing while blocks are outstanding.
-__device__ void forwarder(const RParams &p, int lane) {
-    HostRing *h = p.h;
-    DevRing *d = p.d;
-    uint64_t fwd = p.first, col = p.first;
-    uint64_t last = now();
-    uint64_t rtt_sum = 0, rtt_n = 0;
-    for (;;) {
-        bool progress = false;
-        const uint64_t t_poll = p.stamps ? now() : 0;
-        // the next 64 tickets' host slots, one load per lane (ring reuse:
-        // ticket t only once t - kRing is complete; `col` from the previous
-        // pass, so the collector's word and the host slots load together)
-        const uint64_t cand = fwd + uint64_t(lane);
-        const bool room = cand < col + kRing;
-        const uint32_t sl = uint32_t(cand % kRing);
-        const uint64_t w0 = room ? ld_sys(&h->slot[sl][0]) : 0, w1 = room ? ld_sys(&h->slot[sl][1]) : 0;
-        const uint64_t c = ld_dev(&d->col);
-        if (c != col) {
-            col = c;
-            progress = true;
-        }
-        const bool ok = room && (w0 & ~kAddrMask) == tag_of(cand) && (w1 & ~kAddrMask) == tag_of(cand);
-        const uint64_t ready = __ballot(ok);
-        if (p.stamps) {  // (the ballot waited for the host loads)
-            rtt_sum += now() - t_poll;
-            ++rtt_n;
-        }
-        const uint32_t n = ~ready ? uint32_t(__builtin_ctzll(~ready)) : 64u;  // consecutive ready tickets from fwd
-        if (n) {
-            if (uint32_t(lane) < n) {
-                st_dev(&d->slot[sl][0], w0);
-                st_dev(&d->slot[sl][1], w1);
-                if (p.stamps) st_dev(&p.stamps[4 * (cand % kStampRing)], now());
-            }
-            fwd += n;
-            if (lane == 0) st_dev(&d->fwd, fwd);
-            progress = true;
-        }
-        const uint64_t t = now();
-        if (progress) {
-            last = t;
-            continue;
-        }
-        if (ld_sys(&h->stop)) break;
-        if (col == fwd && t - last > p.idle_ticks) break;                  // idle
-        if (col < fwd && t - last > kStuckMs * 1000 * kTicksPerUs) break;  // no progress: give up
-        __builtin_amdgcn_s_sleep(2);
-    }
-    if (lane == 0) {
-        st_dev(&d->stop, 1u);
-        if (p.stamps) {
-            st_dev(&d->rtt_sum, ld_dev(&d->rtt_sum) + rtt_sum);
-            st_dev(&d->rtt_n, ld_dev(&d->rtt_n) + rtt_n);
-        }
-    }
-}
-
-// Collector (workgroup 1's last wave): block t is complete when every
-// workgroup's flag for its slot holds t + 1; the (up to 8) oldest
-// outstanding blocks' flags are loaded together and completed in ticket
-// order (hdone[slot] = t + 1 in host memory).  Ends once the forwarder has
-// stopped and nothing it forwarded is outstanding (or kStuckMs later), then
-// records where it stopped for the next launch.
-__device__ void collector(const RParams &p, int lane) {
-    HostRing *h = p.h;
-    DevRing *d = p.d;
-    uint64_t col = p.first;
-    uint64_t last = now();
-    const uint32_t ng = gridDim.x;
-    for (;;) {
-        const uint32_t stop = ld_dev(&d->stop);
-        const uint64_t fwd = ld_dev(&d->fwd);
-        bool progress = false;
-        constexpr uint32_t kCheck = 8;
-        const uint64_t nout = fwd > col ? fwd - col : 0;
-        uint32_t f[kCheck][4];
-#pragma unroll
-        for (uint32_t c = 0; c < kCheck; ++c)
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                const uint32_t wg = 4u * uint32_t(lane) + k;
-                f[c][k] = (c < nout && wg < ng) ? ld_dev(&d->flag[(col + c) % kRing][wg]) : 0u;
-            }
-#pragma unroll
-        for (uint32_t c = 0; c < kCheck; ++c) {
-            if (c >= nout) break;
-            const uint32_t want = uint32_t(col + 1);
-            bool ok = true;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k)
-                if (4u * uint32_t(lane) + k < ng && f[c][k] != want) ok = false;
-            if (__ballot(!ok)) break;
-            if (lane == 0) {
-                st_sys(&h->done[col % kRing], col + 1);
-                if (p.stamps) st_dev(&p.stamps[4 * (col % kStampRing) + 3], now());
-            }
-            ++col;
-            progress = true;
-        }
-        if (progress) {
-            if (lane == 0) st_dev(&d->col, col);
-            last = now();
-            continue;
-        }
-        if (stop && col >= fwd) break;
-        if (stop && now() - last > kStuckMs * 1000 * kTicksPerUs) break;
-        if (now() - last > kWorkerMs * 1000 * kTicksPerUs) break;  // (the forwarder is gone)
-        __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0) {
-        st_sys(&h->exit_col, col);
-        wait_vmem();
-        st_sys(&h->exits, ld_sys(&h->exits) + 1);
-    }
-}
-
-template <uint32_t kWaves, uint32_t kPhases, uint32_t kPer>
-__global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RParams p) {
-    constexpr uint32_t kWorkers = kWaves - 1;
-    constexpr uint32_t kStage = kS4StageBytes;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 4 * kRing];
-    uint32_t *lcnt = reinterpret_cast<uint32_t *>(lds + kStage);  // per slot: this workgroup's workers done
-    const int lane = int(threadIdx.x & 63u);
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    constexpr uint32_t kChunks = kStage / 1024u;
-    const uint32_t rot = (blockIdx.x * 37u) % kChunks;
-    for (uint32_t i = wv; i < kChunks; i += kWaves) {
-        const uint32_t c = i + rot < kChunks ? i + rot : i + rot - kChunks;
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void *)(p.table_s4 + c * 1024u + 16u * uint32_t(lane)),
-            (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
-    }
-    if (threadIdx.x < kRing) lcnt[threadIdx.x] = 0;
-    __syncthreads();
-    if (wv == kWaves - 1) {
-        if (blockIdx.x == 0) forwarder(p, lane);
-        if (blockIdx.x == 1) collector(p, lane);
-        return;
-    }
-    // Worker: phase (b + w) % P; the workgroup's waves of a phase rank in
-    // wave order; the first kPer take tiles kPer b + rank (+ kPer G, ...).
-    const uint32_t b = blockIdx.x, G = gridDim.x;
-    const uint32_t phase = (b + wv) % kPhases;
-    uint32_t rank = 0, expect = 0;
-    for (uint32_t w = 0; w < kWorkers; ++w)
-        if ((b + w) % kPhases == phase) {
-            if (w < wv) ++rank;
-            ++expect;
-        }
-    DevRing *d = p.d;
-    uint64_t j = p.first + (phase + kPhases - uint32_t(p.first % kPhases)) % kPhases;  // first block of the phase
-    uint64_t last = now();
-    for (;;) {
-        const uint32_t sl = uint32_t(j % kRing);
-        bool stop = false;
-        uint64_t w0 = 0, w1 = 0;
-        for (uint32_t polls = 0;; ++polls) {
-            w0 = ld_dev(&d->slot[sl][0]);
-            w1 = ld_dev(&d->slot[sl][1]);
-            if ((w0 & ~kAddrMask) == tag_of(j) && (w1 & ~kAddrMask) == tag_of(j)) break;
-            if ((polls & 15u) == 15u && (ld_dev(&d->stop) || now() - last > kWorkerMs * 1000 * kTicksPerUs)) {
-                stop = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (stop) break;
-        const bool stamp = p.stamps && b == 0 && lane == 0;
-        if (stamp) st_dev(&p.stamps[4 * (j % kStampRing) + 1], now());
-        const uint8_t *payload = reinterpret_cast<const uint8_t *>(w0 & kAddrMask);
-        uint32_t *out = reinterpret_cast<uint32_t *>(w1 & kAddrMask);
-        if (kPer == 1) {  // (rank 0: this workgroup's tiles b, b + G, ..., two at a time)
-            for (uint32_t idx = b; idx < p.ntiles; idx += 2u * G) {
-                if (idx + G < p.ntiles)
-                    run_tile_pair(p, lds, payload, out, idx, idx + G, lane);
-                else
-                    run_tile(p, lds, payload, out, idx, lane);
-            }
-        } else if (rank < kPer) {
-            for (uint32_t idx = kPer * b + rank; idx < p.ntiles; idx += kPer * G)
-                run_tile(p, lds, payload, out, idx, lane);
-        }
-        wait_vmem();  // (this wave's checksum stores have completed)
-        if (stamp && rank == 0) st_dev(&p.stamps[4 * (j % kStampRing) + 2], now());
-        if (lane == 0) {
-            const uint32_t old = atomicAdd(&lcnt[sl], 1u);
-            if (old + 1u == expect) {
-                lcnt[sl] = 0;
-                st_dev(&d->flag[sl][b], uint32_t(j + 1));
-            }
-        }
-        j += kPhases;
-        last = now();
-    }
+template <uint32_t W, uint32_t P, uint32_t K>
+hipError_t launch_shape(const RParams &p, uint32_t grid, hipStream_t stream) {
+    hipLaunchKernelGGL((resident_kernel<W, P, K>), dim3(grid), dim3(W * 64), 0, stream, p);
+    return hipGetLastError();
 }
 
 }  // namespace
 
 struct crc32c_resident {
-    crc32c_plan *plan = nullptr;
-    int device = 0;
-    uint32_t grid = 0;
-    uint64_t idle_ticks = 0;
-    HostRing *h = nullptr;    // host view
-    HostRing *h_dev = nullptr;  // the same memory, device view
-    DevRing *d = nullptr;
-    hipStream_t stream = nullptr;
-    std::atomic<uint64_t> next{0};
-    int shape = 0;           // A/B: HDFS_CRC32C_RESIDENT_WAVES (0: 12 / 5 / 2, 1: 16 / 7 / 2, 2: 12 / 11 / 1, 3: 16 / 15 / 1)
-    std::mutex mu;           // launches
-    bool running = false;    // a launch may be on the GPU (under mu)
-    std::atomic<uint64_t> launches{0};
-    uint64_t *stamps = nullptr;  // trace (HDFS_CRC32C_RESIDENT_STAMPS=1)
+    hdfs_crc::ResidentEngine *e = nullptr;
 };
-
-namespace {
-
-// Launches the kernel unless one is running (caller holds r->mu).  A launch
-// that has exited shows as an idle stream.
-int ensure_running(crc32c_resident *r) {
-    if (r->running) {
-        const hipError_t q = hipStreamQuery(r->stream);
-        if (q == hipErrorNotReady) return 0;
-        if (q != hipSuccess) return hdfs_crc::fail(-EIO, "resident kernel: %s", hipGetErrorString(q));
-        r->running = false;
-    }
-    const uint64_t col = __atomic_load_n(&r->h->exit_col, __ATOMIC_ACQUIRE);
-    if (col >= r->next.load(std::memory_order_acquire)) return 0;  // nothing queued
-    hdfs_crc::KParams kp = hdfs_crc::plan_params(r->plan, nullptr, nullptr);
-    RParams p{};
-    p.h = r->h_dev;
-    p.d = r->d;
-    p.tiles = kp.tiles;
-    p.table_s4 = kp.table_s4;
-    p.ntiles = kp.ntiles;
-    p.flags = kp.flags;
-    for (int i = 0; i < 5; ++i) p.c_lg[i] = kp.c_lg[i];
-    p.first = col;
-    p.idle_ticks = r->idle_ticks;
-    p.stamps = r->stamps;
-    hdfs_crc::DeviceGuard guard(r->device);
-    // (fresh control words; the device slots keep their tags: a tag names its ticket)
-    const uint64_t ctl[3] = {col, col, 0};
-    HIP_TRY(hipMemcpyAsync(&r->d->fwd, ctl, sizeof ctl, hipMemcpyHostToDevice, r->stream));
-    HIP_TRY(hipStreamSynchronize(r->stream));  // (ctl is on this stack)
-    switch (r->shape) {
-        case 1: hipLaunchKernelGGL((resident_kernel<16, 7, 2>), dim3(r->grid), dim3(16 * 64), 0, r->stream, p); break;
-        case 2: hipLaunchKernelGGL((resident_kernel<12, 11, 1>), dim3(r->grid), dim3(12 * 64), 0, r->stream, p); break;
-        case 3: hipLaunchKernelGGL((resident_kernel<16, 15, 1>), dim3(r->grid), dim3(16 * 64), 0, r->stream, p); break;
-        default: hipLaunchKernelGGL((resident_kernel<12, 5, 2>), dim3(r->grid), dim3(12 * 64), 0, r->stream, p);
-    }
-    HIP_TRY(hipGetLastError());
-    r->running = true;
-    r->launches.fetch_add(1, std::memory_order_release);
-    return 0;
-}
-
-}  // namespace
 
 extern "C" {
 
 int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_resident **out) {
-    using namespace hdfs_crc;
-    if (!plan || !out) return fail(-EINVAL, "plan/out == NULL");
+    if (!out) return hdfs_crc::fail(-EINVAL, "out == NULL");
     *out = nullptr;
-    const DevicePlan &dp = plan->dp;
-    if (dp.ngen || dp.nseg || dp.nconst || dp.general || dp.misaligned || !dp.ntiles || plan->absolute)
-        return fail(-EINVAL, "the resident kernel runs plans of aligned power-of-two tiles only");
-    std::unique_ptr<crc32c_resident, int (*)(crc32c_resident *)> r(new crc32c_resident, crc32c_debug_resident_destroy);
-    r->plan = plan;
-    r->device = plan->ctx->device;
-    r->grid = uint32_t(std::min(plan->ctx->num_cu, int(kMaxWg)));
-    r->idle_ticks = uint64_t(idle_us ? idle_us : 2000) * kTicksPerUs;
+    hdfs_crc::ResidentLaunch launch = launch_shape<12, 5, 2>;
     if (const char *w = std::getenv("HDFS_CRC32C_RESIDENT_WAVES")) {
         const std::string s(w);
-        r->shape = s == "16" ? 1 : s == "12x11" ? 2 : s == "16x15" ? 3 : 0;
+        if (s == "16") launch = hdfs_crc::resident_launch_product;
+        if (s == "12x11") launch = launch_shape<12, 11, 1>;
+        if (s == "16x15") launch = launch_shape<16, 15, 1>;
     }
-    hdfs_crc::DeviceGuard guard(r->device);
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&r->h), sizeof(HostRing), hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(static_cast<void *>(r->h), 0, sizeof(HostRing));
-    void *hd = nullptr;
-    HIP_TRY(hipHostGetDevicePointer(&hd, r->h, 0));
-    r->h_dev = static_cast<HostRing *>(hd);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&r->d), sizeof(DevRing)));
-    HIP_TRY(hipMemset(r->d, 0, sizeof(DevRing)));
-    HIP_TRY(hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking));
-    if (const char *st = std::getenv("HDFS_CRC32C_RESIDENT_STAMPS"); st && st[0] == '1') {
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&r->stamps), sizeof(uint64_t) * 4 * kStampRing));
-        HIP_TRY(hipMemset(r->stamps, 0, sizeof(uint64_t) * 4 * kStampRing));
+    const char *st = std::getenv("HDFS_CRC32C_RESIDENT_STAMPS");
+    crc32c_resident *r = new crc32c_resident;
+    if (int rc = hdfs_crc::resident_create(plan, idle_us, launch, st && st[0] == '1', &r->e)) {
+        delete r;
+        return rc;
     }
-    // (the plan's descriptors are uploaded on the context's upload stream)
-    if (plan->dp.uploaded) HIP_TRY(hipStreamWaitEvent(r->stream, plan->dp.uploaded, 0));
-    *out = r.release();
+    *out = r;
     return 0;
 }
 
 int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
-    using namespace hdfs_crc;
-    if (!r || !dev_payload || !dev_out) return fail(-EINVAL, "bad arguments");
-    if (reinterpret_cast<uintptr_t>(dev_payload) & 15u) return fail(-EINVAL, "payload must be 16-byte aligned");
-    const uint64_t t = r->next.fetch_add(1, std::memory_order_acq_rel);
-    const uint32_t sl = uint32_t(t % kRing);
-    // the slot's previous block (t - kRing) must be complete
-    if (t >= kRing)
-        while (__atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE) < t - kRing + 1) {
-            if (int rc = crc32c_debug_resident_wait(r, t - kRing)) return rc;
-        }
-    __atomic_store_n(&r->h->slot[sl][0], (reinterpret_cast<uint64_t>(dev_payload) & kAddrMask) | tag_of(t),
-                     __ATOMIC_RELAXED);
-    __atomic_store_n(&r->h->slot[sl][1], (reinterpret_cast<uint64_t>(dev_out) & kAddrMask) | tag_of(t),
-                     __ATOMIC_RELEASE);
-    if (ticket) *ticket = t;
-    // every launch so far has exited (or is exiting): start one (a launch
-    // still running forwards this ticket; one that exits before seeing it is
-    // relaunched by the waiter)
-    if (__atomic_load_n(&r->h->exits, __ATOMIC_ACQUIRE) >= r->launches.load(std::memory_order_acquire)) {
-        std::lock_guard<std::mutex> lock(r->mu);
-        return ensure_running(r);
-    }
-    return 0;
+    if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
+    return hdfs_crc::resident_submit(r->e, dev_payload, dev_out, ticket);
 }
 
 int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket) {
-    using namespace hdfs_crc;
-    if (!r) return fail(-EINVAL, "resident == NULL");
-    if (ticket >= r->next.load(std::memory_order_acquire)) return fail(-EINVAL, "ticket never handed out");
-    const uint32_t sl = uint32_t(ticket % kRing);
-    auto t0 = std::chrono::steady_clock::now();
-    const auto deadline = t0 + std::chrono::seconds(5);
-    for (uint32_t i = 0;; ++i) {
-        const uint64_t v = __atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE);
-        if (v >= ticket + 1) return 0;  // (a later ticket in the slot implies this one completed)
-        if ((i & 255u) == 255u) {
-            const auto t = std::chrono::steady_clock::now();
-            if (t > deadline) return fail(-ETIMEDOUT, "resident kernel: block %llu not done", (unsigned long long)ticket);
-            if (t - t0 > std::chrono::microseconds(100)) {  // the kernel may have exited: relaunch it
-                std::lock_guard<std::mutex> lock(r->mu);
-                if (int rc = ensure_running(r)) return rc;
-                t0 = t;
-            }
-            std::this_thread::yield();
-        } else {
-            __builtin_ia32_pause();
-        }
-    }
+    if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
+    return hdfs_crc::resident_wait(r->e, ticket);
 }
 
 int crc32c_debug_resident_stats(const crc32c_resident *r, uint64_t *launches) {
     if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
-    if (launches) *launches = r->launches.load();
+    if (launches) *launches = hdfs_crc::resident_launches(r->e);
     return 0;
 }
 
 int crc32c_debug_resident_trace(crc32c_resident *r, uint64_t *stamps, uint64_t *rtt_ticks, uint64_t *rtt_polls) {
-    using namespace hdfs_crc;
-    if (!r || !stamps || !rtt_ticks || !rtt_polls) return fail(-EINVAL, "bad arguments");
-    if (!r->stamps) return fail(-EINVAL, "no trace: create with HDFS_CRC32C_RESIDENT_STAMPS=1");
-    DeviceGuard guard(r->device);
-    std::lock_guard<std::mutex> lock(r->mu);
-    // (the launch ends first: the forwarder's round-trip sums are written at its exit)
-    __atomic_store_n(&r->h->stop, 1u, __ATOMIC_RELEASE);
-    HIP_TRY(hipStreamSynchronize(r->stream));
-    __atomic_store_n(&r->h->stop, 0u, __ATOMIC_RELEASE);
-    r->running = false;
-    HIP_TRY(hipMemcpy(stamps, r->stamps, sizeof(uint64_t) * 4 * kStampRing, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(rtt_ticks, &r->d->rtt_sum, sizeof(uint64_t), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(rtt_polls, &r->d->rtt_n, sizeof(uint64_t), hipMemcpyDeviceToHost));
-    return 0;
+    if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
+    return hdfs_crc::resident_trace(r->e, stamps, rtt_ticks, rtt_polls);
 }
 
+// (round 4's semantics: the stop word at once, queued blocks may be dropped)
 int crc32c_debug_resident_destroy(crc32c_resident *r) {
     if (!r) return 0;
-    if (r->h) __atomic_store_n(&r->h->stop, 1u, __ATOMIC_RELEASE);
-    hdfs_crc::DeviceGuard guard(r->device);
-    if (r->stream) {
-        (void)hipStreamSynchronize(r->stream);  // (the kernel exits on the stop word)
-        (void)hipStreamDestroy(r->stream);
-    }
-    if (r->d) (void)hipFree(r->d);
-    if (r->stamps) (void)hipFree(r->stamps);
-    if (r->h) (void)hipHostFree(r->h);
+    (void)hdfs_crc::resident_destroy(r->e, false);
     delete r;
     return 0;
 }

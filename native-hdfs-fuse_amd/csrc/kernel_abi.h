@@ -62,8 +62,10 @@ struct KParams {
     const uint32_t *expect;
     uint32_t *result;
     // Optional (crc32c_plan_verify_bitmap): bit i set for every mismatching
-    // checksum i; zeroed by the runtime before the launch.
+    // checksum i; its bad_words u32s are zeroed by workgroup 0 of the launch
+    // itself before it publishes the launch key (crc32c_device.h verify_init).
     uint32_t *bad_bits;
+    uint32_t bad_words;
     // Verification slot of this launch (kSlotWords u32s): the key of the
     // launch that initialised p.result.
     uint32_t *sched;

@@ -14,6 +14,10 @@
 #include "kernel_abi.h"
 #include "plan.h"
 
+namespace hdfs_crc_res {
+struct RParams;  // resident_engine.h
+}
+
 namespace hdfs_crc {
 
 // (fail(): errors.h)
@@ -206,5 +210,26 @@ void release_pools(crc32c_ctx *ctx);
 // Creates a plan object from a built HostPlan (absolute: rebased, base given).
 int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute, uint64_t abs_base,
               crc32c_plan **out);
+
+// ---- the resident kernel's host side (crc32c_resident.hip; kernel:
+// resident_engine.h).  A launcher starts one instance of resident_kernel
+// (its shape) with `grid` workgroups on `stream`.
+using ResidentLaunch = hipError_t (*)(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
+struct ResidentEngine;
+// Plans of aligned power-of-two tiles only (one block's shape, as the
+// queue's); idle_us = 0: 2000.  stamps: per-ticket trace (debug A/B).
+int resident_create(crc32c_plan *plan, uint32_t idle_us, ResidentLaunch launch, bool stamps, ResidentEngine **out);
+int resident_submit(ResidentEngine *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket);
+int resident_wait(ResidentEngine *r, uint64_t ticket);
+uint64_t resident_launches(const ResidentEngine *r);
+uint64_t resident_tickets(const ResidentEngine *r);
+// Ends the running launch (stop word), then copies the trace out.
+int resident_trace(ResidentEngine *r, uint64_t *stamps, uint64_t *rtt_ticks, uint64_t *rtt_polls);
+// drain: every ticket handed out completes first (a bounded wait each);
+// then the stop word, the stream drained, everything freed.  Submits from
+// the moment destroy begins are refused.
+int resident_destroy(ResidentEngine *r, bool drain);
+// The product's shape (16 waves, 7 phases, 2 waves per phase and workgroup).
+hipError_t resident_launch_product(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
 
 }  // namespace hdfs_crc

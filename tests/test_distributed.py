@@ -203,3 +203,62 @@ def test_layout_helpers():
     bad["out_idx"][1] += 7  # a hole inside group 0
     with pytest.raises(hdfs.Crc32cError):
         shard.layout(bad, PKTS_PER_BLOCK, 2)
+
+
+# ---- bench.py's rank-consistent graph capture (native-hdfs-fuse_amd/graphs.py) --
+def _capture_worker(rank: int, world: int, port: int, fail_rank: int, probe_fail_rank: int, result_path: str):
+    import torch.distributed as dist
+
+    load_package()
+    from hdfs_crc32c_amd.graphs import capture_agreed
+
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        calls = {"probe": 0, "capture": 0, "abandon": 0}
+
+        def probe():
+            calls["probe"] += 1
+            if rank == probe_fail_rank:
+                raise RuntimeError("probe capture failed on purpose")
+
+        def capture():
+            calls["capture"] += 1
+            return {"graph": rank}
+
+        def abandon():  # bench.py rebuilds the communicator here: a collective every rank joins
+            calls["abandon"] += 1
+            dist.barrier()
+
+        got, err = capture_agreed(capture, world, None, probe=probe, on_abandon=abandon,
+                                  inject_fail=(rank == fail_rank))
+        with open("%s.%d" % (result_path, rank), "w") as f:
+            json.dump({"got": got, "err": err, "calls": calls}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank,probe_fail_rank", [(2, -1, -1), (2, 1, -1), (3, 0, -1), (3, -1, 2)])
+def test_capture_fallback_is_rank_consistent(tmp_path, world, fail_rank, probe_fail_rank):
+    """bench.py's graph capture of a step holding RCCL calls (config 4's
+    crc32c_multi_plan_exec) is agreed over the ranks: a step-capture failure
+    injected on ONE rank (BENCH_CAPTURE_FAIL_RANK's hook) makes EVERY rank drop
+    its graphs, run the communicator rebuild together and issue from the host;
+    a probe failure (no collective captured yet) stops every rank before any
+    step capture; with no failure every rank keeps its own graph."""
+    res = str(tmp_path / "r")
+    mp.start_processes(_capture_worker, args=(world, _free_port(), fail_rank, probe_fail_rank, res), nprocs=world,
+                       join=True, start_method="spawn")
+    out = []
+    for r in range(world):
+        with open("%s.%d" % (res, r)) as f:
+            out.append(json.load(f))
+    for r, d in enumerate(out):
+        assert d["calls"]["probe"] == 1
+        if probe_fail_rank >= 0:
+            assert d["got"] is None and d["calls"]["capture"] == 0 and d["calls"]["abandon"] == 0
+            assert ("probe" in d["err"]) if r == probe_fail_rank else ("another rank" in d["err"])
+        elif fail_rank >= 0:
+            assert d["got"] is None and d["calls"]["abandon"] == 1, d
+            assert ("injected" in d["err"]) if r == fail_rank else ("another rank" in d["err"])
+        else:
+            assert d["got"] == {"graph": r} and d["err"] is None and d["calls"]["abandon"] == 0

@@ -50,6 +50,30 @@ def test_bench_one_gpu_contract():
     assert rf["bound"] == "hbm" and rf["algorithmic_bytes_per_launch"] == 4096 * 65536
     assert 0 < rf["frac"] < 1 and rf["kernel_avg_us"] > 0
     assert d["value"] > 0 and d["config"]["config"] == "c2"
+    # the other two shapes of the 1/2/4/8-GPU curve ride on the default line
+    c4 = d["config4"]
+    assert c4["bit_exact"] is True and c4["mode"] == "rccl" and c4["n_ranks"] == 1
+    assert c4["bit_exact_checks"]["before_warmup_file0"] is True and all(c4["bit_exact_checks"].values())
+    assert c4["kernel_step_us"] > 0 and c4["gib_s"] > 0 and c4["shard_kernel_us"] > 0
+    assert "hip graph" in c4["launch"] and c4["communicator_rebuilt"] == 0 and c4["transfers"] == 0
+    st = d["strong_scaling"]
+    assert st["bit_exact"] is True and st["n_ranks"] == 1 and st["packets_per_rank"] == 4096
+    assert st["gib_s"] > 0 and 0 < st["frac_of_hbm_roofline_per_gpu"] < 1
+
+
+def test_bench_injected_capture_failure_falls_back_and_rebuilds():
+    """BENCH_CAPTURE_FAIL_RANK=0 at N = 1, config 4 through RCCL (self-send):
+    the step capture fails, the communicator is rebuilt, the steps are issued
+    from the host and the gathered file is still bit-exact."""
+    env = dict(os.environ, BENCH_CAPTURE_FAIL_RANK="0", BENCH_C4_SELF_SEND="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "c4", "--steps", "20",
+                        "--warmup", "5", "--no-cpu", "--nbuf", "2", "--settle-ms", "20"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    c4 = _line(r.stdout)["config4"]
+    assert c4["bit_exact"] is True and c4["self_send"] is True and c4["transfers"] == 1
+    assert c4["communicator_rebuilt"] == 1 and c4["launch"].startswith("host-issued")
+    assert "injected" in c4["launch"]
 
 
 @pytest.mark.parametrize("config", ["c2", "c5"])
@@ -67,6 +91,30 @@ def test_bench_two_ranks_rehearsal(config):
     assert d["host_resident_ranks"] == 2 and d["host_resident_gib_s"] > 0
     assert d["gather_ms"] is not None and d["cpu_baseline"] is None
     assert d["config"]["payload_bytes_per_rank"] > 0
+    if config == "c2":  # the sub-objects at N = 2 (config 4 as a gloo rehearsal: ranks share the GPU)
+        c4 = d["config4"]
+        assert c4["n_ranks"] == 2 and c4["bit_exact"] is True and c4["mode"].startswith("gloo rehearsal")
+        assert c4["transfers"] == 16 and all(c4["bit_exact_checks"].values())
+        st = d["strong_scaling"]
+        assert st["n_ranks"] == 2 and st["packets_per_rank"] == 2048 and st["bit_exact"] is True
+    else:
+        assert d["config4"] is None and d["strong_scaling"] is None
+
+
+def test_bench_two_ranks_capture_failure_on_one_rank():
+    """A graph-capture failure on rank 1 only: both ranks issue from the host
+    (the MIN-agreed fallback), and the line is still bit-exact."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DIST_BACKEND="gloo", BENCH_CAPTURE_FAIL_RANK="1")
+    port = 29500 + random.randrange(2000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu", "--no-host", "--nbuf", "2", "--no-config4"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["bit_exact_vs_reference"] is True
+    assert d["launch"].startswith("host-issued") and "another rank" in d["launch"]  # rank 0 captured, yet fell back
+    assert d["strong_scaling"]["launch"].startswith("host-issued")
 
 
 def test_bench_gpus_flag_spawns_ranks():
