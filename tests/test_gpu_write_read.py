@@ -908,6 +908,101 @@ def test_resident_kernel_blocks(hdfs, gpu_ctx, orc, shape, monkeypatch):
     plan.close()
 
 
+def test_block_queue_resident_mode(hdfs, gpu_ctx, orc):
+    """crc32c_blocks_create_resident -- the PRODUCT library's resident-kernel
+    mode of the block queue (opt-in): 16 writer threads, 2 blocks in flight
+    each through the queue calls (crc32c_block_submit / _wait, and
+    crc32c_block_checksums), every block bit-exact against the oracle; the
+    kernel exits idle_us after the last block and the next submit relaunches
+    it; flush is a no-op; a misaligned payload and a plan with general items
+    are refused; destroy with blocks queued completes them, refuses later
+    submits, and a plain launch runs after it.  Every wave of the kernel has
+    a bounded wait, so nothing here can hang the GPU."""
+    import threading
+    import time
+
+    torch = _torch()
+    pk = _block_shape("full")
+    n = oracle.total_checksums(pk)
+    nthreads, per, depth = 16, 24, 2
+    hosts = [oracle.xorshift64_bytes(64 * 65536, 8300 + k) for k in range(nthreads * depth)]
+    want = [orc.batch(h, pk, n) for h in hosts]
+    devs = [torch.from_numpy(h).cuda() for h in hosts]
+    outs = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in hosts]
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    q = plan.blocks(resident=True, idle_us=500)
+    errs = []
+    go = threading.Barrier(nthreads)
+
+    # (outputs are cleared by host-to-device copies, which need no CU: while
+    # the resident kernel runs it holds every CU, and a fill kernel would
+    # wait for its idle exit)
+    zeros = torch.zeros(n, dtype=torch.int32).pin_memory()
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            ring = [None] * depth
+            go.wait()
+            for i in range(per + depth):
+                slot = i % depth
+                b = k * depth + slot
+                if ring[slot] is not None:
+                    q.wait(ring[slot])
+                    assert np.array_equal(outs[b].cpu().numpy().view(np.uint32), want[b]), (k, i)
+                if i < per:
+                    with torch.cuda.stream(s):
+                        outs[b].copy_(zeros, non_blocking=True)
+                    s.synchronize()
+                    ring[slot] = q.submit(devs[b].data_ptr(), outs[b].data_ptr())
+                else:
+                    ring[slot] = None
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    launches, blocks = q.stats()
+    assert blocks == nthreads * per and 1 <= launches < blocks // 8, (launches, blocks)
+    # idle exit, then a relaunch on the next block (crc32c_block_checksums = submit + wait)
+    time.sleep(0.05)
+    outs[0].zero_()
+    torch.cuda.synchronize()
+    q.flush()
+    q.checksums(devs[0].data_ptr(), outs[0].data_ptr())
+    assert np.array_equal(outs[0].cpu().numpy().view(np.uint32), want[0])
+    assert q.stats()[0] > launches
+    with pytest.raises(hdfs.Crc32cError) as ei:
+        q.submit(devs[0].data_ptr() + 4, outs[0].data_ptr())
+    assert ei.value.rc == -22
+    with pytest.raises(hdfs.Crc32cError):
+        q.wait(10**9)
+    # destroy with blocks queued: every one of them completes
+    for i in range(10):
+        outs[i].zero_()
+    torch.cuda.synchronize()
+    for i in range(10):
+        q.submit(devs[i].data_ptr(), outs[i].data_ptr())
+    q.close()
+    for i in range(10):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), want[i]), i
+    outs[1].zero_()
+    plan.exec(devs[1].data_ptr(), outs[1].data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(outs[1].cpu().numpy().view(np.uint32), want[1])
+    plan.close()
+    gplan = gpu_ctx.plan(_block_shape("bpc1536"))
+    with pytest.raises(hdfs.Crc32cError) as ei:
+        gplan.blocks(resident=True)
+    assert ei.value.rc == -22 and "power-of-two" in str(ei.value)
+    gplan.close()
+
+
 def test_block_queue_ring_reuse_two_in_flight(hdfs, gpu_ctx, orc):
     """crc32c_blocks with more tickets than its ring has slots (1024): 16
     threads keep two blocks in flight each (submit the next, then wait for

@@ -13,10 +13,12 @@
 //              then wait for the previous)
 //   kernel  -- one thread issuing crc32c_plan_exec_blocks of B blocks back to
 //              back: the GPU's time per block in a multi-block launch (events)
-//   resident, resident2 -- the debug library's resident kernel
-//              (crc32c_debug_resident_*: no launch per block), one / two
-//              blocks in flight per thread, every block checked against the
-//              queue's checksums of the same buffer
+//   rqueue, rqueue2 -- the queue's resident mode (crc32c_blocks_create_resident:
+//              a resident kernel, no launch per block), one / two blocks in
+//              flight per thread, every block checked against the queue's
+//              checksums of the same buffer
+//   resident, resident2 -- the debug library's A/B shapes of that kernel
+//              (crc32c_debug_resident_*, HDFS_CRC32C_RESIDENT_WAVES)
 // Every line has cpu_us_per_block: the process's CPU time (getrusage) per
 // block -- the submitting threads' and the queue worker's spinning included;
 // queue lines also the worker thread's own (worker_cpu_us_per_block, and
@@ -178,12 +180,51 @@ int main(int argc, char **argv) {
                         double(wc1 - wc0) * 1e-3 / (double(nthreads) * iters), double(wc1 - wc0) * 1e-9 / qs, w);
             CHECK(crc32c_blocks_destroy(q) == 0);
         }
-    // resident kernel (A/B, debug library): depth 1 and 2; the outputs are
-    // compared with the queue's (the last queue run wrote every buffer's)
+    // resident kernel: the product queue's resident mode
+    // (crc32c_blocks_create_resident: rqueue, rqueue2) and the debug
+    // library's A/B shapes (resident, resident2), depth 1 and 2; the outputs
+    // are compared with the queue's (the last queue run wrote every buffer's)
     {
         std::vector<std::vector<uint32_t>> want(nbuf, std::vector<uint32_t>(nout));
         CHECK(hipDeviceSynchronize() == hipSuccess);
         for (int i = 0; i < nbuf; ++i) CHECK(hipMemcpy(want[i].data(), outs[i], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        auto check_outs = [&](int depth) {
+            int bad = 0;
+            std::vector<uint32_t> got(nout);
+            for (int k = 0; k < nthreads; ++k)
+                for (int slot = 0; slot < depth; ++slot) {
+                    const int b = depth * k + slot;
+                    CHECK(hipMemcpy(got.data(), outs[b], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
+                    bad += got != want[b];
+                }
+            return bad;
+        };
+        for (int depth = 1; depth <= std::min(maxdepth, 2); ++depth)
+            for (int w = 0; w < 2; ++w) {
+                for (int i = 0; i < nbuf; ++i) CHECK(hipMemset(outs[i], 0, nout * 4) == hipSuccess);
+                CHECK(hipDeviceSynchronize() == hipSuccess);
+                crc32c_blocks *q = nullptr;
+                CHECK(crc32c_blocks_create_resident(plan, 2000, &q) == 0);
+                run(depth == 1 ? "rqueue" : "rqueue2", [&](int k) {
+                    if (depth == 1) {
+                        for (int i = 0; i < iters; ++i) CHECK(crc32c_block_checksums(q, bufs[k], outs[k]) == 0);
+                        return;
+                    }
+                    std::vector<uint64_t> ring(depth);
+                    for (int i = 0; i < iters; ++i) {
+                        const int slot = i % depth;
+                        if (i >= depth) CHECK(crc32c_block_wait(q, ring[slot]) == 0);
+                        const int b = depth * k + slot;
+                        CHECK(crc32c_block_submit(q, bufs[b], outs[b], &ring[slot]) == 0);
+                    }
+                    for (int i = std::max(0, iters - depth); i < iters; ++i) CHECK(crc32c_block_wait(q, ring[i % depth]) == 0);
+                });
+                uint64_t launches = 0, blocks = 0;
+                CHECK(crc32c_blocks_stats(q, &launches, &blocks) == 0);
+                CHECK(crc32c_blocks_destroy(q) == 0);
+                std::printf(", \"launches\": %llu, \"blocks_wrong\": %d, \"pass\": %d}\n", (unsigned long long)launches,
+                            check_outs(depth), w);
+            }
         for (int depth = 1; depth <= std::min(maxdepth, 2); ++depth)
             for (int w = 0; w < 2; ++w) {
                 for (int i = 0; i < nbuf; ++i) CHECK(hipMemset(outs[i], 0, nout * 4) == hipSuccess);
