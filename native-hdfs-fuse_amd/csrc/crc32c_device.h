@@ -889,13 +889,20 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     // launch of constant runs only needs none.
     const bool tables = (p.ntiles | p.ngen | p.nseg) != 0;
     constexpr uint32_t kStageChunks = kStage / 1024u;
+    // (a batch with no Z^(512 s) shift -- bpc-512 tiles only -- leaves the
+    // image's Z section out: 144 of 152 chunks, compact 20 of 28)
+    constexpr uint32_t kNoZChunks = !S4 ? kStageChunks : C ? uint32_t(hdfs_crc::kS4CShiftOff / 1024u)
+                                                           : uint32_t(hdfs_crc::kS4ShiftOff / 1024u);
+    static_assert(!S4 || kNoZChunks * 1024u == (C ? hdfs_crc::kS4CShiftOff : hdfs_crc::kS4ShiftOff),
+                  "the Z section starts on a staging chunk");
+    const uint32_t nstage = p.skip_z ? kNoZChunks : kStageChunks;
     if (!NOSTAGE && tables) {
-        // Every workgroup copies the same 152 chunks: start each one at a
+        // Every workgroup copies the same chunks: start each one at a
         // different chunk (the 32 CUs of an XCD would otherwise walk the same
         // L2 lines, hence the same L2 channel, in lock step).
-        const uint32_t rot = (blockIdx.x * 37u) % kStageChunks;
-        for (uint32_t i = wv; i < kStageChunks; i += kWaves) {
-            const uint32_t c = i + rot < kStageChunks ? i + rot : i + rot - kStageChunks;
+        const uint32_t rot = (blockIdx.x * 37u) % nstage;
+        for (uint32_t i = wv; i < nstage; i += kWaves) {
+            const uint32_t c = i + rot < nstage ? i + rot : i + rot - nstage;
             __builtin_amdgcn_global_load_lds(
                 (const __attribute__((address_space(1))) void *)(table + c * 1024u + 16u * uint32_t(lane)),
                 (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);

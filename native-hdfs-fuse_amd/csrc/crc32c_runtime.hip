@@ -93,6 +93,17 @@ static bool has_general(const HostPlan &hp) {
     return false;
 }
 
+// Some work item shifts block results by Z^(512 s): power-of-two tiles of
+// bpc > 512 (lg > 0), general tiles and the general / spanning items.  A
+// batch of bpc-512 tiles only (configs 2, 3, 4) stages the image without
+// its Z section: 144 of 152 KiB (full image), 20 of 28 KiB (compact).
+static bool needs_z(const HostPlan &hp) {
+    if (!hp.gen.empty() || !hp.seg.empty()) return true;
+    for (const FastTile &t : hp.tiles)
+        if ((t.meta & kGeneralTile) || ((t.meta >> 8) & 0xffu)) return true;
+    return false;
+}
+
 // Some general tile's full chunks are padded (bpc not a multiple of 512).
 // Such batches run the general build with both paths even without shifted
 // tiles: the general-tiles-only build, which helps unpadded general tiles
@@ -132,6 +143,7 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     // the general builds: general tiles (bit 0), shifted loads of tiles off 16-byte alignment (bit 1)
     p.general = (dp.general ? kGeneralItems : 0u) |
                 ((dp.misaligned || dp.padded || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
+    p.skip_z = dp.needs_z ? 0u : 1u;
     return p;
 }
 
@@ -235,6 +247,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->general = has_general(hp);
     dp->misaligned = has_misaligned(hp);
     dp->padded = has_padded_general(hp);
+    dp->needs_z = needs_z(hp);
     dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
     dp->tiles_off = (kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
@@ -707,6 +720,7 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         // alignment take the general build's shifted loads, as in plans)
         p.general = (has_general(plan) ? kGeneralItems : 0u) |
                     ((has_misaligned(plan) || has_padded_general(plan)) ? kGeneralShift : 0u);
+        p.skip_z = needs_z(plan) ? 0u : 1u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(s.done, s.stream));

@@ -52,6 +52,7 @@ struct KParams {
     uint32_t nconst;
     uint32_t general;  // kGeneralItems: tiles[] holds general tiles; kGeneralShift: some tile is off 16-byte
                        // alignment (each selects a build that has that code)
+    uint32_t skip_z;   // 1: no item shifts by Z^(512 s): the S4 images are staged without their Z section
     uint32_t flags;
     uint32_t c_lg[5];
     uint32_t c_small[4];

@@ -62,6 +62,10 @@ for s in ${STEPS:-calls multi}; do
     syncp) run sync_default 120 python tools/sync_probe.py && run sync_spin 120 python tools/sync_probe.py --spin ;;
     tbenchq) run tbenchq 900 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 400 --timeout-method thread ;;
     tverify) run tverify 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "verify or bitmap or overlapping" ;;
+    fcp) run fcp 600 python -u tools/fixed_cost_probe.py --rounds ${FCP_ROUNDS:-3} ;;
+    tres5) run tres5 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "resident or block_queue" ;;
+    brate5) run brate5 400 tools/block_rate 16 400 16 30 2 1 ;;
+    tall) run tall 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
     tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
