@@ -838,6 +838,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     __shared__ __attribute__((aligned(16))) uint8_t lds[kStage + 32 + (VERIFY ? 4 * kBadList : 0)];
     uint32_t *pool_ctr = reinterpret_cast<uint32_t *>(lds + kStage);
     uint32_t *vacc = pool_ctr + 1;
+    uint32_t *exit_ctr = pool_ctr + 5;  // waves of the workgroup done
     const uint8_t *table = !S4 ? p.table : C ? p.table_s4 + hdfs_crc::kS4COff : p.table_s4;
     const int lane = int(threadIdx.x & 63u);
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in workgroup
@@ -860,6 +861,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     const uint32_t tend = uint32_t((nunits * (rng + 1)) / gridDim.x);
     if (threadIdx.x == 0) {
         *pool_ctr = tbeg + kWaves;
+        *exit_ctr = 0;
         if (VERIFY) {
             vacc[0] = 0;
             vacc[1] = 0xffffffffu;
@@ -947,6 +949,16 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     if (VERIFY) {
         __syncthreads();
         verify_finish<THREADS>(p, vacc);
+    }
+    // The plan's completion count: the workgroup's last wave adds 1 (every
+    // wave of it has finished reading the plan's memory by then).
+    if (p.done_ctr) {
+        uint32_t n = 0;
+        if (lane == 0) n = atomicAdd(exit_ctr, 1u);
+        n = __builtin_amdgcn_readfirstlane(n);
+        if (n == kWaves - 1u && lane == 0)
+            __hip_atomic_fetch_add(p.done_ctr + (blockIdx.x % hdfs_crc::kDoneCtrs) * (hdfs_crc::kDoneCtrStride / 8u),
+                                   1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (STAMPS && lane == 0 && p.stamps) {  // (no buffer: a plan exec of a stamped variant)
         const uint64_t t_end = __builtin_amdgcn_s_memrealtime();

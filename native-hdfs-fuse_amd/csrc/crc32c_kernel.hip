@@ -41,7 +41,8 @@ constexpr uint64_t kSmallBatchItemsPerCu = 16;
 constexpr uint64_t kQuarterTilesPerCu = 3;
 }  // namespace
 
-hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop) {
+hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop,
+                              uint32_t *grid) {
     using namespace hdfs_crc_dev;
     constexpr int kProd = kModeS4 | kModeNt;
     constexpr int kGen = kModeGeneral;
@@ -51,6 +52,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     const bool small = items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
+    if (grid) *grid = g.x;
 #define LAUNCH(K)                                                                  \
     do {                                                                           \
         if (stop)                                                                  \

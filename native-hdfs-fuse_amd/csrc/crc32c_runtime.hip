@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -144,6 +145,7 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     p.general = (dp.general ? kGeneralItems : 0u) |
                 ((dp.misaligned || dp.padded || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
     p.skip_z = dp.needs_z ? 0u : 1u;
+    p.done_ctr = reinterpret_cast<unsigned long long *>(dp.d + kDoneCtrOff);
     return p;
 }
 
@@ -174,6 +176,44 @@ void drop_block(BlockPool &pool, uint8_t *p) {
 // Moves every release whose events have all completed back into the pools
 // (non-blocking queries), then trims the free lists to kFreeBlocksMax.
 // Caller holds ctx->pool_mu.
+// The launches of a release's plan have all completed: its completion
+// counters, read back into its pinned staging block on the upload stream by
+// the previous call (a read is issued here when none is in flight), sum to
+// the workgroups launched.  Non-blocking.  Caller holds ctx->pool_mu.
+bool launches_done(crc32c_ctx *ctx, Release &r) {
+    if (!r.d || !r.expected) return true;
+    if (r.reading) {
+        const hipError_t q = hipEventQuery(r.read_ev);
+        if (q == hipErrorNotReady) return false;
+        r.reading = false;
+        if (q != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        uint64_t sum = 0;
+        for (uint32_t k = 0; k < kDoneCtrs; ++k) {
+            uint64_t v;
+            std::memcpy(&v, r.h + kDoneCtrOff + k * kDoneCtrStride, sizeof v);
+            sum += v;
+        }
+        if (sum >= r.expected) return true;
+    }
+    if (!r.read_ev && !(r.read_ev = take_event(ctx)) &&
+        hipEventCreateWithFlags(&r.read_ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        r.read_ev = nullptr;
+        return false;
+    }
+    if (hipMemcpyAsync(r.h + kDoneCtrOff, r.d + kDoneCtrOff, kDoneCtrs * kDoneCtrStride, hipMemcpyDeviceToHost,
+                       ctx->upload_stream) != hipSuccess ||
+        hipEventRecord(r.read_ev, ctx->upload_stream) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    r.reading = true;
+    return false;
+}
+
 void reap_releases(crc32c_ctx *ctx) {
     for (size_t i = 0; i < ctx->releases.size();) {
         Release &r = ctx->releases[i];
@@ -185,13 +225,14 @@ void reap_releases(crc32c_ctx *ctx) {
             done = false;
             break;
         }
-        if (!done) {
+        if (!done || !launches_done(ctx, r)) {
             ++i;
             continue;
         }
         if (r.d) ctx->dev_pool.free.emplace_back(r.d, r.dcap);
         if (r.h) ctx->host_pool.free.emplace_back(r.h, r.hcap);
         ctx->spare_events.insert(ctx->spare_events.end(), r.events.begin(), r.events.end());
+        if (r.read_ev) ctx->spare_events.push_back(r.read_ev);
         ctx->releases[i] = std::move(ctx->releases.back());
         ctx->releases.pop_back();
     }
@@ -248,8 +289,9 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->misaligned = has_misaligned(hp);
     dp->padded = has_padded_general(hp);
     dp->needs_z = needs_z(hp);
-    dp->slots_off = 0;  // the verify slots first (256-byte aligned), then the work items
-    dp->tiles_off = (kSlotWords * sizeof(uint32_t) + 255) / 256 * 256;
+    dp->slots_off = 0;  // the verify slot first, the completion counters, then the work items
+    static_assert(kSlotWords * sizeof(uint32_t) <= kDoneCtrOff, "the verify slot precedes the counters");
+    dp->tiles_off = kPlanHeadBytes;
     dp->gen_off = dp->tiles_off + hp.tiles.size() * sizeof(FastTile);
     dp->seg_off = dp->gen_off + hp.gen.size() * sizeof(GenItem);
     dp->pieces_off = dp->seg_off + hp.seg.size() * sizeof(SegItem);
@@ -266,6 +308,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     if (!dp->uploaded) HIP_TRY(hipEventCreateWithFlags(&dp->uploaded, hipEventDisableTiming));
     uint8_t *img = dp->h;
     init_sched_slots(reinterpret_cast<uint32_t *>(img + dp->slots_off));
+    std::memset(img + kDoneCtrOff, 0, kDoneCtrs * kDoneCtrStride);
     std::memcpy(img + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
     std::memcpy(img + dp->gen_off, hp.gen.data(), hp.gen.size() * sizeof(GenItem));
     std::memcpy(img + dp->seg_off, hp.seg.data(), hp.seg.size() * sizeof(SegItem));
@@ -280,15 +323,14 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
 // Orders a launch on `stream` after the plan's upload: nothing once the
 // upload is known complete; else a stream wait on its event (or, while the
 // stream is being captured into a graph, a host wait: a capture cannot wait
-// on work outside it).  Notes the stream for the plan's release.
-int prepare_launch(crc32c_plan *plan, hipStream_t stream) {
+// on work outside it).
+int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing_out) {
     RelaxedCapture relaxed;  // (the queries below while another thread captures a graph)
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIP_TRY(hipStreamIsCapturing(stream, &cs));
     const bool capturing = cs != hipStreamCaptureStatusNone;
     if (capturing) plan->captured = true;
-    if (std::find(plan->launch_streams.begin(), plan->launch_streams.end(), stream) == plan->launch_streams.end())
-        plan->launch_streams.push_back(stream);
+    if (capturing_out) *capturing_out = capturing;
     DevicePlan *dp = &plan->dp;
     if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
         const hipError_t q = hipEventQuery(dp->uploaded);
@@ -307,12 +349,6 @@ int prepare_launch(crc32c_plan *plan, hipStream_t stream) {
     return 0;
 }
 
-void plan_forget_stream(crc32c_plan *plan, hipStream_t stream) {
-    std::lock_guard<std::mutex> lock(plan->mu);
-    auto &v = plan->launch_streams;
-    v.erase(std::remove(v.begin(), v.end(), stream), v.end());
-}
-
 void release_plan_blocks(crc32c_plan *plan) {
     crc32c_ctx *ctx = plan->ctx;
     DevicePlan *dp = &plan->dp;
@@ -322,43 +358,10 @@ void release_plan_blocks(crc32c_plan *plan) {
     r.dcap = dp->cap;
     r.h = dp->h;
     r.hcap = dp->hcap;
-    bool held = plan->captured;
-    // Per launch stream: nothing when it is idle (its launches of the plan
-    // are done -- the usual case: exec, synchronise, destroy), else an event
-    // recorded now (it completes after them).  The streams must still exist:
-    // a plan is destroyed before the streams it was launched on.
-    for (hipStream_t s : plan->launch_streams) {
-        if (held) break;
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
-            (void)hipGetLastError();
-            held = true;  // (a capture in progress on it may hold the plan's launches)
-            break;
-        }
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess) continue;
-        if (q != hipErrorNotReady) {
-            (void)hipGetLastError();
-            held = true;
-            break;
-        }
-        hipEvent_t e = nullptr;
-        {
-            std::lock_guard<std::mutex> lock(ctx->pool_mu);
-            e = take_event(ctx);
-        }
-        if ((!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) || hipEventRecord(e, s) != hipSuccess) {
-            (void)hipGetLastError();
-            if (e) {
-                std::lock_guard<std::mutex> lock(ctx->pool_mu);
-                ctx->spare_events.push_back(e);
-            }
-            held = true;
-            break;
-        }
-        r.events.push_back(e);
-    }
-    plan->launch_streams.clear();
+    // (no stream of the plan's launches is touched: the completion counters
+    // tell when they are done, reap_releases)
+    r.expected = plan->wgs_issued;
+    const bool held = plan->captured || plan->unaccounted || (r.expected && !r.h);
     if (dp->uploaded) r.events.push_back(dp->uploaded);
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
     if (held && r.d) {
@@ -378,7 +381,25 @@ void release_pools(crc32c_ctx *ctx) {
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
     for (Release &r : ctx->releases)
         for (hipEvent_t e : r.events) (void)hipEventSynchronize(e);
-    reap_releases(ctx);
+    // the destroyed plans' launches: their counters read back until they are
+    // complete (bounded: after 10 s the device is synchronised instead)
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+    for (;;) {
+        reap_releases(ctx);
+        if (ctx->releases.empty()) break;
+        if (std::chrono::steady_clock::now() > deadline) {
+            (void)hipDeviceSynchronize();
+            for (Release &r : ctx->releases) {
+                if (r.reading) (void)hipEventSynchronize(r.read_ev);
+                r.reading = false;
+                r.expected = 0;
+            }
+            reap_releases(ctx);
+            break;
+        }
+        (void)hipStreamSynchronize(ctx->upload_stream);  // (the read-backs)
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     if (!ctx->held.empty()) (void)hipDeviceSynchronize();  // (blocks graphs captured; graphs outlived by the context)
     for (auto &b : ctx->dev_pool.all) (void)hipFreeAsync(b.first, ctx->upload_stream);
     for (auto &b : ctx->held) (void)hipFreeAsync(b.first, ctx->upload_stream);
@@ -408,8 +429,10 @@ int alloc_slots(SchedSlots &s) {
 
 // Launches p on `stream`.  Verification launches use the sequence's slot
 // (left reset by the previous one); the caller keeps launches on `slots`
-// in GPU order.
-int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream, hipEvent_t stop = nullptr) {
+// in GPU order.  *grid: the workgroups launched (0: none).
+int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stream, hipEvent_t stop = nullptr,
+           uint32_t *grid = nullptr) {
+    if (grid) *grid = 0;
     const uint64_t items = uint64_t(p.ntiles) + p.ngen + p.nseg + p.nconst;
     if (!items) {
         if (stop) HIP_TRY(hipEventRecord(stop, stream));
@@ -421,7 +444,7 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
         if (rc) return rc;
         p.sched = slots.d;
     }
-    HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream, stop));
+    HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream, stop, grid));
     return 0;
 }
 
@@ -442,14 +465,20 @@ int order_plan_launch(crc32c_plan *plan, hipStream_t stream) {
 
 int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream, hipEvent_t stop = nullptr) {
     std::lock_guard<std::mutex> lock(plan->mu);
-    if (int rc = prepare_launch(plan, stream)) return rc;
+    bool capturing = false;
+    if (int rc = prepare_launch(plan, stream, &capturing)) return rc;
     if (p.expect) {  // only verify launches use the plan's scheduler slots
         int rc = order_plan_launch(plan, stream);
         if (rc) return rc;
         // (the mismatch bitmap is cleared by the launch itself, after that
         // wait: a previous verify still setting bits in it has finished)
     }
-    return launch(plan->ctx, p, plan->sched, stream, stop);
+    uint32_t grid = 0;
+    const int rc = launch(plan->ctx, p, plan->sched, stream, stop, &grid);
+    // (its workgroups count themselves into the plan's completion counters;
+    // a captured launch's plan block is never reused anyway)
+    if (!rc && !capturing) plan->wgs_issued += grid;
+    return rc;
 }
 
 constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK;
@@ -808,6 +837,7 @@ int crc32c_device_count(void) {
 int crc32c_ctx_create(int device, crc32c_ctx **out) {
     if (!out) return fail(-EINVAL, "out == NULL");
     *out = nullptr;
+    crc32c_ctx_destroy(nullptr);  // (tears down contexts a plan's destroy left for later)
     const int ndev = crc32c_device_count();
     if (ndev <= 0) return fail(-ENODEV, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(-ENODEV, "device %d out of range (%d visible)", device, ndev);
@@ -865,8 +895,30 @@ void ctx_teardown(crc32c_ctx *ctx) {
     delete ctx;
 }
 
-void ctx_release(crc32c_ctx *ctx) {
-    if (ctx->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) ctx_teardown(ctx);
+// Contexts whose last reference went with a plan's destroy: torn down by
+// the next crc32c_ctx_create / crc32c_ctx_destroy (plan destroy never
+// synchronises, frees device memory or destroys a stream: it may run while
+// another thread captures a graph), or left to process exit.
+std::mutex g_zombie_mu;
+std::vector<crc32c_ctx *> g_zombies;
+
+void reap_zombies() {
+    std::vector<crc32c_ctx *> z;
+    {
+        std::lock_guard<std::mutex> lock(g_zombie_mu);
+        z.swap(g_zombies);
+    }
+    for (crc32c_ctx *c : z) ctx_teardown(c);
+}
+
+void ctx_release(crc32c_ctx *ctx, bool defer) {
+    if (ctx->refs.fetch_sub(1, std::memory_order_acq_rel) != 1) return;
+    if (defer) {
+        std::lock_guard<std::mutex> lock(g_zombie_mu);
+        g_zombies.push_back(ctx);
+        return;
+    }
+    ctx_teardown(ctx);
 }
 
 }  // namespace
@@ -874,8 +926,9 @@ void ctx_release(crc32c_ctx *ctx) {
 extern "C" {
 
 int crc32c_ctx_destroy(crc32c_ctx *ctx) {
+    reap_zombies();
     if (!ctx) return 0;
-    ctx_release(ctx);
+    ctx_release(ctx, false);
     return 0;
 }
 
@@ -1066,7 +1119,7 @@ int crc32c_plan_destroy(crc32c_plan *plan) {
         if (plan->last_done) (void)hipEventDestroy(plan->last_done);
     }
     delete plan;
-    ctx_release(ctx);
+    ctx_release(ctx, true);
     return 0;
 }
 

@@ -135,8 +135,10 @@ extern "C" int crc32c_debug_plan_exec_variant(crc32c_plan *plan, const void *dev
     DeviceGuard guard(plan->ctx->device);
     KParams p = plan_params(plan, dev_payload, dev_out);
     p.stamps = dev_stamps;
+    p.done_ctr = nullptr;  // (not counted: the plan's block is never reused)
     const hipStream_t s = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lock(plan->mu);
+    plan->unaccounted = true;
     if (int rc = prepare_launch(plan, s)) return rc;
     HIP_TRY(variant == 0 ? launch_plan_kernel(p, uint32_t(plan->ctx->num_cu), s)
                          : launch_variant(p, *v, uint32_t(plan->ctx->num_cu), s));

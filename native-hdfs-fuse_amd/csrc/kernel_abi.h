@@ -70,6 +70,10 @@ struct KParams {
     // Verification slot of this launch (kSlotWords u32s): the key of the
     // launch that initialised p.result.
     uint32_t *sched;
+    // The plan's completion counters (kDoneCtrs u64s, kDoneCtrStride bytes
+    // apart), or null (launches that are not a plan's): the last wave of
+    // every workgroup adds 1 to counter blockIdx % kDoneCtrs.
+    unsigned long long *done_ctr;
     // Multi-block launch: nblocks > 0 runs the plan's block_tiles tiles once
     // per block (tile j = block j / block_tiles, tile j % block_tiles); the
     // plan has tiles only.  0: an ordinary launch.
@@ -89,6 +93,19 @@ struct KParams {
 constexpr uint32_t kEpochWord = 0;  // u64
 constexpr uint32_t kSlotWords = 32;
 
+// A plan's completion counters (crc32c_plan_destroy without touching the
+// launch streams): in the plan's device block after its verify slot,
+// kDoneCtrs u64 counters kDoneCtrStride bytes apart (one per XCD's
+// workgroups: workgroup b runs on XCD b % 8), zero at upload.  The last wave
+// of every workgroup of a plan launch adds 1 (a non-returning device-scope
+// atomic, after every read of the plan's memory); the host counts the
+// workgroups it launched, so a destroyed plan's block is reusable once the
+// counters sum to that (read back on the context's upload stream).
+constexpr uint32_t kDoneCtrOff = 256;
+constexpr uint32_t kDoneCtrs = 8;
+constexpr uint32_t kDoneCtrStride = 128;
+constexpr uint32_t kPlanHeadBytes = kDoneCtrOff + kDoneCtrs * kDoneCtrStride;  // the work items follow
+
 // Fills a slot's initial state (kSlotWords words): no launch's key.
 inline void init_sched_slots(uint32_t *w) {
     for (uint32_t i = 0; i < kSlotWords; ++i) w[i] = 0;
@@ -99,6 +116,8 @@ inline void init_sched_slots(uint32_t *w) {
 // min(work items, CUs) of them; p.expect selects the verification mode.
 // `stop` (optional): an event the launch itself completes (hipExtLaunchKernel's
 // stop event -- no extra command on the stream, unlike an hipEventRecord).
-hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop = nullptr);
+// `grid` (optional): the workgroups launched.
+hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop = nullptr,
+                              uint32_t *grid = nullptr);
 
 }  // namespace hdfs_crc

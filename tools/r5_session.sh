@@ -66,6 +66,10 @@ for s in ${STEPS:-calls multi}; do
     tres5) run tres5 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "resident or block_queue" ;;
     brate5) run brate5 400 tools/block_rate 16 400 16 30 2 1 ;;
     tall) run tall 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    callsab) for r in 1 2 3; do run calls_base_$r 120 abwt/tools/launch_rate calls 64 4000 && run calls_cand_$r 120 tools/launch_rate calls 64 4000 || exit 1; done ;;
+    kb16) run kb16_p2048 300 python tools/kbench.py --config p2048 --variants 0,2 --rounds 9 --iters 300 &&
+          run kb16_c2 300 python tools/kbench.py --config c2 --variants 0,2 --rounds 7 --iters 300 ;;
+    halvestrace) run halvestrace 300 rocprofv3 --kernel-trace -d $OUT/halvestrace -o run --output-format csv -- python3 tools/fixed_cost_probe.py --modes c2,c2_halves --rounds 1 --steps 300 ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
     tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
