@@ -61,6 +61,10 @@ int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n);
  * in ns: what the queue itself costs beside the submitting threads. */
 int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns);
 
+/* The device address of the pooled block holding a plan's descriptors (0:
+ * none): tests see a destroyed plan's block come back from the pool. */
+uint64_t crc32c_debug_plan_block(const crc32c_plan *plan);
+
 /* ---- 2. libhdfs_crc32c_debug.so only ---- */
 
 /* Launch of a plan with an explicit kernel variant (0 = production; see

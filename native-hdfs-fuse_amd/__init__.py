@@ -225,6 +225,7 @@ def _bind(L):
         "crc32c_blocks_stats": (i32, [vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]),
         "crc32c_blocks_destroy": (i32, [vp]),
         "crc32c_blocks_create_resident": (i32, [vp, u32, pp]),
+        "crc32c_debug_plan_block": (u64, [vp]),
         "crc32c_debug_blocks_fail_flushes": (i32, [vp, u32]),
         "crc32c_verify_frames_host": (i32, [vp, vp, sz, u32, u64, u32, ctypes.POINTER(FramesResult)]),
     }

@@ -22,6 +22,7 @@
 
 #include "crc_math.h"
 #include "hdfs_crc32c.h"
+#include "hdfs_crc32c_debug.h"
 #include "kernel_abi.h"
 #include "plan.h"
 #include "host_copy.h"
@@ -1124,6 +1125,9 @@ int crc32c_plan_destroy(crc32c_plan *plan) {
 }
 
 uint64_t crc32c_plan_nchecksums(const crc32c_plan *plan) { return plan ? plan->nchecksums : 0; }
+uint64_t crc32c_debug_plan_block(const crc32c_plan *plan) {
+    return plan ? uint64_t(reinterpret_cast<uintptr_t>(plan->dp.d)) : 0;
+}
 uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan) { return plan ? plan->payload_bytes : 0; }
 
 int crc32c_chunks_dev(crc32c_ctx *ctx, const crc32c_packet *pkts, size_t npkts, const void *dev_payload,

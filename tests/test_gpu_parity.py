@@ -734,6 +734,49 @@ def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
         ctx.close()
 
 
+def test_plan_destroyed_after_its_stream(hdfs, orc):
+    """a C caller (a FUSE daemon with per-thread streams)
+    may destroy a launch stream BEFORE the plan launched on it -- plan
+    destroy touches no stream; the plan's block returns to the pool once its
+    launches' workgroups have counted themselves complete (the completion
+    counters).  Raw HIP streams (torch pools its streams and never destroys
+    them): each plan is launched on a fresh stream, the stream destroyed at
+    once (its launch may still run), then the plan destroyed; later plans
+    reuse the destroyed plans' blocks, and every output is exact."""
+    import ctypes
+
+    torch = _torch()
+    hip = ctypes.CDLL("libamdhip64.so")  # (the process's HIP runtime, loaded by torch)
+    ctx = hdfs.Context(0)
+    pk = oracle.uniform_packets(8)
+    n = hdfs.total_checksums(pk)
+    try:
+        blocks, seen_again, jobs = set(), 0, []
+        for i in range(60):
+            payload = oracle.xorshift64_bytes(8 * 65536, 4400 + i)
+            dev = torch.from_numpy(payload).cuda()
+            out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            plan = hdfs.Plan(ctx, pk)
+            blk = int(hdfs.lib().crc32c_debug_plan_block(plan.handle))
+            seen_again += blk in blocks
+            blocks.add(blk)
+            s = ctypes.c_void_p()
+            assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+            plan.exec(dev.data_ptr(), out.data_ptr(), s.value)
+            assert hip.hipStreamDestroy(s) == 0  # (before the plan; its launch may still run)
+            plan.close()
+            jobs.append((payload, dev, out))
+            if i % 10 == 9:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        for payload, _, out in jobs:
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), orc.batch(payload, pk, n))
+        assert seen_again > 0, "no destroyed plan's block was reused"
+    finally:
+        ctx.close()
+
+
 def test_plan_destroyed_after_its_context(hdfs, orc):
     """A plan outliving crc32c_ctx_destroy (a garbage collector freeing a
     plan late, e.g. one a failed test's traceback held): the context is
