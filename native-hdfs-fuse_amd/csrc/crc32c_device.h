@@ -301,7 +301,9 @@ __device__ __forceinline__ uint32_t out_order(uint32_t crc, uint32_t flags) {
 // the bad-index list (vacc + kVaccList, kBadList of them), vacc[3] flags.
 constexpr uint32_t kBadList = 256;
 constexpr uint32_t kVaccList = 7;
-constexpr uint32_t kVaccTimedOut = 1u;  // vacc[3]: a key wait of this workgroup gave up
+constexpr uint32_t kVaccTimedOut = 1u;        // vacc[3]: a key wait of this workgroup gave up
+constexpr uint32_t kVaccFinishTimedOut = 2u;  // ... verify_finish's own (thread 0)
+constexpr uint32_t kVaccRedo = 4u;            // ... and the key appeared later: bits set again
 constexpr uint32_t kVerifyKeyPolls = 1u << 17;
 constexpr uint32_t kVerifyOverlapBit = 0x80000000u;
 
@@ -448,20 +450,24 @@ template <uint32_t THREADS>
 __device__ __forceinline__ void verify_finish(const KParams &p, uint32_t *vacc) {
     if (!vacc[0]) return;  // (uniform: read after the barrier)
     if (threadIdx.x == 0) {
-        if (!wait_launch_key(p)) vacc[3] |= kVaccTimedOut;
+        // (kVaccTimedOut may also come from a mismatch past the LDS list
+        // that gave up waiting: the result is then marked indeterminate)
+        if (!wait_launch_key(p)) vacc[3] |= kVaccTimedOut | kVaccFinishTimedOut;
         add_to_result(p, vacc, (vacc[3] & kVaccTimedOut) != 0);
     }
     __syncthreads();
     set_listed_bits<THREADS>(p, vacc);
-    if (!(vacc[3] & kVaccTimedOut)) return;
+    if (!(vacc[3] & kVaccFinishTimedOut)) return;  // (uniform)
+    // this workgroup added before workgroup 0's initialisation may have run:
+    // once the key appears (the initialisation done), add again
     __syncthreads();
     if (threadIdx.x == 0) {
         const bool late_init = wait_launch_key(p);
         if (late_init) add_to_result(p, vacc, true);
-        vacc[3] = late_init ? 2u : 0u;
+        vacc[3] = late_init ? kVaccRedo : 0u;
     }
     __syncthreads();
-    if (vacc[3] == 2u) set_listed_bits<THREADS>(p, vacc);
+    if (vacc[3] == kVaccRedo) set_listed_bits<THREADS>(p, vacc);
 }
 
 // ---- tiles: one wave, 16 blocks ------------------------------------------

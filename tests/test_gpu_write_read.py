@@ -384,6 +384,69 @@ def test_multi_plan_config4_rccl_gather(hdfs, golden, orc, self_send):
     m.close()
 
 
+def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc):
+    """several point-to-point transfers from ONE sender inside one
+    RCCL group, eagerly and graph-captured.  A file of 12 groups whose
+    checksum ranges leave gaps between groups (out_idx of group g starts at
+    g (n + 37)): the sender's local array is dense, the file-order places are
+    not, so no two transfers merge -- 12 ncclSend / ncclRecv pairs to self
+    (CRC32C_MULTI_SELF_SEND) match in posting order.  Every group's checksums
+    land in place, the gaps keep their sentinel, also after the stream
+    switches and in two graph replays; a second stream object freed before
+    the switch is kept alive by the plan (the next exec records an event on
+    it)."""
+    import gc
+
+    torch = _torch()
+    gp, ngroups, gap = 3, 12, 37
+    pk = oracle.uniform_packets(gp * ngroups)
+    per = 128 * gp
+    pk["out_idx"] = np.array([(i // gp) * (per + gap) + (i % gp) * 128 for i in range(pk.size)], np.uint64)
+    ln, xs = hdfs.multi_transfers(pk, gp, 1, hdfs.CRC32C_MULTI_SELF_SEND)
+    assert xs.shape == (ngroups, 4) and list(ln) == [per * ngroups]
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 16, 515)
+    total = int((pk["out_idx"] + 128).max())
+    want = np.full(total, 0x5A5A5A5A, np.uint32)
+    want_idx = np.concatenate([np.arange(g * (per + gap), g * (per + gap) + per) for g in range(ngroups)])
+    want[want_idx] = orc.batch(payload, pk, total)[want_idx]
+    m = hdfs.Multi([0])
+    mp = m.plan(pk, gp, hdfs.CRC32C_MULTI_SELF_SEND)
+    assert mp.nchecksums == total
+    layout, sb = hdfs.multi_layout(pk, gp, 1)
+    host = np.zeros(int(sb[0]) + 16, np.uint8)
+    for _, soff, poff, nbytes in layout.astype(np.int64):
+        host[soff:soff + nbytes] = payload[poff:poff + nbytes]
+    shard = torch.from_numpy(host).cuda()
+    out = torch.full((total,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    mp.exec([shard.data_ptr()], out.data_ptr())
+    m.sync()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    tmp = torch.cuda.Stream()
+    out.fill_(0x5A5A5A5A)
+    torch.cuda.synchronize()
+    mp.exec([shard.data_ptr()], out.data_ptr(), [tmp])
+    del tmp
+    gc.collect()
+    cs = torch.cuda.Stream()
+    mp.exec([shard.data_ptr()], out.data_ptr(), [cs])  # (switch: an event on the freed-by-caller stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cs, capture_error_mode="thread_local"):
+        for _ in range(2):
+            mp.exec([shard.data_ptr()], out.data_ptr(), [cs])
+    for _ in range(2):
+        out.fill_(0x5A5A5A5A)
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+    del graph
+    mp.close()
+    m.close()
+
+
 def test_multi_rank_mode_single_rank(hdfs, orc):
     """One-process-per-GPU communicator (ncclCommInitRank with an id from
     crc32c_multi_unique_id), nranks = 1: mixed-bpc blocks of ragged packets

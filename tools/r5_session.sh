@@ -70,6 +70,10 @@ for s in ${STEPS:-calls multi}; do
     kb16) run kb16_p2048 300 python tools/kbench.py --config p2048 --variants 0,2 --rounds 9 --iters 300 &&
           run kb16_c2 300 python tools/kbench.py --config c2 --variants 0,2 --rounds 7 --iters 300 ;;
     halvestrace) run halvestrace 300 rocprofv3 --kernel-trace -d $OUT/halvestrace -o run --output-format csv -- python3 tools/fixed_cost_probe.py --modes c2,c2_halves --rounds 1 --steps 300 ;;
+    calls4) for r in 1 2; do for w in abwt abwt_noatomic abwt_wg .; do n=$(basename $w); run calls_${n}_$r 120 $w/tools/launch_rate calls 64 4000 || exit 1; done; done ;;
+    tstream) run tstream 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "destroyed or recycled or context" ;;
+    pmcg) for c in ${PMCCFGS:-c2 c2b1000 c2b700}; do run pmc_$c 900 env PMC_CONFIG=$c PMC_OUT=$OUT/pmc_$c bash tools/pmc_session.sh || exit 1; done ;;
+    tmulti5) run tmulti5 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "multi" ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
     tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
