@@ -32,6 +32,7 @@ CRC32C_TYPE_CRC32 = 0x2  # Hadoop CHECKSUM_CRC32 (zlib polynomial) instead of CR
 CRC32C_DEVICE_ADDRESSES = 0x4  # plan flag: payload_off are device addresses; exec/verify take payload 0
 CRC32C_CPU_FALLBACK = 0x8  # crc32c_chunks / crc32c_batch_host: finish on the host CPU if the GPU fails
 CRC32C_MULTI_SELF_SEND = 0x10  # multi plan: rank 0's own checksums also go through RCCL (one-GPU transport test)
+CRC32C_COUNT_COMPLETION = 0x20  # plan: launches count their completion on the GPU; destroy after the streams is safe
 CRC32C_VERIFY_OVERLAP = 0x80000000  # bit 31 of a verify result's count: overlapping verify launches
 PATH_NONE, PATH_GPU, PATH_CPU = 0, 1, 2  # crc32c_last_path()
 

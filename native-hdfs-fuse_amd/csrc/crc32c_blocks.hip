@@ -505,6 +505,7 @@ int crc32c_blocks_destroy(crc32c_blocks *q) {
     DeviceGuard guard(q->device);
     if (q->stream) {
         (void)hipStreamSynchronize(q->stream);
+        plan_forget_stream(q->plan, q->stream);  // (idle now; the plan must not touch it once destroyed)
         (void)hipStreamDestroy(q->stream);
     }
     for (const auto &f : q->inflight)

@@ -146,7 +146,7 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     p.general = (dp.general ? kGeneralItems : 0u) |
                 ((dp.misaligned || dp.padded || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
     p.skip_z = dp.needs_z ? 0u : 1u;
-    p.done_ctr = reinterpret_cast<unsigned long long *>(dp.d + kDoneCtrOff);
+    p.done_ctr = plan->counted ? reinterpret_cast<unsigned long long *>(dp.d + kDoneCtrOff) : nullptr;
     return p;
 }
 
@@ -332,6 +332,9 @@ int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing_out) {
     const bool capturing = cs != hipStreamCaptureStatusNone;
     if (capturing) plan->captured = true;
     if (capturing_out) *capturing_out = capturing;
+    if (!plan->counted &&
+        std::find(plan->launch_streams.begin(), plan->launch_streams.end(), stream) == plan->launch_streams.end())
+        plan->launch_streams.push_back(stream);
     DevicePlan *dp = &plan->dp;
     if (!dp->ready.load(std::memory_order_acquire) && dp->uploaded) {
         const hipError_t q = hipEventQuery(dp->uploaded);
@@ -350,6 +353,12 @@ int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing_out) {
     return 0;
 }
 
+void plan_forget_stream(crc32c_plan *plan, hipStream_t stream) {
+    std::lock_guard<std::mutex> lock(plan->mu);
+    auto &v = plan->launch_streams;
+    v.erase(std::remove(v.begin(), v.end(), stream), v.end());
+}
+
 void release_plan_blocks(crc32c_plan *plan) {
     crc32c_ctx *ctx = plan->ctx;
     DevicePlan *dp = &plan->dp;
@@ -359,10 +368,50 @@ void release_plan_blocks(crc32c_plan *plan) {
     r.dcap = dp->cap;
     r.h = dp->h;
     r.hcap = dp->hcap;
-    // (no stream of the plan's launches is touched: the completion counters
-    // tell when they are done, reap_releases)
-    r.expected = plan->wgs_issued;
-    const bool held = plan->captured || plan->unaccounted || (r.expected && !r.h);
+    bool held = plan->captured || plan->unaccounted;
+    if (plan->counted) {
+        // (no stream of the plan's launches is touched: the completion
+        // counters tell when they are done, reap_releases)
+        r.expected = plan->wgs_issued;
+        held = held || (r.expected && !r.h);
+    }
+    // Per launch stream: nothing when it is idle (its launches of the plan
+    // are done -- the usual case: exec, synchronise, destroy), else an event
+    // recorded now (it completes after them).  The streams must still exist:
+    // a plan without CRC32C_COUNT_COMPLETION is destroyed before the streams
+    // it was launched on.
+    for (hipStream_t s : plan->launch_streams) {
+        if (held) break;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+            (void)hipGetLastError();
+            held = true;  // (a capture in progress on it may hold the plan's launches)
+            break;
+        }
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) continue;
+        if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            held = true;
+            break;
+        }
+        hipEvent_t e = nullptr;
+        {
+            std::lock_guard<std::mutex> lock(ctx->pool_mu);
+            e = take_event(ctx);
+        }
+        if ((!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) || hipEventRecord(e, s) != hipSuccess) {
+            (void)hipGetLastError();
+            if (e) {
+                std::lock_guard<std::mutex> lock(ctx->pool_mu);
+                ctx->spare_events.push_back(e);
+            }
+            held = true;
+            break;
+        }
+        r.events.push_back(e);
+    }
+    plan->launch_streams.clear();
     if (dp->uploaded) r.events.push_back(dp->uploaded);
     std::lock_guard<std::mutex> lock(ctx->pool_mu);
     if (held && r.d) {
@@ -482,7 +531,8 @@ int launch_plan(crc32c_plan *plan, const KParams &p, hipStream_t stream, hipEven
     return rc;
 }
 
-constexpr uint32_t kKnownFlags = CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK;
+constexpr uint32_t kKnownFlags =
+    CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32 | CRC32C_DEVICE_ADDRESSES | CRC32C_CPU_FALLBACK | CRC32C_COUNT_COMPLETION;
 
 int check_flags(uint32_t flags) {
     if (flags & ~kKnownFlags) return fail(-EINVAL, "unknown flags 0x%x", flags & ~kKnownFlags);
@@ -811,6 +861,7 @@ int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute
     p->nchecksums = hp.nchecksums;
     p->payload_bytes = hp.payload_bytes;
     p->flags = flags & (CRC32C_BIG_ENDIAN | CRC32C_TYPE_CRC32);
+    p->counted = (flags & CRC32C_COUNT_COMPLETION) != 0;
     p->abs_base = abs_base;
     p->absolute = absolute;
     DeviceGuard guard(ctx->device);

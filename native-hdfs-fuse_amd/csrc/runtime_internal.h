@@ -106,15 +106,16 @@ struct BlockPool {
 constexpr size_t kFreeBlocksMax = 48;
 
 // A destroyed plan's blocks, waiting for the GPU work that may still read
-// them: its upload's event, and its launches' workgroups -- the plan's
-// completion counters (kernel_abi.h kDoneCtrOff) must sum to `expected`,
-// the workgroups the plan's launches were issued with.  The counters are
-// read back (into the plan's pinned staging block) on the context's upload
-// stream; nothing touches the streams the plan was launched on, so a plan
-// may be destroyed after them.  Reusable once all of it has completed
-// (queried without blocking when a block is next needed) -- no device-wide
-// synchronisation, so other streams, other libraries' work and graph
-// captures on other threads are never waited on or disturbed.
+// them: an event recorded at destroy time on every stream the plan was
+// launched on that was still busy, and its upload's event -- or, for a
+// CRC32C_COUNT_COMPLETION plan, its upload's event and its launches'
+// workgroups: the plan's completion counters (kernel_abi.h kDoneCtrOff) must
+// sum to `expected`, read back (into the plan's pinned staging block) on the
+// context's upload stream, so nothing touches the streams the plan was
+// launched on.  Reusable once all of it has completed (queried without
+// blocking when a block is next needed) -- no device-wide synchronisation,
+// so other streams, other libraries' work and graph captures on other
+// threads are never waited on or disturbed.
 struct Release {
     uint8_t *d = nullptr, *h = nullptr;  // device block / pinned staging block (either may be null)
     size_t dcap = 0, hcap = 0;
@@ -178,15 +179,20 @@ struct crc32c_plan {
     hipStream_t last_stream = nullptr;
     hipEvent_t last_done = nullptr;
     bool launched = false;
-    // Workgroups the plan's launches were issued with (their completion
-    // counters gate the block's reuse, kernel_abi.h kDoneCtrOff), and whether
-    // a launch went into a graph capture or bypassed the count (then the
-    // block is never reused).  Round 4 noted every launch stream instead and
-    // queried / recorded events on them at destroy, so a plan had to be
-    // destroyed before its streams; round 3 gave every launch a stop event,
-    // which cost every launch.
-    uint64_t wgs_issued = 0;
+    // Every stream a launch of the plan went on (at destroy time: nothing to
+    // do for an idle one, else an event recorded on it gates the block's
+    // reuse), and whether a launch went into a graph capture (then the block
+    // is never reused).  (Round 3 first gave every launch a stop event to
+    // complete instead; that cost every launch)
+    std::vector<hipStream_t> launch_streams;
     bool captured = false;
+    // CRC32C_COUNT_COMPLETION plans: the workgroups their launches were
+    // issued with; their completion counters (kernel_abi.h kDoneCtrOff) gate
+    // the block's reuse instead of the streams, so such a plan may be
+    // destroyed after its streams.  unaccounted: a launch bypassed the count
+    // (debug variants): the block is never reused.
+    bool counted = false;
+    uint64_t wgs_issued = 0;
     bool unaccounted = false;
     hdfs_crc::DevicePlan dp;
     uint64_t nchecksums = 0, payload_bytes = 0;
@@ -206,9 +212,13 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
 // device (into *dp), asynchronously; plan_ready orders a launch after it.
 int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp);
 // Before a launch of `plan` on `stream` (caller holds plan->mu): orders it
-// after the plan's upload; *capturing: the stream is being captured (the
-// plan is then marked captured: its block is never reused).
+// after the plan's upload and notes the stream for the plan's release
+// (unless the plan counts its completion); *capturing: the stream is being
+// captured (the plan is then marked captured: its block is never reused).
 int prepare_launch(crc32c_plan *plan, hipStream_t stream, bool *capturing = nullptr);
+// `stream` (idle, about to be destroyed by the library itself: a block
+// queue's) no longer needs an event at the plan's release.
+void plan_forget_stream(crc32c_plan *plan, hipStream_t stream);
 // crc32c_plan_exec_blocks; `stop` (optional) is completed by the last launch.
 int exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs, size_t nblocks,
                 hipStream_t stream, hipEvent_t stop);

@@ -702,7 +702,8 @@ def test_plan_launches_across_streams(hdfs, gpu_ctx, orc):
     plan.close()
 
 
-def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
+@pytest.mark.parametrize("flags", [0, 0x20])  # (0x20: CRC32C_COUNT_COMPLETION, the counters gate reuse)
+def test_plans_destroyed_in_flight_and_recycled(hdfs, orc, flags):
     """Plan descriptors come from a recycled pool and are uploaded
     asynchronously: 100 plans of different shapes are each created, launched
     at once on a fresh non-blocking stream (the launch must wait for the
@@ -723,7 +724,7 @@ def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
             dev = torch.from_numpy(payload).cuda()
             out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
             torch.cuda.synchronize()
-            plan = hdfs.Plan(ctx, pk)
+            plan = hdfs.Plan(ctx, pk, flags)
             plan.exec(dev.data_ptr(), out.data_ptr(), s.cuda_stream)
             plan.close()  # (launch possibly still in flight)
             jobs.append((payload, pk, n, dev, out))
@@ -735,11 +736,11 @@ def test_plans_destroyed_in_flight_and_recycled(hdfs, orc):
 
 
 def test_plan_destroyed_after_its_stream(hdfs, orc):
-    """a C caller (a FUSE daemon with per-thread streams)
-    may destroy a launch stream BEFORE the plan launched on it -- plan
-    destroy touches no stream; the plan's block returns to the pool once its
-    launches' workgroups have counted themselves complete (the completion
-    counters).  Raw HIP streams (torch pools its streams and never destroys
+    """with CRC32C_COUNT_COMPLETION a C caller (a FUSE
+    daemon with per-thread streams) may destroy a launch stream BEFORE the
+    plan launched on it -- plan destroy touches no stream; the plan's block
+    returns to the pool once its launches' workgroups have counted
+    themselves complete (the completion counters).  Raw HIP streams (torch pools its streams and never destroys
     them): each plan is launched on a fresh stream, the stream destroyed at
     once (its launch may still run), then the plan destroyed; later plans
     reuse the destroyed plans' blocks, and every output is exact."""
@@ -757,7 +758,7 @@ def test_plan_destroyed_after_its_stream(hdfs, orc):
             dev = torch.from_numpy(payload).cuda()
             out = torch.full((n,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
             torch.cuda.synchronize()
-            plan = hdfs.Plan(ctx, pk)
+            plan = hdfs.Plan(ctx, pk, hdfs.CRC32C_COUNT_COMPLETION)
             blk = int(hdfs.lib().crc32c_debug_plan_block(plan.handle))
             seen_again += blk in blocks
             blocks.add(blk)
