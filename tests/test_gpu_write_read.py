@@ -743,6 +743,70 @@ def test_plans_created_while_another_thread_captures(hdfs, gpu_ctx, orc):
     plan.close()
 
 
+def test_last_plan_of_a_closed_context_destroyed_during_a_capture(hdfs, orc):
+    """a plan that outlives crc32c_ctx_destroy (a garbage
+    collector freeing it late) is the context's last reference; destroying it
+    must not tear the context down on the spot (stream synchronisation,
+    hipFree) while another thread captures a graph in global mode.  The
+    teardown is deferred to the next crc32c_ctx_create / _destroy: the
+    capture stays valid and replays exactly; the deferred context is torn
+    down by the next create."""
+    import threading
+
+    torch = _torch()
+    payload = oracle.xorshift64_bytes(64 * 65536, 56)
+    dpay = torch.from_numpy(payload).cuda()
+    pk = oracle.uniform_packets(64)
+    want = orc.batch(payload, pk, 8192)
+    keep = hdfs.Context(0)  # (its plan is what the capture records)
+    plan = keep.plan(pk)
+    out_g = torch.zeros(8192, dtype=torch.int32, device="cuda")
+    plan.exec(dpay.data_ptr(), out_g.data_ptr(), torch.cuda.current_stream())
+    doomed_ctx = hdfs.Context(0)
+    doomed = [doomed_ctx.plan(pk) for _ in range(3)]
+    outs = [torch.zeros(8192, dtype=torch.int32, device="cuda") for _ in doomed]
+    side = torch.cuda.Stream()
+    for p_, o in zip(doomed, outs):
+        p_.exec(dpay.data_ptr(), o.data_ptr(), side)
+    torch.cuda.synchronize()
+    doomed_ctx.close()  # (the plans hold it)
+    started, finished, errs = threading.Event(), threading.Event(), []
+
+    def worker():
+        started.wait(60)
+        try:
+            for p_ in doomed:
+                p_.close()  # (the last one drops the context's last reference)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+        finished.set()
+
+    t = threading.Thread(target=worker)
+    t.start()
+    g = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    try:
+        with torch.cuda.graph(g, stream=cap):  # capture_error_mode="global"
+            plan.exec(dpay.data_ptr(), out_g.data_ptr(), cap.cuda_stream)
+            started.set()
+            assert finished.wait(120)
+    finally:
+        started.set()
+        t.join()
+    assert not errs, errs
+    out_g.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out_g.cpu().numpy().view(np.uint32), want)
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want)
+    del g
+    hdfs.Context(0).close()  # (a create tears the deferred context down)
+    plan.close()
+    keep.close()
+
+
 # ---- many blocks of one shape in one launch (concurrent block writes) -------
 def _block_shape(kind):
     if kind == "full":  # one 4 MiB block of 64 x 64 KiB packets
