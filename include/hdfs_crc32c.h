@@ -151,11 +151,16 @@ int crc32c_device_count(void);
  * plan's device block is recycled only once those events (and its upload)
  * have completed.  So a plan is destroyed BEFORE the streams it was
  * launched on (an idle stream is only queried; HIP does not validate a
- * destroyed stream's handle).  Tracking every launch's completion instead
- * would lift that rule, but costs every eager launch (an event record:
- * +2.6 us of GPU time per 4 MiB block; a stop event per launch: a cost that
- * grows the longer a process runs).  A context may be
- * destroyed before its plans: it lives until its last plan is destroyed.
+ * destroyed stream's handle) -- unless it was created with
+ * CRC32C_COUNT_COMPLETION: its launches then count their own completion on
+ * the GPU (+~0.65 us per launch), destroy touches none of its streams, and
+ * the block is reused once the count is complete.  (An event record per
+ * launch costs +2.6 us of GPU time per 4 MiB block; a stop event per launch
+ * a cost that grows the longer a process runs)  A
+ * context may be destroyed before its plans: it lives until its last plan
+ * is destroyed, and is then torn down by the next crc32c_ctx_create /
+ * crc32c_ctx_destroy call (crc32c_ctx_destroy(NULL) does only that), never
+ * inside crc32c_plan_destroy.
  * No device-wide synchronisation on any plan create / destroy path, so work
  * of other streams and libraries is never waited on, and plans may be
  * created and destroyed while another thread captures a graph.  A plan must
