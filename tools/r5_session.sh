@@ -75,6 +75,8 @@ for s in ${STEPS:-calls multi}; do
     pmcg) for c in ${PMCCFGS:-c2 c2b1000 c2b700}; do run pmc_$c 900 env PMC_CONFIG=$c PMC_OUT=$OUT/pmc_$c bash tools/pmc_session.sh || exit 1; done ;;
     tmulti5) run tmulti5 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "multi" ;;
     calls2) for r in 1 2; do run calls_base_$r 120 abwt/tools/launch_rate calls 64 4000 && run calls_head_$r 120 tools/launch_rate calls 64 4000 || exit 1; done ;;
+    prof5) run prof5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5 -o run --output-format csv -- python3 bench.py --no-config4 --no-strong ;;
+    prof5d) run prof5d 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5d -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
     tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
