@@ -419,7 +419,9 @@ int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t
  * execs on the same stream cost no extra HIP call; an exec on another stream
  * than the plan's previous one records an event on that previous stream, so
  * that stream must still exist then.  flags: CRC32C_BIG_ENDIAN,
- * CRC32C_TYPE_CRC32, CRC32C_MULTI_SELF_SEND. */
+ * CRC32C_TYPE_CRC32, CRC32C_MULTI_SELF_SEND, CRC32C_COUNT_COMPLETION.  A plan
+ * whose gather would post more than 4096 transfers (crc32c_multi_transfers;
+ * a tiny group_packets over a large file) is refused with -E2BIG. */
 #define CRC32C_MULTI_SELF_SEND 0x10u /* crc32c_multi_plan_create: rank 0's own checksums also travel
                                        through RCCL (a send to itself) instead of being written in
                                        place -- exercises the transport on a one-GPU communicator */

@@ -201,6 +201,8 @@ struct Xfer {
     int rank;
     uint64_t local, file, count;
 };
+// Transfers one exec's RCCL group may hold (crc32c_multi_plan_create refuses more).
+constexpr size_t kMaxGatherTransfers = 4096;
 
 bool sends(int rank, bool self_send) { return rank != 0 || self_send; }
 
@@ -475,6 +477,12 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
     }
     build_transfers(mp->groups, mp->self_send, &mp->xfers);
     if (mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
+    // (every transfer is one ncclSend / ncclRecv of the exec's one RCCL
+    // group: bounded, so a tiny group_packets cannot post thousands of
+    // point-to-point operations per exec)
+    if (mp->xfers.size() > kMaxGatherTransfers)
+        return fail(-E2BIG, "%zu gather transfers (at most %zu): use a larger group_packets", mp->xfers.size(),
+                    kMaxGatherTransfers);
     *out = mp.release();
     return 0;
 }

@@ -447,6 +447,22 @@ def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc):
     m.close()
 
 
+def test_multi_plan_refuses_too_many_gather_transfers(hdfs):
+    """A gather of more than 4096 point-to-point transfers in one RCCL group
+    (here 4100 one-packet groups whose checksum ranges leave gaps, sent to
+    self) is refused at plan creation with -E2BIG instead of being posted."""
+    pk = oracle.uniform_packets(4100, 512, 512)
+    pk["out_idx"] = np.arange(4100, dtype=np.uint64) * 2  # (a gap after every group)
+    m = hdfs.Multi([0])
+    try:
+        with pytest.raises(hdfs.Crc32cError) as e:
+            m.plan(pk, 1, hdfs.CRC32C_MULTI_SELF_SEND)
+        assert e.value.rc == -7 and "group_packets" in str(e.value)  # -E2BIG
+        m.plan(pk[:4000], 1, hdfs.CRC32C_MULTI_SELF_SEND).close()  # (4000 transfers: accepted)
+    finally:
+        m.close()
+
+
 def test_multi_rank_mode_single_rank(hdfs, orc):
     """One-process-per-GPU communicator (ncclCommInitRank with an id from
     crc32c_multi_unique_id), nranks = 1: mixed-bpc blocks of ragged packets
