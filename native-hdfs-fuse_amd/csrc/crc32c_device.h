@@ -106,9 +106,10 @@ constexpr int kModeGeneral = 256;   // the batch has general tiles (a plan witho
 // schedule to itself
 constexpr int kModeNoShift = 32768;
 constexpr int kModeNoGItems = 65536;
+constexpr int kModeGHoist = 131072;  // A/B: a general item's next subtile facts computed before this subtile's lookups
 // GEN bits of the tile helpers below: general tiles, shifted (unaligned)
 // tiles, general items gathered 4 subtiles at a time (finish_gtile GROUP)
-constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8;
+constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16;
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -709,8 +710,8 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
                                             uint4 v[9], uint32_t ev, int lane) {
     uint32_t pc[8];
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
-        finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, (GEN & kGenGroup4) ? 4u : (GEN & kGenGroup2) ? 2u : 1u>(
-            p, lds, vacc, t, v, ev, lane);
+        finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, (GEN & kGenGroup4) ? 4u : (GEN & kGenGroup2) ? 2u : 1u,
+                     (GEN & kGenHoist) != 0>(p, lds, vacc, t, v, ev, lane);
         return;
     }
     const uint32_t r = (GEN & kGenShift) && !COMPDIAG ? tile_misalign(p, t) : 0u;
@@ -831,7 +832,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
     constexpr bool GENERAL = (MODE & kModeGeneral) != 0;
     constexpr int GEN = !GENERAL ? 0
                                  : ((MODE & kModeNoGItems) ? 0 : kGenItems) |
-                                       ((MODE & kModeNoShift) ? kGenGroup4 : (kGenShift | kGenGroup2));
+                                       ((MODE & kModeNoShift) ? kGenGroup4 : (kGenShift | kGenGroup2)) |
+                                       ((MODE & kModeGHoist) ? kGenHoist : 0);
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
     constexpr bool XCDMAP = (MODE & kModeXcdMap) != 0;

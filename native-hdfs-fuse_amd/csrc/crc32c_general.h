@@ -267,7 +267,7 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
 // -> 69.7 us, bpc 1000 58.1 -> 57.3; with 4, bpc 1000's verify had run
 // 61.8 -> 63.5).  Each subtile's loads are issued
 // after the previous one's lookups.
-template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, uint32_t GROUP = 1>
+template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, uint32_t GROUP = 1, bool HOIST = false>
 __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                              uint4 v[8], uint32_t ev, int lane) {
     const GShape g = gshape(t);
@@ -288,17 +288,25 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     uint32_t acc = 0;
     uint32_t comb = 0;  // row r: subtile 4 q + r's blocks, in block order
     uint32_t shv = 0;   // ... and each block's distance to its chunk's end
+    // (HOIST, A/B: subtile s + 1's facts are computed right after subtile
+    // s's loads are issued, so their scalar loads overlap its lookups and a
+    // padded subtile's loads need not wait for them)
+    GSub gsn = HOIST ? gsub(g, 0, st) : GSub{};
     for (uint32_t s = 0; s < nsub; ++s) {
         // Unpadded items' loads need no block facts: issue them before the
         // subtile's pattern-table fetches (two dependent scalar loads).
         const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
         if (contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
-        const GSub gs = gsub(g, s, st);
+        const GSub gs = HOIST ? gsn : gsub(g, s, st);
         if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
+        if (HOIST) {
+            gstate_next(g, gs, st);
+            if (s + 1u < nsub) gsn = gsub(g, s + 1u, st);
+        }
         uint32_t pc[8];
         gsub_pieces<DIAG, S4, IMG>(lds, g, gs, kp, v, pc, lane);
         const uint32_t x = block_lin(pc, lane);
-        gstate_next(g, gs, st);
+        if (!HOIST) gstate_next(g, gs, st);
         if (DIAG & 2) {  // DIAGNOSTIC (debug variants only, wrong results): no per-subtile gather
             acc ^= x;
             continue;

@@ -61,6 +61,9 @@ constexpr Variant kVariants[] = {
     {72, "s4_nt_compute_only_nogather_nomask", 768, 1, false},
     {73, "s4_nt_nogather", 768, 1, false},
     {74, "s4_nt_nomask", 768, 1, false},
+    // A/B (round 5): the general build (49) with a general item's next
+    // subtile facts computed right after the current subtile's loads
+    {75, "s4_nt_general_hoist_prodgrid", 768, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -113,6 +116,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 72: HDFS_LAUNCH(768, 3, kS4Nt | kModeCompDiag | kModeGDiagNoGather | kModeGDiagNoMask); break;
     case 73: HDFS_LAUNCH(768, 3, kS4Nt | kModeGDiagNoGather); break;
     case 74: HDFS_LAUNCH(768, 3, kS4Nt | kModeGDiagNoMask); break;
+    case 75: HDFS_LAUNCH(768, 3, kS4Nt | kModeGHoist); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
