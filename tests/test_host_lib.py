@@ -545,6 +545,15 @@ def test_plan_keeps_stream_objects_alive():
     p._streams = {}
     s = FakeStream()
     assert p._stream(s) == 0x1234 and p._stream(7) == 7
+    # (None = the default stream, numpy integers are handles too)
+    import numpy as np
+    assert p._stream(None) == 0 and p._stream(np.int64(9)) == 9 and p._stream(np.uint64(11)) == 11
     assert p._streams == {0x1234: s}
     p.close()
     assert p._streams == {}
+    mp = pkg.MultiPlan.__new__(pkg.MultiPlan)  # (MultiPlan.exec keeps its stream objects the same way)
+    mp.handle = None
+    mp._streams = {}
+    assert pkg._stream_handle(s, mp._streams) == 0x1234 and mp._streams == {0x1234: s}
+    mp.close()
+    assert mp._streams == {}
