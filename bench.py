@@ -637,7 +637,9 @@ def run_config4(hdfs, args, env) -> dict:
         "shard_bytes_max": per_rank_max,
         "shard_frac_of_hbm_roofline": None if not shard_max else
         round(per_rank_max / (shard_max * 1e-6) / 1e9 / PEAK_HBM_GBS, 4),
-        "gather_us": None if shard_max is None else round(step_kernel_us - shard_max, 3),
+        # (what the in-step gather adds: the step minus the shard's launch;
+        # none without transfers -- N = 1 in place)
+        "gather_us": None if (shard_max is None or not int(xs.shape[0])) else round(step_kernel_us - shard_max, 3),
         "transfers": int(xs.shape[0]), "self_send": self_send,
         "bit_exact": exact,
         "bit_exact_checks": {"before_warmup_file0": gate, "timed_file_buf%d" % b_last: timed} if rank == 0 else None,
