@@ -616,6 +616,12 @@ def run_config4(hdfs, args, env) -> dict:
         rs = time_steps(env, args, sstep, sstep, use_graph=r["use_graph"], settle_ms=min(args.settle_ms, 50.0))
         shard_max = rs["kernel_ms"] * 1e3  # (max over ranks)
     exact = agree_min(env, gate and timed)
+    # the step graphs hold the RCCL group's captured calls: destroyed before
+    # the communicator
+    torch.cuda.synchronize()
+    r["graphs"].clear()
+    if "rs" in locals():
+        rs["graphs"].clear()
     close_multi()
     if splan is not None:
         splan.close()
