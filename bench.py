@@ -610,6 +610,7 @@ def run_config4(hdfs, args, env) -> dict:
     # when the step was: what the gather adds to a step is the difference
     # (every rank or none: the timing holds collectives)
     shard_max = None
+    rs = None
     if not rehearsal and agree_min(env, splan is not None):
         def sstep(i, sp=None):
             splan.exec(bufs[i % nbuf].data_ptr(), local_out.data_ptr(), sptr if sp is None else sp)
@@ -620,7 +621,7 @@ def run_config4(hdfs, args, env) -> dict:
     # the communicator
     torch.cuda.synchronize()
     r["graphs"].clear()
-    if "rs" in locals():
+    if rs is not None:
         rs["graphs"].clear()
     close_multi()
     if splan is not None:
