@@ -754,6 +754,9 @@ def main():
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-config4", action="store_true", help="skip the config4 sub-object of the c2 line")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong_scaling sub-object of the c2 line")
+    ap.add_argument("--sub-timeout-s", type=float, default=300.0,
+                    help="bound on the config4 + strong_scaling sub-runs and the teardown after them: past it "
+                         "rank 0 prints the main line with the sub-objects marked timed out and every rank exits")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak (default): every rank checksums its own config batch; strong: the config-2/5 batch's "
                          "packets are split evenly over the ranks (SURVEY.md section 8e)")
@@ -1164,16 +1167,7 @@ def main():
                 host_sweep = {"sizes": host_sweep,
                               "gpu_pinned_beats_reference_1t_from_bytes": min(cross) if cross else None}
 
-    # The other two shapes of the 1/2/4/8-GPU curve, on the default line at
-    # every N (the driver only runs the default command): config 4's file
-    # step with its in-step RCCL gather, and config 2 split over the ranks.
-    config4 = strong = None
-    if args.config == "c2" and args.scaling == "weak":
-        if not args.no_config4:
-            config4 = run_config4(hdfs, args, env)
-        if not args.no_strong:
-            strong = run_strong(hdfs, args, env, ctx)
-
+    line = None
     if rank == 0:
         pmc = latest_pmc(os.path.join(ROOT, "profiles"), args.config)
         traffic = traffic_commit = None
@@ -1226,14 +1220,97 @@ def main():
             "gather_ms": None if gather_ms is None else round(gather_ms, 3),
             "launch": launch_text(r),
             "eager_ms_per_step": None if eager_ms is None else round(eager_ms, 5),
-            "config4": config4,
-            "strong_scaling": strong,
+            "config4": None,
+            "strong_scaling": None,
         }
+
+    # The other two shapes of the 1/2/4/8-GPU curve, on the default line at
+    # every N (the driver only runs the default command): config 4's file
+    # step with its in-step RCCL gather, and config 2 split over the ranks.
+    # They run after the main line is complete, under a watchdog: a sub-run
+    # that raises is reported in its sub-object, and one that hangs (a
+    # collective some rank never joins) or a teardown that does cannot cost
+    # the main line.
+    sub = args.config == "c2" and args.scaling == "weak" and not (args.no_config4 and args.no_strong)
+    wd = SubRunWatchdog(args.sub_timeout_s, line) if sub else None
+    if sub:
+        wd.start()
+        if not args.no_config4:
+            line_set(line, "config4", wd.run("config4", run_config4, hdfs, args, env))
+        if not args.no_strong and not wd.failed:
+            line_set(line, "strong_scaling", wd.run("strong_scaling", run_strong, hdfs, args, env, ctx))
+    if wd is not None:
+        wd.publish()
+    elif line is not None:
         print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+    if wd is not None:
+        wd.cancel()
+
+
+def line_set(line, key, value):
+    if line is not None:
+        line[key] = value
+
+
+class SubRunWatchdog:
+    """Bounds the sub-runs that follow the main measurement (and the teardown
+    after them).  A sub-run that raises is recorded as {"error": ...} in its
+    sub-object and the sub-runs after it are skipped (a rank that left a
+    collective sequence would leave its peers waiting).  If the bound passes
+    first, rank 0 prints the main line -- the sub-objects it has, the others
+    marked timed out -- and every rank ends its process: the peers of a hung
+    collective are stuck in the same place, each under its own watchdog."""
+
+    def __init__(self, seconds, line):
+        import threading
+
+        self.seconds, self.line = seconds, line
+        self.failed = False
+        self.printed = False
+        self.current = None
+        self.lock = threading.Lock()
+        self.timer = threading.Timer(seconds, self._fire)
+        self.timer.daemon = True
+
+    def start(self):
+        self.timer.start()
+
+    def run(self, name, fn, *a):
+        self.current = name
+        try:
+            return fn(*a)
+        except Exception as e:  # (reported, not raised: the main line is already measured)
+            self.failed = True
+            return {"error": "%s: %s" % (type(e).__name__, e)}
+        finally:
+            self.current = None
+
+    def publish(self):
+        with self.lock:
+            if self.line is not None and not self.printed:
+                print(json.dumps(self.line), flush=True)
+                self.printed = True
+
+    def cancel(self):
+        self.timer.cancel()
+
+    def _fire(self):
+        with self.lock:
+            if self.line is not None and not self.printed:
+                for key in ("config4", "strong_scaling"):
+                    if self.line.get(key) is None:
+                        self.line[key] = {"error": "timed out: the sub-runs passed --sub-timeout-s %.0f s%s"
+                                          % (self.seconds, " in " + self.current if self.current else "")}
+                print(json.dumps(self.line), flush=True)
+                self.printed = True
+            sys.stdout.flush()
+            sys.stderr.write("bench: sub-run watchdog fired after %.0f s; exiting\n" % self.seconds)
+            sys.stderr.flush()
+            os._exit(0)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,8 @@
 //     tails) and the shifted loads of tiles off 16-byte alignment, in three
 //     forms: both paths, general tiles only, shifted tiles only (a build
 //     without the path a batch does not need has its registers and schedule
-//     to the other path);
+//     to the other path); the both-paths form, which padded chunks run,
+//     computes a general item's next subtile facts ahead (kModeGHoist);
 //   * compact image (28 KiB staged instead of 152 KiB, with the general-tile
 //     code): batches of at most kSmallBatchItemsPerCu work items per CU,
 //     where the table staging is most of a launch (one 4 MiB block: 5.8 ->
@@ -71,7 +72,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
         else if (p.general == kGeneralShift)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoGItems | kModeVerify>));
         else if (p.general)
-            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeVerify>));
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeVerify>));
         else
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeVerify>));
     } else {
@@ -84,7 +85,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
         else if (p.general == kGeneralShift)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoGItems>));
         else if (p.general)
-            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen>));
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist>));
         else
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd>));
     }

@@ -44,7 +44,7 @@ constexpr Variant kVariants[] = {
     {46, "s4c_wg256_nt_early", 256, 4, true},              // 44, first tile's loads before the staging
     {47, "s4c_wg128_nt_early", 128, 8, true},              // 45, first tile's loads before the staging
     {48, "s4c_nt_early_prodgrid", 768, 1, true, true},     // 41, first tile's loads before the staging
-    {49, "s4_nt_general_prodgrid", 768, 1, true, true},    // the full-image production build, any batch size
+    {49, "s4_nt_general_prodgrid", 768, 1, true, true},    // the full-image general build without the hoist (75), any batch
     {51, "s4c_nt_quarter_prodgrid", 768, 1, true, true},   // 41 with quarter units (4 per tile)
     {52, "s4c_nt_quarter_early_prodgrid", 768, 1, true, true},  // 51, first unit's loads before the staging
     {53, "s4_nt_quarter_prodgrid", 768, 1, true, true},    // 49 (full image) with quarter units
@@ -61,9 +61,15 @@ constexpr Variant kVariants[] = {
     {72, "s4_nt_compute_only_nogather_nomask", 768, 1, false},
     {73, "s4_nt_nogather", 768, 1, false},
     {74, "s4_nt_nomask", 768, 1, false},
-    // A/B (round 5): the general build (49) with a general item's next
+    // (round 5, production since): the general build (49) with a general item's next
     // subtile facts computed right after the current subtile's loads
     {75, "s4_nt_general_hoist_prodgrid", 768, 1, true, true},
+    // the general-tiles-only production build (what variant 0 runs for a
+    // batch of general items and no shifted tiles) with the same hoist, with
+    // a 2-subtile gather, and with both
+    {76, "s4_nt_gitems_hoist_prodgrid", 768, 1, true, true},
+    {77, "s4_nt_gitems_group2_prodgrid", 768, 1, true, true},
+    {78, "s4_nt_gitems_group2_hoist_prodgrid", 768, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -117,6 +123,9 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 73: HDFS_LAUNCH(768, 3, kS4Nt | kModeGDiagNoGather); break;
     case 74: HDFS_LAUNCH(768, 3, kS4Nt | kModeGDiagNoMask); break;
     case 75: HDFS_LAUNCH(768, 3, kS4Nt | kModeGHoist); break;
+    case 76: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGHoist); break;
+    case 77: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGGroup2); break;
+    case 78: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGGroup2 | kModeGHoist); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
