@@ -77,7 +77,7 @@ for s in ${STEPS:-calls multi}; do
     calls2) for r in 1 2; do run calls_base_$r 120 abwt/tools/launch_rate calls 64 4000 && run calls_head_$r 120 tools/launch_rate calls 64 4000 || exit 1; done ;;
     prof5) run prof5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5 -o run --output-format csv -- python3 bench.py --no-config4 --no-strong ;;
     prof5d) run prof5d 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5d -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
-    kbhoist) for c in ${KBCFGS:-c2b1000 c2b700 c2b1536}; do run kbh_$c 300 python tools/kbench.py --config $c --variants 0,49,75,2 --rounds 9 --iters 300 || exit 1; done ;;
+    kbhoist) for c in ${KBCFGS:-c2b1000 c2b700 c2b1536}; do run kbh_$c 300 python tools/kbench.py --config $c --variants ${KBV:-0,49,75,2} --rounds 9 --iters 300 || exit 1; done ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
     c4x20) for r in 1 2; do run c4_20_$r 300 python bench.py --config c4 --steps 20 --warmup 5 --no-cpu --no-host || exit 1; done ;;
     tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
