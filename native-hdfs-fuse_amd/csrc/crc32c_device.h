@@ -592,10 +592,11 @@ __device__ __forceinline__ uint32_t block_lin(const uint32_t pc[8], int lane) {
     return x;
 }
 
-// Power-of-two tile: blocks combined per chunk, chunk checksums stored (or compared).
+// Power-of-two tile: blocks combined per chunk, chunk checksums stored (or
+// compared); cst = the chunk length's affine constant crc(0, zeros(bpc)).
 template <bool S4, bool VERIFY, int IMG>
 __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
-                                            const uint32_t pc[8], uint32_t ev, int lane) {
+                                            const uint32_t pc[8], uint32_t ev, int lane, uint32_t cst) {
     const uint32_t nb = t.meta & 0xffu;
     const uint32_t lg = (t.meta >> 8) & 0xffu;
     uint32_t x = block_lin(pc, lane);
@@ -609,8 +610,13 @@ __device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds
         if (lg >= 3) x ^= dpp<kDppXor2>(x);                               // block bit 2 = lane bit 1
         if (lg >= 4) x ^= dpp<kDppXor1>(x);                               // block bit 3 = lane bit 0
     }
-    const uint32_t crc = x ^ p.c_lg[lg];
+    const uint32_t crc = x ^ cst;
     if (rep_lane(lane, blk, nb, lg)) emit<VERIFY>(p, vacc, t.out + (blk >> lg), crc, ev);
+}
+template <bool S4, bool VERIFY, int IMG>
+__device__ __forceinline__ void reduce_emit(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            const uint32_t pc[8], uint32_t ev, int lane) {
+    reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane, p.c_lg[(t.meta >> 8) & 0xffu]);
 }
 
 }  // namespace hdfs_crc_dev
@@ -707,6 +713,52 @@ struct ShiftPrep {
     }
 };
 
+// ---- padded power-of-two tiles (builds with the general-tile code) -------
+// bpc = 512 * 2^lg - pad (plan.h): chunk j of the tile is virtual blocks
+// j 2^lg .. (j + 1) 2^lg - 1, its data right-aligned behind pad zero bytes
+// (leading zeros leave lin() unchanged), so the tile reduces like a
+// power-of-two one and only the affine constant differs.  Lane q of block b
+// reads bytes 512 (b mod 2^lg) + 16 q - pad of chunk b >> lg through a
+// descriptor that starts 16 bytes before the tile (the straddling lane
+// reads up to 15 bytes before a chunk); lanes wholly inside a pad read
+// zeros without touching memory, and the straddling lane's bytes before the
+// chunk are masked (PadPrep).  Round 5: these chunks ran as general items
+// before (per-subtile gather, block facts on the scalar unit).
+__device__ __forceinline__ uint32_t tile_pad(FastTile t) { return (t.meta >> 18) & 511u; }
+
+template <int AUX, bool VERIFY>
+__device__ __forceinline__ void load_tile_padded(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
+    const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu, pad = tile_pad(t);
+    const uint32_t bpc = (512u << lg) - pad;
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + t.src - 16u, 16u + (nb >> lg) * bpc);
+    const uint32_t h = uint32_t(lane) >> 5, q16 = 16u * (uint32_t(lane) & 31u);
+    const uint32_t km = (1u << lg) - 1u;
+    const bool inpad = q16 + 16u <= pad;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t b = 2u * uint32_t(i) + h;
+        const uint32_t w = b & km;  // block of its chunk
+        const bool skip = (w == 0u && inpad) || b >= nb;
+        const uint32_t off = 16u + (b >> lg) * bpc + 512u * w + q16 - pad;
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, skip ? 0x80000000u : off, 0, AUX);
+        v[i] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+    if (VERIFY) {
+        const uint32_t blk = rep_block(lane);
+        if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// A chunk's first block: lane q keeps its bytes at positions >= pad - 16 q.
+struct PadPrep {
+    uint4 kp;
+    uint32_t h, km;
+    __device__ __forceinline__ void operator()(int i, uint4 &x) const {
+        apply_keep(x, kp, 0u - uint32_t(((2u * uint32_t(i) + h) & km) == 0u));
+    }
+};
+
 template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, int GEN>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             uint4 v[9], uint32_t ev, int lane) {
@@ -714,6 +766,16 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, (GEN & kGenGroup4) ? 4u : (GEN & kGenGroup2) ? 2u : 1u,
                      (GEN & kGenHoist) != 0>(p, lds, vacc, t, v, ev, lane);
+        return;
+    }
+    if ((GEN & kGenItems) && tile_pad(t)) {
+        const uint32_t pad = tile_pad(t), lg = (t.meta >> 8) & 0xffu;
+        const PadPrep prep{keep_masks(int(pad) - int(16u * (uint32_t(lane) & 31u))), uint32_t(lane) >> 5,
+                           (1u << lg) - 1u};
+        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, prep);
+        typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
+        const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
+        reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane, zc[(512u << lg) - pad]);
         return;
     }
     const uint32_t r = (GEN & kGenShift) && !COMPDIAG ? tile_misalign(p, t) : 0u;
@@ -736,6 +798,8 @@ template <int AUX, bool COMPDIAG, bool VERIFY, int GEN>
 __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[9], uint32_t &ev) {
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         load_gtile<VERIFY>(p, t, lane, ev);
+    } else if ((GEN & kGenItems) && !COMPDIAG && tile_pad(t)) {
+        load_tile_padded<AUX, VERIFY>(p, t, lane, v, ev);
     } else if ((GEN & kGenShift) && !COMPDIAG && tile_misalign(p, t)) {
         load_tile_shifted<AUX, VERIFY>(p, t, tile_misalign(p, t), lane, v, ev);
     } else {
@@ -761,7 +825,7 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     const FastTile x = tile_at(p, j / SPLIT);
     const uint32_t u = j % SPLIT;
     const uint32_t lg = (x.meta >> 8) & 0xffu;
-    if (((GEN & kGenItems) && (x.meta & kGeneralTile)) || (1u << lg) > kUB) {
+    if (((GEN & kGenItems) && ((x.meta & kGeneralTile) || tile_pad(x))) || (1u << lg) > kUB) {
         if (u) return 0;
         ft = x;
         load_any<AUX, COMPDIAG, VERIFY, GEN>(p, ft, lane, v, ev);

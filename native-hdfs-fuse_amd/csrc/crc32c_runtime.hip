@@ -89,9 +89,11 @@ static KParams base_params(const crc32c_ctx *ctx, const void *payload, uint32_t 
     return p;
 }
 
+// General tiles or padded power-of-two tiles: both run in the builds with
+// the general-tile code (kGeneralItems).
 static bool has_general(const HostPlan &hp) {
     for (const FastTile &t : hp.tiles)
-        if (t.meta & kGeneralTile) return true;
+        if ((t.meta & kGeneralTile) || tile_pad_bits(t.meta)) return true;
     return false;
 }
 
@@ -126,7 +128,7 @@ static bool has_padded_general(const HostPlan &hp) {
 // shifted loads read it from the aligned address below).
 static bool has_misaligned(const HostPlan &hp) {
     for (const FastTile &t : hp.tiles)
-        if (!(t.meta & kGeneralTile) && (t.src & 15u)) return true;
+        if (!(t.meta & kGeneralTile) && !tile_pad_bits(t.meta) && (t.src & 15u)) return true;
     return false;
 }
 

@@ -69,6 +69,13 @@ static uint64_t item_chunks(uint32_t k) {
     return n;
 }
 
+// Padded power-of-two tiles for bpc = 512 * 2^lg - pad (plan.h); A/B knob
+// HDFS_CRC32C_PADDED_TILES=0 sends those chunks to general items instead.
+static bool padded_tiles_on() {
+    static const bool on = env_long("HDFS_CRC32C_PADDED_TILES") != 0;
+    return on;
+}
+
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
     // A zero-length packet (the block's last-packet marker, hadooprpc.c:644,
     // 853-856) has no checksums whatever its bpc; any other needs bpc > 0.
@@ -110,12 +117,38 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         // (offset >= 16) or, for device addresses, the same page.
         const uint32_t k = (p.bpc + kBlockBytes - 1) / kBlockBytes;
         const uint32_t pad = k * kBlockBytes - p.bpc;
+        const auto early_ok = [&](uint64_t src) { return absolute ? (src & 4095u) >= 16 : src >= 16; };
+        uint64_t c = 0;
+        const int klg = fast_lg(k * kBlockBytes);
+        if (klg >= 0 && padded_tiles_on()) {
+            // k a power of two: padded power-of-two tiles of 16 >> lg chunks.
+            // A tail chunk (>= 4 bytes) still rides in a general item, with
+            // the last 1 .. 16 >> lg full chunks before it.
+            const uint64_t cpt = kTileBlocks >> klg;
+            uint64_t upto = nfull;
+            if (tail >= 4 && nfull) upto = nfull - (nfull % cpt ? nfull % cpt : cpt);
+            while (c < upto) {
+                const uint64_t src = p.payload_off + c * p.bpc;
+                if (!early_ok(src)) {
+                    push_gen(plan, src, p.out_idx + c, p.bpc);
+                    ++c;
+                    continue;
+                }
+                const uint64_t nch = std::min(cpt, upto - c);
+                FastTile t;
+                t.src = src;
+                t.out = uint32_t(p.out_idx + c);
+                t.meta = padded_meta(uint32_t(nch << klg), uint32_t(klg), pad);
+                plan->tiles.push_back(t);
+                c += nch;
+            }
+        }
         // (k dividing 16: whole chunks fill subtiles exactly, and one subtile
         // per item keeps the item loop out of the way)
         const uint64_t per = item_chunks(k);
-        for (uint64_t c = 0; c < nfull;) {
+        while (c < nfull) {
             const uint64_t src = p.payload_off + c * p.bpc;
-            if (pad && !(absolute ? (src & 4095u) >= 16 : src >= 16)) {
+            if (pad && !early_ok(src)) {
                 push_gen(plan, src, p.out_idx + c, p.bpc);
                 ++c;
                 continue;

@@ -8,6 +8,13 @@
 //    one wave-tile) of FULL chunks of one packet whose bpc is 512 << lg
 //    (lg = 0..4), at any alignment.  A tile never straddles a chunk, so a
 //    wave finishes every chunk it starts.
+//  * FastTile, padded power-of-two form (pad bits set, bit 31 clear): up to
+//    16 >> lg FULL chunks of one packet whose bpc is 512 << lg minus a pad
+//    of 1..511 bytes (lg = 0..4: bpc 4..511, 513..1023, 1537..2047,
+//    3585..4095, 7681..8191).  Each chunk is right-aligned into its 2^lg
+//    virtual 512-byte blocks behind pad leading zeros, so the tile runs the
+//    power-of-two reduce (no per-subtile gather): only the lanes of each
+//    chunk's first block are masked, and the affine constant is bpc's.
 //  * FastTile, general form (meta bit 31): a general item of up to 16 FULL
 //    chunks of one packet with any other bpc in [4, 8192], k = ceil(bpc /
 //    512) virtual 512-byte blocks per chunk.  Each chunk is right-aligned
@@ -46,6 +53,7 @@ struct FastTile {
     uint64_t src;
     uint32_t out;   // checksum index of the tile's first chunk
     // power-of-two form: bits 0-7 = blocks in tile (1..16), bits 8-15 = lg = log2(bpc / 512);
+    // padded power-of-two form: the same, bits 8-15 = lg = log2(k) and bits 18-26 = pad = 512 k - bpc;
     // general form: bit 31, bits 0-7 = subtiles ceil((nch * k + kt) / 16), bits 8-12 = k, bits 13-17 = nch
     //               (full chunks in the item, 1..16), bits 18-26 = pad = 512 k - bpc
     uint32_t meta;
@@ -53,6 +61,10 @@ struct FastTile {
 static_assert(sizeof(FastTile) == 16, "FastTile is 16 bytes");
 constexpr uint64_t kSrcMask = (1ull << 48) - 1;
 constexpr uint32_t kGeneralChunks = 16;  // full chunks per general item
+
+inline uint32_t padded_meta(uint32_t nb, uint32_t lg, uint32_t pad) { return nb | (lg << 8) | (pad << 18); }
+// pad of a power-of-two tile (0: unpadded; general tiles keep their own at the same bits)
+inline uint32_t tile_pad_bits(uint32_t meta) { return (meta >> 18) & 511u; }
 
 inline uint32_t general_meta(uint32_t nch, uint32_t k, uint32_t pad, uint32_t kt = 0) {
     return kGeneralTile | ((nch * k + kt + kTileBlocks - 1) / kTileBlocks) | (k << 8) | (nch << 13) | (pad << 18);

@@ -171,10 +171,14 @@ void plans_and_framing(std::mt19937_64 &rng) {
                 CHECK(pad == 0 || src >= 16, "padded tile too close to the payload start");
                 CHECK(tl == 0 || (tl >= 4 && tl < bpc), "tail chunk length %u", tl);
             } else {
-                const uint32_t nb = meta & 0xffu, lg = (meta >> 8) & 0xffu;
+                // (bits 18-26: the pad of a padded power-of-two tile, bpc = (512 << lg) - pad)
+                const uint32_t nb = meta & 0xffu, lg = (meta >> 8) & 0xffu, pad = (meta >> 18) & 511u;
                 CHECK(nb >= 1 && nb <= 16 && lg <= 4 && (nb % (1u << lg)) == 0 && tl == 0, "tile meta %x", meta);
+                CHECK((meta & ~(0xffffu | (511u << 18))) == 0, "tile meta %x", meta);
                 nch = nb >> lg;
-                bpc = 512u << lg;
+                bpc = (512u << lg) - pad;
+                CHECK(bpc >= 4 && (pad == 0 || src >= 16), "padded tile meta %x src %llu", meta,
+                      (unsigned long long)src);
             }
             CHECK(src + uint64_t(bpc) * nch + tl <= extent, "tile past the payload");
             for (uint32_t c = 0; c < nch + (tl ? 1u : 0u); ++c)
@@ -290,10 +294,11 @@ void write_plans(std::mt19937_64 &rng) {
                 nch = (t.meta >> 13) & 31u;
                 tb = ((t.meta >> 8) & 31u) * 512u - ((t.meta >> 18) & 511u);
                 CHECK(((t.meta >> 18) & 511u) == 0 || (src & 4095u) >= 16, "padded tile page rule");
-            } else {
+            } else {  // (padded power-of-two tiles: bpc = (512 << lg) - pad)
                 nch = (t.meta & 0xffu) >> ((t.meta >> 8) & 0xffu);
-                tb = 512u << ((t.meta >> 8) & 0xffu);
+                tb = (512u << ((t.meta >> 8) & 0xffu)) - ((t.meta >> 18) & 511u);
                 CHECK(tl == 0, "tail on a power-of-two tile");
+                CHECK(((t.meta >> 18) & 511u) == 0 || (src & 4095u) >= 16, "padded tile page rule");
             }
             for (uint32_t c = 0; c < nch; ++c) put(t.out + c, crc_at(src + uint64_t(c) * tb, tb));
             if (tl) put(t.out + nch, crc_at(src + uint64_t(nch) * tb, tl));

@@ -924,3 +924,86 @@ def test_entry_points_reject_bad_arguments(hdfs, gpu_ctx):
     aplan.exec(0, exp.data_ptr(), 0)
     torch.cuda.synchronize()
     aplan.close()
+
+
+PADDED_BPCS = [4, 100, 511, 513, 700, 1000, 1023, 1537, 2000, 2047, 3585, 4000, 4095, 7681, 8000, 8191]
+
+
+@pytest.mark.parametrize("npk", [3, 40, 600])
+def test_padded_power_of_two_tiles(hdfs, gpu_ctx, orc, npk):
+    """Chunks of bpc = 512 * 2^lg - pad run as padded power-of-two tiles
+    (round 5): every pad class of lg = 0..4, packets with and without a tail
+    chunk, first chunks at offsets < 16 (those take a GenItem) and at odd
+    offsets; 3 / 40 packets run the compact builds, 600 the full image; exec
+    in both byte orders and verify (clean, a corrupted payload byte, a
+    corrupted expectation) bit-exact against the reference."""
+    torch = _torch()
+    rng = np.random.default_rng(1700 + npk)
+    pk = np.zeros(npk, oracle.PACKET_DTYPE)
+    pk["bpc"] = rng.choice(PADDED_BPCS, npk)
+    pk["len"] = np.where(rng.random(npk) < 0.5, 65536, rng.integers(1, 65537, npk))
+    gaps = rng.integers(0, 41, npk)
+    gaps[0] = rng.integers(0, 21)
+    pk["payload_off"] = np.cumsum(gaps) + np.concatenate([[0], np.cumsum(pk["len"].astype(np.int64))[:-1]])
+    per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    tiles, _ = hdfs.debug_plan(pk)
+    meta = tiles["meta"].astype(np.int64)
+    assert np.any(((meta >> 18) & 511) & ~(meta >> 31))  # some padded power-of-two tiles
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 1800 + npk)
+    n = hdfs.total_checksums(pk)
+    for flags in (0, hdfs.CRC32C_BIG_ENDIAN):
+        want = orc.batch(payload, pk, n, big_endian=bool(flags))
+        assert np.array_equal(run_dev(hdfs, gpu_ctx, payload, pk, flags), want)
+        assert np.array_equal(run_dev(hdfs, gpu_ctx, payload, pk, flags, offset=5), want)
+    want = orc.batch(payload, pk, n)
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def verify():
+        plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        return res.cpu().numpy().view(np.uint32).tolist()
+
+    assert verify() == [0, 0xFFFFFFFF]
+    p = pk[npk // 2]
+    off = int(p["len"]) // 3
+    dev[int(p["payload_off"]) + off] ^= 0x40
+    bad = int(p["out_idx"]) + off // int(p["bpc"])
+    assert verify() == [1, bad]
+    dev[int(p["payload_off"]) + off] ^= 0x40
+    exp[n - 1] ^= 1
+    assert verify() == [1, n - 1]
+    plan.close()
+
+
+@pytest.mark.parametrize("bpc", [1000, 4000, 300])
+def test_padded_tiles_multi_block_launch(hdfs, gpu_ctx, orc, bpc):
+    """crc32c_plan_exec_blocks with a one-block plan of padded tiles over
+    blocks at 16-byte-aligned and odd device addresses."""
+    torch = _torch()
+    pk = oracle.uniform_packets(64)
+    pk["bpc"] = bpc
+    per = (pk["len"].astype(np.uint64) + bpc - 1) // bpc
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    n = hdfs.total_checksums(pk)
+    block = 64 * 65536
+    offs = [0, block + 64, 2 * block + 205]
+    dev = torch.zeros(3 * block + 512, dtype=torch.uint8, device="cuda")
+    wants = []
+    for b, o in enumerate(offs):
+        host = oracle.xorshift64_bytes(block, 2000 + b)
+        dev[o:o + block].copy_(torch.from_numpy(host))
+        wants.append(orc.batch(host, pk, n))
+    outs = torch.zeros((3, n), dtype=torch.int32, device="cuda")
+    plan = hdfs.Plan(gpu_ctx, pk)
+    stream = torch.cuda.current_stream()
+    plan.exec_blocks([dev.data_ptr() + o for o in offs], [outs[b].data_ptr() for b in range(3)], stream.cuda_stream)
+    stream.synchronize()
+    plan.close()
+    got = outs.cpu().numpy().view(np.uint32)
+    for b in range(3):
+        assert np.array_equal(got[b], wants[b]), b

@@ -66,9 +66,10 @@ def test_product_library_has_no_variant_switch(hdfs):
     assert b"KVARIANT" not in blob
     kernels = set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", blob))
     # modes: 3 = S4 | NT, + 64 verify, + 256 general-tile code, + 512 compact image (small batches),
-    # + 4096 quarter units (the smallest batches), + 32768 no shifted tiles, + 65536 no general tiles
+    # + 4096 quarter units (the smallest batches), + 32768 no shifted tiles, + 65536 no general tiles,
+    # + 131072 general items' next subtile facts hoisted (the build with both general and shifted tiles)
     assert kernels == {b"_Z23hdfs_crc32c_plan_kernelILi768ELi3ELi%dEEvN8hdfs_crc7KParamsE" % m
-                       for m in (3, 67, 259, 323, 771, 835, 4867, 4931, 33027, 33091, 65795, 65859)}, kernels
+                       for m in (3, 67, 131331, 131395, 771, 835, 4867, 4931, 33027, 33091, 65795, 65859)}, kernels
     dblob = open(hdfs.DEBUG_LIB_PATH, "rb").read()
     assert len(set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", dblob))) >= 9
 
@@ -234,6 +235,14 @@ def _cases():
     odd["bpc"] = [512, 512, 100, 512, 1024, 1536]
     odd["out_idx"] = np.cumsum([0] + [(l + b - 1) // b for l, b in zip(odd["len"][:-1], odd["bpc"][:-1])])
     yield "odd", odd
+    # padded power-of-two tiles (bpc = 512 * 2^lg - pad), with and without
+    # tails, a first chunk too close to the buffer start for the early loads
+    pad_pk = np.zeros(9, oracle.PACKET_DTYPE)
+    pad_pk["payload_off"] = [3, 9000, 30000, 70000, 80017, 120000, 140000, 200000, 300000]
+    pad_pk["len"] = [5000, 20000, 33000, 9000, 40000, 16380, 65536, 65536, 70000]
+    pad_pk["bpc"] = [1000, 700, 2000, 100, 4000, 8000, 1000, 511, 8191]
+    pad_pk["out_idx"] = np.cumsum([0] + [(l + b - 1) // b for l, b in zip(pad_pk["len"][:-1], pad_pk["bpc"][:-1])])
+    yield "padded", pad_pk
 
 
 @pytest.mark.parametrize("name,pk", list(_cases()))
@@ -257,9 +266,12 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
             assert pad == 0 or src >= 16  # padded loads start up to 15 bytes early
             assert tl == 0 or 4 <= tl < bpc  # a packet's tail chunk after the full ones
         else:
-            nb, lg = meta & 0xFF, (meta >> 8) & 0xFF
+            nb, lg, pad = meta & 0xFF, (meta >> 8) & 0xFF, (meta >> 18) & 511
             assert 1 <= nb <= 16 and nb % (1 << lg) == 0 and tl == 0  # any alignment (unaligned tile loads)
-            bpc, nch = 512 << lg, nb >> lg
+            assert meta & ~(0xFFFF | (511 << 18)) == 0 and lg <= 4
+            # padded power-of-two tiles: chunks of 512 << lg minus pad bytes
+            assert pad == 0 or (src >= 16 and (512 << lg) - pad >= 4)  # (pad < 512: k = ceil(bpc / 512))
+            bpc, nch = (512 << lg) - pad, nb >> lg
         for c in range(nch + (1 if tl else 0)):
             s = src + c * bpc
             got[int(t["out"]) + c] = orc.crc32c(payload[s:s + (bpc if c < nch else tl)])
@@ -281,6 +293,19 @@ def test_plan_fast_path_shapes(hdfs):
     assert gen.size == 0 and int(tiles["src"][-1]) >> 48 == 65436 % 512 and int(tiles["meta"][-1]) >> 31
     tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65539))  # a 3-byte tail: general path
     assert gen.size == 1 and int(gen["len"][0]) == 3
+    # bpc 1000 (k = 2, pad 24): 65 full chunks and a 536-byte tail -> 8 padded
+    # tiles of 8 chunks, then one general item of the last chunk + the tail
+    pk = oracle.uniform_packets(1)
+    pk["bpc"], pk["payload_off"] = 1000, 64  # (a first chunk at offset < 16 would be a GenItem)
+    tiles, gen = hdfs.debug_plan(pk)
+    meta = tiles["meta"].astype(np.int64)
+    assert gen.size == 0 and tiles.size == 9
+    assert list(meta[:8]) == [16 | (1 << 8) | (24 << 18)] * 8 and meta[8] >> 31 and (meta[8] >> 13) & 31 == 1
+    # no tail: every chunk in padded tiles (bpc 4000, k = 8: 2 chunks per tile)
+    pk = oracle.uniform_packets(1, pkt_len=64000)
+    pk["bpc"], pk["payload_off"] = 4000, 64
+    tiles, gen = hdfs.debug_plan(pk)
+    assert gen.size == 0 and tiles.size == 8 and np.all(tiles["meta"] == 16 | (3 << 8) | (96 << 18))
 
 
 @pytest.fixture(scope="module")
@@ -305,6 +330,24 @@ def test_kernel_model_fast_tiles(orc, model, lg):
     got = model.fast_chunks(data, lg)
     want = orc.chunks(data, bpc)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("bpc", [4, 100, 511, 513, 700, 1000, 1023, 1537, 2000, 3585, 4000, 7681, 8191])
+def test_kernel_model_padded_tiles(orc, model, bpc):
+    """Padded power-of-two tiles: each chunk right-aligned into its 2^lg
+    virtual blocks behind pad zeros, reduced like a power-of-two chunk, with
+    crc(0, zeros(bpc)) as the affine constant instead of 512 << lg's."""
+    lg = max(0, (bpc - 1).bit_length() - 9)
+    k = 1 << lg
+    pad = 512 * k - bpc
+    assert 0 < pad < 512
+    data = oracle.xorshift64_bytes(bpc * 5, 300 + bpc)
+    data[bpc:2 * bpc] = 0xFF
+    virt = np.zeros((5, 512 * k), np.uint8)
+    virt[:, pad:] = data.reshape(5, bpc)
+    got = model.fast_chunks(virt.reshape(-1), lg) ^ np.uint32(model.c_lg[lg]) ^ np.uint32(
+        orc.crc32c(np.zeros(bpc, np.uint8)))
+    assert np.array_equal(got, orc.chunks(data, bpc))
 
 
 def test_kernel_model_general_chunks(orc, model):

@@ -79,6 +79,10 @@ for s in ${STEPS:-calls multi}; do
     prof5d) run prof5d 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5d -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 ;;
     kbhoist) for c in ${KBCFGS:-c2b1000 c2b700 c2b1536}; do run kbh_$c 300 python tools/kbench.py --config $c --variants ${KBV:-0,49,75,2} --rounds 9 --iters 300 || exit 1; done ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
+    tpad) run tpad 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "padded or general or golden or random or fuzz or mixed or edge or small or verify or write_plan" ;;
+    padab) for r in $(seq 1 ${PADR:-1}); do for c in ${PADCFGS:-c2b1000 c2b700 c2b4000 c2b2000 c2b100}; do
+             run padab_gen_${c}_$r 300 env HDFS_CRC32C_PADDED_TILES=0 python bench.py --config $c --no-cpu --no-host &&
+             run padab_tile_${c}_$r 300 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
     c4x20) for r in 1 2; do run c4_20_$r 300 python bench.py --config c4 --steps 20 --warmup 5 --no-cpu --no-host || exit 1; done ;;
     tbench) run tbench 600 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 300 --timeout-method thread ;;
     configs) for c in ${CFGS:-c3 c4 c5 c2b1536 c2b1000 c2t c2u c3u}; do run cfg_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
