@@ -119,8 +119,9 @@ def latest_pmc(profile_dir: str, config: str):
 
 
 def config_name(name: str) -> str:
-    """--config: a BASELINE.json config or one of its variants (c2b<bpc>: config 2 with that bytesPerChecksum)."""
-    if name in ("c2", "c3", "c4", "c5", "c2u", "c2t", "c3u") or (name.startswith("c2b") and name[3:].isdigit()
+    """--config: a BASELINE.json config or one of its variants (c2b<bpc>: config 2 with that bytesPerChecksum;
+    c2w<bpc>: the same with packets cut to whole chunks, no tail chunk)."""
+    if name in ("c2", "c3", "c4", "c5", "c2u", "c2t", "c3u") or (name[:3] in ("c2b", "c2w") and name[3:].isdigit()
                                                                     and 4 <= int(name[3:]) <= 65536):
         return name
     raise argparse.ArgumentTypeError("unknown config %r" % name)

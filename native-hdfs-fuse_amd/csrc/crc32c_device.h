@@ -729,18 +729,23 @@ __device__ __forceinline__ uint32_t tile_pad(FastTile t) { return (t.meta >> 18)
 template <int AUX, bool VERIFY>
 __device__ __forceinline__ void load_tile_padded(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
     const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu, pad = tile_pad(t);
-    const uint32_t bpc = (512u << lg) - pad;
+    const uint32_t bpc = (512u << lg) - pad, km = (1u << lg) - 1u;
     const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + t.src - 16u, 16u + (nb >> lg) * bpc);
+    // Offset of lane l in instruction i = a wave-uniform part + a lane part:
+    //   lg >= 1: blocks 2i, 2i + 1 are blocks w, w + 1 of chunk 2i >> lg
+    //            (1 KiB contiguous): (2i >> lg) bpc + 512 w - pad, + 16 l;
+    //   lg = 0:  block 2i + h is chunk 2i + h: 2i bpc - pad, + h bpc + 16 q.
+    // A lane wholly inside a first block's pad reads nothing (bit 31: past
+    // the range).  Blocks past nb read what they read: their lin() is never
+    // combined with a block of the tile's chunks nor stored.
     const uint32_t h = uint32_t(lane) >> 5, q16 = 16u * (uint32_t(lane) & 31u);
-    const uint32_t km = (1u << lg) - 1u;
-    const bool inpad = q16 + 16u <= pad;
+    const uint32_t lane_all = lg ? 16u * uint32_t(lane) : h * bpc + q16;
+    const uint32_t lane_first = (q16 + 16u <= pad && (lg == 0u || h == 0u)) ? 0x80000000u : lane_all;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint32_t b = 2u * uint32_t(i) + h;
-        const uint32_t w = b & km;  // block of its chunk
-        const bool skip = (w == 0u && inpad) || b >= nb;
-        const uint32_t off = 16u + (b >> lg) * bpc + 512u * w + q16 - pad;
-        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, skip ? 0x80000000u : off, 0, AUX);
+        const uint32_t b2 = 2u * uint32_t(i), w = b2 & km;  // (uniform)
+        const uint32_t ubase = 16u + (b2 >> lg) * bpc + 512u * w - pad;
+        const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (w ? lane_all : lane_first) + ubase, 0, AUX);
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
     if (VERIFY) {
@@ -750,12 +755,21 @@ __device__ __forceinline__ void load_tile_padded(const KParams &p, FastTile t, i
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// A chunk's first block: lane q keeps its bytes at positions >= pad - 16 q.
+// The lanes of a chunk's first block keep their bytes at positions >= pad -
+// 16 q (kp; all ones in other blocks' lanes).  Only a pad that is not a
+// multiple of 16 leaves a lane straddling the chunk start; otherwise the
+// skipped loads' zeros are the whole prefix and nothing is masked.
 struct PadPrep {
     uint4 kp;
-    uint32_t h, km;
+    uint32_t km;
+    bool mask;
     __device__ __forceinline__ void operator()(int i, uint4 &x) const {
-        apply_keep(x, kp, 0u - uint32_t(((2u * uint32_t(i) + h) & km) == 0u));
+        if (mask && ((2u * uint32_t(i)) & km) == 0u) {  // (uniform)
+            x.x &= kp.x;
+            x.y &= kp.y;
+            x.z &= kp.z;
+            x.w &= kp.w;
+        }
     }
 };
 
@@ -770,8 +784,10 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     }
     if ((GEN & kGenItems) && tile_pad(t)) {
         const uint32_t pad = tile_pad(t), lg = (t.meta >> 8) & 0xffu;
-        const PadPrep prep{keep_masks(int(pad) - int(16u * (uint32_t(lane) & 31u))), uint32_t(lane) >> 5,
-                           (1u << lg) - 1u};
+        const bool first = lg == 0u || lane < 32;  // (lanes of a chunk's first block where instruction i holds one)
+        const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+        const PadPrep prep{first ? keep_masks(int(pad) - int(16u * (uint32_t(lane) & 31u))) : ones, (1u << lg) - 1u,
+                           (pad & 15u) != 0u};
         tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, prep);
         typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
         const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);

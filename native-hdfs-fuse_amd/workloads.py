@@ -63,6 +63,11 @@ def config_packets(name: str):
         return uniform_packets(4096, bpc=1536), "4096 x 64KiB packets, 1536B chunks (general path)"
     if name == "c2b1000":  # config 2 with bytesPerChecksum 1000 (padded general tiles)
         return uniform_packets(4096, bpc=1000), "4096 x 64KiB packets, 1000B chunks (padded general tiles)"
+    if name.startswith("c2w") and name[3:].isdigit():  # chunk-aligned packets: whole chunks, no tail
+        bpc = int(name[3:])
+        plen = PACKET_BYTES // bpc * bpc
+        return (uniform_packets(4096, pkt_len=plen, stride=PACKET_BYTES, bpc=bpc),
+                "4096 x %dB packets (%d whole %dB chunks each, 64KiB stride)" % (plen, plen // bpc, bpc))
     if name.startswith("c2b") and name[3:].isdigit():  # config 2 with any other bytesPerChecksum
         bpc = int(name[3:])
         return uniform_packets(4096, bpc=bpc), "4096 x 64KiB packets, %dB chunks (general path)" % bpc

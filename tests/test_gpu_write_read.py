@@ -62,7 +62,8 @@ def _verify(plan, expected: np.ndarray, stream, payload=0):
 @pytest.mark.parametrize("bpc", [4, 7, 100, 511, 513, 1000, 1536, 2560, 3072, 4000, 6144, 7680, 8191])
 def test_general_tiles_any_bpc(hdfs, gpu_ctx, orc, bpc):
     """Packets of bpc outside 512 * 2^k take general tiles (16 // k chunks of k
-    virtual blocks): at offset 0 (padded tiles fall back to the general path
+    virtual blocks), or padded power-of-two tiles where k is a power of two
+    (the packet's tail still in a general tile): at offset 0 (padded tiles fall back to the general path
     only for the first chunk), at every phase mod 16, with ragged tails; exec
     and verify against the oracle."""
     torch = _torch()
@@ -77,7 +78,8 @@ def test_general_tiles_any_bpc(hdfs, gpu_ctx, orc, bpc):
         off += ln + (i % 16) + 1
     pk = np.array(rows, hdfs.PACKET_DTYPE)
     tiles, gen = hdfs.debug_plan(pk)
-    assert np.any(tiles["meta"] & 0x80000000)
+    meta = tiles["meta"].astype(np.int64)
+    assert np.any(meta >> 31) or np.any((meta >> 18) & 511)  # general or padded power-of-two tiles
     if 16 <= bpc <= 7680:  # (8191: a 16-block chunk leaves a tile no room)
         assert np.any(tiles["src"] >> np.uint64(48))  # tails in tiles
     payload = oracle.xorshift64_bytes(off + 64, 3000 + bpc)

@@ -80,6 +80,9 @@ for s in ${STEPS:-calls multi}; do
     kbhoist) for c in ${KBCFGS:-c2b1000 c2b700 c2b1536}; do run kbh_$c 300 python tools/kbench.py --config $c --variants ${KBV:-0,49,75,2} --rounds 9 --iters 300 || exit 1; done ;;
     benchd) run benchd 600 python bench.py --steps 20 --warmup 5 ;;
     tpad) run tpad 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "padded or general or golden or random or fuzz or mixed or edge or small or verify or write_plan" ;;
+    padw) for c in ${PADWCFGS:-c2w1000 c2w2000 c2w4000 c2w700 c2w100 c2b2048}; do
+             run padw_gen_$c 300 env HDFS_CRC32C_PADDED_TILES=0 python bench.py --config $c --no-cpu --no-host &&
+             run padw_tile_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     padab) for r in $(seq 1 ${PADR:-1}); do for c in ${PADCFGS:-c2b1000 c2b700 c2b4000 c2b2000 c2b100}; do
              run padab_gen_${c}_$r 300 env HDFS_CRC32C_PADDED_TILES=0 python bench.py --config $c --no-cpu --no-host &&
              run padab_tile_${c}_$r 300 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
