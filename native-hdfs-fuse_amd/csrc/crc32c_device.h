@@ -756,20 +756,15 @@ __device__ __forceinline__ void load_tile_padded(const KParams &p, FastTile t, i
 }
 
 // The lanes of a chunk's first block keep their bytes at positions >= pad -
-// 16 q (kp; all ones in other blocks' lanes).  Only a pad that is not a
-// multiple of 16 leaves a lane straddling the chunk start; otherwise the
-// skipped loads' zeros are the whole prefix and nothing is masked.
+// 16 q (kp; all ones in other blocks' lanes), selected per piece without a
+// branch (a branch between the two interleaved lookup chains of a piece pair
+// would split them).  Only a pad that is not a multiple of 16 leaves a lane
+// straddling the chunk start; otherwise the tile runs without this prep.
 struct PadPrep {
     uint4 kp;
     uint32_t km;
-    bool mask;
     __device__ __forceinline__ void operator()(int i, uint4 &x) const {
-        if (mask && ((2u * uint32_t(i)) & km) == 0u) {  // (uniform)
-            x.x &= kp.x;
-            x.y &= kp.y;
-            x.z &= kp.z;
-            x.w &= kp.w;
-        }
+        apply_keep(x, kp, 0u - uint32_t(((2u * uint32_t(i)) & km) == 0u));
     }
 };
 
@@ -784,14 +779,19 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     }
     if ((GEN & kGenItems) && tile_pad(t)) {
         const uint32_t pad = tile_pad(t), lg = (t.meta >> 8) & 0xffu;
-        const bool first = lg == 0u || lane < 32;  // (lanes of a chunk's first block where instruction i holds one)
-        const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
-        const PadPrep prep{first ? keep_masks(int(pad) - int(16u * (uint32_t(lane) & 31u))) : ones, (1u << lg) - 1u,
-                           (pad & 15u) != 0u};
-        tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, prep);
         typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
         const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
-        reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane, zc[(512u << lg) - pad]);
+        const uint32_t cst = zc[(512u << lg) - pad];  // (a scalar load, in flight during the lookups)
+        if (pad & 15u) {  // (uniform) a lane straddles each chunk start
+            const bool first = lg == 0u || lane < 32;  // (a first block's lanes, where instruction i holds one)
+            const uint4 ones = make_uint4(~0u, ~0u, ~0u, ~0u);
+            tile_pieces<DIAG, S4, IMG>(
+                lds, v, pc, lane,
+                PadPrep{first ? keep_masks(int(pad) - int(16u * (uint32_t(lane) & 31u))) : ones, (1u << lg) - 1u});
+        } else {
+            tile_pieces<DIAG, S4, IMG>(lds, v, pc, lane, NoPrep{});
+        }
+        reduce_emit<S4, VERIFY, IMG>(p, lds, vacc, t, pc, ev, lane, cst);
         return;
     }
     const uint32_t r = (GEN & kGenShift) && !COMPDIAG ? tile_misalign(p, t) : 0u;

@@ -108,11 +108,13 @@ static bool needs_z(const HostPlan &hp) {
     return false;
 }
 
-// Some general tile's full chunks are padded (bpc not a multiple of 512).
-// Such batches run the general build with both paths even without shifted
-// tiles: the general-tiles-only build, which helps unpadded general tiles
-// (412-byte tails: 48.2 -> 46.2 us), measured slower for padded ones (bpc
-// 1000: 62.8 -> 64.3 us, same box, 3 rounds).
+// Some general tile's full chunks are padded (bpc not a multiple of 512), or
+// some tile is a padded power-of-two one.  Such batches run the general build
+// with both paths even without shifted tiles: the general-tiles-only build,
+// which helps unpadded general tiles (412-byte tails: 48.2 -> 46.2 us), was
+// measured slower for padded ones (bpc 1000: 62.8 -> 64.3 us, same box, 3
+// rounds; padded power-of-two tiles of bpc 2000, kbench: 48.46 against
+// 46.77 us, round 5).
 static bool has_padded_general(const HostPlan &hp) {
     static const bool off = [] {  // (A/B: HDFS_CRC32C_PADDED_FULL=0 sends them to the general-tiles-only build)
         const char *e = std::getenv("HDFS_CRC32C_PADDED_FULL");
@@ -120,7 +122,7 @@ static bool has_padded_general(const HostPlan &hp) {
     }();
     if (off) return false;
     for (const FastTile &t : hp.tiles)
-        if ((t.meta & kGeneralTile) && ((t.meta >> 18) & 511u)) return true;
+        if (tile_pad_bits(t.meta)) return true;  // (general or padded power-of-two tiles)
     return false;
 }
 

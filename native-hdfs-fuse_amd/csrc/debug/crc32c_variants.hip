@@ -70,6 +70,9 @@ constexpr Variant kVariants[] = {
     {76, "s4_nt_gitems_hoist_prodgrid", 768, 1, true, true},
     {77, "s4_nt_gitems_group2_prodgrid", 768, 1, true, true},
     {78, "s4_nt_gitems_group2_hoist_prodgrid", 768, 1, true, true},
+    // the general-tiles-only production build itself (what a batch of padded
+    // tiles and general items with no shifted tile runs), for any batch
+    {79, "s4_nt_gitems_prodgrid", 768, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -126,6 +129,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 76: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGHoist); break;
     case 77: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGGroup2); break;
     case 78: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGGroup2 | kModeGHoist); break;
+    case 79: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
