@@ -109,6 +109,8 @@ constexpr int kModeNoGItems = 65536;
 constexpr int kModeGHoist = 131072;  // a general item's next subtile facts computed before this subtile's lookups
                                      // (the both-paths general build: padded chunks 0.5-2 % faster, round 5)
 constexpr int kModeGGroup2 = 262144;  // A/B: (with kModeNoShift) general items gathered 2 subtiles at a time, not 4
+constexpr int kModeOvl = 524288;      // A/B: the first tile's loads issued right after the table staging's, before
+                                      // the barrier that waits for the staging (their latencies overlap)
 // GEN bits of the tile helpers below: general tiles, shifted (unaligned)
 // tiles, general items gathered 4 subtiles at a time (finish_gtile GROUP)
 constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16;
@@ -918,6 +920,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                                                               : (kGenShift | kGenGroup2)) |
                                        ((MODE & kModeGHoist) ? kGenHoist : 0);
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
+    constexpr bool OVL = !EARLY && (MODE & kModeOvl) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;
     constexpr bool XCDMAP = (MODE & kModeXcdMap) != 0;
     constexpr int SPLIT = (MODE & kModeHalves) ? 2 : 4;  // units per tile
@@ -1001,6 +1004,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                 (__attribute__((address_space(3))) void *)(lds + c * 1024u), 16, 0, 0);
         }
     }
+    if (OVL && t < tend) load_next(t);
     __syncthreads();
     if (STAMPS) t_staged = __builtin_amdgcn_s_memrealtime();
     // (the last wave: idle in small batches; in large ones the workgroup's
@@ -1026,7 +1030,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
         }
     };
 
-    if (!EARLY && t < tend) load_next(t);
+    if (!EARLY && !OVL && t < tend) load_next(t);
     while (t < tend) {
         if (!QUARTER || kind == 1)
             finish_tile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, GEN>(p, lds, vacc, ft, v, ev, lane);

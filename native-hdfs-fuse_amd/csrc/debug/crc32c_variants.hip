@@ -73,6 +73,10 @@ constexpr Variant kVariants[] = {
     // the general-tiles-only production build itself (what a batch of padded
     // tiles and general items with no shifted tile runs), for any batch
     {79, "s4_nt_gitems_prodgrid", 768, 1, true, true},
+    // the power-of-two production build (62) with the first tile's loads
+    // issued right after the staging's, before the barrier; stamped twin
+    {80, "s4_nt_pow2only_ovl_prodgrid", 768, 1, true, true},
+    {81, "s4_nt_pow2only_ovl_stamps_prodgrid", 768, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -130,6 +134,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 77: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGGroup2); break;
     case 78: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift | kModeGGroup2 | kModeGHoist); break;
     case 79: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift); break;
+    case 80: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeOvl); break;
+    case 81: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeOvl | kModeStamps); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
