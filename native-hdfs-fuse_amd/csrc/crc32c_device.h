@@ -567,7 +567,9 @@ struct NoPrep {
 // bits 0, 1, 3 (8 values -> 1), then all-reduce over lane bits 2 and 4.
 // Afterwards lane l holds lin() of block rep_block(l) = 2*i + h with
 // i = b3 + 2*b1 + 4*b0 (b = bits of l).
-__device__ __forceinline__ uint32_t block_lin(const uint32_t pc[8], int lane) {
+// (whole = false: the last all-reduce step is skipped, so lanes 0..15 and
+// 16..31 of the block keep the lin() of their own half; half tiles)
+__device__ __forceinline__ uint32_t block_lin(const uint32_t pc[8], int lane, bool whole = true) {
     const bool b0 = lane & 1, b1 = lane & 2, b3 = lane & 8;
     uint32_t u[4];
 #pragma unroll
@@ -590,8 +592,8 @@ __device__ __forceinline__ uint32_t block_lin(const uint32_t pc[8], int lane) {
         x = keep ^ dpp<kDppXor8>(send);
     }
     x ^= swz_xor<4>(x);
-    x ^= swz_xor<16>(x);
-    return x;
+    const uint32_t y = swz_xor<16>(x);
+    return whole ? x ^ y : x;
 }
 
 // Power-of-two tile: blocks combined per chunk, chunk checksums stored (or
@@ -770,6 +772,103 @@ struct PadPrep {
     }
 };
 
+// ---- half tiles (builds with the general-tile code) -----------------------
+// bpc <= 256 (M = 0) or 512 < bpc <= 768 (M = 1): a chunk is M full 512-byte
+// blocks after a partial part of r = bpc - 512 M <= 256 bytes, right-aligned
+// into a 256-byte half block behind padh = 256 - r zeros.  Two partial parts
+// share one block: its upper half (lanes 16..31, whose columns are the last
+// 256 bytes before a block end) holds chunk 2m's, its lower half (lanes
+// 0..15) chunk 2m + 1's, those lanes taking the N_q finishing operators of
+// columns q + 16 (the T tables are the same in every column, so their
+// lookups keep their own, conflict-free columns).  A pair block's lin() is
+// reduced per half (block_lin without its last all-reduce step).
+//   M = 0: 16 pair blocks, up to 32 chunks per tile.
+//   M = 1: block c < 10 is chunk c's full block, block 10 + m the pair block
+//          of chunks 2m, 2m + 1 (up to 10 chunks per tile, 15 blocks); chunk
+//          c's lin = Z^512(its partial half's lin) ^ its full block's lin.
+// The tile holds n chunks; slots past n read what they read (never stored).
+// Round 5: bpc 700 took 2 virtual blocks per chunk as a padded tile, 1.5
+// here.
+__device__ __forceinline__ bool is_half(FastTile t) { return (t.meta & 0xC0000000u) == hdfs_crc::kHalfTile; }
+
+template <int AUX, bool VERIFY, uint32_t M>
+__device__ __forceinline__ void load_tile_half(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
+    const uint32_t n = t.meta & 0xffu, padh = (t.meta >> 18) & 511u;
+    const uint32_t r = 256u - padh, bpc = 512u * M + r;
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + t.src - 16u, 16u + n * bpc);
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u, u = q >> 4, q16h = 16u * (q & 15u);
+    // pair instruction j: half-wave h is pair block 2j + h (chunks 4j + 2h,
+    // 4j + 2h + 1), lane (u, q') of it reads 16 q' past chunk 4j + 2h + 1 - u's
+    // half-block start c bpc - padh; full instruction i (M = 1, i < 5):
+    // half-wave h is chunk 2i + h's full block, from c bpc + r
+    const uint32_t lane_pair = q16h + 16u <= padh ? 0x80000000u : (2u * h + 1u - u) * bpc + q16h;
+    const uint32_t lane_full = h * bpc + 16u * q;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t voff;
+        if (M == 0 || i >= 5) {
+            const uint32_t j = M ? uint32_t(i) - 5u : uint32_t(i);
+            voff = lane_pair + (16u + 4u * j * bpc - padh);
+        } else {
+            voff = lane_full + (16u + 2u * uint32_t(i) * bpc + r);
+        }
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, AUX);
+        v[i] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if (VERIFY) {
+        const uint32_t blk = rep_block(lane);
+        const uint32_t c = M ? blk : 2u * blk + 1u - ((uint32_t(lane) >> 4) & 1u);
+        const bool rep = M ? ((lane & 0x14) == 0 && blk < 10u) : (lane & 4) == 0;
+        if (rep && c < n) ev = p.expect[t.out + c];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int DIAG, bool S4, bool VERIFY, int IMG, uint32_t M>
+__device__ __forceinline__ void finish_half(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                            uint4 v[8], uint32_t ev, int lane) {
+    const uint32_t n = t.meta & 0xffu, padh = (t.meta >> 18) & 511u;
+    typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
+    const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
+    const uint32_t cst = zc[512u * M + 256u - padh];  // (a scalar load, in flight during the lookups)
+    const uint32_t q = uint32_t(lane) & 31u;
+    // a pair block's lanes keep their bytes at positions >= padh - 16 q' of
+    // their half (lanes wholly inside the pad loaded nothing)
+    const uint4 kp = keep_masks(int(padh) - int(16u * (q & 15u)));
+    const LaneCols cols = lane_cols<IMG>(q);
+    LaneCols colp = cols;
+    colp.nib = lane_cols<IMG>(q | 16u).nib;
+    uint32_t pc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const bool pair = M == 0 || i >= 5;
+        if (pair && !(DIAG & 4)) {
+            v[i].x &= kp.x;
+            v[i].y &= kp.y;
+            v[i].z &= kp.z;
+            v[i].w &= kp.w;
+        }
+        pc[i] = piece<S4, DIAG, IMG>(lds, v[i], pair ? colp : cols);
+        opaque(pc[i]);
+        if (!S4 || (i & 1)) __builtin_amdgcn_sched_barrier(0);
+    }
+    const uint32_t blk = rep_block(lane);
+    uint32_t x = block_lin(pc, lane, M != 0 && blk < 10u);
+    uint32_t c;
+    bool rep;
+    if (M == 0) {  // lane bit 4: the half, upper = chunk 2 blk
+        c = 2u * blk + 1u - ((uint32_t(lane) >> 4) & 1u);
+        rep = (lane & 4) == 0;
+    } else {  // full block c's lane takes its chunk's partial half from pair block 10 + c / 2
+        c = blk;
+        const uint32_t src = blk < 10u ? block_lane(10u + (blk >> 1)) | ((1u - (blk & 1u)) << 4) : uint32_t(lane);
+        const uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(x)));
+        x ^= zshift<S4, IMG>(lds, 1u, y);
+        rep = (lane & 0x14) == 0 && blk < 10u;
+    }
+    if (rep && c < n) emit<VERIFY>(p, vacc, t.out + c, x ^ cst, ev);
+}
+
 template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, int GEN>
 __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             uint4 v[9], uint32_t ev, int lane) {
@@ -777,6 +876,13 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         finish_gtile<AUX, DIAG, COMPDIAG, S4, VERIFY, IMG, (GEN & kGenGroup4) ? 4u : (GEN & kGenGroup2) ? 2u : 1u,
                      (GEN & kGenHoist) != 0>(p, lds, vacc, t, v, ev, lane);
+        return;
+    }
+    if ((GEN & kGenItems) && is_half(t)) {
+        if ((t.meta >> 8) & 0xffu)
+            finish_half<DIAG, S4, VERIFY, IMG, 1>(p, lds, vacc, t, v, ev, lane);
+        else
+            finish_half<DIAG, S4, VERIFY, IMG, 0>(p, lds, vacc, t, v, ev, lane);
         return;
     }
     if ((GEN & kGenItems) && tile_pad(t)) {
@@ -816,6 +922,11 @@ template <int AUX, bool COMPDIAG, bool VERIFY, int GEN>
 __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[9], uint32_t &ev) {
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         load_gtile<VERIFY>(p, t, lane, ev);
+    } else if ((GEN & kGenItems) && !COMPDIAG && is_half(t)) {
+        if ((t.meta >> 8) & 0xffu)
+            load_tile_half<AUX, VERIFY, 1>(p, t, lane, v, ev);
+        else
+            load_tile_half<AUX, VERIFY, 0>(p, t, lane, v, ev);
     } else if ((GEN & kGenItems) && !COMPDIAG && tile_pad(t)) {
         load_tile_padded<AUX, VERIFY>(p, t, lane, v, ev);
     } else if ((GEN & kGenShift) && !COMPDIAG && tile_misalign(p, t)) {
@@ -843,7 +954,7 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     const FastTile x = tile_at(p, j / SPLIT);
     const uint32_t u = j % SPLIT;
     const uint32_t lg = (x.meta >> 8) & 0xffu;
-    if (((GEN & kGenItems) && ((x.meta & kGeneralTile) || tile_pad(x))) || (1u << lg) > kUB) {
+    if (((GEN & kGenItems) && ((x.meta & kGeneralTile) || is_half(x) || tile_pad(x))) || (1u << lg) > kUB) {
         if (u) return 0;
         ft = x;
         load_any<AUX, COMPDIAG, VERIFY, GEN>(p, ft, lane, v, ev);

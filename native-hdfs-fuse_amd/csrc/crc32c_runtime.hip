@@ -93,7 +93,7 @@ static KParams base_params(const crc32c_ctx *ctx, const void *payload, uint32_t 
 // the general-tile code (kGeneralItems).
 static bool has_general(const HostPlan &hp) {
     for (const FastTile &t : hp.tiles)
-        if ((t.meta & kGeneralTile) || tile_pad_bits(t.meta)) return true;
+        if ((t.meta & (kGeneralTile | kHalfTile)) || tile_pad_bits(t.meta)) return true;
     return false;
 }
 
@@ -122,7 +122,7 @@ static bool has_padded_general(const HostPlan &hp) {
     }();
     if (off) return false;
     for (const FastTile &t : hp.tiles)
-        if (tile_pad_bits(t.meta)) return true;  // (general or padded power-of-two tiles)
+        if (tile_pad_bits(t.meta) || (t.meta & kHalfTile)) return true;  // (general, padded or half tiles)
     return false;
 }
 
@@ -130,7 +130,7 @@ static bool has_padded_general(const HostPlan &hp) {
 // shifted loads read it from the aligned address below).
 static bool has_misaligned(const HostPlan &hp) {
     for (const FastTile &t : hp.tiles)
-        if (!(t.meta & kGeneralTile) && !tile_pad_bits(t.meta) && (t.src & 15u)) return true;
+        if (!(t.meta & (kGeneralTile | kHalfTile)) && !tile_pad_bits(t.meta) && (t.src & 15u)) return true;
     return false;
 }
 

@@ -75,6 +75,12 @@ static bool padded_tiles_on() {
     static const bool on = env_long("HDFS_CRC32C_PADDED_TILES") != 0;
     return on;
 }
+// Half tiles for bpc <= 256 and 512 < bpc <= 768 (plan.h); A/B knob
+// HDFS_CRC32C_HALF_TILES=0 sends those chunks to the forms above instead.
+static bool half_tiles_on() {
+    static const bool on = env_long("HDFS_CRC32C_HALF_TILES") != 0;
+    return on;
+}
 
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
     // A zero-length packet (the block's last-packet marker, hadooprpc.c:644,
@@ -120,7 +126,30 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         const auto early_ok = [&](uint64_t src) { return absolute ? (src & 4095u) >= 16 : src >= 16; };
         uint64_t c = 0;
         const int klg = fast_lg(k * kBlockBytes);
-        if (klg >= 0 && padded_tiles_on()) {
+        const bool half = (p.bpc <= 256 || (p.bpc > 512 && p.bpc <= 768)) && half_tiles_on();
+        if (half) {
+            // Half tiles of up to 32 (bpc <= 256) or 10 chunks; a tail chunk
+            // rides in a general item with the last 1 .. 32 / 10 full chunks.
+            const uint32_t m = p.bpc > 512 ? 1u : 0u, padh = 256u - (p.bpc - 512u * m);
+            const uint64_t cpt = m ? 10 : 32;
+            uint64_t upto = nfull;
+            if (tail >= 4 && nfull) upto = nfull - (nfull % cpt ? nfull % cpt : cpt);
+            while (c < upto) {
+                const uint64_t src = p.payload_off + c * p.bpc;
+                if (!early_ok(src)) {
+                    push_gen(plan, src, p.out_idx + c, p.bpc);
+                    ++c;
+                    continue;
+                }
+                const uint64_t nch = std::min(cpt, upto - c);
+                FastTile t;
+                t.src = src;
+                t.out = uint32_t(p.out_idx + c);
+                t.meta = half_meta(uint32_t(nch), m, padh);
+                plan->tiles.push_back(t);
+                c += nch;
+            }
+        } else if (klg >= 0 && padded_tiles_on()) {
             // k a power of two: padded power-of-two tiles of 16 >> lg chunks.
             // A tail chunk (>= 4 bytes) still rides in a general item, with
             // the last 1 .. 16 >> lg full chunks before it.

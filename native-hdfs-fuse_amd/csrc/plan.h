@@ -15,6 +15,11 @@
 //    virtual 512-byte blocks behind pad leading zeros, so the tile runs the
 //    power-of-two reduce (no per-subtile gather): only the lanes of each
 //    chunk's first block are masked, and the affine constant is bpc's.
+//  * FastTile, half form (meta bit 30): up to 32 (M = 0: bpc 4..256) or 10
+//    (M = 1: bpc 513..768) FULL chunks of one packet, each M whole 512-byte
+//    blocks after a partial part of r = bpc - 512 M bytes right-aligned into
+//    a 256-byte half block behind padh = 256 - r zeros; two chunks' partial
+//    parts share one block (crc32c_device.h, half tiles).
 //  * FastTile, general form (meta bit 31): a general item of up to 16 FULL
 //    chunks of one packet with any other bpc in [4, 8192], k = ceil(bpc /
 //    512) virtual 512-byte blocks per chunk.  Each chunk is right-aligned
@@ -45,6 +50,7 @@ constexpr uint32_t kTileBlocks = 16;  // 512-byte blocks per tile
 constexpr uint32_t kBlockBytes = 512;
 constexpr uint32_t kMaxTileBpc = kTileBlocks * kBlockBytes;  // 8192
 constexpr uint32_t kGeneralTile = 0x80000000u;
+constexpr uint32_t kHalfTile = 0x40000000u;
 
 struct FastTile {
     // payload byte offset of the tile's first chunk (bits 0-47); general
@@ -54,6 +60,7 @@ struct FastTile {
     uint32_t out;   // checksum index of the tile's first chunk
     // power-of-two form: bits 0-7 = blocks in tile (1..16), bits 8-15 = lg = log2(bpc / 512);
     // padded power-of-two form: the same, bits 8-15 = lg = log2(k) and bits 18-26 = pad = 512 k - bpc;
+    // half form: bit 30, bits 0-7 = chunks, bits 8-15 = M, bits 18-26 = padh = 256 - (bpc - 512 M);
     // general form: bit 31, bits 0-7 = subtiles ceil((nch * k + kt) / 16), bits 8-12 = k, bits 13-17 = nch
     //               (full chunks in the item, 1..16), bits 18-26 = pad = 512 k - bpc
     uint32_t meta;
@@ -63,6 +70,7 @@ constexpr uint64_t kSrcMask = (1ull << 48) - 1;
 constexpr uint32_t kGeneralChunks = 16;  // full chunks per general item
 
 inline uint32_t padded_meta(uint32_t nb, uint32_t lg, uint32_t pad) { return nb | (lg << 8) | (pad << 18); }
+inline uint32_t half_meta(uint32_t n, uint32_t m, uint32_t padh) { return kHalfTile | n | (m << 8) | (padh << 18); }
 // pad of a power-of-two tile (0: unpadded; general tiles keep their own at the same bits)
 inline uint32_t tile_pad_bits(uint32_t meta) { return (meta >> 18) & 511u; }
 

@@ -162,7 +162,14 @@ void plans_and_framing(std::mt19937_64 &rng) {
             const uint64_t src = tiles[i].src & hdfs_crc::kSrcMask;
             const uint32_t tl = uint32_t(tiles[i].src >> 48), kt = (tl + 511u) / 512u;
             uint32_t nch, bpc;
-            if (meta & hdfs_crc::kGeneralTile) {
+            if ((meta & 0xC0000000u) == hdfs_crc::kHalfTile) {  // half tile: n chunks of 512 M + r bytes
+                const uint32_t m = (meta >> 8) & 0xffu, padh = (meta >> 18) & 511u;
+                nch = meta & 0xffu;
+                bpc = 512u * m + 256u - padh;
+                CHECK(m <= 1 && nch >= 1 && nch <= (m ? 10u : 32u) && padh < 256 && tl == 0 && bpc >= 4,
+                      "half tile meta %x", meta);
+                CHECK(padh == 0 || src >= 16, "half tile too close to the payload start");
+            } else if (meta & hdfs_crc::kGeneralTile) {
                 const uint32_t k = (meta >> 8) & 31u, pad = (meta >> 18) & 511u;
                 nch = (meta >> 13) & 31u;
                 bpc = k * 512u - pad;
@@ -290,7 +297,11 @@ void write_plans(std::mt19937_64 &rng) {
             uint32_t nch, tb;
             const uint64_t src = t.src & hdfs_crc::kSrcMask;
             const uint32_t tl = uint32_t(t.src >> 48);
-            if (t.meta & hdfs_crc::kGeneralTile) {
+            if ((t.meta & 0xC0000000u) == hdfs_crc::kHalfTile) {
+                nch = t.meta & 0xffu;
+                tb = 512u * ((t.meta >> 8) & 0xffu) + 256u - ((t.meta >> 18) & 511u);
+                CHECK(((t.meta >> 18) & 511u) == 0 || (src & 4095u) >= 16, "half tile page rule");
+            } else if (t.meta & hdfs_crc::kGeneralTile) {
                 nch = (t.meta >> 13) & 31u;
                 tb = ((t.meta >> 8) & 31u) * 512u - ((t.meta >> 18) & 511u);
                 CHECK(((t.meta >> 18) & 511u) == 0 || (src & 4095u) >= 16, "padded tile page rule");

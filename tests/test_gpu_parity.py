@@ -1007,3 +1007,63 @@ def test_padded_tiles_multi_block_launch(hdfs, gpu_ctx, orc, bpc):
     got = outs.cpu().numpy().view(np.uint32)
     for b in range(3):
         assert np.array_equal(got[b], wants[b]), b
+
+
+HALF_BPCS = [4, 17, 100, 200, 255, 256, 513, 600, 700, 767, 768]
+
+
+@pytest.mark.parametrize("npk", [3, 40, 600])
+def test_half_tiles(hdfs, gpu_ctx, orc, npk):
+    """bpc <= 256 and 512 < bpc <= 768 run as half tiles (round 5: two
+    chunks' partial parts per 512-byte block, the lower half on the columns
+    q + 16): packets with and without a tail chunk, first chunks at offsets
+    < 16 and odd offsets, both byte orders, verify with a corrupted payload
+    byte and a corrupted expectation; bit-exact against the reference."""
+    torch = _torch()
+    rng = np.random.default_rng(1900 + npk)
+    pk = np.zeros(npk, oracle.PACKET_DTYPE)
+    pk["bpc"] = rng.choice(HALF_BPCS, npk)
+    pk["len"] = np.where(rng.random(npk) < 0.5, 65536, rng.integers(1, 65537, npk))
+    gaps = rng.integers(0, 41, npk)
+    gaps[0] = rng.integers(0, 21)
+    pk["payload_off"] = np.cumsum(gaps) + np.concatenate([[0], np.cumsum(pk["len"].astype(np.int64))[:-1]])
+    per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    tiles, _ = hdfs.debug_plan(pk)
+    meta = tiles["meta"].astype(np.int64)
+    assert np.any((meta >> 30) == 1)  # some half tiles
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 2100 + npk)
+    n = hdfs.total_checksums(pk)
+    for flags in (0, hdfs.CRC32C_BIG_ENDIAN):
+        want = orc.batch(payload, pk, n, big_endian=bool(flags))
+        assert np.array_equal(run_dev(hdfs, gpu_ctx, payload, pk, flags), want)
+        assert np.array_equal(run_dev(hdfs, gpu_ctx, payload, pk, flags, offset=7), want)
+    want = orc.batch(payload, pk, n)
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def verify():
+        plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+        stream.synchronize()
+        return res.cpu().numpy().view(np.uint32).tolist()
+
+    assert verify() == [0, 0xFFFFFFFF]
+    p = pk[npk // 2]
+    off = int(p["len"]) // 3
+    dev[int(p["payload_off"]) + off] ^= 0x02
+    bad = int(p["out_idx"]) + off // int(p["bpc"])
+    assert verify() == [1, bad]
+    dev[int(p["payload_off"]) + off] ^= 0x02
+    exp[0] ^= 1
+    assert verify() == [1, 0]
+    plan.close()
+
+
+@pytest.mark.parametrize("bpc", [700, 100, 768, 256])
+def test_half_tiles_multi_block_launch(hdfs, gpu_ctx, orc, bpc):
+    """crc32c_plan_exec_blocks with a one-block plan of half tiles over blocks
+    at 16-byte-aligned and odd device addresses."""
+    test_padded_tiles_multi_block_launch(hdfs, gpu_ctx, orc, bpc)

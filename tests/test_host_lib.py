@@ -257,7 +257,12 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
     seen = np.zeros(n, np.int32)
     for t in tiles:
         meta, src, tl = int(t["meta"]), int(t["src"]) & ((1 << 48) - 1), int(t["src"]) >> 48
-        if meta & 0x80000000:  # general tile: nch chunks of any bpc in [4, 8192], k virtual blocks each
+        if meta & 0xC0000000 == 0x40000000:  # half tile: n chunks of M blocks + a partial half block each
+            nch, m, padh = meta & 0xFF, (meta >> 8) & 0xFF, (meta >> 18) & 511
+            bpc = 512 * m + 256 - padh
+            assert m in (0, 1) and 1 <= nch <= (10 if m else 32) and padh < 256 and tl == 0 and bpc >= 4
+            assert padh == 0 or src >= 16
+        elif meta & 0x80000000:  # general tile: nch chunks of any bpc in [4, 8192], k virtual blocks each
             k, nch, pad = (meta >> 8) & 31, (meta >> 13) & 31, (meta >> 18) & 511
             bpc, kt = k * 512 - pad, (tl + 511) // 512
             assert meta & 0xFF == (nch * k + kt + 15) // 16 and 1 <= nch <= 16 and 4 <= bpc <= 8192 and pad < 512
@@ -301,6 +306,17 @@ def test_plan_fast_path_shapes(hdfs):
     meta = tiles["meta"].astype(np.int64)
     assert gen.size == 0 and tiles.size == 9
     assert list(meta[:8]) == [16 | (1 << 8) | (24 << 18)] * 8 and meta[8] >> 31 and (meta[8] >> 13) & 31 == 1
+    # half tiles: bpc 700 (M = 1) -> 93 chunks and a 436-byte tail: 9 tiles of
+    # 10 chunks, one general item of 3 chunks + the tail; bpc 100 (M = 0): 655
+    # chunks and a 36-byte tail: 20 tiles of 32, one general item of 15 + tail
+    for bpc, ntiles, mhead, rest in ((700, 9, 10 | (1 << 8) | (68 << 18), 3), (100, 20, 32 | (156 << 18), 15)):
+        pk = oracle.uniform_packets(1)
+        pk["bpc"], pk["payload_off"] = bpc, 64
+        tiles, gen = hdfs.debug_plan(pk)
+        meta = tiles["meta"].astype(np.int64)
+        assert gen.size == 0 and tiles.size == ntiles + 1, bpc
+        assert list(meta[:ntiles]) == [0x40000000 | mhead] * ntiles, bpc
+        assert meta[ntiles] >> 31 and (meta[ntiles] >> 13) & 31 == rest, bpc
     # no tail: every chunk in padded tiles (bpc 4000, k = 8: 2 chunks per tile)
     pk = oracle.uniform_packets(1, pkt_len=64000)
     pk["bpc"], pk["payload_off"] = 4000, 64
@@ -348,6 +364,25 @@ def test_kernel_model_padded_tiles(orc, model, bpc):
     got = model.fast_chunks(virt.reshape(-1), lg) ^ np.uint32(model.c_lg[lg]) ^ np.uint32(
         orc.crc32c(np.zeros(bpc, np.uint8)))
     assert np.array_equal(got, orc.chunks(data, bpc))
+
+
+@pytest.mark.parametrize("bpc", [4, 17, 100, 255, 256, 513, 600, 700, 767, 768])
+def test_kernel_model_half_tiles(orc, model, bpc):
+    """Half tiles: a chunk's partial part (bpc - 512 M <= 256 bytes) right-
+    aligned into the upper half of a zero block -- what a lane of the lower
+    half computes with the columns q + 16 -- then, for M = 1, shifted by
+    Z^512 past the chunk's full block."""
+    m = 1 if bpc > 512 else 0
+    r = bpc - 512 * m
+    data = oracle.xorshift64_bytes(bpc * 3, 700 + bpc)
+    for c in range(3):
+        chunk = data[c * bpc:(c + 1) * bpc]
+        half = np.zeros(512, np.uint8)
+        half[512 - r:] = chunk[:r]
+        x = int(model.block_lin(half.reshape(1, 512))[0])
+        if m:
+            x = model.zshift(1, x) ^ int(model.block_lin(chunk[r:].reshape(1, 512))[0])
+        assert x ^ orc.crc32c(np.zeros(bpc, np.uint8)) == orc.crc32c(chunk), (bpc, c)
 
 
 def test_kernel_model_general_chunks(orc, model):
