@@ -109,11 +109,13 @@ constexpr int kModeNoGItems = 65536;
 constexpr int kModeGHoist = 131072;  // a general item's next subtile facts computed before this subtile's lookups
                                      // (the both-paths general build: padded chunks 0.5-2 % faster, round 5)
 constexpr int kModeGGroup2 = 262144;  // A/B: (with kModeNoShift) general items gathered 2 subtiles at a time, not 4
+constexpr int kModeHalfT = 1048576;   // (with kModeGeneral) the build also runs half tiles (their own builds: the
+                                      // code costs the other general builds 3-8 %, round 5)
 constexpr int kModeOvl = 524288;      // A/B: the first tile's loads issued right after the table staging's, before
                                       // the barrier that waits for the staging (their latencies overlap)
 // GEN bits of the tile helpers below: general tiles, shifted (unaligned)
 // tiles, general items gathered 4 subtiles at a time (finish_gtile GROUP)
-constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16;
+constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16, kGenHalf = 32;
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -878,7 +880,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
                      (GEN & kGenHoist) != 0>(p, lds, vacc, t, v, ev, lane);
         return;
     }
-    if ((GEN & kGenItems) && is_half(t)) {
+    if ((GEN & kGenHalf) && is_half(t)) {
         if ((t.meta >> 8) & 0xffu)
             finish_half<DIAG, S4, VERIFY, IMG, 1>(p, lds, vacc, t, v, ev, lane);
         else
@@ -922,7 +924,7 @@ template <int AUX, bool COMPDIAG, bool VERIFY, int GEN>
 __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane, uint4 v[9], uint32_t &ev) {
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         load_gtile<VERIFY>(p, t, lane, ev);
-    } else if ((GEN & kGenItems) && !COMPDIAG && is_half(t)) {
+    } else if ((GEN & kGenHalf) && !COMPDIAG && is_half(t)) {
         if ((t.meta >> 8) & 0xffu)
             load_tile_half<AUX, VERIFY, 1>(p, t, lane, v, ev);
         else
@@ -954,7 +956,8 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     const FastTile x = tile_at(p, j / SPLIT);
     const uint32_t u = j % SPLIT;
     const uint32_t lg = (x.meta >> 8) & 0xffu;
-    if (((GEN & kGenItems) && ((x.meta & kGeneralTile) || is_half(x) || tile_pad(x))) || (1u << lg) > kUB) {
+    if (((GEN & kGenItems) && ((x.meta & kGeneralTile) || tile_pad(x))) || ((GEN & kGenHalf) && is_half(x)) ||
+        (1u << lg) > kUB) {
         if (u) return 0;
         ft = x;
         load_any<AUX, COMPDIAG, VERIFY, GEN>(p, ft, lane, v, ev);
@@ -1029,7 +1032,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                                  : ((MODE & kModeNoGItems) ? 0 : kGenItems) |
                                        ((MODE & kModeNoShift) ? ((MODE & kModeGGroup2) ? kGenGroup2 : kGenGroup4)
                                                               : (kGenShift | kGenGroup2)) |
-                                       ((MODE & kModeGHoist) ? kGenHoist : 0);
+                                       ((MODE & kModeGHoist) ? kGenHoist : 0) | ((MODE & kModeHalfT) ? kGenHalf : 0);
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool OVL = !EARLY && (MODE & kModeOvl) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;

@@ -61,9 +61,18 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
         else                                                                       \
             hipLaunchKernelGGL(K, g, b, 0, stream, p);                             \
     } while (0)
+    // Half tiles run in builds of their own, any batch size (the full image):
+    // with the shifted loads only where some tile is off 16-byte alignment
+    // (padded general items -- a packet's tail -- do not need them there).
+    const bool half = (p.general & kGeneralHalf) != 0;
+    const bool half_shift = half && (p.general & kGeneralShift) != 0;
     if (p.expect) {
         if (!p.result || !p.sched) return hipErrorInvalidValue;
-        if (quarter)
+        if (half_shift)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeHalfT | kModeVerify>));
+        else if (half)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT | kModeVerify>));
+        else if (quarter)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>));
         else if (small)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>));
@@ -76,7 +85,11 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
         else
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeVerify>));
     } else {
-        if (quarter)
+        if (half_shift)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeHalfT>));
+        else if (half)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT>));
+        else if (quarter)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>));
         else if (small)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>));

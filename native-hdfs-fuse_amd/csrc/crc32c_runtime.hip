@@ -122,7 +122,13 @@ static bool has_padded_general(const HostPlan &hp) {
     }();
     if (off) return false;
     for (const FastTile &t : hp.tiles)
-        if (tile_pad_bits(t.meta) || (t.meta & kHalfTile)) return true;  // (general, padded or half tiles)
+        if (tile_pad_bits(t.meta) && !(t.meta & kHalfTile)) return true;  // (general or padded power-of-two tiles)
+    return false;
+}
+
+static bool has_half(const HostPlan &hp) {
+    for (const FastTile &t : hp.tiles)
+        if ((t.meta & (kGeneralTile | kHalfTile)) == kHalfTile) return true;
     return false;
 }
 
@@ -148,7 +154,10 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
     p.nconst = dp.nconst;
     // the general builds: general tiles (bit 0), shifted loads of tiles off 16-byte alignment (bit 1)
     p.general = (dp.general ? kGeneralItems : 0u) |
-                ((dp.misaligned || dp.padded || (reinterpret_cast<uintptr_t>(p.payload) & 15u)) ? kGeneralShift : 0u);
+                ((dp.misaligned || (dp.padded && !dp.half) || (reinterpret_cast<uintptr_t>(p.payload) & 15u))
+                     ? kGeneralShift
+                     : 0u) |
+                (dp.half ? kGeneralHalf : 0u);
     p.skip_z = dp.needs_z ? 0u : 1u;
     p.done_ctr = plan->counted ? reinterpret_cast<unsigned long long *>(dp.d + kDoneCtrOff) : nullptr;
     return p;
@@ -293,6 +302,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->general = has_general(hp);
     dp->misaligned = has_misaligned(hp);
     dp->padded = has_padded_general(hp);
+    dp->half = has_half(hp);
     dp->needs_z = needs_z(hp);
     dp->slots_off = 0;  // the verify slot first, the completion counters, then the work items
     static_assert(kSlotWords * sizeof(uint32_t) <= kDoneCtrOff, "the verify slot precedes the counters");
@@ -803,7 +813,8 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         // (the staged slices keep every packet's 16-byte phase: tiles off
         // alignment take the general build's shifted loads, as in plans)
         p.general = (has_general(plan) ? kGeneralItems : 0u) |
-                    ((has_misaligned(plan) || has_padded_general(plan)) ? kGeneralShift : 0u);
+                    ((has_misaligned(plan) || (has_padded_general(plan) && !has_half(plan))) ? kGeneralShift : 0u) |
+                    (has_half(plan) ? kGeneralHalf : 0u);
         p.skip_z = needs_z(plan) ? 0u : 1u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;

@@ -52,10 +52,11 @@ def test_exports_every_declared_symbol(hdfs):
 def test_product_library_has_no_variant_switch(hdfs):
     """The public path launches only the production kernel: the product .so
     exports no variant entry point or read probe, never reads a kernel-variant
-    environment variable, and holds exactly the twelve production kernels
+    environment variable, and holds exactly the sixteen production kernels
     (exec, verify; full image without general-tile code, with general tiles
     and shifted tiles, general tiles only, shifted tiles only; compact
-    image, compact image with quarter units); the A/B kernels live in the
+    image, compact image with quarter units; half tiles with general tiles,
+    with and without shifted tiles); the A/B kernels live in the
     debug library."""
     import ctypes
 
@@ -67,9 +68,11 @@ def test_product_library_has_no_variant_switch(hdfs):
     kernels = set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", blob))
     # modes: 3 = S4 | NT, + 64 verify, + 256 general-tile code, + 512 compact image (small batches),
     # + 4096 quarter units (the smallest batches), + 32768 no shifted tiles, + 65536 no general tiles,
-    # + 131072 general items' next subtile facts hoisted (the build with both general and shifted tiles)
+    # + 131072 general items' next subtile facts hoisted (the build with both general and shifted tiles),
+    # + 1048576 half tiles (their own builds: general tiles, with and without shifted tiles)
     assert kernels == {b"_Z23hdfs_crc32c_plan_kernelILi768ELi3ELi%dEEvN8hdfs_crc7KParamsE" % m
-                       for m in (3, 67, 131331, 131395, 771, 835, 4867, 4931, 33027, 33091, 65795, 65859)}, kernels
+                       for m in (3, 67, 131331, 131395, 771, 835, 4867, 4931, 33027, 33091, 65795, 65859,
+                                 1081603, 1081667, 1179907, 1179971)}, kernels
     dblob = open(hdfs.DEBUG_LIB_PATH, "rb").read()
     assert len(set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", dblob))) >= 9
 
