@@ -24,7 +24,8 @@ sys.path.insert(0, ROOT)
 
 
 def batch(hdfs, rng, size):
-    bpcs = rng.choice([512, 1024, 2048, 4096, 8192, 1536, 1000, 100, 3000, 513, 9000], size=size)
+    bpcs = rng.choice([512, 1024, 2048, 4096, 8192, 1536, 1000, 100, 3000, 513, 9000, 700, 2000, 4000, 256, 768, 7681],
+                      size=size)
     pk = np.zeros(size, hdfs.PACKET_DTYPE)
     off = out = 0
     for i in range(size):
@@ -76,7 +77,7 @@ def write_round(torch, hdfs, orc, ctx, rng, stream):
     sb = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
     bo = int(rng.integers(0, sb.size // 3 + 1))
     length = int(rng.integers(0, sb.size - bo + 1))
-    bpc = int(rng.choice([512, 1024, 4096, 100, 1536]))
+    bpc = int(rng.choice([512, 1024, 4096, 100, 1536, 700, 1000]))
     blockoffset = int(rng.integers(0, 3)) * int(rng.integers(0, 1 << 20))
     psize = int(rng.choice([65536, bpc * 7]))
     want = write_sums(orc, sb, bo, length, blockoffset, psize, bpc)
