@@ -102,10 +102,11 @@ def baseline_metric() -> str:
 
 def latest_pmc(profile_dir: str, config: str):
     """HBM bytes per launch of the kernel from the newest committed rocprofv3
-    PMC summary of this config (profiles/[rNN/]rNN_pmc_<config>.json, written
+    PMC summary of this config (profiles/[rNN/[pmc/]]rNN_pmc_<config>.json, written
     by tools/pmc_summary.py)."""
     files = glob.glob(os.path.join(profile_dir, "*pmc_c*.json")) + \
-        glob.glob(os.path.join(profile_dir, "r*", "*pmc_c*.json"))
+        glob.glob(os.path.join(profile_dir, "r*", "*pmc_c*.json")) + \
+        glob.glob(os.path.join(profile_dir, "r*", "pmc", "*pmc_c*.json"))
     best = None
     for fn in sorted(files, key=os.path.basename):
         try:
