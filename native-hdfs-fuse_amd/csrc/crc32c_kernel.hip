@@ -3,7 +3,7 @@
 //
 // libhdfs_crc32c.so ships the slicing-by-4 kernel with non-temporal payload
 // loads, 12 waves (768 threads) per workgroup and one workgroup per CU, in
-// three builds, each storing checksums (crc32c_plan_exec) or comparing them
+// these builds, each storing checksums (crc32c_plan_exec) or comparing them
 // (crc32c_plan_verify):
 //   * full image, power-of-two tiles only: the bulk path (config 2);
 //   * full image with the general-tile code (bpc outside 512 * 2^k, packet
@@ -19,7 +19,11 @@
 //   * the same with quarter units (each tile split over 4 waves, 2 pieces
 //     per lane): batches of at most kQuarterTilesPerCu tiles per CU, where
 //     one wave's load -> lookups chain is the launch (one 4 MiB block,
-//     graph-replayed: 4.36 -> 3.71 us).
+//     graph-replayed: 4.36 -> 3.71 us);
+//   * full image with the general-tile code and half tiles (bpc <= 256 and
+//     513..768), with and without the shifted loads, for any batch holding
+//     half tiles (compiled into the builds above, their code cost those
+//     3-8 %).
 // A/B and diagnostic variants are built only into libhdfs_crc32c_debug.so
 // (debug/crc32c_variants.hip).
 #include <hip/hip_ext.h>
@@ -50,7 +54,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     constexpr int kSmall = kModeS4C | kModeGeneral;
     constexpr int kQuarter = kSmall | kModeQuarter;
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
-    const bool small = items <= kSmallBatchItemsPerCu * num_cu;
+    const bool half = (p.general & kGeneralHalf) != 0;  // (half tiles: builds of their own, full image)
+    const bool small = !half && items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
     if (grid) *grid = g.x;
@@ -64,7 +69,6 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     // Half tiles run in builds of their own, any batch size (the full image):
     // with the shifted loads only where some tile is off 16-byte alignment
     // (padded general items -- a packet's tail -- do not need them there).
-    const bool half = (p.general & kGeneralHalf) != 0;
     const bool half_shift = half && (p.general & kGeneralShift) != 0;
     if (p.expect) {
         if (!p.result || !p.sched) return hipErrorInvalidValue;

@@ -152,10 +152,13 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         } else if (klg >= 0 && padded_tiles_on()) {
             // k a power of two: padded power-of-two tiles of 16 >> lg chunks.
             // A tail chunk (>= 4 bytes) still rides in a general item, with
-            // the last 1 .. 16 >> lg full chunks before it.
+            // the last 1 .. 16 >> lg full chunks before it.  (A/B knob
+            // HDFS_CRC32C_PADDED_TAIL_GEN=1: every full chunk in tiles, the
+            // tail alone a GenItem.)
+            static const bool tail_gen = env_long("HDFS_CRC32C_PADDED_TAIL_GEN") == 1;
             const uint64_t cpt = kTileBlocks >> klg;
             uint64_t upto = nfull;
-            if (tail >= 4 && nfull) upto = nfull - (nfull % cpt ? nfull % cpt : cpt);
+            if (tail >= 4 && nfull && !tail_gen) upto = nfull - (nfull % cpt ? nfull % cpt : cpt);
             while (c < upto) {
                 const uint64_t src = p.payload_off + c * p.bpc;
                 if (!early_ok(src)) {
