@@ -775,7 +775,8 @@ struct PadPrep {
 };
 
 // ---- half tiles (builds with the general-tile code) -----------------------
-// bpc <= 256 (M = 0) or 512 < bpc <= 768 (M = 1): a chunk is M full 512-byte
+// bpc <= 256 (M = 0), 512 < bpc <= 768 (M = 1) or 1024 < bpc <= 1280 (M = 2):
+// a chunk is M full 512-byte
 // blocks after a partial part of r = bpc - 512 M <= 256 bytes, right-aligned
 // into a 256-byte half block behind padh = 256 - r zeros.  Two partial parts
 // share one block: its upper half (lanes 16..31, whose columns are the last
@@ -788,39 +789,53 @@ struct PadPrep {
 //   M = 1: block c < 10 is chunk c's full block, block 10 + m the pair block
 //          of chunks 2m, 2m + 1 (up to 10 chunks per tile, 15 blocks); chunk
 //          c's lin = Z^512(its partial half's lin) ^ its full block's lin.
+//   M = 2: blocks 2c, 2c + 1 are chunk c's (c < 6), 12 + m the pair blocks
+//          (6 chunks, 15 blocks); lin = Z^1024(partial) ^ Z^512(block 2c)
+//          ^ block 2c + 1.
 // The tile holds n chunks; slots past n read what they read (never stored).
 // Round 5: bpc 700 took 2 virtual blocks per chunk as a padded tile, 1.5
 // here.
 __device__ __forceinline__ bool is_half(FastTile t) { return (t.meta & 0xC0000000u) == hdfs_crc::kHalfTile; }
 
+// Tile geometry of half tiles: full-block load instructions first (M = 1:
+// chunks 2i, 2i + 1, one block each; M = 2: chunk i's two blocks), then the
+// pair instructions; the full chunks' blocks before the pair blocks.
+template <uint32_t M>
+struct HalfShape {
+    static constexpr uint32_t kFullInstr = M == 0 ? 0u : M == 1 ? 5u : 6u;
+    static constexpr uint32_t kFullBlocks = 2u * kFullInstr;  // (pair block m: kFullBlocks + m)
+};
+
 template <int AUX, bool VERIFY, uint32_t M>
 __device__ __forceinline__ void load_tile_half(const KParams &p, FastTile t, int lane, uint4 v[8], uint32_t &ev) {
+    using S = HalfShape<M>;
     const uint32_t n = t.meta & 0xffu, padh = (t.meta >> 18) & 511u;
     const uint32_t r = 256u - padh, bpc = 512u * M + r;
     const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + t.src - 16u, 16u + n * bpc);
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u, u = q >> 4, q16h = 16u * (q & 15u);
     // pair instruction j: half-wave h is pair block 2j + h (chunks 4j + 2h,
     // 4j + 2h + 1), lane (u, q') of it reads 16 q' past chunk 4j + 2h + 1 - u's
-    // half-block start c bpc - padh; full instruction i (M = 1, i < 5):
-    // half-wave h is chunk 2i + h's full block, from c bpc + r
+    // half-block start c bpc - padh; full instruction i: M = 1, half-wave h
+    // is chunk 2i + h's full block, from c bpc + r; M = 2, the wave reads
+    // chunk i's two full blocks (1 KiB from i bpc + r)
     const uint32_t lane_pair = q16h + 16u <= padh ? 0x80000000u : (2u * h + 1u - u) * bpc + q16h;
-    const uint32_t lane_full = h * bpc + 16u * q;
+    const uint32_t lane_full = M == 1 ? h * bpc + 16u * q : 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         uint32_t voff;
-        if (M == 0 || i >= 5) {
-            const uint32_t j = M ? uint32_t(i) - 5u : uint32_t(i);
+        if (uint32_t(i) >= S::kFullInstr) {
+            const uint32_t j = uint32_t(i) - S::kFullInstr;
             voff = lane_pair + (16u + 4u * j * bpc - padh);
         } else {
-            voff = lane_full + (16u + 2u * uint32_t(i) * bpc + r);
+            voff = lane_full + (16u + (M == 1 ? 2u : 1u) * uint32_t(i) * bpc + r);
         }
         const auto x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, AUX);
         v[i] = make_uint4(x[0], x[1], x[2], x[3]);
     }
     if (VERIFY) {
         const uint32_t blk = rep_block(lane);
-        const uint32_t c = M ? blk : 2u * blk + 1u - ((uint32_t(lane) >> 4) & 1u);
-        const bool rep = M ? ((lane & 0x14) == 0 && blk < 10u) : (lane & 4) == 0;
+        const uint32_t c = M == 0 ? 2u * blk + 1u - ((uint32_t(lane) >> 4) & 1u) : blk / (M ? M : 1u);
+        const bool rep = M == 0 ? (lane & 4) == 0 : (lane & 0x14) == 0 && blk < S::kFullBlocks && blk % (M ? M : 1u) == 0;
         if (rep && c < n) ev = p.expect[t.out + c];
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -829,6 +844,7 @@ __device__ __forceinline__ void load_tile_half(const KParams &p, FastTile t, int
 template <int DIAG, bool S4, bool VERIFY, int IMG, uint32_t M>
 __device__ __forceinline__ void finish_half(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
                                             uint4 v[8], uint32_t ev, int lane) {
+    using S = HalfShape<M>;
     const uint32_t n = t.meta & 0xffu, padh = (t.meta >> 18) & 511u;
     typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
     const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
@@ -843,7 +859,7 @@ __device__ __forceinline__ void finish_half(const KParams &p, const uint8_t *lds
     uint32_t pc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const bool pair = M == 0 || i >= 5;
+        const bool pair = uint32_t(i) >= S::kFullInstr;
         if (pair && !(DIAG & 4)) {
             v[i].x &= kp.x;
             v[i].y &= kp.y;
@@ -855,18 +871,28 @@ __device__ __forceinline__ void finish_half(const KParams &p, const uint8_t *lds
         if (!S4 || (i & 1)) __builtin_amdgcn_sched_barrier(0);
     }
     const uint32_t blk = rep_block(lane);
-    uint32_t x = block_lin(pc, lane, M != 0 && blk < 10u);
+    uint32_t x = block_lin(pc, lane, M != 0 && blk < S::kFullBlocks);
     uint32_t c;
     bool rep;
     if (M == 0) {  // lane bit 4: the half, upper = chunk 2 blk
         c = 2u * blk + 1u - ((uint32_t(lane) >> 4) & 1u);
         rep = (lane & 4) == 0;
-    } else {  // full block c's lane takes its chunk's partial half from pair block 10 + c / 2
-        c = blk;
-        const uint32_t src = blk < 10u ? block_lane(10u + (blk >> 1)) | ((1u - (blk & 1u)) << 4) : uint32_t(lane);
+    } else {
+        // chunk c = blk / M: its full blocks (M = 2: block 2c shifted by
+        // Z^512 and joined with block 2c + 1, lane bit 5), then its partial
+        // half from pair block kFullBlocks + c / 2, shifted by Z^(512 M)
+        constexpr uint32_t kM = M ? M : 1u;
+        c = blk / kM;
+        uint32_t xf = x;  // (x itself stays: the pair blocks' lanes are read below)
+        if (M == 2) {
+            const uint32_t xs = (blk & 1u) ? x : zshift<S4, IMG>(lds, 1u, x);
+            xf = xs ^ static_cast<uint32_t>(__shfl_xor(static_cast<int>(xs), 32));
+        }
+        const uint32_t src =
+            blk < S::kFullBlocks ? block_lane(S::kFullBlocks + (c >> 1)) | ((1u - (c & 1u)) << 4) : uint32_t(lane);
         const uint32_t y = uint32_t(__builtin_amdgcn_ds_bpermute(int(src << 2), int(x)));
-        x ^= zshift<S4, IMG>(lds, 1u, y);
-        rep = (lane & 0x14) == 0 && blk < 10u;
+        x = xf ^ zshift<S4, IMG>(lds, kM, y);
+        rep = (lane & 0x14) == 0 && blk < S::kFullBlocks && blk % kM == 0;
     }
     if (rep && c < n) emit<VERIFY>(p, vacc, t.out + c, x ^ cst, ev);
 }
@@ -881,10 +907,11 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
         return;
     }
     if ((GEN & kGenHalf) && is_half(t)) {
-        if ((t.meta >> 8) & 0xffu)
-            finish_half<DIAG, S4, VERIFY, IMG, 1>(p, lds, vacc, t, v, ev, lane);
-        else
-            finish_half<DIAG, S4, VERIFY, IMG, 0>(p, lds, vacc, t, v, ev, lane);
+        switch ((t.meta >> 8) & 0xffu) {  // (uniform) M
+            case 0: finish_half<DIAG, S4, VERIFY, IMG, 0>(p, lds, vacc, t, v, ev, lane); break;
+            case 1: finish_half<DIAG, S4, VERIFY, IMG, 1>(p, lds, vacc, t, v, ev, lane); break;
+            default: finish_half<DIAG, S4, VERIFY, IMG, 2>(p, lds, vacc, t, v, ev, lane); break;
+        }
         return;
     }
     if ((GEN & kGenItems) && tile_pad(t)) {
@@ -925,10 +952,11 @@ __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane,
     if ((GEN & kGenItems) && (t.meta & kGeneralTile)) {
         load_gtile<VERIFY>(p, t, lane, ev);
     } else if ((GEN & kGenHalf) && !COMPDIAG && is_half(t)) {
-        if ((t.meta >> 8) & 0xffu)
-            load_tile_half<AUX, VERIFY, 1>(p, t, lane, v, ev);
-        else
-            load_tile_half<AUX, VERIFY, 0>(p, t, lane, v, ev);
+        switch ((t.meta >> 8) & 0xffu) {
+            case 0: load_tile_half<AUX, VERIFY, 0>(p, t, lane, v, ev); break;
+            case 1: load_tile_half<AUX, VERIFY, 1>(p, t, lane, v, ev); break;
+            default: load_tile_half<AUX, VERIFY, 2>(p, t, lane, v, ev); break;
+        }
     } else if ((GEN & kGenItems) && !COMPDIAG && tile_pad(t)) {
         load_tile_padded<AUX, VERIFY>(p, t, lane, v, ev);
     } else if ((GEN & kGenShift) && !COMPDIAG && tile_misalign(p, t)) {

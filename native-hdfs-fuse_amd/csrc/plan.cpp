@@ -126,12 +126,14 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
         const auto early_ok = [&](uint64_t src) { return absolute ? (src & 4095u) >= 16 : src >= 16; };
         uint64_t c = 0;
         const int klg = fast_lg(k * kBlockBytes);
-        const bool half = (p.bpc <= 256 || (p.bpc > 512 && p.bpc <= 768)) && half_tiles_on();
+        const bool half = (p.bpc <= 256 || (p.bpc > 512 && p.bpc <= 768) || (p.bpc > 1024 && p.bpc <= 1280)) &&
+                          half_tiles_on();
         if (half) {
-            // Half tiles of up to 32 (bpc <= 256) or 10 chunks; a tail chunk
-            // rides in a general item with the last 1 .. 32 / 10 full chunks.
-            const uint32_t m = p.bpc > 512 ? 1u : 0u, padh = 256u - (p.bpc - 512u * m);
-            const uint64_t cpt = m ? 10 : 32;
+            // Half tiles of up to 32 (bpc <= 256), 10 (M = 1) or 6 (M = 2)
+            // chunks; a tail chunk rides in a general item with the last
+            // chunks that did not fill a tile.
+            const uint32_t m = p.bpc / 512u, padh = 256u - (p.bpc - 512u * m);
+            const uint64_t cpt = m == 0 ? 32 : m == 1 ? 10 : 6;
             uint64_t upto = nfull;
             if (tail >= 4 && nfull) upto = nfull - (nfull % cpt ? nfull % cpt : cpt);
             while (c < upto) {

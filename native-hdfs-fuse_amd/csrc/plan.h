@@ -15,8 +15,9 @@
 //    virtual 512-byte blocks behind pad leading zeros, so the tile runs the
 //    power-of-two reduce (no per-subtile gather): only the lanes of each
 //    chunk's first block are masked, and the affine constant is bpc's.
-//  * FastTile, half form (meta bit 30): up to 32 (M = 0: bpc 4..256) or 10
-//    (M = 1: bpc 513..768) FULL chunks of one packet, each M whole 512-byte
+//  * FastTile, half form (meta bit 30): up to 32 (M = 0: bpc 4..256), 10
+//    (M = 1: bpc 513..768) or 6 (M = 2: bpc 1025..1280) FULL chunks of one
+//    packet, each M whole 512-byte
 //    blocks after a partial part of r = bpc - 512 M bytes right-aligned into
 //    a 256-byte half block behind padh = 256 - r zeros; two chunks' partial
 //    parts share one block (crc32c_device.h, half tiles).

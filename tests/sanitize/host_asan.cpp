@@ -166,7 +166,8 @@ void plans_and_framing(std::mt19937_64 &rng) {
                 const uint32_t m = (meta >> 8) & 0xffu, padh = (meta >> 18) & 511u;
                 nch = meta & 0xffu;
                 bpc = 512u * m + 256u - padh;
-                CHECK(m <= 1 && nch >= 1 && nch <= (m ? 10u : 32u) && padh < 256 && tl == 0 && bpc >= 4,
+                CHECK(m <= 2 && nch >= 1 && nch <= (m == 0 ? 32u : m == 1 ? 10u : 6u) && padh < 256 && tl == 0 &&
+                          bpc >= 4,
                       "half tile meta %x", meta);
                 CHECK(padh == 0 || src >= 16, "half tile too close to the payload start");
             } else if (meta & hdfs_crc::kGeneralTile) {

@@ -1009,7 +1009,7 @@ def test_padded_tiles_multi_block_launch(hdfs, gpu_ctx, orc, bpc):
         assert np.array_equal(got[b], wants[b]), b
 
 
-HALF_BPCS = [4, 17, 100, 200, 255, 256, 513, 600, 700, 767, 768]
+HALF_BPCS = [4, 17, 100, 200, 255, 256, 513, 600, 700, 767, 768, 1025, 1100, 1280]
 
 
 @pytest.mark.parametrize("npk", [3, 40, 600])
@@ -1062,7 +1062,7 @@ def test_half_tiles(hdfs, gpu_ctx, orc, npk):
     plan.close()
 
 
-@pytest.mark.parametrize("bpc", [700, 100, 768, 256])
+@pytest.mark.parametrize("bpc", [700, 100, 768, 256, 1100])
 def test_half_tiles_multi_block_launch(hdfs, gpu_ctx, orc, bpc):
     """crc32c_plan_exec_blocks with a one-block plan of half tiles over blocks
     at 16-byte-aligned and odd device addresses."""

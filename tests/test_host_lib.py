@@ -263,7 +263,7 @@ def test_plan_covers_every_chunk_once(hdfs, orc, name, pk):
         if meta & 0xC0000000 == 0x40000000:  # half tile: n chunks of M blocks + a partial half block each
             nch, m, padh = meta & 0xFF, (meta >> 8) & 0xFF, (meta >> 18) & 511
             bpc = 512 * m + 256 - padh
-            assert m in (0, 1) and 1 <= nch <= (10 if m else 32) and padh < 256 and tl == 0 and bpc >= 4
+            assert m in (0, 1, 2) and 1 <= nch <= (32, 10, 6)[m] and padh < 256 and tl == 0 and bpc >= 4
             assert padh == 0 or src >= 16
         elif meta & 0x80000000:  # general tile: nch chunks of any bpc in [4, 8192], k virtual blocks each
             k, nch, pad = (meta >> 8) & 31, (meta >> 13) & 31, (meta >> 18) & 511
@@ -369,13 +369,13 @@ def test_kernel_model_padded_tiles(orc, model, bpc):
     assert np.array_equal(got, orc.chunks(data, bpc))
 
 
-@pytest.mark.parametrize("bpc", [4, 17, 100, 255, 256, 513, 600, 700, 767, 768])
+@pytest.mark.parametrize("bpc", [4, 17, 100, 255, 256, 513, 600, 700, 767, 768, 1025, 1100, 1280])
 def test_kernel_model_half_tiles(orc, model, bpc):
     """Half tiles: a chunk's partial part (bpc - 512 M <= 256 bytes) right-
     aligned into the upper half of a zero block -- what a lane of the lower
-    half computes with the columns q + 16 -- then, for M = 1, shifted by
-    Z^512 past the chunk's full block."""
-    m = 1 if bpc > 512 else 0
+    half computes with the columns q + 16 -- then, for M >= 1, shifted by
+    Z^(512 M) past the chunk's full blocks."""
+    m = bpc // 512
     r = bpc - 512 * m
     data = oracle.xorshift64_bytes(bpc * 3, 700 + bpc)
     for c in range(3):
@@ -383,8 +383,11 @@ def test_kernel_model_half_tiles(orc, model, bpc):
         half = np.zeros(512, np.uint8)
         half[512 - r:] = chunk[:r]
         x = int(model.block_lin(half.reshape(1, 512))[0])
-        if m:
-            x = model.zshift(1, x) ^ int(model.block_lin(chunk[r:].reshape(1, 512))[0])
+        if m:  # the partial half shifted past the chunk's M full blocks, which are joined like a chunk's
+            x = model.zshift(m, x)
+            for j in range(m):
+                b = int(model.block_lin(chunk[r + 512 * j:r + 512 * (j + 1)].reshape(1, 512))[0])
+                x ^= model.zshift(m - 1 - j, b) if m - 1 - j else b
         assert x ^ orc.crc32c(np.zeros(bpc, np.uint8)) == orc.crc32c(chunk), (bpc, c)
 
 

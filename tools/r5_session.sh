@@ -85,7 +85,7 @@ for s in ${STEPS:-calls multi}; do
              run padw_tile_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     kbgen) for c in ${KBGCFGS:-c2 c2b2048 c2w2000}; do run kbg_$c 300 python tools/kbench.py --config $c --variants ${KBGV:-0,49,79,62} --rounds 7 --iters 300 || exit 1; done ;;
     kbovl) for c in ${KBOCFGS:-c2 p2048 c5 p1024}; do run kbo_$c 300 python tools/kbench.py --config $c --variants ${KBOV:-0,62,80} --rounds 9 --iters 300 || exit 1; done ;;
-    halfab) for c in ${HALFCFGS:-c2b700 c2b600 c2b768 c2b100 c2b200 c2w700}; do
+    halfab) for c in ${HALFCFGS:-c2b700 c2b600 c2b768 c2b100 c2b200 c2w700 c2b1100 c2b1280}; do
              run halfab_off_$c 300 env HDFS_CRC32C_HALF_TILES=0 python bench.py --config $c --no-cpu --no-host &&
              run halfab_on_$c 300 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     thalf) run thalf 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "half or padded or general or golden or random or fuzz or mixed or edge or small or verify or write_plan" ;;
