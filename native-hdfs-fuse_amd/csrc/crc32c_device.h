@@ -115,7 +115,8 @@ constexpr int kModeOvl = 524288;      // A/B: the first tile's loads issued righ
                                       // the barrier that waits for the staging (their latencies overlap)
 // GEN bits of the tile helpers below: general tiles, shifted (unaligned)
 // tiles, general items gathered 4 subtiles at a time (finish_gtile GROUP)
-constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16, kGenHalf = 32;
+constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16, kGenHalf = 32,
+              kGenPadded = 64;  // (padded power-of-two tiles: the full-image general builds only)
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -928,7 +929,7 @@ __device__ __forceinline__ void finish_tile(const KParams &p, const uint8_t *lds
         }
         return;
     }
-    if ((GEN & kGenItems) && tile_pad(t)) {
+    if ((GEN & kGenPadded) && tile_pad(t)) {
         const uint32_t pad = tile_pad(t), lg = (t.meta >> 8) & 0xffu;
         typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
         const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
@@ -971,7 +972,7 @@ __device__ __forceinline__ void load_any(const KParams &p, FastTile t, int lane,
             case 1: load_tile_half<AUX, VERIFY, 1>(p, t, lane, v, ev); break;
             default: load_tile_half<AUX, VERIFY, 2>(p, t, lane, v, ev); break;
         }
-    } else if ((GEN & kGenItems) && !COMPDIAG && tile_pad(t)) {
+    } else if ((GEN & kGenPadded) && !COMPDIAG && tile_pad(t)) {
         load_tile_padded<AUX, VERIFY>(p, t, lane, v, ev);
     } else if ((GEN & kGenShift) && !COMPDIAG && tile_misalign(p, t)) {
         load_tile_shifted<AUX, VERIFY>(p, t, tile_misalign(p, t), lane, v, ev);
@@ -998,7 +999,8 @@ __device__ __forceinline__ int load_unit(const KParams &p, uint32_t j, int lane,
     const FastTile x = tile_at(p, j / SPLIT);
     const uint32_t u = j % SPLIT;
     const uint32_t lg = (x.meta >> 8) & 0xffu;
-    if (((GEN & kGenItems) && ((x.meta & kGeneralTile) || tile_pad(x))) || ((GEN & kGenHalf) && is_half(x)) ||
+    if (((GEN & kGenItems) && (x.meta & kGeneralTile)) || ((GEN & kGenPadded) && tile_pad(x)) ||
+        ((GEN & kGenHalf) && is_half(x)) ||
         (1u << lg) > kUB) {
         if (u) return 0;
         ft = x;
@@ -1074,7 +1076,8 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                                  : ((MODE & kModeNoGItems) ? 0 : kGenItems) |
                                        ((MODE & kModeNoShift) ? ((MODE & kModeGGroup2) ? kGenGroup2 : kGenGroup4)
                                                               : (kGenShift | kGenGroup2)) |
-                                       ((MODE & kModeGHoist) ? kGenHoist : 0) | ((MODE & kModeHalfT) ? kGenHalf : 0);
+                                       ((MODE & kModeGHoist) ? kGenHoist : 0) | ((MODE & kModeHalfT) ? kGenHalf : 0) |
+                                       ((!(MODE & kModeNoGItems) && !C && !(MODE & kModeQuarter)) ? kGenPadded : 0);
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool OVL = !EARLY && (MODE & kModeOvl) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;

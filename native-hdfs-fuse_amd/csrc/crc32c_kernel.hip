@@ -55,7 +55,9 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     constexpr int kQuarter = kSmall | kModeQuarter;
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const bool half = (p.general & kGeneralHalf) != 0;  // (half tiles: builds of their own, full image)
-    const bool small = !half && items <= kSmallBatchItemsPerCu * num_cu;
+    // (padded power-of-two tiles and half tiles only run in full-image
+    // builds: their code in the small-batch builds cost config 3 ~4 %)
+    const bool small = !half && !(p.general & kGeneralPadded) && items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
     if (grid) *grid = g.x;

@@ -126,6 +126,12 @@ static bool has_padded_general(const HostPlan &hp) {
     return false;
 }
 
+static bool has_padded_tiles(const HostPlan &hp) {
+    for (const FastTile &t : hp.tiles)
+        if (!(t.meta & (kGeneralTile | kHalfTile)) && tile_pad_bits(t.meta)) return true;
+    return false;
+}
+
 static bool has_half(const HostPlan &hp) {
     for (const FastTile &t : hp.tiles)
         if ((t.meta & (kGeneralTile | kHalfTile)) == kHalfTile) return true;
@@ -157,7 +163,7 @@ KParams plan_params(const crc32c_plan *plan, const void *payload, uint32_t *out)
                 ((dp.misaligned || (dp.padded && !dp.half) || (reinterpret_cast<uintptr_t>(p.payload) & 15u))
                      ? kGeneralShift
                      : 0u) |
-                (dp.half ? kGeneralHalf : 0u);
+                (dp.half ? kGeneralHalf : 0u) | (dp.padtiles ? kGeneralPadded : 0u);
     p.skip_z = dp.needs_z ? 0u : 1u;
     p.done_ctr = plan->counted ? reinterpret_cast<unsigned long long *>(dp.d + kDoneCtrOff) : nullptr;
     return p;
@@ -303,6 +309,7 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->misaligned = has_misaligned(hp);
     dp->padded = has_padded_general(hp);
     dp->half = has_half(hp);
+    dp->padtiles = has_padded_tiles(hp);
     dp->needs_z = needs_z(hp);
     dp->slots_off = 0;  // the verify slot first, the completion counters, then the work items
     static_assert(kSlotWords * sizeof(uint32_t) <= kDoneCtrOff, "the verify slot precedes the counters");
@@ -814,7 +821,7 @@ int batch_host_locked(crc32c_ctx *ctx, const uint8_t *payload, const crc32c_pack
         // alignment take the general build's shifted loads, as in plans)
         p.general = (has_general(plan) ? kGeneralItems : 0u) |
                     ((has_misaligned(plan) || (has_padded_general(plan) && !has_half(plan))) ? kGeneralShift : 0u) |
-                    (has_half(plan) ? kGeneralHalf : 0u);
+                    (has_half(plan) ? kGeneralHalf : 0u) | (has_padded_tiles(plan) ? kGeneralPadded : 0u);
         p.skip_z = needs_z(plan) ? 0u : 1u;
         rc = launch(ctx, p, s.sched, s.stream);
         if (rc) return rc;

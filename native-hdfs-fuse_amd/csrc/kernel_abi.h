@@ -34,7 +34,7 @@ struct BlockRef {
 // Blocks one launch carries (in the kernel arguments: 16 B each).
 constexpr uint32_t kMaxLaunchBlocks = 32;
 
-constexpr uint32_t kGeneralItems = 1u, kGeneralShift = 2u, kGeneralHalf = 4u;  // KParams::general bits
+constexpr uint32_t kGeneralItems = 1u, kGeneralShift = 2u, kGeneralHalf = 4u, kGeneralPadded = 8u;  // KParams::general
 
 struct KParams {
     const FastTile *tiles;  // power-of-two and general tiles
@@ -51,7 +51,8 @@ struct KParams {
     uint32_t nseg;
     uint32_t nconst;
     uint32_t general;  // kGeneralItems: tiles[] holds general tiles; kGeneralShift: some tile is off 16-byte
-                       // alignment; kGeneralHalf: half tiles (each selects a build that has that code)
+                       // alignment; kGeneralHalf: half tiles; kGeneralPadded: padded power-of-two tiles (each
+                       // selects a build that has that code)
     uint32_t skip_z;   // 1: no item shifts by Z^(512 s): the S4 images are staged without their Z section
     uint32_t flags;
     uint32_t c_lg[5];

@@ -91,6 +91,7 @@ struct DevicePlan {
     bool misaligned = false;  // some power-of-two tile's offset is not a multiple of 16
     bool padded = false;      // some general tile's full chunks are padded (bpc not 512 k)
     bool half = false;        // some tile is a half tile (their own builds)
+    bool padtiles = false;    // some tile is a padded power-of-two tile (full-image general builds)
     bool needs_z = true;      // some item shifts by Z^(512 s) (the image's last 7.5 KiB)
     size_t tiles_off = 0, gen_off = 0, seg_off = 0, pieces_off = 0, consts_off = 0, slots_off = 0;
 };
