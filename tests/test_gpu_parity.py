@@ -842,13 +842,15 @@ def test_fuzz_mixed_batches(hdfs, gpu_ctx, orc, seed):
     """Seeded random batches that mix every work-item kind the plan can
     build -- power-of-two tiles at any alignment (shifted or not), general
     items (padded and unpadded bpc, tails riding behind full chunks, chunks
-    spanning subtiles), GenItems (tails under 4 bytes, bpc > 8192) -- at
-    sizes that select each kernel build (quarter units, compact image, full
-    image); exec and verify against the oracle."""
+    spanning subtiles), padded power-of-two tiles, half tiles, GenItems
+    (tails under 4 bytes, bpc > 8192) -- at sizes that select each kernel
+    build (quarter units, compact image, full image; half-tile builds with
+    and without shifted loads); exec and verify against the oracle."""
     torch = _torch()
     rng = np.random.default_rng(seed)
     for size in (12, 90, 700):  # packets: quarter-unit, compact and full-image builds
-        bpcs = rng.choice([512, 1024, 4096, 8192, 1536, 1000, 100, 3000, 513, 9000], size=size)
+        bpcs = rng.choice([512, 1024, 4096, 8192, 1536, 1000, 100, 3000, 513, 9000, 700, 1100, 2000, 256],
+                          size=size)
         pk = np.zeros(size, hdfs.PACKET_DTYPE)
         off = out = 0
         for i in range(size):
