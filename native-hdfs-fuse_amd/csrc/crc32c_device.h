@@ -111,12 +111,14 @@ constexpr int kModeGHoist = 131072;  // a general item's next subtile facts comp
 constexpr int kModeGGroup2 = 262144;  // A/B: (with kModeNoShift) general items gathered 2 subtiles at a time, not 4
 constexpr int kModeHalfT = 1048576;   // (with kModeGeneral) the build also runs half tiles (their own builds: the
                                       // code costs the other general builds 3-8 %, round 5)
+constexpr int kModeNoPadT = 2097152;  // (general builds) no padded power-of-two tiles: the production small-batch
+                                      // builds (their code there cost config 3 ~4 %, round 5)
 constexpr int kModeOvl = 524288;      // A/B: the first tile's loads issued right after the table staging's, before
                                       // the barrier that waits for the staging (their latencies overlap)
 // GEN bits of the tile helpers below: general tiles, shifted (unaligned)
 // tiles, general items gathered 4 subtiles at a time (finish_gtile GROUP)
 constexpr int kGenItems = 1, kGenShift = 2, kGenGroup4 = 4, kGenGroup2 = 8, kGenHoist = 16, kGenHalf = 32,
-              kGenPadded = 64;  // (padded power-of-two tiles: the full-image general builds only)
+              kGenPadded = 64;  // (padded power-of-two tiles: not in builds with kModeNoPadT)
 
 // Work descriptors are read-only for the whole launch: reading them through
 // the constant address space lets every (wave-uniform) descriptor fetch be a
@@ -1077,7 +1079,7 @@ __global__ __launch_bounds__(THREADS, WPS) void hdfs_crc32c_plan_kernel(hdfs_crc
                                        ((MODE & kModeNoShift) ? ((MODE & kModeGGroup2) ? kGenGroup2 : kGenGroup4)
                                                               : (kGenShift | kGenGroup2)) |
                                        ((MODE & kModeGHoist) ? kGenHoist : 0) | ((MODE & kModeHalfT) ? kGenHalf : 0) |
-                                       ((!(MODE & kModeNoGItems) && !C && !(MODE & kModeQuarter)) ? kGenPadded : 0);
+                                       ((!(MODE & (kModeNoGItems | kModeNoPadT))) ? kGenPadded : 0);
     constexpr bool EARLY = (MODE & kModeEarly) != 0;
     constexpr bool OVL = !EARLY && (MODE & kModeOvl) != 0;
     constexpr bool QUARTER = (MODE & kModeQuarter) != 0;

@@ -51,7 +51,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     using namespace hdfs_crc_dev;
     constexpr int kProd = kModeS4 | kModeNt;
     constexpr int kGen = kModeGeneral;
-    constexpr int kSmall = kModeS4C | kModeGeneral;
+    constexpr int kSmall = kModeS4C | kModeGeneral | kModeNoPadT;
     constexpr int kQuarter = kSmall | kModeQuarter;
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const bool half = (p.general & kGeneralHalf) != 0;  // (half tiles: builds of their own, full image)

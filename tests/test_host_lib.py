@@ -69,10 +69,12 @@ def test_product_library_has_no_variant_switch(hdfs):
     # modes: 3 = S4 | NT, + 64 verify, + 256 general-tile code, + 512 compact image (small batches),
     # + 4096 quarter units (the smallest batches), + 32768 no shifted tiles, + 65536 no general tiles,
     # + 131072 general items' next subtile facts hoisted (the build with both general and shifted tiles),
-    # + 1048576 half tiles (their own builds: general tiles, with and without shifted tiles)
+    # + 1048576 half tiles (their own builds: general tiles, with and without shifted tiles),
+    # + 2097152 (NP) no padded power-of-two tiles (the small-batch builds)
+    NP = 2097152
     assert kernels == {b"_Z23hdfs_crc32c_plan_kernelILi768ELi3ELi%dEEvN8hdfs_crc7KParamsE" % m
-                       for m in (3, 67, 131331, 131395, 771, 835, 4867, 4931, 33027, 33091, 65795, 65859,
-                                 1081603, 1081667, 1179907, 1179971)}, kernels
+                       for m in (3, 67, 131331, 131395, 771 + NP, 835 + NP, 4867 + NP, 4931 + NP, 33027, 33091, 65795,
+                                 65859, 1081603, 1081667, 1179907, 1179971)}, kernels
     dblob = open(hdfs.DEBUG_LIB_PATH, "rb").read()
     assert len(set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", dblob))) >= 9
 
