@@ -106,7 +106,15 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             t.src = p.payload_off + b * kBlockBytes;
             t.out = uint32_t(p.out_idx + (b >> lg));
             t.meta = uint32_t(nb) | (uint32_t(lg) << 8);
-            if (b + nb == blocks && tail >= 4) {
+            // A tail of at most one 512-byte block is a GenItem on its own
+            // (the batch then keeps the power-of-two build: 412-byte tails,
+            // same box, 46.25 -> 44.89 us, round 5); a longer one rides
+            // behind the packet's last chunks in a general item, since a
+            // GenItem runs its blocks one after another at the launch's end.
+            // A/B knob HDFS_CRC32C_POW2_TAIL_GEN: 1 always a GenItem, 0 never.
+            static const long pow2_tail_knob = env_long("HDFS_CRC32C_POW2_TAIL_GEN");
+            const bool pow2_tail_gen = pow2_tail_knob == 1 || (pow2_tail_knob != 0 && tail <= kBlockBytes);
+            if (b + nb == blocks && tail >= 4 && !pow2_tail_gen) {
                 // the packet's short tail chunk rides behind its last chunks:
                 // that tile becomes a general item (k = 2^lg, no pad)
                 t.src |= uint64_t(tail) << 48;

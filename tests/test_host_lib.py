@@ -299,8 +299,14 @@ def test_plan_fast_path_shapes(hdfs):
     assert tiles.size == 4096 * 8 and gen.size == 0 and np.all(tiles["meta"] == 16)
     tiles, gen = hdfs.debug_plan(oracle.mixed_packets(3))
     assert list(tiles["meta"][:1]) == [16] and set(int(m) >> 8 for m in tiles["meta"]) == {0, 1, 3}
-    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65436))  # the tail rides in the last tile
-    assert gen.size == 0 and int(tiles["src"][-1]) >> 48 == 65436 % 512 and int(tiles["meta"][-1]) >> 31
+    # a tail of at most 512 bytes is a GenItem of its own (the tiles stay power-of-two ones) ...
+    tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65436))
+    assert gen.size == 1 and int(gen["len"][0]) == 65436 % 512 and not np.any(tiles["meta"] >> 31)
+    # ... a longer one rides in the last tile, which becomes a general item
+    pk = oracle.uniform_packets(1, pkt_len=65436)
+    pk["bpc"] = 1024
+    tiles, gen = hdfs.debug_plan(pk)
+    assert gen.size == 0 and int(tiles["src"][-1]) >> 48 == 65436 % 1024 and int(tiles["meta"][-1]) >> 31
     tiles, gen = hdfs.debug_plan(oracle.uniform_packets(1, pkt_len=65539))  # a 3-byte tail: general path
     assert gen.size == 1 and int(gen["len"][0]) == 3
     # bpc 1000 (k = 2, pad 24): 65 full chunks and a 536-byte tail -> 8 padded

@@ -95,6 +95,9 @@ for s in ${STEPS:-calls multi}; do
     tailab) for r in 1 2; do for c in ${TAILCFGS:-c2b1000 c2b2000 c2b4000}; do
              run tailab_item_${c}_$r 300 python bench.py --config $c --no-cpu --no-host &&
              run tailab_gen_${c}_$r 300 env HDFS_CRC32C_PADDED_TAIL_GEN=1 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
+    p2tail) for r in 1 2; do for c in ${P2CFGS:-c2t c5}; do
+             run p2t_item_${c}_$r 300 python bench.py --config $c --no-cpu --no-host &&
+             run p2t_gen_${c}_$r 300 env HDFS_CRC32C_POW2_TAIL_GEN=1 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
     padab) for r in $(seq 1 ${PADR:-1}); do for c in ${PADCFGS:-c2b1000 c2b700 c2b4000 c2b2000 c2b100}; do
              run padab_gen_${c}_$r 300 env HDFS_CRC32C_PADDED_TILES=0 python bench.py --config $c --no-cpu --no-host &&
              run padab_tile_${c}_$r 300 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
