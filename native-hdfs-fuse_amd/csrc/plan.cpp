@@ -142,8 +142,15 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             // chunks that did not fill a tile.
             const uint32_t m = p.bpc / 512u, padh = 256u - (p.bpc - 512u * m);
             const uint64_t cpt = m == 0 ? 32 : m == 1 ? 10 : 6;
+            // (as next to padded tiles: the tail alone a GenItem when the
+            // general item would span two subtiles; A/B knob
+            // HDFS_CRC32C_HALF_TAIL_GEN: 1 always, 0 never)
+            static const long half_tail_knob = env_long("HDFS_CRC32C_HALF_TAIL_GEN");
+            const uint64_t last = nfull % cpt ? nfull % cpt : cpt;
+            const bool tail_gen = half_tail_knob == 1 ||
+                                  (half_tail_knob != 0 && last * k + (tail + kBlockBytes - 1) / kBlockBytes > kTileBlocks);
             uint64_t upto = nfull;
-            if (tail >= 4 && nfull) upto = nfull - (nfull % cpt ? nfull % cpt : cpt);
+            if (tail >= 4 && nfull && !tail_gen) upto = nfull - last;
             while (c < upto) {
                 const uint64_t src = p.payload_off + c * p.bpc;
                 if (!early_ok(src)) {

@@ -98,6 +98,10 @@ for s in ${STEPS:-calls multi}; do
     p2tail) for r in 1 2; do for c in ${P2CFGS:-c2t c5}; do
              run p2t_item_${c}_$r 300 python bench.py --config $c --no-cpu --no-host &&
              run p2t_gen_${c}_$r 300 env HDFS_CRC32C_POW2_TAIL_GEN=1 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
+    htail) for c in ${HTCFGS:-c2b700 c2b1100 c2b100 c2b600}; do
+             run ht_rule_$c 300 python bench.py --config $c --no-cpu --no-host &&
+             run ht_never_$c 300 env HDFS_CRC32C_HALF_TAIL_GEN=0 python bench.py --config $c --no-cpu --no-host &&
+             run ht_always_$c 300 env HDFS_CRC32C_HALF_TAIL_GEN=1 python bench.py --config $c --no-cpu --no-host || exit 1; done ;;
     padab) for r in $(seq 1 ${PADR:-1}); do for c in ${PADCFGS:-c2b1000 c2b700 c2b4000 c2b2000 c2b100}; do
              run padab_gen_${c}_$r 300 env HDFS_CRC32C_PADDED_TILES=0 python bench.py --config $c --no-cpu --no-host &&
              run padab_tile_${c}_$r 300 python bench.py --config $c --no-cpu --no-host || exit 1; done; done ;;
