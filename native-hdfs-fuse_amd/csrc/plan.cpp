@@ -82,6 +82,16 @@ static bool half_tiles_on() {
     return on;
 }
 
+// Whether a packet's tail chunk (tl >= 4 bytes) next to tiles of whole
+// chunks goes alone into a GenItem rather than into a general item with the
+// packet's last `last` full chunks (k virtual blocks each): when that item
+// would not fit one 16-block subtile.  knob (an A/B environment variable): 1
+// always a GenItem, 0 never, unset the rule.
+static bool tail_alone(long knob, uint64_t last, uint32_t k, uint32_t tl) {
+    if (knob == 1 || knob == 0) return knob == 1;
+    return last * k + (tl + kBlockBytes - 1) / kBlockBytes > kTileBlocks;
+}
+
 int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
     // A zero-length packet (the block's last-packet marker, hadooprpc.c:644,
     // 853-856) has no checksums whatever its bpc; any other needs bpc > 0.
@@ -147,8 +157,7 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             // HDFS_CRC32C_HALF_TAIL_GEN: 1 always, 0 never)
             static const long half_tail_knob = env_long("HDFS_CRC32C_HALF_TAIL_GEN");
             const uint64_t last = nfull % cpt ? nfull % cpt : cpt;
-            const bool tail_gen = half_tail_knob == 1 ||
-                                  (half_tail_knob != 0 && last * k + (tail + kBlockBytes - 1) / kBlockBytes > kTileBlocks);
+            const bool tail_gen = tail_alone(half_tail_knob, last, k, tail);
             uint64_t upto = nfull;
             if (tail >= 4 && nfull && !tail_gen) upto = nfull - last;
             while (c < upto) {
@@ -178,8 +187,7 @@ int append_packet(const crc32c_packet &p, HostPlan *plan, bool absolute) {
             static const long tail_knob = env_long("HDFS_CRC32C_PADDED_TAIL_GEN");
             const uint64_t cpt = kTileBlocks >> klg;
             const uint64_t last = nfull % cpt ? nfull % cpt : cpt;
-            const bool tail_gen = tail_knob == 1 ||
-                                  (tail_knob != 0 && last * k + (tail + kBlockBytes - 1) / kBlockBytes > kTileBlocks);
+            const bool tail_gen = tail_alone(tail_knob, last, k, tail);
             uint64_t upto = nfull;
             if (tail >= 4 && nfull && !tail_gen) upto = nfull - last;
             while (c < upto) {
