@@ -228,6 +228,69 @@ def cpu_baseline(pk, payload_np: np.ndarray, seconds: float, nbuf: int = 4):
     }
 
 
+CPU_BASELINE_KEY = "bench/cpu_baseline_done"
+
+
+def cpu_baseline_on_rank0(env, fn, wait_s: float = 900.0):
+    """The CPU baseline leg at any N (north_star: the 1/2/4/8-GPU figures
+    "next to src/crc32c.c timed on the same box's host cores in the same
+    run"): rank 0 runs fn() once every rank has finished its GPU timed
+    regions and collectives; the other ranks wait for it on the process
+    group's store -- a blocking socket read, not a spinning collective, so
+    they take no host CPU time from the baseline's threads.  Returns fn()'s
+    result on rank 0, None elsewhere."""
+    if env.world == 1:
+        return fn()
+    import datetime
+
+    import torch.distributed as dist
+
+    store = dist.distributed_c10d._get_default_store()
+    if env.rank == 0:
+        try:
+            return fn()
+        finally:
+            store.set(CPU_BASELINE_KEY, "1")
+    store.wait([CPU_BASELINE_KEY], datetime.timedelta(seconds=wait_s))
+    return None
+
+
+def roofline_node(nbytes_per_rank: int, kernel_us_max: float, world: int) -> dict:
+    """Node-level roofline fields beside the per-GPU ones: every rank's bytes
+    over the slowest rank's kernel time, against N GPUs' HBM peak."""
+    achieved = world * nbytes_per_rank / (kernel_us_max * 1e-6) / 1e9 if kernel_us_max > 0 else 0.0
+    return {"achieved_node": round(achieved, 1), "peak_node": PEAK_HBM_GBS * world,
+            "frac_node": round(achieved / (PEAK_HBM_GBS * world), 4)}
+
+
+# What every printed line carries (the driver's contract plus this path's
+# roofline / cpu_baseline objects); checked by the tests against real lines.
+LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+ROOFLINE_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "achieved_node", "peak_node", "frac_node")
+CPU_BASELINE_KEYS = ("value", "unit", "cores", "kind", "sample")
+
+
+def line_problems(d: dict, want_cpu: bool = True) -> list:
+    """What a bench line lacks against the contract (empty when complete)."""
+    bad = ["missing %s" % k for k in LINE_KEYS if k not in d]
+    rf = d.get("roofline") or {}
+    bad += ["roofline missing %s" % k for k in ROOFLINE_KEYS if k not in rf]
+    if "peak_node" in rf and rf["peak_node"] != PEAK_HBM_GBS * d.get("n_gpus", 0):
+        bad.append("roofline.peak_node is not n_gpus x %.0f GB/s" % PEAK_HBM_GBS)
+    if "frac_node" in rf and not (0 < (rf["frac_node"] or 0) < 1):
+        bad.append("roofline.frac_node out of (0, 1)")
+    cb = d.get("cpu_baseline")
+    if want_cpu:
+        if not isinstance(cb, dict):
+            bad.append("cpu_baseline is %r" % (cb,))
+        else:
+            bad += ["cpu_baseline missing %s" % k for k in CPU_BASELINE_KEYS if k not in cb]
+            if cb.get("unit") != d.get("unit"):
+                bad.append("cpu_baseline unit differs from the line's")
+    return bad
+
+
 def free_port() -> int:
     import socket
 
@@ -756,9 +819,10 @@ def main():
     ap.add_argument("--no-host", action="store_true")
     ap.add_argument("--no-config4", action="store_true", help="skip the config4 sub-object of the c2 line")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong_scaling sub-object of the c2 line")
-    ap.add_argument("--sub-timeout-s", type=float, default=300.0,
-                    help="bound on the config4 + strong_scaling sub-runs and the teardown after them: past it "
-                         "rank 0 prints the main line with the sub-objects marked timed out and every rank exits")
+    ap.add_argument("--sub-timeout-s", type=float, default=420.0,
+                    help="bound on the config4 + strong_scaling sub-runs, the CPU baseline and the teardown after "
+                         "them: past it rank 0 prints the main line with the sub-objects marked timed out and every "
+                         "rank exits")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak (default): every rank checksums its own config batch; strong: the config-2/5 batch's "
                          "packets are split evenly over the ranks (SURVEY.md section 8e)")
@@ -834,18 +898,25 @@ def main():
                 "config": {"workload": c4["workload"], "config": "c4",
                            "parallelism": "dp%d (block shards, crc32c_multi_plan: RCCL send/recv gather of the "
                                           "checksums to rank 0 inside every step)" % world},
-                "roofline": {"bound": "hbm", "achieved": round(C4_BLOCKS * shard.BLOCK_BYTES / (kus * 1e-6) / 1e9, 1),
-                             "peak": PEAK_HBM_GBS * world, "unit": "GB/s", "frac": c4["frac_of_hbm_roofline"],
-                             "traffic": None, "kernel": KERNEL_NAME, "kernel_avg_us": kus,
-                             "algorithmic_bytes_per_launch": C4_BLOCKS * shard.BLOCK_BYTES},
+                # (the step's bytes are the whole file's, over N GPUs: peak and
+                # frac are node-level here; the _node fields say the same)
+                "roofline": dict({"bound": "hbm", "achieved": round(C4_BLOCKS * shard.BLOCK_BYTES / (kus * 1e-6) / 1e9, 1),
+                                  "peak": PEAK_HBM_GBS * world, "unit": "GB/s", "frac": c4["frac_of_hbm_roofline"],
+                                  "traffic": None, "kernel": KERNEL_NAME, "kernel_avg_us": kus,
+                                  "algorithmic_bytes_per_launch": C4_BLOCKS * shard.BLOCK_BYTES,
+                                  "shard_frac_per_gpu": c4["shard_frac_of_hbm_roofline"]},
+                                 **roofline_node(C4_BLOCKS * shard.BLOCK_BYTES // world, kus, world)),
                 "cpu_baseline": None, "bit_exact_vs_reference": c4["bit_exact"], "config4": c4,
             }
-            if not args.no_cpu and world == 1:
-                from hdfs_crc32c_amd.workloads import uniform_packets
+        if not args.no_cpu:  # (rank 0, after every rank's GPU work; the others wait)
+            from hdfs_crc32c_amd.workloads import uniform_packets
 
-                line["cpu_baseline"] = cpu_baseline(uniform_packets(C4_GROUP_PACKETS * C4_BLOCKS),
-                                                    synthetic_bytes(C4_BLOCKS * shard.BLOCK_BYTES, 2024),
-                                                    args.cpu_seconds)
+            cb = cpu_baseline_on_rank0(env, lambda: cpu_baseline(
+                uniform_packets(C4_GROUP_PACKETS * C4_BLOCKS), synthetic_bytes(C4_BLOCKS * shard.BLOCK_BYTES, 2024),
+                args.cpu_seconds))
+            if rank == 0:
+                line["cpu_baseline"] = cb
+        if rank == 0:
             print(json.dumps(line), flush=True)
         if world > 1:
             dist.destroy_process_group()
@@ -1177,8 +1248,6 @@ def main():
                 and PRODUCTION_KERNEL in pmc.get("dispatch_meta", {}).get("Kernel_Name", "")):
             traffic = pmc.get("hbm_bytes_per_launch")
             traffic_commit = pmc.get("commit")
-        # the CPU baseline is an N = 1 figure (timed on rank 0's host cores)
-        cpu = None if args.no_cpu or world > 1 else cpu_baseline(pk, payload0, args.cpu_seconds)
         line = {
             "metric": baseline_metric(),
             "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
@@ -1193,7 +1262,7 @@ def main():
                        "payload_bytes_per_rank": nbytes, "checksums_per_rank": nout,
                        "parallelism": "dp%d (independent shards, %s gather of checksums after timing)"
                                       % (world, "RCCL" if backend == "nccl" else backend + " rehearsal")},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "roofline": dict({"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "traffic_source": None if traffic is None else
                          "rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE per launch, profiles/ summary at commit %s"
@@ -1206,8 +1275,8 @@ def main():
                          "lead_steps": "host-issued" if (r["lead_host"] or not use_graph) else "graph",
                          "host_issue_us_per_step": round(r["host_issue_us"], 2),
                          "window_avg_us_all_steps": round(window_ms * 1e3, 2),
-                         "algorithmic_bytes_per_launch": nbytes},
-            "cpu_baseline": cpu,
+                         "algorithmic_bytes_per_launch": nbytes}, **roofline_node(nbytes, kernel_ms * 1e3, world)),
+            "cpu_baseline": None,  # (filled in last: after every GPU timed region, below)
             "bit_exact_vs_reference": bit_exact and timed_exact,
             "bit_exact_checks": dict({"before_warmup_buf0": gate_exact}, **timed_checks),
             "host_resident_gib_s": host,
@@ -1241,6 +1310,12 @@ def main():
             line_set(line, "config4", wd.run("config4", run_config4, hdfs, args, env))
         if not args.no_strong and not wd.failed:
             line_set(line, "strong_scaling", wd.run("strong_scaling", run_strong, hdfs, args, env, ctx))
+    # The CPU baseline, last: rank 0's host cores once no rank has GPU work or
+    # collectives left (at N > 1 the other ranks wait on the store), so it
+    # neither competes with the timed regions nor holds peers in a collective.
+    if not args.no_cpu:
+        line_set(line, "cpu_baseline", cpu_baseline_on_rank0(env, lambda: cpu_baseline(pk, payload0,
+                                                                                      args.cpu_seconds)))
     if wd is not None:
         wd.publish()
     elif line is not None:

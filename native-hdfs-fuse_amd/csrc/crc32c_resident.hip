@@ -133,21 +133,28 @@ int resident_create(crc32c_plan *plan, uint32_t idle_us, ResidentLaunch launch, 
 
 int resident_submit(ResidentEngine *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
     if (!r || !dev_payload || !dev_out) return fail(-EINVAL, "bad arguments");
-    if (reinterpret_cast<uintptr_t>(dev_payload) & 15u) return fail(-EINVAL, "payload must be 16-byte aligned");
-    // the stop check and the ticket are one atomic step (kStop)
+    const uint64_t pa = reinterpret_cast<uint64_t>(dev_payload), oa = reinterpret_cast<uint64_t>(dev_out);
+    if (pa & 15u) return fail(-EINVAL, "payload must be 16-byte aligned");
+    if (oa & 3u) return fail(-EINVAL, "dev_out must be 4-byte aligned");
+    if ((pa | oa) & ~kAddrMask) return fail(-EINVAL, "address above 2^48: does not fit a ring slot");
+    // The ticket is taken only once its slot is free (block t - kRing
+    // complete), so no error can leave a ticket without its slot written: a
+    // hole would stop the forwarder (it forwards consecutive tickets) and
+    // with it every later ticket.  The stop check and the ticket are one
+    // atomic step (kStop); a lost race re-checks the next ticket's slot.
     uint64_t t = r->next.load(std::memory_order_relaxed);
-    do {
+    for (;;) {
         if (t & kStop) return fail(-EINVAL, "queue is being destroyed");
-    } while (!r->next.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel, std::memory_order_relaxed));
+        if (t >= kRing && __atomic_load_n(&r->h->done[t % kRing], __ATOMIC_ACQUIRE) < t - kRing + 1) {
+            if (int rc = resident_wait(r, t - kRing)) return rc;  // (no ticket taken: the queue is intact)
+            t = r->next.load(std::memory_order_relaxed);
+            continue;
+        }
+        if (r->next.compare_exchange_weak(t, t + 1, std::memory_order_acq_rel, std::memory_order_relaxed)) break;
+    }
     const uint32_t sl = uint32_t(t % kRing);
-    // the slot's previous block (t - kRing) must be complete
-    if (t >= kRing)
-        while (__atomic_load_n(&r->h->done[sl], __ATOMIC_ACQUIRE) < t - kRing + 1)
-            if (int rc = resident_wait(r, t - kRing)) return rc;
-    __atomic_store_n(&r->h->slot[sl][0], (reinterpret_cast<uint64_t>(dev_payload) & kAddrMask) | tag_of(t),
-                     __ATOMIC_RELAXED);
-    __atomic_store_n(&r->h->slot[sl][1], (reinterpret_cast<uint64_t>(dev_out) & kAddrMask) | tag_of(t),
-                     __ATOMIC_RELEASE);
+    __atomic_store_n(&r->h->slot[sl][0], pa | tag_of(t), __ATOMIC_RELAXED);
+    __atomic_store_n(&r->h->slot[sl][1], oa | tag_of(t), __ATOMIC_RELEASE);
     if (ticket) *ticket = t;
     // every launch so far has exited (or is exiting): start one (a launch
     // still running forwards this ticket; one that exits before seeing it is

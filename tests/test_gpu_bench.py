@@ -40,6 +40,10 @@ def test_bench_one_gpu_contract():
                         "--no-cpu", "--no-host"], cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = _line(r.stdout)
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.line_problems(d, want_cpu=False) == [] and d["cpu_baseline"] is None  # (--no-cpu)
     assert d["n_gpus"] == 1 and d["steps"] == 200 and d["unit"] == "GiB/s" and d["higher_is_better"]
     assert d["bit_exact_vs_reference"] is True
     # the gate before warm-up, the timed launches on buffer 0 and on a device-random buffer
@@ -78,18 +82,31 @@ def test_bench_injected_capture_failure_falls_back_and_rebuilds():
 
 @pytest.mark.parametrize("config", ["c2", "c5"])
 def test_bench_two_ranks_rehearsal(config):
+    """N = 2 (gloo rehearsal): the line is complete at N > 1 -- node-level
+    roofline fields and, on c2, the reference CPU baseline timed on rank 0
+    after both ranks' GPU work (c5 runs with --no-cpu)."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DIST_BACKEND="gloo")
     port = 29500 + random.randrange(2000)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "20", "--warmup", "5", "--config", config, "--no-cpu", "--nbuf", "2"]
+           "--gpus", "2", "--steps", "20", "--warmup", "5", "--config", config, "--nbuf", "2"]
+    cmd += ["--cpu-seconds", "0.3"] if config == "c2" else ["--no-cpu"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     d = _line(r.stdout)
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.line_problems(d, want_cpu=config == "c2") == []
     assert d["n_gpus"] == 2 and d["scaling"] == "weak"
+    assert d["roofline"]["peak_node"] == 16000.0 and 0 < d["roofline"]["frac_node"] < 1
     assert d["bit_exact_vs_reference"] is True  # MIN over ranks, host-resident runs included
     assert d["host_resident_ranks"] == 2 and d["host_resident_gib_s"] > 0
-    assert d["gather_ms"] is not None and d["cpu_baseline"] is None
+    assert d["gather_ms"] is not None
+    if config == "c2":
+        assert d["cpu_baseline"]["kind"] == "reference" and d["cpu_baseline"]["value"] > 0
+    else:
+        assert d["cpu_baseline"] is None
     assert d["config"]["payload_bytes_per_rank"] > 0
     if config == "c2":  # the sub-objects at N = 2 (config 4 as a gloo rehearsal: ranks share the GPU)
         c4 = d["config4"]
@@ -99,6 +116,25 @@ def test_bench_two_ranks_rehearsal(config):
         assert st["n_ranks"] == 2 and st["packets_per_rank"] == 2048 and st["bit_exact"] is True
     else:
         assert d["config4"] is None and d["strong_scaling"] is None
+
+
+def test_bench_config4_line_two_ranks_complete():
+    """`--config c4` at N = 2 (gloo rehearsal): the c4 main line also carries
+    the reference CPU baseline and the node-level roofline fields."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", BENCH_DIST_BACKEND="gloo")
+    port = 29500 + random.randrange(2000)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "10", "--warmup", "2", "--config", "c4", "--nbuf", "2", "--cpu-seconds", "0.3"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    d = _line(r.stdout)
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.line_problems(d) == []
+    assert d["n_gpus"] == 2 and d["bit_exact_vs_reference"] is True and d["cpu_baseline"]["kind"] == "reference"
+    assert d["roofline"]["frac_node"] == pytest.approx(d["roofline"]["frac"], abs=2e-4)  # (c4's step bytes are the whole file's)
 
 
 def test_bench_two_ranks_capture_failure_on_one_rank():
