@@ -63,6 +63,7 @@ PRODUCTION_KERNEL = "hdfs_crc32c_plan_kernel<768, 3, 3>"
 C4_BLOCKS = 32        # config 4: 128 MiB file = 32 x 4 MiB blocks
 C4_GROUP_PACKETS = 64  # one 4 MiB block = 64 packets of 64 KiB
 MULTI_SELF_SEND = 0x10  # CRC32C_MULTI_SELF_SEND
+MULTI_PIPELINE = 0x40  # CRC32C_MULTI_PIPELINE
 
 
 def load_package():
@@ -411,7 +412,7 @@ def settle_for(env, ms: float, fn, collective: bool) -> int:
 
 
 def time_steps(env, args, step, warm_step, *, collective=False, use_graph=True, zero=None, probe=None,
-               on_abandon=None, settle_ms=None) -> dict:
+               on_abandon=None, settle_ms=None, finish=None) -> dict:
     """Capture, settle, warm up and time args.steps steps of `step(i, stream)`.
 
     - The K timed steps are captured into HIP graphs and replayed: each step
@@ -431,6 +432,9 @@ def time_steps(env, args, step, warm_step, *, collective=False, use_graph=True, 
       from the host (its first launch starts within a few us, and the main
       part's graph launch hides behind it).  BENCH_CAPTURE_FAIL_RANK=r makes
       rank r's step capture fail (every rank then issues from the host).
+    - `finish(stream)` (pipelined steps: config 4's multi plan) runs after
+      each part's steps, inside its capture: the part's end event then
+      follows every step of it.
     - Outputs are zeroed (`zero`) BEFORE the power settle, so the GPU goes
       from settle to warm-up to the timed steps with no idle gap; settle and
       warm-up steps (`warm_step`) write scratch outputs.  Back-to-back
@@ -484,6 +488,8 @@ def time_steps(env, args, step, warm_step, *, collective=False, use_graph=True, 
                         cap = torch.cuda.current_stream(dev)
                         for i in range(lo, hi):
                             step(i, cap.cuda_stream)
+                        if finish is not None:  # (pipelined steps join the capture stream before it ends)
+                            finish(cap.cuda_stream)
                     gs[k] = g_
                 for g_ in gs.values():
                     g_.replay()  # (first replay uploads the graph)
@@ -517,6 +523,8 @@ def time_steps(env, args, step, warm_step, *, collective=False, use_graph=True, 
         else:
             for i in range(lo, hi):
                 step(i)
+            if finish is not None:
+                finish(env.sptr)
         evs[k + 1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -580,6 +588,10 @@ def run_config4(hdfs, args, env) -> dict:
     rehearsal = world > 1 and env.backend != "nccl"
     self_send = os.environ.get("BENCH_C4_SELF_SEND") == "1"  # (tests: rank 0's array through RCCL too)
     flags = MULTI_SELF_SEND if self_send else 0
+    # CRC32C_MULTI_PIPELINE: step k + 1's shard launch overlaps step k's tail
+    # and gather (each step's file and root array its own; joined at the end
+    # of every timed part).  BENCH_C4_PIPELINE=0: every step in stream order.
+    pipeline = not rehearsal and os.environ.get("BENCH_C4_PIPELINE", "1") != "0"
     nbuf = max(1, args.nbuf)
     file0 = synthetic_bytes(file_bytes_total, 2024)
     bufs = []
@@ -597,8 +609,10 @@ def run_config4(hdfs, args, env) -> dict:
     sctx = hdfs.Context(env.local_rank)
     splan = sctx.plan(mine) if mine.size else None
     local_out = torch.zeros(max(nlocal, 1), dtype=torch.int32, device=dev)
-    root_out = torch.zeros(max(nchk, 1), dtype=torch.int32, device=dev)
-    scratch_root = torch.zeros_like(root_out)
+    # file b's checksums land in root_outs[b] (rank 0), the warm-up steps' in
+    # scratch_roots[b]
+    root_outs = [torch.zeros(max(nchk, 1), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+    scratch_roots = [torch.zeros_like(root_outs[0]) for _ in range(nbuf)]
     sptr = env.sptr
 
     state = {}
@@ -611,7 +625,7 @@ def run_config4(hdfs, args, env) -> dict:
             dist.broadcast_object_list(obj, src=0)
             m = hdfs.Multi(device=env.local_rank, rank=rank, nranks=world, uid=obj[0])
         state["multi"] = m
-        state["mplan"] = m.plan(file_pk, gp, flags)
+        state["mplan"] = m.plan(file_pk, gp, flags | (MULTI_PIPELINE if pipeline else 0))
 
     def close_multi():
         if state.get("mplan") is not None:
@@ -634,7 +648,7 @@ def run_config4(hdfs, args, env) -> dict:
     if not rehearsal:
         make_multi()
 
-    def step_into(i, out_t, sp):
+    def step_into(i, outs_, sp):
         b = i % nbuf
         if rehearsal:
             if splan is not None:
@@ -642,15 +656,20 @@ def run_config4(hdfs, args, env) -> dict:
             torch.cuda.synchronize()
             got = shard.gather_checksums(local_out.cpu(), file_pk, gp, world, rank, flags)
             if rank == 0:
-                out_t[:nchk].copy_(torch.from_numpy(got.view(np.int32).copy()))
+                outs_[b][:nchk].copy_(torch.from_numpy(got.view(np.int32).copy()))
         else:
-            state["mplan"].exec([bufs[b].data_ptr()], out_t.data_ptr() if rank == 0 else 0, [sp])
+            state["mplan"].exec([bufs[b].data_ptr()], outs_[b].data_ptr() if rank == 0 else 0, [sp])
 
     def step(i, sp=None):
-        step_into(i, root_out, sptr if sp is None else sp)
+        step_into(i, root_outs, sptr if sp is None else sp)
+
+    def join(sp):
+        if not rehearsal:
+            state["mplan"].join([sp])
 
     def warm_step(i):
-        step_into(i, scratch_root, sptr)
+        step_into(i, scratch_roots, sptr)
+        join(sptr)  # (the settle paces itself on the launch stream)
 
     def probe():
         if splan is None:
@@ -666,18 +685,26 @@ def run_config4(hdfs, args, env) -> dict:
     # correctness gate (outside the timed region): the whole file's checksums
     # gathered on rank 0 against the reference
     step(0)
+    join(sptr)
     torch.cuda.synchronize()
     want0 = reference_checksums(file0, file_pk, nchk) if rank == 0 else None
-    gate = rank != 0 or bool(np.array_equal(root_out.cpu().numpy().view(np.uint32)[:nchk], want0))
+    gate = rank != 0 or bool(np.array_equal(root_outs[0].cpu().numpy().view(np.uint32)[:nchk], want0))
+
+    def zero_roots():
+        for o in root_outs:
+            o.zero_()
+
     r = time_steps(env, args, step, warm_step, collective=world > 1, use_graph=not (args.no_graph or rehearsal),
-                   zero=lambda: root_out.zero_(), probe=probe, on_abandon=abandon,
-                   settle_ms=0 if rehearsal else None)
+                   zero=zero_roots, probe=probe, on_abandon=abandon, settle_ms=0 if rehearsal else None,
+                   finish=join)
+    # every file the timed steps gathered, against the reference (rank 0;
+    # root_outs[b] holds the last timed step on buffer b)
     timed = True
-    b_last = (args.steps - 1) % nbuf
-    if rank == 0 and args.steps > 0:
-        wb = want0 if b_last == 0 else reference_checksums(synthetic_bytes(file_bytes_total, 2024 + b_last),
-                                                           file_pk, nchk)
-        timed = bool(np.array_equal(root_out.cpu().numpy().view(np.uint32)[:nchk], wb))
+    timed_bufs = sorted({i % nbuf for i in range(args.steps)})
+    if rank == 0:
+        for b in timed_bufs:
+            wb = want0 if b == 0 else reference_checksums(synthetic_bytes(file_bytes_total, 2024 + b), file_pk, nchk)
+            timed = timed and bool(np.array_equal(root_outs[b].cpu().numpy().view(np.uint32)[:nchk], wb))
     # the shard's plan launch alone (no gather), same buffers, graph-replayed
     # when the step was: what the gather adds to a step is the difference
     # (every rank or none: the timing holds collectives)
@@ -698,7 +725,7 @@ def run_config4(hdfs, args, env) -> dict:
         a500 = copy.copy(args)
         a500.steps, a500.warmup = 500, 0
         rst = time_steps(env, a500, step, warm_step, collective=world > 1, use_graph=r["use_graph"],
-                         zero=lambda: root_out.zero_(), settle_ms=0)
+                         zero=zero_roots, settle_ms=0, finish=join)
         steady = rst["kernel_ms"] * 1e3
         rst["graphs"].clear()
     exact = agree_min(env, gate and timed)
@@ -735,7 +762,9 @@ def run_config4(hdfs, args, env) -> dict:
         "gather_us": None if (shard_max is None or not int(xs.shape[0])) else round(step_kernel_us - shard_max, 3),
         "transfers": int(xs.shape[0]), "self_send": self_send,
         "bit_exact": exact,
-        "bit_exact_checks": {"before_warmup_file0": gate, "timed_file_buf%d" % b_last: timed} if rank == 0 else None,
+        "bit_exact_checks": {"before_warmup_file0": gate,
+                             "timed_files_buf%s" % "_".join(str(b) for b in timed_bufs): timed} if rank == 0 else None,
+        "pipelined": pipeline,
         "launch": launch, "lead_steps": "host-issued" if (r["lead_host"] or not r["use_graph"]) else "graph",
         "host_issue_us_per_step": round(r["host_issue_us"], 2),
         "kernel_step_us_500": None if steady is None else round(steady, 3),

@@ -300,13 +300,29 @@ int crc32c_plan_create_buffers(crc32c_ctx *ctx, const crc32c_buffer *buffers, ui
  * whole LDS on EVERY CU -- other kernels on the device (plan execs, other
  * queues) wait for CUs until it exits.  It exits idle_us after the last
  * block completes (0 = 2000 us), 50 ms after it stops making progress, or
- * at destroy; the next submit relaunches it.  Plans of whole power-of-two
- * tiles only (bpc 512 << k, chunks not split by a packet end: -EINVAL
- * otherwise); payloads 16-byte aligned (submit returns -EINVAL otherwise).
+ * at destroy; the next submit relaunches it.  Plans of power-of-two tiles
+ * and general chunks (bpc 512 << k; packet tails and the trimmed first packet
+ * of an append at an unaligned block offset, hadooprpc.c:832-840, included),
+ * payload offsets from the block's start (not CRC32C_DEVICE_ADDRESSES, not
+ * crc32c_plan_create_buffers): -EINVAL otherwise.  Payloads at any
+ * alignment (a block off 16-byte alignment takes the kernel's shifted loads).
  * crc32c_block_flush does nothing (every block is taken at once);
  * crc32c_blocks_stats reports the kernel's launches and the blocks
  * submitted; destroy lets every submitted block complete, then stops the
- * kernel.  A wait gives up with -ETIMEDOUT after 5 s without its block.
+ * kernel.  A wait gives up with -ETIMEDOUT after 5 s without its block; a
+ * submit whose ring slot is still busy waits for it first and, if that wait
+ * gives up, returns its error without taking a ticket (the queue goes on).
+ *
+ * crc32c_block_submit_plan: a block of ANOTHER shape through the same queue
+ * -- e.g. the first block of an append at an unaligned offset
+ * (hadoop_fuse_do_write, src/fuse.c:488-574, through write_block at
+ * blockoffset > 0) beside the whole blocks of the queue's plan.  plan ==
+ * NULL is the queue's plan (crc32c_block_submit).  The plan must be on the
+ * queue's device and describe one block (offsets from its start); a
+ * resident queue also needs the queue plan's checksum type and byte order
+ * and the shapes above.  The group-commit queue sends consecutive blocks of
+ * one plan out as one launch.  The plan must stay alive until its blocks'
+ * waits have returned.
  * ------------------------------------------------------------------------- */
 int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, uint32_t *const *dev_outs,
                             size_t nblocks, void *stream);
@@ -314,6 +330,8 @@ int crc32c_plan_exec_blocks(crc32c_plan *plan, const void *const *dev_payloads, 
 typedef struct crc32c_blocks crc32c_blocks;
 int crc32c_blocks_create(crc32c_plan *plan, uint32_t max_blocks, uint32_t window_us, crc32c_blocks **out);
 int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket);
+int crc32c_block_submit_plan(crc32c_blocks *q, crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
+                             uint64_t *ticket);
 int crc32c_block_flush(crc32c_blocks *q);
 int crc32c_block_wait(crc32c_blocks *q, uint64_t ticket);
 int crc32c_block_checksums(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out);
@@ -425,11 +443,28 @@ int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t
 #define CRC32C_MULTI_SELF_SEND 0x10u /* crc32c_multi_plan_create: rank 0's own checksums also travel
                                        through RCCL (a send to itself) instead of being written in
                                        place -- exercises the transport on a one-GPU communicator */
+/* CRC32C_MULTI_PIPELINE (plan flag): consecutive execs overlap -- exec k + 1's
+ * shard launch runs beside exec k's tail and RCCL gather (the files of a
+ * stream of block writes, src/fuse.c:580-647, are independent).  An exec
+ * forks from the caller's stream (it starts after the caller's work so far)
+ * onto one of the plan's two exec streams (alternating), into one of two
+ * local arrays (alternating), and issues the PREVIOUS exec's gather on the
+ * caller's stream (after that exec's launch); the last exec's gather is
+ * issued by crc32c_multi_plan_join(mp, streams), which then makes every
+ * local stream wait for every launch.  So root_out and the shards belong to
+ * the plan until the join; call it before reading root_out, before a graph
+ * capture of execs begins and before it ends (on the capturing stream).
+ * Execs writing the same root_out keep their in-place launches on rank 0 in
+ * order (an exec waits for the previous one's launch); execs into different
+ * root_out arrays overlap fully.  crc32c_multi_plan_join on a plan without
+ * the flag does nothing. */
+#define CRC32C_MULTI_PIPELINE 0x40u
 typedef struct crc32c_multi_plan crc32c_multi_plan;
 int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
                              uint32_t flags, crc32c_multi_plan **out);
 int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards, uint32_t *root_out,
                            void *const *streams);
+int crc32c_multi_plan_join(crc32c_multi_plan *mp, void *const *streams);
 int crc32c_multi_plan_destroy(crc32c_multi_plan *mp);
 uint64_t crc32c_multi_plan_nchecksums(const crc32c_multi_plan *mp);
 uint64_t crc32c_multi_plan_shard_bytes(const crc32c_multi_plan *mp, int rank);

@@ -57,6 +57,12 @@ void crc32c_debug_affine_constants(uint32_t flags, uint32_t *c_lg5, uint32_t *c_
  * return the error. */
 int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n);
 
+/* Resident queues only: hold != 0 keeps the kernel from being launched
+ * (submits queue up in the ring; 0 launches what is queued), and the next
+ * fail_waits waits -- a submit's wait for a busy slot included -- return
+ * -ETIMEDOUT at once. */
+int crc32c_debug_blocks_resident_inject(crc32c_blocks *q, int hold, uint32_t fail_waits);
+
 /* CPU time the queue's worker thread has used so far (its thread CPU clock),
  * in ns: what the queue itself costs beside the submitting threads. */
 int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns);

@@ -33,6 +33,7 @@ CRC32C_DEVICE_ADDRESSES = 0x4  # plan flag: payload_off are device addresses; ex
 CRC32C_CPU_FALLBACK = 0x8  # crc32c_chunks / crc32c_batch_host: finish on the host CPU if the GPU fails
 CRC32C_MULTI_SELF_SEND = 0x10  # multi plan: rank 0's own checksums also go through RCCL (one-GPU transport test)
 CRC32C_COUNT_COMPLETION = 0x20  # plan: launches count their completion on the GPU; destroy after the streams is safe
+CRC32C_MULTI_PIPELINE = 0x40  # multi plan: consecutive execs overlap; results complete after join()
 CRC32C_VERIFY_OVERLAP = 0x80000000  # bit 31 of a verify result's count: overlapping verify launches
 PATH_NONE, PATH_GPU, PATH_CPU = 0, 1, 2  # crc32c_last_path()
 
@@ -213,6 +214,7 @@ def _bind(L):
         "crc32c_multi_transfers": (ctypes.c_int64, [vp, sz, u32, i32, u32, vp, vp, sz]),
         "crc32c_multi_plan_create": (i32, [vp, vp, sz, u32, u32, pp]),
         "crc32c_multi_plan_exec": (i32, [vp, vp, vp, vp]),
+        "crc32c_multi_plan_join": (i32, [vp, vp]),
         "crc32c_multi_plan_destroy": (i32, [vp]),
         "crc32c_multi_plan_nchecksums": (u64, [vp]),
         "crc32c_multi_plan_shard_bytes": (u64, [vp, i32]),
@@ -220,6 +222,7 @@ def _bind(L):
         "crc32c_plan_exec_blocks": (i32, [vp, vp, vp, sz, vp]),
         "crc32c_blocks_create": (i32, [vp, u32, u32, pp]),
         "crc32c_block_submit": (i32, [vp, vp, vp, ctypes.POINTER(u64)]),
+        "crc32c_block_submit_plan": (i32, [vp, vp, vp, vp, ctypes.POINTER(u64)]),
         "crc32c_block_flush": (i32, [vp]),
         "crc32c_block_wait": (i32, [vp, u64]),
         "crc32c_block_checksums": (i32, [vp, vp, vp]),
@@ -228,6 +231,7 @@ def _bind(L):
         "crc32c_blocks_create_resident": (i32, [vp, u32, pp]),
         "crc32c_debug_plan_block": (u64, [vp]),
         "crc32c_debug_blocks_fail_flushes": (i32, [vp, u32]),
+        "crc32c_debug_blocks_resident_inject": (i32, [vp, i32, u32]),
         "crc32c_verify_frames_host": (i32, [vp, vp, sz, u32, u64, u32, ctypes.POINTER(FramesResult)]),
     }
     for name, (res, args) in sig.items():
@@ -485,10 +489,13 @@ class Blocks:
         self.plan = plan  # the plan outlives the queue
         self.handle = h
 
-    def submit(self, dev_payload: int, dev_out: int) -> int:
+    def submit(self, dev_payload: int, dev_out: int, plan: "Plan | None" = None) -> int:
+        """crc32c_block_submit (plan None: the queue's) / crc32c_block_submit_plan
+        (a block of another shape; the plan must outlive its blocks' waits)."""
         t = ctypes.c_uint64(0)
-        _check(lib().crc32c_block_submit(self.handle, ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
-                                         ctypes.byref(t)), "crc32c_block_submit")
+        _check(lib().crc32c_block_submit_plan(self.handle, None if plan is None else plan.handle,
+                                              ctypes.c_void_p(dev_payload), ctypes.c_void_p(dev_out),
+                                              ctypes.byref(t)), "crc32c_block_submit_plan")
         return int(t.value)
 
     def flush(self) -> None:
@@ -505,6 +512,12 @@ class Blocks:
     def debug_fail_flushes(self, n: int) -> None:
         """crc32c_debug_blocks_fail_flushes: the next n flushes fail at issue (tests of the error path)."""
         _check(lib().crc32c_debug_blocks_fail_flushes(self.handle, n), "crc32c_debug_blocks_fail_flushes")
+
+    def debug_resident_inject(self, hold: bool, fail_waits: int = 0) -> None:
+        """crc32c_debug_blocks_resident_inject: hold = no kernel launch (submits queue
+        up); the next fail_waits waits return -ETIMEDOUT at once."""
+        _check(lib().crc32c_debug_blocks_resident_inject(self.handle, int(hold), fail_waits),
+               "crc32c_debug_blocks_resident_inject")
 
     def stats(self):
         f, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
@@ -601,6 +614,14 @@ class MultiPlan:
             *[ctypes.c_void_p(_stream_handle(x, self._streams)) for x in streams])
         _check(lib().crc32c_multi_plan_exec(self.handle, shards, ctypes.c_void_p(root_out), ss),
                "crc32c_multi_plan_exec")
+
+    def join(self, streams=None) -> None:
+        """crc32c_multi_plan_join (CRC32C_MULTI_PIPELINE plans): every local
+        stream waits for every exec issued so far."""
+        n = len(self.multi.local_devices)
+        ss = None if streams is None else (ctypes.c_void_p * n)(
+            *[ctypes.c_void_p(_stream_handle(x, self._streams)) for x in streams])
+        _check(lib().crc32c_multi_plan_join(self.handle, ss), "crc32c_multi_plan_join")
 
     def close(self) -> None:
         if self.handle:

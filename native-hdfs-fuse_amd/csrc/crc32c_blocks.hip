@@ -60,6 +60,7 @@ struct alignas(64) Slot {
     std::atomic<uint64_t> seq{0};  // ticket + 1 once payload/out hold ticket's block
     const void *payload = nullptr;
     uint32_t *out = nullptr;
+    crc32c_plan *plan = nullptr;  // the block's shape (crc32c_block_submit_plan; else the queue's)
 };
 }  // namespace
 
@@ -96,6 +97,7 @@ struct crc32c_blocks {
         hipEvent_t ev;
         int err;  // its issue failed (nothing to wait for)
         size_t trace_idx;
+        crc32c_plan *plan;  // its blocks' shape
     };
     std::deque<Flush> inflight;     // worker only
     std::vector<hipEvent_t> spare;  // worker only
@@ -190,10 +192,22 @@ void relax() {
     for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
 }
 
-// Tickets from `from` whose blocks are published, contiguous, at most `cap`.
-uint32_t ready_from(const crc32c_blocks *q, uint64_t from, uint32_t cap) {
+// Tickets from `from` whose blocks are published, contiguous, of one plan
+// (one launch runs one block shape), at most `cap`; *cut: the run ended at
+// a published block of another plan (nothing more can join this batch).
+uint32_t ready_from(const crc32c_blocks *q, uint64_t from, uint32_t cap, bool *cut) {
     uint32_t n = 0;
-    while (n < cap && q->slots[(from + n) & q->mask].seq.load(std::memory_order_acquire) == from + n + 1) ++n;
+    const crc32c_plan *plan = nullptr;
+    *cut = false;
+    while (n < cap && q->slots[(from + n) & q->mask].seq.load(std::memory_order_acquire) == from + n + 1) {
+        const crc32c_plan *p = q->slots[(from + n) & q->mask].plan;
+        if (n && p != plan) {
+            *cut = true;
+            break;
+        }
+        plan = p;
+        ++n;
+    }
     return n;
 }
 
@@ -202,6 +216,7 @@ void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point
                   std::vector<const void *> &pays, std::vector<uint32_t *> &outs) {
     pays.resize(n);
     outs.resize(n);
+    crc32c_plan *const plan = q->slots[from & q->mask].plan;  // (one plan: ready_from)
     for (uint32_t i = 0; i < n; ++i) {
         const Slot &s = q->slots[(from + i) & q->mask];
         pays[i] = s.payload;
@@ -224,8 +239,8 @@ void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point
     const Clock::time_point issue0 = Clock::now();
     // the flush's event is the last launch's own stop event
     if (!rc)
-        rc = q->record_events ? crc32c_plan_exec_blocks(q->plan, pays.data(), outs.data(), n, q->stream)
-                              : exec_blocks(q->plan, pays.data(), outs.data(), n, q->stream, ev);
+        rc = q->record_events ? crc32c_plan_exec_blocks(plan, pays.data(), outs.data(), n, q->stream)
+                              : exec_blocks(plan, pays.data(), outs.data(), n, q->stream, ev);
     if (!rc && q->record_events && hipEventRecord(ev, q->stream) != hipSuccess) rc = fail(-EIO, "hipEventRecord failed");
     const Clock::time_point issue1 = Clock::now();
     size_t tidx = SIZE_MAX;
@@ -239,7 +254,7 @@ void launch_batch(crc32c_blocks *q, uint64_t from, uint32_t n, Clock::time_point
         if (ev) q->spare.push_back(ev);
         ev = nullptr;
     }
-    q->inflight.push_back({from, from + n, ev, rc, tidx});
+    q->inflight.push_back({from, from + n, ev, rc, tidx, plan});
 }
 
 // Wakes waiters asleep on done_upto (worker).  Called after the launch
@@ -267,6 +282,13 @@ bool complete_front(crc32c_blocks *q) {
     }
     if (err) record_failure(q, f.lo, f.hi, err);  // (before done_upto: a waiter that sees it sees this)
     q->inflight.pop_front();
+    // A block of another plan (crc32c_block_submit_plan): once its last
+    // flush in flight is complete, the plan no longer needs the queue's
+    // stream at its release -- it may be destroyed as soon as its waits
+    // return, and the queue's stream may go before it.
+    if (f.plan != q->plan && std::none_of(q->inflight.begin(), q->inflight.end(),
+                                          [&](const crc32c_blocks::Flush &o) { return o.plan == f.plan; }))
+        plan_forget_stream(f.plan, q->stream);
     if (f.trace_idx != SIZE_MAX) q->trace[f.trace_idx].done = ns(Clock::now());
     q->done_upto.store(f.hi, std::memory_order_seq_cst);
     return true;
@@ -283,12 +305,13 @@ void worker_loop(crc32c_blocks *q) {
     bool have_first = false;  // a ready block seen since the last launch
     Clock::time_point first, idle_since = Clock::now();
     for (;;) {
-        const uint32_t n = q->inflight.size() < max_inflight() ? ready_from(q, launched, q->max_blocks) : 0u;
+        bool cut = false;
+        const uint32_t n = q->inflight.size() < max_inflight() ? ready_from(q, launched, q->max_blocks, &cut) : 0u;
         if (n) {
             const Clock::time_point now = Clock::now();
             if (!have_first) first = now, have_first = true;
             const bool stopping = q->stop.load(std::memory_order_acquire);
-            if (n >= q->max_blocks || q->flush_upto.load(std::memory_order_acquire) > launched || stopping ||
+            if (n >= q->max_blocks || cut || q->flush_upto.load(std::memory_order_acquire) > launched || stopping ||
                 now >= first + q->window) {
                 launch_batch(q, launched, n, first, pays, outs);
                 launched += n;
@@ -388,14 +411,23 @@ int crc32c_blocks_create_resident(crc32c_plan *plan, uint32_t idle_us, crc32c_bl
     std::unique_ptr<crc32c_blocks> q(new crc32c_blocks);
     q->plan = plan;
     q->device = plan->ctx->device;
-    if (int rc = resident_create(plan, idle_us, resident_launch_product, false, &q->res)) return rc;
+    if (int rc = resident_create(plan, idle_us, resident_launch_product, false, &q->res, resident_launch_product_general))
+        return rc;
     *out = q.release();
     return 0;
 }
 
 int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
+    return crc32c_block_submit_plan(q, nullptr, dev_payload, dev_out, ticket);
+}
+
+int crc32c_block_submit_plan(crc32c_blocks *q, crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
+                             uint64_t *ticket) {
     if (!q || !dev_out) return fail(-EINVAL, "queue/out == NULL");
-    if (q->res) return resident_submit(q->res, dev_payload, dev_out, ticket);
+    if (q->res) return resident_submit(q->res, plan, dev_payload, dev_out, ticket);
+    if (!plan) plan = q->plan;
+    if (plan != q->plan && (plan->ctx->device != q->device || plan->absolute))
+        return fail(-EINVAL, "the plan must be one block's shape (offsets from the block start) on the queue's device");
     // the stop check and the ticket are one atomic step (kStopBit)
     uint64_t t = q->next_ticket.load(std::memory_order_relaxed);
     do {
@@ -406,6 +438,7 @@ int crc32c_block_submit(crc32c_blocks *q, const void *dev_payload, uint32_t *dev
     Slot &s = q->slots[t & q->mask];
     s.payload = dev_payload;
     s.out = dev_out;
+    s.plan = plan;
     s.seq.store(t + 1, std::memory_order_release);
     if (ticket) *ticket = t;
     wake_worker(q);
@@ -470,6 +503,12 @@ int crc32c_debug_blocks_fail_flushes(crc32c_blocks *q, uint32_t n) {
     if (q->res) return fail(-EINVAL, "a resident queue has no flushes");
     q->inject_fail.store(n, std::memory_order_relaxed);
     return 0;
+}
+
+int crc32c_debug_blocks_resident_inject(crc32c_blocks *q, int hold, uint32_t fail_waits) {
+    if (!q) return fail(-EINVAL, "queue == NULL");
+    if (!q->res) return fail(-EINVAL, "not a resident queue");
+    return resident_inject(q->res, hold != 0, fail_waits);
 }
 
 int crc32c_debug_blocks_worker_cpu_ns(crc32c_blocks *q, uint64_t *ns) {

@@ -646,11 +646,12 @@ __device__ __forceinline__ uint32_t tile_misalign(const KParams &p, FastTile t) 
     return uint32_t(reinterpret_cast<uintptr_t>(p.payload + t.src)) & 15u;
 }
 
-template <int AUX, bool VERIFY>
-__device__ __forceinline__ void load_tile_shifted(const KParams &p, FastTile t, uint32_t r, int lane, uint4 v[9],
-                                                  uint32_t &ev) {
+// (the loads alone, from a payload base: also the resident kernel's,
+// resident_engine.h)
+template <int AUX>
+__device__ __forceinline__ void load_shifted_raw(const uint8_t *payload, FastTile t, uint32_t r, int lane, uint4 v[9]) {
     const uint32_t nb = t.meta & 0xffu;
-    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + t.src - r, r + nb * 512u);
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(payload + t.src - r, r + nb * 512u);
     const uint32_t voff = 16u * uint32_t(lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -664,8 +665,14 @@ __device__ __forceinline__ void load_tile_shifted(const KParams &p, FastTile t, 
                                                              AUX);
         v[8] = make_uint4(x[0], x[1], x[2], x[3]);
     }
+}
+
+template <int AUX, bool VERIFY>
+__device__ __forceinline__ void load_tile_shifted(const KParams &p, FastTile t, uint32_t r, int lane, uint4 v[9],
+                                                  uint32_t &ev) {
+    load_shifted_raw<AUX>(p.payload, t, r, lane, v);
     if (VERIFY) {
-        const uint32_t lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
+        const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu, blk = rep_block(lane);
         if (rep_lane(lane, blk, nb, lg)) ev = p.expect[t.out + (blk >> lg)];
     }
     __builtin_amdgcn_sched_barrier(0);

@@ -111,8 +111,8 @@ __device__ __forceinline__ void gstate_next(const GShape &g, const GSub &gs, GSt
 // without touching memory; the straddling lane's bytes before the chunk are
 // masked in gsub_pieces.
 template <int AUX, bool COMPDIAG>
-__device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, const GSub &gs, uint32_t s, int lane,
-                                          uint4 v[8]) {
+__device__ __forceinline__ void load_gsub(const uint8_t *payload, const GShape &g, const GSub &gs, uint32_t s,
+                                          int lane, uint4 v[8]) {
     if (COMPDIAG) {  // synthetic data, no memory traffic
         const uint32_t x = uint32_t(g.src) * 2654435761u + s * 97u + uint32_t(lane) * 40503u;
 #pragma unroll
@@ -122,7 +122,7 @@ __device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, con
     const uint32_t bytes = g.nch * g.bpc + g.tl;
     if (g.pad == 0 && g.padt == 0) {
         const __amdgpu_buffer_rsrc_t rsrc =
-            uniform_rsrc(p.payload + g.src, bytes);
+            uniform_rsrc(payload + g.src, bytes);
         const uint32_t voff = 8192u * s + 16u * uint32_t(lane);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -133,7 +133,7 @@ __device__ __forceinline__ void load_gsub(const KParams &p, const GShape &g, con
         return;
     }
     const uint32_t shift = 16u;
-    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(p.payload + g.src - shift, shift + bytes);
+    const __amdgpu_buffer_rsrc_t rsrc = uniform_rsrc(payload + g.src - shift, shift + bytes);
     const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
     const uint32_t upto = 2u << h;  // (upto << 2i) - 1: blocks 0 .. b
     const uint32_t sth = gs.start >> h, vh = gs.valid >> h, th = gs.tailm >> h;
@@ -267,9 +267,11 @@ __device__ __forceinline__ uint32_t dpp_zero(uint32_t v) {  // lanes without a s
 // -> 69.7 us, bpc 1000 58.1 -> 57.3; with 4, bpc 1000's verify had run
 // 61.8 -> 63.5).  Each subtile's loads are issued
 // after the previous one's lookups.
-template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, uint32_t GROUP = 1, bool HOIST = false>
-__device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
-                                             uint4 v[8], uint32_t ev, int lane) {
+// (returns lane c's chunk checksum, defined for c < the item's chunks;
+// payload / table_s4 as in KParams: also the resident kernel's)
+template <int AUX, int DIAG, bool COMPDIAG, bool S4, int IMG, uint32_t GROUP = 1, bool HOIST = false>
+__device__ __forceinline__ uint32_t gtile_crc(const uint8_t *payload, const uint8_t *table_s4, const uint8_t *lds,
+                                              FastTile t, uint4 v[8], int lane) {
     const GShape g = gshape(t);
     const uint32_t c = uint32_t(lane);
     const uint32_t nout = g.nch + (g.kt ? 1u : 0u);
@@ -281,7 +283,7 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
     const uint32_t nsub = (g.nb + 15u) >> 4;
     // lane c's affine constant crc(0, zeros(n)), n = bpc or tl (scalar loads)
     typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
-    const ConstU32 zc = (ConstU32)(p.table_s4 + hdfs_crc::kZeroCrcOff);
+    const ConstU32 zc = (ConstU32)(table_s4 + hdfs_crc::kZeroCrcOff);
     const uint32_t cf = zc[g.bpc], ct = zc[g.tl];
     const uint4 kp = keep_masks(int(g.pad) - int(16u * (uint32_t(lane) & 31u)));
     GState st;
@@ -297,9 +299,9 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         // Unpadded items' loads need no block facts: issue them before the
         // subtile's pattern-table fetches (two dependent scalar loads).
         const bool contiguous = COMPDIAG || (g.pad == 0 && g.padt == 0);
-        if (contiguous) load_gsub<AUX, COMPDIAG>(p, g, GSub{}, s, lane, v);
+        if (contiguous) load_gsub<AUX, COMPDIAG>(payload, g, GSub{}, s, lane, v);
         const GSub gs = HOIST ? gsn : gsub(g, s, st);
-        if (!contiguous) load_gsub<AUX, COMPDIAG>(p, g, gs, s, lane, v);
+        if (!contiguous) load_gsub<AUX, COMPDIAG>(payload, g, gs, s, lane, v);
         if (HOIST) {
             gstate_next(g, gs, st);
             if (s + 1u < nsub) gsn = gsub(g, s + 1u, st);
@@ -357,7 +359,15 @@ __device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *ld
         comb = 0;
         shv = 0;
     }
-    if (c < nout) emit<VERIFY>(p, vacc, t.out + c, acc ^ (c < g.nch ? cf : ct), ev);
+    return acc ^ (c < g.nch ? cf : ct);
+}
+
+template <int AUX, int DIAG, bool COMPDIAG, bool S4, bool VERIFY, int IMG, uint32_t GROUP = 1, bool HOIST = false>
+__device__ __forceinline__ void finish_gtile(const KParams &p, const uint8_t *lds, uint32_t *vacc, FastTile t,
+                                             uint4 v[8], uint32_t ev, int lane) {
+    const uint32_t crc = gtile_crc<AUX, DIAG, COMPDIAG, S4, IMG, GROUP, HOIST>(p.payload, p.table_s4, lds, t, v, lane);
+    const GShape g = gshape(t);
+    if (uint32_t(lane) < g.nch + (g.kt ? 1u : 0u)) emit<VERIFY>(p, vacc, t.out + uint32_t(lane), crc, ev);
 }
 
 }  // namespace hdfs_crc_dev

@@ -39,19 +39,20 @@ __device__ __forceinline__ uint4 funnel(const uint32_t w[8], uint32_t sh) {
                       __builtin_amdgcn_alignbyte(s3, s2, bi), __builtin_amdgcn_alignbyte(s4, s3, bi));
 }
 
-template <bool S4, bool VERIFY, int IMG>
-__device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
-                                         int lane) {
-    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
-    const uint32_t idx = 2u * pair + h;
-    const bool valid = idx < p.ngen;
-    GenItem g{0, 0, 0};
-    if (valid) g = p.gen[idx];
+// lin() of the half-wave's GenItem g (chunk at payload + g.src), in every
+// lane of the half-wave: the chunk right-aligned into zero-prefixed virtual
+// 512-byte blocks, Horner-combined with Z^512.  Both half-waves take part
+// (the reduction and the loop bound span the wave).  Also the resident
+// kernel's (resident_engine.h).
+template <bool S4, int IMG>
+__device__ __forceinline__ uint32_t gen_item_lin(const uint8_t *payload, const uint8_t *lds, const GenItem &g,
+                                                 int lane) {
+    const uint32_t q = uint32_t(lane) & 31u;
     const uint32_t r = g.len;
     const uint32_t nbv = (r + 511u) >> 9;  // virtual 512-byte blocks
     const uint32_t nmax = max(__builtin_amdgcn_readlane(nbv, 0), __builtin_amdgcn_readlane(nbv, 32));
     const int64_t pad = int64_t(nbv) * 512 - int64_t(r);
-    const uintptr_t cbeg = reinterpret_cast<uintptr_t>(p.payload) + g.src;
+    const uintptr_t cbeg = reinterpret_cast<uintptr_t>(payload) + g.src;
     const uintptr_t cend = cbeg + r;
     const uintptr_t ffend = r >= 4 ? cbeg + 4 : cbeg;
     const LaneCols cols = lane_cols<IMG>(q);
@@ -70,7 +71,20 @@ __device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, u
         lin = allreduce32(lin);
         if (m < nbv) acc = zshift<S4, IMG>(lds, 1, acc) ^ lin;
     }
+    return acc;
+}
+
+template <bool S4, bool VERIFY, int IMG>
+__device__ __forceinline__ void gen_pair(const KParams &p, const uint8_t *lds, uint32_t *vacc, uint32_t pair,
+                                         int lane) {
+    const uint32_t h = uint32_t(lane) >> 5, q = uint32_t(lane) & 31u;
+    const uint32_t idx = 2u * pair + h;
+    const bool valid = idx < p.ngen;
+    GenItem g{0, 0, 0};
+    if (valid) g = p.gen[idx];
+    const uint32_t acc = gen_item_lin<S4, IMG>(p.payload, lds, g, lane);
     if (valid && q == 0) {
+        const uint32_t r = g.len;
         const uint32_t crc = acc ^ (r >= 4 ? 0xffffffffu : p.c_small[r]);
         emit<VERIFY>(p, vacc, g.out, crc, VERIFY ? p.expect[g.out] : 0u);
     }

@@ -26,6 +26,8 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -266,6 +268,29 @@ struct crc32c_multi_plan {
     std::vector<hipStream_t> last_stream;
     std::vector<hipEvent_t> last_done;
     std::vector<char> launched;
+    // CRC32C_MULTI_PIPELINE: per local device, the plan's two exec streams
+    // and events (Pipe), a second local array (exec k uses array k % 2),
+    // the execs issued so far, the previous exec's root_out, and the gather
+    // of the previous exec, issued by the next exec (or the join) on the
+    // caller's streams -- after the next exec's fork point, so that exec's
+    // launch runs beside this gather.
+    bool pipeline = false;
+    struct Pipe {
+        hipStream_t exec[2] = {nullptr, nullptr};  // exec k's shard launch on exec[k % 2]
+        hipEvent_t fork = nullptr;                 // on the caller's stream at an exec
+        hipEvent_t kern[2] = {nullptr, nullptr};   // exec[b] after its launch
+        hipEvent_t tail = nullptr;                 // crc32c_multi_plan_join
+        uint64_t cap = 0;  // the caller's capture the streams follow (0: none; follow_capture)
+        bool kern_rec[2] = {false, false};  // recorded, still to be waited on
+        bool used[2] = {false, false};      // exec[b] issued since the last join
+    };
+    std::vector<Pipe> pipes;
+    std::vector<uint32_t *> d_local2;  // per local device: local array 1
+    uint64_t nexec = 0;
+    uint32_t *last_root = nullptr;
+    bool gather_pending = false;  // the previous exec's gather is not issued yet
+    uint32_t pend_b = 0;          // ... its local arrays and root_out
+    uint32_t *pend_root = nullptr;
 };
 
 namespace {
@@ -285,10 +310,122 @@ int order_exec(crc32c_multi_plan *mp, size_t i, hipStream_t s) {
     if (prev != hipStreamCaptureStatusNone) return 0;
     HIP_TRY(hipEventRecord(mp->last_done[i], mp->last_stream[i]));
     HIP_TRY(hipStreamIsCapturing(s, &cur));
-    if (cur != hipStreamCaptureStatusNone)
+    if (cur != hipStreamCaptureStatusNone) {
+        RelaxedCapture relaxed;  // (a host wait on this thread during its capture)
         HIP_TRY(hipEventSynchronize(mp->last_done[i]));
-    else
+    } else {
         HIP_TRY(hipStreamWaitEvent(s, mp->last_done[i], 0));
+    }
+    return 0;
+}
+
+// 1 + the capture id of `s` (0: not capturing; HIP's ids may start at 0).
+int capture_id(hipStream_t s, uint64_t *id) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long cid = 0;
+    HIP_TRY(hipStreamGetCaptureInfo(s, &st, &cid));
+    *id = st == hipStreamCaptureStatusActive ? uint64_t(cid) + 1 : 0;
+    return 0;
+}
+
+// Records `e` on `s`.
+int record(hipEvent_t e, hipStream_t s) {
+    HIP_TRY(hipEventRecord(e, s));
+    return 0;
+}
+
+// The plan's exec streams of one local device follow the caller's stream
+// `s` into (or out of) a graph capture.  Entering one: they are drained by
+// the host first (they hold only work from before the capture), so no wait
+// inside the capture names an event recorded outside it (HIP refuses a host
+// wait on an event whose stream has since joined a capture, and a capture
+// cannot wait on work outside it).  Leaving one: the events recorded inside
+// it are graph nodes, ordered by the caller's graph launches.  Either way
+// the pending waits are dropped.
+int follow_capture(crc32c_multi_plan::Pipe &P, hipStream_t s) {
+    uint64_t cur = 0;
+    if (int rc = capture_id(s, &cur)) return rc;
+    if (cur == P.cap) return 0;
+    if (P.cap == 0) {
+        RelaxedCapture relaxed;  // (host waits on this thread during its capture)
+        for (hipStream_t x : P.exec) HIP_TRY(hipStreamSynchronize(x));
+    }
+    P.cap = cur;
+    P.kern_rec[0] = P.kern_rec[1] = false;
+    return 0;
+}
+
+// The gather of the exec that used local arrays b, into root_out: on every
+// local device's caller stream, after that exec's launch (an event wait),
+// one RCCL group (the same transfers as an ordinary exec's).
+int issue_gather(crc32c_multi_plan *mp, uint32_t b, uint32_t *root_out, void *const *streams) {
+    crc32c_multi *m = mp->m;
+    if (int rc = ensure_comms(m)) return rc;
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        crc32c_multi_plan::Pipe &P = mp->pipes[i];
+        DeviceGuard guard(m->ctxs[i]->device);
+        const hipStream_t s = local_stream(m, i, streams);
+        if (int rc = follow_capture(P, s)) return rc;
+        if (P.kern_rec[b]) HIP_TRY(hipStreamWaitEvent(s, P.kern[b], 0));
+    }
+    NCCL_TRY(rccl().GroupStart());
+    ncclResult_t r = ncclSuccess;
+    for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
+        const hipStream_t s = local_stream(m, i, streams);
+        const int me = m->ranks[i];
+        const uint32_t *src = b ? mp->d_local2[i] : mp->d_local[i];
+        for (const Xfer &x : mp->xfers) {
+            if (r != ncclSuccess) break;
+            if (x.rank == me) r = rccl().Send(src + x.local, x.count, ncclUint32, 0, m->comms[i], s);
+            if (me == 0 && r == ncclSuccess) r = rccl().Recv(root_out + x.file, x.count, ncclUint32, x.rank, m->comms[i], s);
+        }
+    }
+    const ncclResult_t e = rccl().GroupEnd();
+    NCCL_TRY(r);
+    NCCL_TRY(e);
+    return 0;
+}
+
+// One pipelined exec (CRC32C_MULTI_PIPELINE; see crc32c_multi_plan_exec).
+int exec_pipelined(crc32c_multi_plan *mp, const void *const *dev_shards, uint32_t *root_out, void *const *streams) {
+    crc32c_multi *m = mp->m;
+    const uint32_t b = uint32_t(mp->nexec & 1u);
+    const bool same_root = root_out && root_out == mp->last_root;
+    // 1. every local device's shard launch on the plan's exec stream b,
+    //    forked from the caller's stream: after the caller's work so far --
+    //    the gather of exec k - 2, the last reader of local array b,
+    //    included -- but not after exec k - 1's launch (on exec[1 - b]) or
+    //    gather (issued below); after exec k - 1's launch only when both
+    //    write the same root_out in place
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        crc32c_multi_plan::Pipe &P = mp->pipes[i];
+        DeviceGuard guard(m->ctxs[i]->device);
+        const hipStream_t s = local_stream(m, i, streams), E = P.exec[b];
+        if (int rc = follow_capture(P, s)) return rc;
+        HIP_TRY(hipEventRecord(P.fork, s));
+        HIP_TRY(hipStreamWaitEvent(E, P.fork, 0));
+        P.used[b] = true;
+        if (!mp->local_nout[size_t(m->ranks[i])]) continue;
+        const bool in_place = !mp->d_local[i];
+        if (in_place && same_root && P.kern_rec[1 - b]) HIP_TRY(hipStreamWaitEvent(E, P.kern[1 - b], 0));
+        uint32_t *dst = in_place ? root_out : (b ? mp->d_local2[i] : mp->d_local[i]);
+        if (int rc = crc32c_plan_exec(mp->plans[i], dev_shards[i], dst, E)) return rc;
+        HIP_TRY(hipEventRecord(P.kern[b], E));
+        P.kern_rec[b] = true;
+    }
+    mp->last_root = root_out;
+    mp->nexec++;
+    // 2. exec k - 1's gather, now (it runs beside this launch); this exec's
+    //    waits for the next exec or the join
+    if (mp->gather_pending) {
+        mp->gather_pending = false;
+        if (int rc = issue_gather(mp, mp->pend_b, mp->pend_root, streams)) return rc;
+    }
+    if (!mp->xfers.empty()) {
+        mp->gather_pending = true;
+        mp->pend_b = b;
+        mp->pend_root = root_out;
+    }
     return 0;
 }
 
@@ -454,7 +591,8 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
         HIP_TRY(hipEventCreateWithFlags(&mp->last_done[i], hipEventDisableTiming));
     }
     mp->self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
-    flags &= ~CRC32C_MULTI_SELF_SEND;
+    mp->pipeline = (flags & CRC32C_MULTI_PIPELINE) != 0;
+    flags &= ~(CRC32C_MULTI_SELF_SEND | CRC32C_MULTI_PIPELINE);
     if (int rc = build_layout(pkts, npkts, group_packets, m->nranks, &mp->groups, &mp->shard_bytes, &mp->local_nout))
         return rc;
     for (const Group &G : mp->groups) mp->nchecksums = std::max(mp->nchecksums, G.omin + G.n);
@@ -474,6 +612,22 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
             HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), mp->local_nout[size_t(r)] * sizeof(uint32_t)));
         }
         mp->d_local.push_back(d);
+        uint32_t *d2 = nullptr;
+        if (mp->pipeline && d) {
+            DeviceGuard guard(m->ctxs[i]->device);
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d2), mp->local_nout[size_t(r)] * sizeof(uint32_t)));
+        }
+        mp->d_local2.push_back(d2);
+    }
+    if (mp->pipeline) {
+        mp->pipes.resize(m->ctxs.size());
+        for (size_t i = 0; i < m->ctxs.size(); ++i) {
+            crc32c_multi_plan::Pipe &P = mp->pipes[i];
+            DeviceGuard guard(m->ctxs[i]->device);
+            for (hipStream_t *st : {&P.exec[0], &P.exec[1]}) HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+            for (hipEvent_t *ev : {&P.fork, &P.kern[0], &P.kern[1], &P.tail})
+                HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        }
     }
     build_transfers(mp->groups, mp->self_send, &mp->xfers);
     if (mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
@@ -503,6 +657,7 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
         if (mp->local_nout[size_t(m->ranks[i])] && (!dev_shards || !dev_shards[i]))
             return fail(-EINVAL, "local device %zu: shard payload == NULL", i);
     if (mp->root_local >= 0 && mp->nchecksums && !root_out) return fail(-EINVAL, "root_out == NULL on rank 0");
+    if (mp->pipeline) return exec_pipelined(mp, dev_shards, root_out, streams);
     // 0. after the previous exec when it ran on another stream (its sends may
     //    still read the local arrays this one overwrites)
     for (size_t i = 0; i < m->ctxs.size(); ++i)
@@ -540,8 +695,44 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
     return 0;
 }
 
+int crc32c_multi_plan_join(crc32c_multi_plan *mp, void *const *streams) {
+    if (!mp) return fail(-EINVAL, "plan == NULL");
+    if (!mp->pipeline) return 0;  // (an ordinary exec is complete with its stream)
+    crc32c_multi *m = mp->m;
+    std::lock_guard<std::mutex> lock(m->mu);
+    // the last exec's gather, then every exec stream's launches
+    if (mp->gather_pending) {
+        mp->gather_pending = false;
+        if (int rc = issue_gather(mp, mp->pend_b, mp->pend_root, streams)) return rc;
+    }
+    for (size_t i = 0; i < m->ctxs.size(); ++i) {
+        crc32c_multi_plan::Pipe &P = mp->pipes[i];
+        DeviceGuard guard(m->ctxs[i]->device);
+        const hipStream_t s = local_stream(m, i, streams);
+        if (int rc = follow_capture(P, s)) return rc;
+        for (int k = 0; k < 2; ++k) {
+            if (!P.used[k]) continue;
+            HIP_TRY(hipEventRecord(P.tail, P.exec[k]));
+            HIP_TRY(hipStreamWaitEvent(s, P.tail, 0));
+            P.used[k] = false;
+        }
+    }
+    return 0;
+}
+
 int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
     if (!mp) return 0;
+    // (the plan's own streams drain first; the shard plans then need no
+    // event on them at their release)
+    for (size_t i = 0; i < mp->pipes.size(); ++i) {
+        crc32c_multi_plan::Pipe &P = mp->pipes[i];
+        DeviceGuard guard(mp->m->ctxs[i]->device);
+        for (hipStream_t st : P.exec)
+            if (st) {
+                (void)hipStreamSynchronize(st);
+                if (i < mp->plans.size()) plan_forget_stream(mp->plans[i], st);
+            }
+    }
     for (size_t i = 0; i < mp->last_done.size(); ++i)
         if (mp->last_done[i]) {
             DeviceGuard guard(mp->m->ctxs[i]->device);
@@ -549,10 +740,17 @@ int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
         }
     for (size_t i = 0; i < mp->plans.size(); ++i) {
         crc32c_plan_destroy(mp->plans[i]);
-        if (i < mp->d_local.size() && mp->d_local[i]) {
-            DeviceGuard guard(mp->m->ctxs[i]->device);
-            (void)hipFree(mp->d_local[i]);
-        }
+        DeviceGuard guard(mp->m->ctxs[i]->device);
+        if (i < mp->d_local.size() && mp->d_local[i]) (void)hipFree(mp->d_local[i]);
+        if (i < mp->d_local2.size() && mp->d_local2[i]) (void)hipFree(mp->d_local2[i]);
+    }
+    for (size_t i = 0; i < mp->pipes.size(); ++i) {
+        crc32c_multi_plan::Pipe &P = mp->pipes[i];
+        DeviceGuard guard(mp->m->ctxs[i]->device);
+        for (hipStream_t st : P.exec)
+            if (st) (void)hipStreamDestroy(st);
+        for (hipEvent_t ev : {P.fork, P.kern[0], P.kern[1], P.tail})
+            if (ev) (void)hipEventDestroy(ev);
     }
     delete mp;
     return 0;

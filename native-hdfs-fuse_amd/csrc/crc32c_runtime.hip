@@ -311,6 +311,12 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     dp->half = has_half(hp);
     dp->padtiles = has_padded_tiles(hp);
     dp->needs_z = needs_z(hp);
+    dp->gen_pow2 = true;
+    for (const FastTile &t : hp.tiles)
+        if ((t.meta & (kGeneralTile | kHalfTile)) == kGeneralTile) {
+            const uint32_t k = (t.meta >> 8) & 31u, pad = (t.meta >> 18) & 511u;  // (crc32c_general.h gshape)
+            if (pad || !k || (k & (k - 1u))) dp->gen_pow2 = false;
+        }
     dp->slots_off = 0;  // the verify slot first, the completion counters, then the work items
     static_assert(kSlotWords * sizeof(uint32_t) <= kDoneCtrOff, "the verify slot precedes the counters");
     dp->tiles_off = kPlanHeadBytes;
@@ -331,6 +337,13 @@ int upload_plan(crc32c_ctx *ctx, const HostPlan &hp, DevicePlan *dp) {
     uint8_t *img = dp->h;
     init_sched_slots(reinterpret_cast<uint32_t *>(img + dp->slots_off));
     std::memset(img + kDoneCtrOff, 0, kDoneCtrs * kDoneCtrStride);
+    ResShape rs{};
+    rs.tiles = reinterpret_cast<const FastTile *>(dp->d + dp->tiles_off);
+    rs.gen = reinterpret_cast<const GenItem *>(dp->d + dp->gen_off);
+    rs.ntiles = dp->ntiles;
+    rs.ngen = dp->ngen;
+    rs.simple = (!dp->ngen && !dp->misaligned && !dp->general) ? 1u : 0u;
+    std::memcpy(img + kResShapeOff, &rs, sizeof rs);
     std::memcpy(img + dp->tiles_off, hp.tiles.data(), hp.tiles.size() * sizeof(FastTile));
     std::memcpy(img + dp->gen_off, hp.gen.data(), hp.gen.size() * sizeof(GenItem));
     std::memcpy(img + dp->seg_off, hp.seg.data(), hp.seg.size() * sizeof(SegItem));

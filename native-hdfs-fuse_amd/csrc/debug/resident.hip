@@ -60,7 +60,7 @@ int crc32c_debug_resident_create(crc32c_plan *plan, uint32_t idle_us, crc32c_res
 
 int crc32c_debug_resident_submit(crc32c_resident *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket) {
     if (!r) return hdfs_crc::fail(-EINVAL, "resident == NULL");
-    return hdfs_crc::resident_submit(r->e, dev_payload, dev_out, ticket);
+    return hdfs_crc::resident_submit(r->e, nullptr, dev_payload, dev_out, ticket);
 }
 
 int crc32c_debug_resident_wait(crc32c_resident *r, uint64_t ticket) {

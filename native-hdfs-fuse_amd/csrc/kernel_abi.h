@@ -107,6 +107,21 @@ constexpr uint32_t kDoneCtrs = 8;
 constexpr uint32_t kDoneCtrStride = 128;
 constexpr uint32_t kPlanHeadBytes = kDoneCtrOff + kDoneCtrs * kDoneCtrStride;  // the work items follow
 
+// A plan's block shape as the resident kernel reads it (resident_engine.h):
+// at kResShapeOff of the plan's device block, between the verify slot and
+// the completion counters, written with the items at upload.  A block
+// submitted to a resident queue names its plan's record in its ring slot.
+struct ResShape {
+    const FastTile *tiles;  // power-of-two tiles (offsets from the block's payload)
+    const GenItem *gen;     // general chunks (a trimmed first packet, packet tails)
+    uint32_t ntiles, ngen;
+    uint32_t simple;  // 1: every tile 16-byte aligned from the block start, no GenItem
+    uint32_t pad;
+};
+constexpr uint32_t kResShapeOff = 128;
+static_assert(kSlotWords * sizeof(uint32_t) <= kResShapeOff && kResShapeOff + sizeof(ResShape) <= kDoneCtrOff,
+              "the shape record sits between the verify slot and the counters");
+
 // Fills a slot's initial state (kSlotWords words): no launch's key.
 inline void init_sched_slots(uint32_t *w) {
     for (uint32_t i = 0; i < kSlotWords; ++i) w[i] = 0;

@@ -13,9 +13,19 @@
 //
 // Protocol (all host words in pinned, device-mapped, coherent memory):
 //  * submit (host): ticket t = an atomic counter; slot t % kRing is reused
-//    only once block t - kRing is complete; the slot's two words (payload
-//    and out pointer) each carry t's tag, so one read of the slot tells a
-//    complete entry from a stale or half-written one.
+//    only once block t - kRing is complete; the slot's words (payload
+//    pointer, out pointer and, for a block of another plan than the
+//    queue's, its plan's ResShape record, kernel_abi.h) each carry t's tag,
+//    so one read of the slot tells a complete entry from a stale or
+//    half-written one.
+//  * shapes: any plan of power-of-two tiles, general tiles and GenItems
+//    (bpc 512 << k; a trimmed first packet of an append at an unaligned
+//    block offset, hadooprpc.c:832-840, and packet tails), at any payload
+//    alignment.  A block whose shape is "simple" (power-of-two tiles only,
+//    16-byte aligned) runs the aligned tile loop; any other takes, per unit,
+//    the shifted loads of crc32c_device.h for tiles off 16-byte alignment,
+//    crc32c_general.h's gtile_crc for general tiles and gen_item_lin for
+//    GenItems (half a wave each).
 //  * forwarder (workgroup 0's last wave): reads 64 host slots per poll (one
 //    PCIe round trip per poll, not per block) and copies the ready ones into
 //    a device ring, tags and all (agent scope).
@@ -68,16 +78,25 @@ constexpr uint64_t kStuckMs = 50;
 constexpr uint32_t kStampRing = 4096;
 constexpr uint64_t kWorkerMs = 200;
 
-// A slot (host ring and device ring alike) is two 64-bit words, payload and
-// out pointer (48-bit GPU addresses), each tagged in bits 48-63 with the low
-// 16 bits of ticket + 1: a reader that sees both with matching tags has the
-// block's pointers (no separate sequence word, no order between the stores).
+// A host slot is two 64-bit words, payload and out pointer (48-bit GPU
+// addresses), each tagged in bits 48-62 with the low 15 bits of ticket + 1:
+// a reader that sees both with matching tags has the block's pointers (no
+// separate sequence word, no order between the stores).  Bit 63 of the out
+// word: the block is of another plan than the queue's -- its shape record's
+// address (tagged the same way) is in shape[slot], which the forwarder then
+// loads too (a second round trip, only for such blocks: the common block
+// costs the poll two loads per lane, not three).  The device ring holds all
+// three words (shape 0: the queue's plan).
 constexpr int kTagShift = 48;
 constexpr uint64_t kAddrMask = (1ull << kTagShift) - 1;
-__host__ __device__ constexpr uint64_t tag_of(uint64_t ticket) { return ((ticket + 1) & 0xffffull) << kTagShift; }
+constexpr uint64_t kTagMask = 0x7fffull << kTagShift;
+constexpr uint64_t kShapeFlag = 1ull << 63;
+__host__ __device__ constexpr uint64_t tag_of(uint64_t ticket) { return ((ticket + 1) & 0x7fffull) << kTagShift; }
+constexpr uint32_t kSlotW = 3;  // (device ring) payload, out, shape
 
 struct HostRing {
-    uint64_t slot[kRing][2];  // host: the ticket's tagged payload / out pointers (the device slot format)
+    uint64_t slot[kRing][2];  // host: the ticket's tagged payload / out pointers
+    uint64_t shape[kRing];    // host: its tagged shape record (out word's kShapeFlag)
     uint64_t done[kRing];     // kernel: ticket + 1 once the block's checksums are stored
     uint32_t stop;            // host: exit now
     uint32_t pad0[15];
@@ -86,7 +105,7 @@ struct HostRing {
 };
 
 struct DevRing {
-    uint64_t slot[kRing][2];
+    uint64_t slot[kRing][kSlotW];
     uint32_t flag[kRing][kMaxWg];  // per slot and workgroup: ticket + 1 once its workers are done
     uint64_t fwd;                  // forwarder: tickets below this are forwarded
     uint64_t col;                  // collector: tickets below this are complete
@@ -94,14 +113,23 @@ struct DevRing {
     uint64_t rtt_sum, rtt_n;       // trace: forwarder poll round trips (ticks), count
 };
 
+// The block's shape (wave-uniform: scalar loads of its plan's ResShape).
+struct Shape {
+    const FastTile *tiles;
+    const GenItem *gen;
+    uint32_t ntiles, ngen, simple;
+};
+
 struct RParams {
     HostRing *h;
     DevRing *d;
-    const FastTile *tiles;
+    // the queue plan's shape: a block of the queue's plan (the common case,
+    // no kShapeFlag) needs no load of its record before its tiles
+    Shape def;
     const uint8_t *table_s4;
-    uint32_t ntiles;
     uint32_t flags;
     uint32_t c_lg[5];
+    uint32_t c_small[4];
     uint64_t first;       // first ticket this launch forwards
     uint64_t idle_ticks;  // forwarder: exit after this long with nothing queued
     uint64_t *stamps;     // trace (nullptr: off), 4 per ticket % kStampRing
@@ -125,12 +153,23 @@ __device__ __forceinline__ void st_dev(T *p, T v) {
 }
 __device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
 
-// One power-of-two tile of a block (the plan's block shape; offsets relative
-// to the block's payload / checksum array): the production tile's loads,
-// lookups and reduce, stores write-through.
-__device__ __forceinline__ FastTile rtile(const RParams &p, uint32_t idx) {
+__device__ __forceinline__ Shape shape_at(uint64_t addr) {
+    typedef const __attribute__((address_space(4))) hdfs_crc::ResShape *CS;
+    const CS r = (CS)(addr);
+    return Shape{r->tiles, r->gen, r->ntiles, r->ngen, r->simple};
+}
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v))));
+    const uint32_t hi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(v >> 32))));
+    return uint64_t(hi) << 32 | lo;
+}
+
+// One power-of-two tile of a block (offsets relative to the block's payload
+// / checksum array): the production tile's loads, lookups and reduce,
+// stores write-through.
+__device__ __forceinline__ FastTile rtile(const FastTile *tiles, uint32_t idx) {
     typedef const __attribute__((address_space(4))) FastTile *CT;
-    const CT tp = (CT)(p.tiles) + idx;
+    const CT tp = (CT)(tiles) + idx;
     return FastTile{tp->src, tp->out, tp->meta};
 }
 __device__ __forceinline__ void rtile_load(const uint8_t *payload, const FastTile &t, int lane, uint4 v[8]) {
@@ -142,11 +181,15 @@ __device__ __forceinline__ void rtile_load(const uint8_t *payload, const FastTil
         v[i] = make_uint4(r[0], r[1], r[2], r[3]);
     }
 }
-__device__ __forceinline__ void rtile_finish(const RParams &p, const uint8_t *lds, uint32_t *out, const FastTile &t,
-                                             uint4 v[8], int lane) {
+// A checksum of the block, write-through (system scope: the waiter's next
+// stream work or copy may run on any XCD or engine).
+__device__ __forceinline__ void rstore(uint32_t *out, uint32_t idx, uint32_t v) {
+    typedef __attribute__((address_space(1))) uint32_t *GU32;  // (a global store, not a flat one)
+    __hip_atomic_store((GU32)(out + idx), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void rtile_reduce(const RParams &p, const uint8_t *lds, uint32_t *out, const FastTile &t,
+                                             const uint32_t pc[8], int lane) {
     const uint32_t nb = t.meta & 0xffu, lg = (t.meta >> 8) & 0xffu;
-    uint32_t pc[8];
-    tile_pieces<0, true, kImgFull>(lds, v, pc, lane, NoPrep{});
     uint32_t x = block_lin(pc, lane);
     const uint32_t blk = rep_block(lane);
     if (lg) {
@@ -158,15 +201,17 @@ __device__ __forceinline__ void rtile_finish(const RParams &p, const uint8_t *ld
         if (lg >= 3) x ^= dpp<kDppXor2>(x);
         if (lg >= 4) x ^= dpp<kDppXor1>(x);
     }
-    if (rep_lane(lane, blk, nb, lg)) {
-        typedef __attribute__((address_space(1))) uint32_t *GU32;  // (a global store, not a flat one)
-        __hip_atomic_store((GU32)(out + t.out + (blk >> lg)), out_order(x ^ p.c_lg[lg], p.flags), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (rep_lane(lane, blk, nb, lg)) rstore(out, t.out + (blk >> lg), out_order(x ^ p.c_lg[lg], p.flags));
+}
+__device__ __forceinline__ void rtile_finish(const RParams &p, const uint8_t *lds, uint32_t *out, const FastTile &t,
+                                             uint4 v[8], int lane) {
+    uint32_t pc[8];
+    tile_pieces<0, true, kImgFull>(lds, v, pc, lane, NoPrep{});
+    rtile_reduce(p, lds, out, t, pc, lane);
 }
 __device__ __forceinline__ void run_tile(const RParams &p, const uint8_t *lds, const uint8_t *payload,
-                                         uint32_t *out, uint32_t idx, int lane) {
-    const FastTile t = rtile(p, idx);
+                                         uint32_t *out, const FastTile *tiles, uint32_t idx, int lane) {
+    const FastTile t = rtile(tiles, idx);
     uint4 v[8];
     rtile_load(payload, t, lane, v);
     __builtin_amdgcn_sched_barrier(0);
@@ -175,8 +220,9 @@ __device__ __forceinline__ void run_tile(const RParams &p, const uint8_t *lds, c
 // Two tiles by one wave: both tiles' loads first, so the second one's
 // latency hides under the first one's lookups.
 __device__ __forceinline__ void run_tile_pair(const RParams &p, const uint8_t *lds, const uint8_t *payload,
-                                              uint32_t *out, uint32_t ia, uint32_t ib, int lane) {
-    const FastTile ta = rtile(p, ia), tb = rtile(p, ib);
+                                              uint32_t *out, const FastTile *tiles, uint32_t ia, uint32_t ib,
+                                              int lane) {
+    const FastTile ta = rtile(tiles, ia), tb = rtile(tiles, ib);
     uint4 va[8], vb[8];
     rtile_load(payload, ta, lane, va);
     rtile_load(payload, tb, lane, vb);
@@ -185,10 +231,99 @@ __device__ __forceinline__ void run_tile_pair(const RParams &p, const uint8_t *l
     rtile_finish(p, lds, out, tb, vb, lane);
 }
 
+// A power-of-two tile of a block of any alignment: the aligned loads, or
+// the shifted loads of crc32c_device.h when it starts off 16-byte alignment.
+__device__ __forceinline__ void run_ptile(const RParams &p, const uint8_t *lds, const uint8_t *payload, uint32_t *out,
+                                          const FastTile &t, int lane) {
+    const uint32_t r = uint32_t(reinterpret_cast<uintptr_t>(payload + t.src)) & 15u;  // (uniform)
+    if (!r) {
+        uint4 v[8];
+        rtile_load(payload, t, lane, v);
+        __builtin_amdgcn_sched_barrier(0);
+        rtile_finish(p, lds, out, t, v, lane);
+        return;
+    }
+    uint4 v[9];
+    load_shifted_raw<2>(payload, t, r, lane, v);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t pc[8];
+    const uint32_t b = r & 3u, li = ((t.meta & 0xffu) - 1u) >> 1;
+    const int ll = int(((t.meta & 0xffu) - 1u) & 1u) * 32 + 31;
+    switch (r >> 2) {
+        case 0: tile_pieces<0, true, kImgFull>(lds, v, pc, lane, ShiftPrep<0>{v, b, lane, li, ll}); break;
+        case 1: tile_pieces<0, true, kImgFull>(lds, v, pc, lane, ShiftPrep<1>{v, b, lane, li, ll}); break;
+        case 2: tile_pieces<0, true, kImgFull>(lds, v, pc, lane, ShiftPrep<2>{v, b, lane, li, ll}); break;
+        default: tile_pieces<0, true, kImgFull>(lds, v, pc, lane, ShiftPrep<3>{v, b, lane, li, ll}); break;
+    }
+    rtile_reduce(p, lds, out, t, pc, lane);
+}
+
+// GenItem chunks: half a wave each (gen_item_lin), the half-wave's item
+// `g` (valid: it has one).
+__device__ __forceinline__ void run_gen_item(const RParams &p, const uint8_t *lds, const uint8_t *payload,
+                                             uint32_t *out, const GenItem &g, bool valid, int lane) {
+    const uint32_t acc = gen_item_lin<true, kImgFull>(payload, lds, g, lane);
+    if (valid && (lane & 31) == 0)
+        rstore(out, g.out, out_order(acc ^ (g.len >= 4 ? 0xffffffffu : p.c_small[g.len]), p.flags));
+}
+
+// A general tile of a block (kGeneralTile: a packet's tail chunk behind up
+// to 16 full chunks).  The resident queue takes only those of unpadded
+// chunks of 2^lg blocks (bytesPerChecksum 512 << lg: crc32c_resident.hip
+// checks), so the full chunks run as power-of-two tiles of 16 blocks and
+// the tail as a GenItem -- no general-item gather code in this kernel.
+__device__ __forceinline__ void run_gtile(const RParams &p, const uint8_t *lds, const uint8_t *payload, uint32_t *out,
+                                          const FastTile &t, int lane) {
+    const GShape g = gshape(t);
+    const uint32_t lg = 31u - uint32_t(__builtin_clz(g.k));
+    for (uint32_t s = 0; 16u * s < g.nfb; ++s) {
+        const uint32_t nb = min(g.nfb - 16u * s, 16u);
+        run_ptile(p, lds, payload, out, FastTile{g.src + 8192u * s, t.out + ((16u * s) >> lg), nb | (lg << 8)}, lane);
+    }
+    if (g.tl) {
+        const GenItem gi{g.src + uint64_t(g.nch) * g.bpc, t.out + g.nch, g.tl};
+        const bool valid = (lane >> 5) == 0;  // (the lower half-wave; the upper runs an empty item)
+        run_gen_item(p, lds, payload, out, valid ? gi : GenItem{0, 0, 0}, valid, lane);
+    }
+}
+
+// Unit `idx` of a block of any shape: tile idx, or, past the tiles, the
+// GenItem pair idx - ntiles.
+__device__ __forceinline__ void run_unit(const RParams &p, const uint8_t *lds, const uint8_t *payload, uint32_t *out,
+                                         const Shape &sh, uint32_t idx, int lane) {
+    if (idx < sh.ntiles) {
+        const FastTile t = rtile(sh.tiles, idx);
+        if (t.meta & hdfs_crc::kGeneralTile)
+            run_gtile(p, lds, payload, out, t, lane);
+        else
+            run_ptile(p, lds, payload, out, t, lane);
+        return;
+    }
+    const uint32_t gi = 2u * (idx - sh.ntiles) + (uint32_t(lane) >> 5);
+    const bool valid = gi < sh.ngen;
+    GenItem g{0, 0, 0};
+    if (valid) g = sh.gen[gi];
+    run_gen_item(p, lds, payload, out, g, valid, lane);
+}
+
+// A block of any shape: units first, first + stride, ... (tiles, then
+// GenItem pairs).
+__device__ __forceinline__ void run_units(const RParams &p, const uint8_t *lds, const uint8_t *payload,
+                                                    uint32_t *out, Shape sh, uint32_t first, uint32_t stride,
+                                                    int lane) {
+    const uint32_t units = sh.ntiles + (sh.ngen + 1u) / 2u;
+    for (uint32_t idx = first; idx < units; idx += stride) run_unit(p, lds, payload, out, sh, idx, lane);
+}
+
 // Forwarder (workgroup 0's last wave): the host ring -> the device ring.
 // One PCIe round trip per poll covers the next 64 tickets.  Decides the
 // launch's end: the host's stop word, idle_ticks with nothing outstanding,
 // or kStuckMs without the collector advancing while blocks are outstanding.
+// The aligned-only build (GENERAL false) never forwards a block that needs
+// the general code (kShapeFlag): at the first one it stops forwarding and
+// ends the launch (its blocks before that complete), and the host launches
+// the general build for it.
+template <bool GENERAL>
 static inline __device__ void forwarder(const RParams &p, int lane) {
     HostRing *h = p.h;
     DevRing *d = p.d;
@@ -210,7 +345,24 @@ static inline __device__ void forwarder(const RParams &p, int lane) {
             col = c;
             progress = true;
         }
-        const bool ok = room && (w0 & ~kAddrMask) == tag_of(cand) && (w1 & ~kAddrMask) == tag_of(cand);
+        const uint64_t tg = tag_of(cand);
+        bool ok = room && (w0 & kTagMask) == tg && (w1 & kTagMask) == tg;
+        uint64_t w2 = 0;
+        const bool need = ok && (w1 & kShapeFlag);
+        bool handoff = false;
+        if (const uint64_t flagged = __ballot(need)) {  // (blocks needing the general build: their shape words)
+            if (GENERAL) {
+                w2 = need ? ld_sys(&h->shape[sl]) : 0;
+                ok = ok && (!need || (w2 & kTagMask) == tg);
+            } else {
+                // forward up to the first such block, then end the launch
+                const uint64_t before = ~__ballot(ok);
+                if (!before || __builtin_ctzll(flagged) <= __builtin_ctzll(before)) {
+                    ok = ok && uint32_t(lane) < uint32_t(__builtin_ctzll(flagged));
+                    handoff = true;
+                }
+            }
+        }
         const uint64_t ready = __ballot(ok);
         if (p.stamps) {  // (the ballot waited for the host loads)
             rtt_sum += now() - t_poll;
@@ -221,12 +373,14 @@ static inline __device__ void forwarder(const RParams &p, int lane) {
             if (uint32_t(lane) < n) {
                 st_dev(&d->slot[sl][0], w0);
                 st_dev(&d->slot[sl][1], w1);
+                st_dev(&d->slot[sl][2], w2);
                 if (p.stamps) st_dev(&p.stamps[4 * (cand % kStampRing)], now());
             }
             fwd += n;
             if (lane == 0) st_dev(&d->fwd, fwd);
             progress = true;
         }
+        if (handoff) break;  // (after forwarding the blocks before it)
         const uint64_t t = now();
         if (progress) {
             last = t;
@@ -305,7 +459,7 @@ static inline __device__ void collector(const RParams &p, int lane) {
     }
 }
 
-template <uint32_t kWaves, uint32_t kPhases, uint32_t kPer>
+template <uint32_t kWaves, uint32_t kPhases, uint32_t kPer, bool GENERAL = false>
 __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RParams p) {
     constexpr uint32_t kWorkers = kWaves - 1;
     constexpr uint32_t kStage = kS4StageBytes;
@@ -324,7 +478,7 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
     if (threadIdx.x < kRing) lcnt[threadIdx.x] = 0;
     __syncthreads();
     if (wv == kWaves - 1) {
-        if (blockIdx.x == 0) forwarder(p, lane);
+        if (blockIdx.x == 0) forwarder<GENERAL>(p, lane);
         if (blockIdx.x == 1) collector(p, lane);
         return;
     }
@@ -344,11 +498,16 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
     for (;;) {
         const uint32_t sl = uint32_t(j % kRing);
         bool stop = false;
-        uint64_t w0 = 0, w1 = 0;
+        uint64_t w0 = 0, w1 = 0, w2 = 0;
+        const uint64_t tg = tag_of(j);
         for (uint32_t polls = 0;; ++polls) {
             w0 = ld_dev(&d->slot[sl][0]);
             w1 = ld_dev(&d->slot[sl][1]);
-            if ((w0 & ~kAddrMask) == tag_of(j) && (w1 & ~kAddrMask) == tag_of(j)) break;
+            if ((w0 & kTagMask) == tg && (w1 & kTagMask) == tg) {
+                if (!GENERAL || !(w1 & kShapeFlag)) break;
+                w2 = ld_dev(&d->slot[sl][2]);  // (a block of another plan: its shape word too)
+                if ((w2 & kTagMask) == tg) break;
+            }
             if ((polls & 15u) == 15u && (ld_dev(&d->stop) || now() - last > kWorkerMs * 1000 * kTicksPerUs)) {
                 stop = true;
                 break;
@@ -358,18 +517,25 @@ __global__ __launch_bounds__(kWaves * 64, kWaves / 4) void resident_kernel(RPara
         if (stop) break;
         const bool stamp = p.stamps && b == 0 && lane == 0;
         if (stamp) st_dev(&p.stamps[4 * (j % kStampRing) + 1], now());
-        const uint8_t *payload = reinterpret_cast<const uint8_t *>(w0 & kAddrMask);
-        uint32_t *out = reinterpret_cast<uint32_t *>(w1 & kAddrMask);
-        if (kPer == 1) {  // (rank 0: this workgroup's tiles b, b + G, ..., two at a time)
-            for (uint32_t idx = b; idx < p.ntiles; idx += 2u * G) {
-                if (idx + G < p.ntiles)
-                    run_tile_pair(p, lds, payload, out, idx, idx + G, lane);
+        const uint8_t *payload = reinterpret_cast<const uint8_t *>(uniform64(w0) & kAddrMask);
+        uint32_t *out = reinterpret_cast<uint32_t *>(uniform64(w1) & kAddrMask);
+        const Shape sh = GENERAL && (w1 & kShapeFlag) ? shape_at(uniform64(w2) & kAddrMask) : p.def;
+        // (aligned tiles only: the round-4 loop; any other block, general
+        // build only: units = its tiles, then its GenItem pairs)
+        const bool simple = !GENERAL || !(w1 & kShapeFlag);
+        if (!simple) {
+            if (kPer == 1 || rank < kPer)
+                run_units(p, lds, payload, out, sh, kPer == 1 ? b : kPer * b + rank, kPer * G, lane);
+        } else if (kPer == 1) {  // (rank 0: this workgroup's tiles b, b + G, ..., two at a time)
+            for (uint32_t idx = b; idx < sh.ntiles; idx += 2u * G) {
+                if (idx + G < sh.ntiles)
+                    run_tile_pair(p, lds, payload, out, sh.tiles, idx, idx + G, lane);
                 else
-                    run_tile(p, lds, payload, out, idx, lane);
+                    run_tile(p, lds, payload, out, sh.tiles, idx, lane);
             }
         } else if (rank < kPer) {
-            for (uint32_t idx = kPer * b + rank; idx < p.ntiles; idx += kPer * G)
-                run_tile(p, lds, payload, out, idx, lane);
+            for (uint32_t idx = kPer * b + rank; idx < sh.ntiles; idx += kPer * G)
+                run_tile(p, lds, payload, out, sh.tiles, idx, lane);
         }
         wait_vmem();  // (this wave's checksum stores have completed)
         if (stamp && rank == 0) st_dev(&p.stamps[4 * (j % kStampRing) + 2], now());

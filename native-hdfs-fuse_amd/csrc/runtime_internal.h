@@ -93,6 +93,7 @@ struct DevicePlan {
     bool half = false;        // some tile is a half tile (their own builds)
     bool padtiles = false;    // some tile is a padded power-of-two tile (full-image general builds)
     bool needs_z = true;      // some item shifts by Z^(512 s) (the image's last 7.5 KiB)
+    bool gen_pow2 = true;     // every general tile's full chunks are 2^lg unpadded blocks (the resident kernel's)
     size_t tiles_off = 0, gen_off = 0, seg_off = 0, pieces_off = 0, consts_off = 0, slots_off = 0;
 };
 
@@ -237,11 +238,19 @@ int make_plan(crc32c_ctx *ctx, const HostPlan &hp, uint32_t flags, bool absolute
 // (its shape) with `grid` workgroups on `stream`.
 using ResidentLaunch = hipError_t (*)(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
 struct ResidentEngine;
-// Plans of aligned power-of-two tiles only (one block's shape, as the
-// queue's); idle_us = 0: 2000.  stamps: per-ticket trace (debug A/B).
-int resident_create(crc32c_plan *plan, uint32_t idle_us, ResidentLaunch launch, bool stamps, ResidentEngine **out);
-int resident_submit(ResidentEngine *r, const void *dev_payload, uint32_t *dev_out, uint64_t *ticket);
+// Plans of power-of-two tiles and GenItems (one block's shape: the queue's
+// default); idle_us = 0: 2000.  stamps: per-ticket trace (debug A/B).
+// launch: the aligned-only build; launch_general: the general build (null:
+// blocks that need it are refused).
+int resident_create(crc32c_plan *plan, uint32_t idle_us, ResidentLaunch launch, bool stamps, ResidentEngine **out,
+                    ResidentLaunch launch_general = nullptr);
+// plan == NULL: the queue's plan.  Any payload alignment.
+int resident_submit(ResidentEngine *r, crc32c_plan *plan, const void *dev_payload, uint32_t *dev_out,
+                    uint64_t *ticket);
 int resident_wait(ResidentEngine *r, uint64_t ticket);
+// Test hooks: hold = no launch (submits queue up); the next fail_waits
+// waits return -ETIMEDOUT at once.
+int resident_inject(ResidentEngine *r, bool hold, uint32_t fail_waits);
 uint64_t resident_launches(const ResidentEngine *r);
 uint64_t resident_tickets(const ResidentEngine *r);
 // Ends the running launch (stop word), then copies the trace out.
@@ -250,7 +259,9 @@ int resident_trace(ResidentEngine *r, uint64_t *stamps, uint64_t *rtt_ticks, uin
 // then the stop word, the stream drained, everything freed.  Submits from
 // the moment destroy begins are refused.
 int resident_destroy(ResidentEngine *r, bool drain);
-// The product's shape (16 waves, 7 phases, 2 waves per phase and workgroup).
+// The product's shape (16 waves, 7 phases, 2 waves per phase and workgroup):
+// its aligned-only and general builds.
 hipError_t resident_launch_product(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
+hipError_t resident_launch_product_general(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
 
 }  // namespace hdfs_crc

@@ -449,6 +449,70 @@ def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc):
     m.close()
 
 
+@pytest.mark.parametrize("self_send", [False, True])
+def test_multi_plan_pipelined(hdfs, orc, self_send):
+    """CRC32C_MULTI_PIPELINE: consecutive execs overlap (two exec streams, two
+    local arrays, the gather on the plan's comm stream); after
+    crc32c_multi_plan_join every file's checksums are in its root array,
+    bit-exact against the oracle -- host-issued over 4 rotating files and
+    root arrays, into ONE root array (the in-place launches stay in exec
+    order: the last file's checksums win), and captured into a graph with
+    the join inside the capture, replayed twice.  With
+    CRC32C_MULTI_SELF_SEND every exec's checksums also travel through the
+    RCCL group on the comm stream."""
+    torch = _torch()
+    gp, nfiles = 4, 4
+    pk = oracle.uniform_packets(8 * gp)  # 8 blocks of 4 packets (2 MiB files)
+    flags = hdfs.CRC32C_MULTI_PIPELINE | (hdfs.CRC32C_MULTI_SELF_SEND if self_send else 0)
+    m = hdfs.Multi([0])
+    mp = m.plan(pk, gp, flags)
+    layout, sb = hdfs.multi_layout(pk, gp, 1)
+    shards, wants = [], []
+    for f in range(nfiles):
+        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 16, 900 + f)
+        host = np.zeros(int(sb[0]) + 16, np.uint8)
+        for _, soff, poff, nbytes in layout.astype(np.int64):
+            host[soff:soff + nbytes] = payload[poff:poff + nbytes]
+        shards.append(torch.from_numpy(host).cuda())
+        wants.append(orc.batch(payload, pk, mp.nchecksums))
+    outs = [torch.zeros(mp.nchecksums, dtype=torch.int32, device="cuda") for _ in range(nfiles)]
+    cs = torch.cuda.Stream()
+    torch.cuda.synchronize()
+
+    def run(n, same=None):
+        for k in range(n):
+            f = k % nfiles
+            mp.exec([shards[f].data_ptr()], (same if same is not None else outs[f]).data_ptr(), [cs])
+        mp.join([cs])
+
+    run(2 * nfiles + 1)
+    cs.synchronize()
+    for f in range(nfiles):
+        assert np.array_equal(outs[f].cpu().numpy().view(np.uint32), wants[f]), f
+    one = torch.zeros_like(outs[0])
+    torch.cuda.synchronize()
+    run(7, same=one)  # (files 0 1 2 3 0 1 2: the last is file 2)
+    cs.synchronize()
+    assert np.array_equal(one.cpu().numpy().view(np.uint32), wants[2])
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cs, capture_error_mode="thread_local"):
+        run(6)
+    for _ in range(2):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        for f in range(nfiles):
+            assert np.array_equal(outs[f].cpu().numpy().view(np.uint32), wants[f]), f
+    del graph
+    mp.close()
+    plain = m.plan(pk, gp, 0)
+    plain.join([cs])  # (no pipeline: nothing to join)
+    plain.close()
+    m.close()
+
+
 def test_multi_plan_refuses_too_many_gather_transfers(hdfs):
     """A gather of more than 4096 point-to-point transfers in one RCCL group
     (here 4100 one-packet groups whose checksum ranges leave gaps, sent to
@@ -1059,8 +1123,8 @@ def test_block_queue_resident_mode(hdfs, gpu_ctx, orc):
     each through the queue calls (crc32c_block_submit / _wait, and
     crc32c_block_checksums), every block bit-exact against the oracle; the
     kernel exits idle_us after the last block and the next submit relaunches
-    it; flush is a no-op; a misaligned payload and a plan with general items
-    are refused; destroy with blocks queued completes them, refuses later
+    it; flush is a no-op; a misaligned output and a plan of half tiles
+    (bpc 700) are refused; destroy with blocks queued completes them, refuses later
     submits, and a plain launch runs after it.  Every wave of the kernel has
     a bounded wait, so nothing here can hang the GPU."""
     import threading
@@ -1122,8 +1186,8 @@ def test_block_queue_resident_mode(hdfs, gpu_ctx, orc):
     q.checksums(devs[0].data_ptr(), outs[0].data_ptr())
     assert np.array_equal(outs[0].cpu().numpy().view(np.uint32), want[0])
     assert q.stats()[0] > launches
-    with pytest.raises(hdfs.Crc32cError) as ei:
-        q.submit(devs[0].data_ptr() + 4, outs[0].data_ptr())
+    with pytest.raises(hdfs.Crc32cError) as ei:  # (payloads at any alignment; outputs 4-byte aligned)
+        q.submit(devs[0].data_ptr(), outs[0].data_ptr() + 2)
     assert ei.value.rc == -22
     with pytest.raises(hdfs.Crc32cError):
         q.wait(10**9)
@@ -1141,10 +1205,10 @@ def test_block_queue_resident_mode(hdfs, gpu_ctx, orc):
     torch.cuda.synchronize()
     assert np.array_equal(outs[1].cpu().numpy().view(np.uint32), want[1])
     plan.close()
-    gplan = gpu_ctx.plan(_block_shape("bpc1536"))
+    gplan = gpu_ctx.plan(oracle.uniform_packets(8, 65536, 700))  # (half tiles: their own kernel builds)
     with pytest.raises(hdfs.Crc32cError) as ei:
         gplan.blocks(resident=True)
-    assert ei.value.rc == -22 and "power-of-two" in str(ei.value)
+    assert ei.value.rc == -22 and "half" in str(ei.value)
     gplan.close()
 
 
@@ -1302,4 +1366,183 @@ def test_verify_result_per_launch_graph_replays(hdfs, gpu_ctx, orc, npk):
         got = [tuple(int(x) for x in r.cpu().numpy().view(np.uint32)) for r in results]
         assert got == [expect_bad, (0, 0xFFFFFFFF), expect_bad], (rep, got)
     del g
+    plan.close()
+
+
+def _append_packets(length, blockoffset, bpc=512):
+    """One block write of hadoop_rpc_send_packets(len = length, blockoffset)
+    (hadooprpc.c:815-860: the first packet trimmed to a chunk boundary), its
+    packets back to back from the block's payload start."""
+    lens = _hdfs_mod().packetize(length, blockoffset, 65536, bpc)
+    pk = np.zeros(len(lens), oracle.PACKET_DTYPE)
+    off = oi = 0
+    for i, ln in enumerate(lens):
+        pk[i]["payload_off"], pk[i]["len"], pk[i]["bpc"], pk[i]["out_idx"] = off, ln, bpc, oi
+        off += ln
+        oi += -(-ln // bpc)
+    return pk
+
+
+def _hdfs_mod():
+    from conftest import load_package
+
+    return load_package()
+
+
+# The shapes a FUSE daemon's block writes take (src/fuse.c:466-650): whole 4
+# MiB blocks (the queue's plan) and the first block of an append at an
+# unaligned offset (updateBlockForPipeline + write_block at blockoffset > 0),
+# some ending mid-chunk (a write that is not a multiple of 512 bytes).
+_APPENDS = [(4 * 2**20 - 100, 100), (4 * 2**20 - 4296, 4296), (4 * 2**20 - 196615, 196615),
+            (1234567, 333), (65536 * 3 + 17, 0), (700, 4000)]
+
+
+@pytest.mark.parametrize("resident", [True, False])
+def test_block_queue_mixed_block_shapes(hdfs, gpu_ctx, orc, resident):
+    """crc32c_block_submit_plan: 16 writer threads, 2 blocks in flight each,
+    alternating whole blocks (the queue's plan) with unaligned appends of
+    _APPENDS (their own plans: a trimmed first packet = a GenItem, tiles off
+    16-byte alignment from it on, tails as general tiles / GenItems) and,
+    through the group-commit queue, a bpc-1536 block (general tiles), the
+    payloads at skews 0..15 -- through the resident kernel and through the
+    group-commit queue; every block bit-exact against the oracle.  The
+    resident queue starts in its aligned-only build and hands over to the
+    general build at the first block that needs it; it refuses a plan of
+    another checksum type and one of bpc 1536."""
+    import threading
+
+    torch = _torch()
+    full = oracle.uniform_packets(64)
+    # (+ through the group-commit queue, a block of bpc 1536: general tiles
+    # of 3-block chunks, which the resident kernel refuses)
+    shapes = [full] + [_append_packets(ln, off) for ln, off in _APPENDS]
+    if not resident:
+        shapes.append(oracle.uniform_packets(48, 65536, 1536))
+    plans = [gpu_ctx.plan(pk) for pk in shapes]
+    nthreads, per, depth = 16, 12, 2
+    jobs = []  # (shape index, skew, host bytes)
+    for k in range(nthreads * depth):
+        si = 0 if k % 2 == 0 else 1 + (k // 2) % (len(shapes) - 1)
+        ext = int((shapes[si]["payload_off"] + shapes[si]["len"]).max())
+        jobs.append((si, (k * 7) % 16, oracle.xorshift64_bytes(ext + 32, 4400 + k)))
+    want = [orc.batch(h[sk:], shapes[si], oracle.total_checksums(shapes[si])) for si, sk, h in jobs]
+    devs = [torch.from_numpy(h).cuda() for _, _, h in jobs]
+    outs = [torch.zeros(max(len(w), 1), dtype=torch.int32, device="cuda") for w in want]
+    torch.cuda.synchronize()
+    q = plans[0].blocks(resident=resident, idle_us=500, max_blocks=8, window_us=20)
+    zeros = torch.zeros(max(o.numel() for o in outs), dtype=torch.int32).pin_memory()
+    errs = []
+    go = threading.Barrier(nthreads)
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream()
+            ring = [None] * depth
+            go.wait()
+            for i in range(per + depth):
+                slot = i % depth
+                b = k * depth + slot
+                si, sk, _ = jobs[b]
+                if ring[slot] is not None:
+                    q.wait(ring[slot])
+                    assert np.array_equal(outs[b].cpu().numpy().view(np.uint32)[:len(want[b])], want[b]), (k, i, si)
+                if i < per:
+                    with torch.cuda.stream(s):
+                        outs[b].copy_(zeros[:outs[b].numel()], non_blocking=True)
+                    s.synchronize()
+                    ring[slot] = q.submit(devs[b].data_ptr() + sk, outs[b].data_ptr(), plan=plans[si] if si else None)
+                else:
+                    ring[slot] = None
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs[:3]
+    if resident:
+        crc32_plan = gpu_ctx.plan(shapes[1], hdfs.CRC32C_TYPE_CRC32)
+        b1536 = gpu_ctx.plan(oracle.uniform_packets(48, 65536, 1536))
+        for pl in (crc32_plan, b1536):
+            with pytest.raises(hdfs.Crc32cError) as ei:
+                q.submit(devs[1].data_ptr(), outs[1].data_ptr(), plan=pl)
+            assert ei.value.rc == -22
+        launches, blocks = q.stats()
+        assert blocks == nthreads * per and launches >= 1
+    q.close()
+    if resident:
+        crc32_plan.close()
+        b1536.close()
+    for pl in plans:
+        pl.close()
+
+
+def test_block_queue_resident_failed_slot_wait_takes_no_ticket(hdfs, gpu_ctx, orc):
+    """a submit whose ring slot is still busy waits for it BEFORE
+    taking a ticket, so a wait that gives up leaves no hole in the ticket
+    sequence.  With the kernel held back (debug hook) 64 submits fill the
+    ring; the 65th's slot wait is made to fail: -ETIMEDOUT, no ticket taken.
+    Released, the same submit then gets ticket 64 and all 65 blocks complete
+    bit-exact -- the queue was not wedged."""
+    torch = _torch()
+    pk = oracle.uniform_packets(8)
+    n = oracle.total_checksums(pk)
+    host = oracle.xorshift64_bytes(8 * 65536, 4242)
+    want = orc.batch(host, pk, n)
+    dev = torch.from_numpy(host).cuda()
+    outs = torch.zeros((65, n), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    q = plan.blocks(resident=True, idle_us=500)
+    q.debug_resident_inject(True, 1)
+    tickets = [q.submit(dev.data_ptr(), outs[i].data_ptr()) for i in range(64)]
+    assert tickets == list(range(64)) and q.stats() == (0, 64)
+    with pytest.raises(hdfs.Crc32cError) as ei:
+        q.submit(dev.data_ptr(), outs[64].data_ptr())
+    assert ei.value.rc == -110  # -ETIMEDOUT
+    assert q.stats() == (0, 64)  # (no ticket was taken)
+    q.debug_resident_inject(False, 0)
+    assert q.submit(dev.data_ptr(), outs[64].data_ptr()) == 64
+    for t in tickets + [64]:
+        q.wait(t)
+    got = outs.cpu().numpy().view(np.uint32)
+    for i in range(65):
+        assert np.array_equal(got[i], want), i
+    q.close()
+    plan.close()
+
+
+def test_block_queue_resident_hands_over_to_general_build(hdfs, gpu_ctx, orc):
+    """The resident queue runs its own plan's aligned blocks in the
+    aligned-only kernel build; the first block that needs more -- here the
+    same plan's block at a misaligned payload -- ends that launch at the
+    block (its forwarder stops there) and starts the general build, which
+    then serves every block: blocks before and after the hand-over bit-exact,
+    two launches in all."""
+    torch = _torch()
+    pk = oracle.uniform_packets(16)
+    n = oracle.total_checksums(pk)
+    host = oracle.xorshift64_bytes(16 * 65536 + 32, 5150)
+    dev = torch.from_numpy(host).cuda()
+    outs = torch.zeros((12, n), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    plan = gpu_ctx.plan(pk)
+    q = plan.blocks(resident=True, idle_us=200000)  # (the aligned-only launch is still running at the hand-over)
+    skews = [0, 0, 0, 0, 5, 0, 0, 13, 0, 16, 3, 0]
+    tickets = []
+    for i, sk in enumerate(skews):
+        tickets.append(q.submit(dev.data_ptr() + sk, outs[i].data_ptr()))
+        if i == 3:
+            for t in tickets:
+                q.wait(t)
+            assert q.stats() == (1, 4)
+    for t in tickets:
+        q.wait(t)
+    assert q.stats() == (2, 12)
+    got = outs.cpu().numpy().view(np.uint32)
+    for i, sk in enumerate(skews):
+        assert np.array_equal(got[i], orc.batch(host[sk:], pk, n)), i
+    q.close()
     plan.close()

@@ -24,8 +24,16 @@
 // queue lines also the worker thread's own (worker_cpu_us_per_block, and
 // worker_busy = its CPU seconds per wall second).
 //
+//   rqueue_mixed, rqueue2_mixed, queue2_mixed -- (mixed = 1) every other block
+//              of a thread is the first block of an append at an unaligned
+//              offset (hadoop_fuse_do_write, src/fuse.c:488-574: write_block at
+//              blockoffset > 0, the first packet trimmed to a chunk boundary,
+//              hadooprpc.c:832-840) through crc32c_block_submit_plan with its own
+//              plan, the payload off 16-byte alignment; checked against
+//              crc32c_plan_exec of the same plan and bytes
+//
 //   tools/block_rate [threads=16] [iterations=400] [max_blocks=16] [window_us=30]
-//                    [max_depth=2] [queue_modes_only=0]
+//                    [max_depth=2] [queue_modes_only=0] [mixed=0: 1 = the mixed modes only]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -103,6 +111,7 @@ int main(int argc, char **argv) {
         CHECK(hipMalloc(&outs[i], nout * 4) == hipSuccess);
     }
     CHECK(hipDeviceSynchronize() == hipSuccess);
+    const bool mixed_only = argc > 7 && std::atoi(argv[7]) != 0;
 
     auto run = [&](const char *mode, auto body) {
         std::atomic<int> ready{0};
@@ -135,6 +144,118 @@ int main(int argc, char **argv) {
     // single: one launch per block
     std::vector<hipStream_t> streams(nthreads);
     for (auto &s : streams) CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess);
+
+    if (mixed_only) {
+        // thread k's unaligned shape: an append of 4 MiB - off at block offset
+        // off (its own file), payload skewed off 16-byte alignment
+        std::vector<crc32c_plan *> uplans(nthreads);
+        std::vector<int> skew(nthreads);
+        for (int k = 0; k < nthreads; ++k) {
+            const uint64_t off = 100 + 4099ull * uint64_t(k), len = kBlock - off;
+            const int64_t np = crc32c_packetize(len, off, 65536, 512, nullptr, 0);
+            CHECK(np > 0);
+            std::vector<uint64_t> lens(static_cast<size_t>(np));
+            CHECK(crc32c_packetize(len, off, 65536, 512, lens.data(), size_t(np)) == np);
+            std::vector<crc32c_packet> up;
+            uint64_t po = 0, oi = 0;
+            for (uint64_t l : lens) {
+                up.push_back(crc32c_packet{po, oi, uint32_t(l), 512u});
+                po += l;
+                oi += crc32c_nchunks(l, 512);
+            }
+            CHECK(oi <= nout);
+            CHECK(crc32c_plan_create(ctx, up.data(), up.size(), 0, &uplans[k]) == 0);
+            skew[k] = 1 + (k * 5) % 15;
+        }
+        // expected: block b of thread k, kind 0 (whole block) or 1 (its append)
+        std::vector<std::vector<uint32_t>> want(2 * size_t(nbuf), std::vector<uint32_t>(nout));
+        auto expect = [&](int b, int kind, int k) {
+            std::vector<uint32_t> &w = want[2 * size_t(b) + size_t(kind)];
+            // (on the launch stream: the streams are non-blocking, so a memset on
+            // the null stream could land after the launch)
+            CHECK(hipMemsetAsync(outs[b], 0, nout * 4, streams[0]) == hipSuccess);
+            if (kind == 0)
+                CHECK(crc32c_plan_exec(plan, bufs[b], outs[b], streams[0]) == 0);
+            else
+                CHECK(crc32c_plan_exec(uplans[k], bufs[b] + skew[k], outs[b], streams[0]) == 0);
+            CHECK(hipStreamSynchronize(streams[0]) == hipSuccess);
+            CHECK(hipMemcpy(w.data(), outs[b], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
+        };
+        const std::pair<bool, int> modes[3] = {{true, 1}, {true, 2}, {false, 2}};  // (resident, depth)
+        for (const auto &md : modes) {
+                const bool res = md.first;
+                const int depth = md.second;
+                for (int k = 0; k < nthreads; ++k)
+                    for (int slot = 0; slot < depth; ++slot) {
+                        const int b = depth * k + slot;
+                        const int last = ((iters - 1 - slot) / depth) * depth + slot;  // last i of this slot
+                        expect(b, last % 2, k);
+                    }
+                for (int w = 0; w < 2; ++w) {
+                    for (int i = 0; i < nbuf; ++i) CHECK(hipMemset(outs[i], 0, nout * 4) == hipSuccess);
+                    CHECK(hipDeviceSynchronize() == hipSuccess);
+                    crc32c_blocks *q = nullptr;
+                    if (res)
+                        CHECK(crc32c_blocks_create_resident(plan, 2000, &q) == 0);
+                    else
+                        CHECK(crc32c_blocks_create(plan, max_blocks, window_us, &q) == 0);
+                    const char *name = res ? (depth == 1 ? "rqueue_mixed" : "rqueue2_mixed") : "queue2_mixed";
+                    run(name, [&](int k) {
+                        std::vector<uint64_t> ring(depth);
+                        for (int i = 0; i < iters; ++i) {
+                            const int slot = i % depth;
+                            if (i >= depth) CHECK(crc32c_block_wait(q, ring[slot]) == 0);
+                            const int b = depth * k + slot;
+                            if (i % 2 == 0)
+                                CHECK(crc32c_block_submit(q, bufs[b], outs[b], &ring[slot]) == 0);
+                            else
+                                CHECK(crc32c_block_submit_plan(q, uplans[k], bufs[b] + skew[k], outs[b], &ring[slot]) == 0);
+                            if (depth == 1) CHECK(crc32c_block_wait(q, ring[slot]) == 0);
+                        }
+                        if (depth > 1)
+                            for (int i = std::max(0, iters - depth); i < iters; ++i)
+                                CHECK(crc32c_block_wait(q, ring[i % depth]) == 0);
+                    });
+                    uint64_t launches = 0, blocks = 0;
+                    CHECK(crc32c_blocks_stats(q, &launches, &blocks) == 0);
+                    CHECK(crc32c_blocks_destroy(q) == 0);
+                    // (the last block of each slot, over its own checksums: a slot
+                    // that alternates shapes keeps the longer one's tail)
+                    int bad = 0, bad_unaligned = 0;
+                    std::vector<uint32_t> got(nout);
+                    for (int k = 0; k < nthreads; ++k)
+                        for (int slot = 0; slot < depth; ++slot) {
+                            const int b = depth * k + slot;
+                            const int last = ((iters - 1 - slot) / depth) * depth + slot;
+                            const size_t nc = size_t(crc32c_plan_nchecksums(last % 2 ? uplans[k] : plan));
+                            CHECK(hipMemcpy(got.data(), outs[b], nout * 4, hipMemcpyDeviceToHost) == hipSuccess);
+                            const std::vector<uint32_t> &w = want[2 * size_t(b) + size_t(last % 2)];
+                            const bool wrong = !std::equal(got.begin(), got.begin() + nc, w.begin());
+                            bad += wrong;
+                            bad_unaligned += wrong && (last % 2);
+                            if (wrong) {  // (diagnostic: where, and the host's crc32c of that chunk)
+                                size_t j = 0, nw = 0;
+                                for (size_t x = 0; x < nc; ++x) nw += got[x] != w[x];
+                                while (got[j] == w[j]) ++j;
+                                const uint64_t off = 100 + 4099ull * uint64_t(k);
+                                const size_t first = (last % 2) ? 512 - off % 512 : 512;
+                                std::vector<uint8_t> chunk(j == 0 ? first : 512, uint8_t(b * 37 + 1));
+                                std::fprintf(stderr, "wrong: mode %s depth %d thread %d slot %d kind %d: %zu of %zu checksums "
+                                             "differ, first at %zu: got %08x want %08x host %08x\n",
+                                             res ? "resident" : "queue", depth, k, slot, last % 2, nw, nc, j, got[j],
+                                             w[j], crc32c(0, chunk.data(), chunk.size()));
+                            }
+                        }
+                    std::printf(", \"launches\": %llu, \"unaligned_share\": 0.5, \"blocks_wrong\": %d, "
+                                "\"wrong_unaligned\": %d, \"pass\": %d}\n",
+                                (unsigned long long)launches, bad, bad_unaligned, w);
+                }
+            }
+        for (crc32c_plan *u : uplans) crc32c_plan_destroy(u);
+        crc32c_plan_destroy(plan);
+        for (auto &s : streams) (void)hipStreamDestroy(s);
+        return 0;
+    }
     for (int w = 0; w < (sweep_only ? 0 : 2); ++w) {
         run("single", [&](int k) {
             for (int i = 0; i < iters; ++i) {
