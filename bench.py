@@ -589,9 +589,14 @@ def run_config4(hdfs, args, env) -> dict:
     self_send = os.environ.get("BENCH_C4_SELF_SEND") == "1"  # (tests: rank 0's array through RCCL too)
     flags = MULTI_SELF_SEND if self_send else 0
     # CRC32C_MULTI_PIPELINE: step k + 1's shard launch overlaps step k's tail
-    # and gather (each step's file and root array its own; joined at the end
-    # of every timed part).  BENCH_C4_PIPELINE=0: every step in stream order.
-    pipeline = not rehearsal and os.environ.get("BENCH_C4_PIPELINE", "1") != "0"
+    # (each step's file and root array its own; joined at the end of every
+    # timed part) -- where the step has no gather: with one, the one-GPU
+    # model measured the overlapped RCCL group and shard launch slower than
+    # stream order (15.4 against 12.8 us graph-replayed).
+    # BENCH_C4_PIPELINE=1 / 0 forces it on / off.
+    ln0, xs0 = shard.transfers(file_pk, gp, world, flags)
+    pipe_env = os.environ.get("BENCH_C4_PIPELINE", "")
+    pipeline = not rehearsal and (pipe_env == "1" or (pipe_env != "0" and not int(xs0.shape[0])))
     nbuf = max(1, args.nbuf)
     file0 = synthetic_bytes(file_bytes_total, 2024)
     bufs = []

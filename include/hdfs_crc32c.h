@@ -213,7 +213,11 @@ uint64_t crc32c_plan_payload_bytes(const crc32c_plan *plan);
  * verify launches of the same plan: the caller must not let those overlap.
  * If they do, the kernels still finish (a mismatching workgroup waits for
  * its launch's key a bounded time) and bit 31 of dev_result[0]
- * (CRC32C_VERIFY_OVERLAP) marks the result indeterminate. */
+ * (CRC32C_VERIFY_OVERLAP) marks the result indeterminate.  The same bit can
+ * appear for a correct result when the launch's first workgroup starts late
+ * -- e.g. while a resident block queue (section 3b) holds every CU -- and a
+ * workgroup with more than 256 mismatches waits for it past its bound:
+ * re-run such a verify once nothing else holds the device. */
 #define CRC32C_VERIFY_OVERLAP 0x80000000u
 int crc32c_plan_verify(crc32c_plan *plan, const void *dev_payload, const uint32_t *dev_expected,
                        uint32_t *dev_result, void *stream);

@@ -20,8 +20,8 @@
 //     per lane): batches of at most kQuarterTilesPerCu tiles per CU, where
 //     one wave's load -> lookups chain is the launch (one 4 MiB block,
 //     graph-replayed: 4.36 -> 3.71 us);
-//   * full image with the general-tile code and half tiles (bpc <= 256 and
-//     513..768), with and without the shifted loads, for any batch holding
+//   * full image with the general-tile code and half tiles (bpc <= 256,
+//     513..768 and 1025..1280), with and without the shifted loads, for any batch holding
 //     half tiles (compiled into the builds above, their code cost those
 //     3-8 %).
 // A/B and diagnostic variants are built only into libhdfs_crc32c_debug.so

@@ -921,10 +921,18 @@ int crc32c_device_count(void) {
     return n;
 }
 
+}  // extern "C"
+
+namespace {
+void reap_zombies(bool block);
+}  // namespace
+
+extern "C" {
+
 int crc32c_ctx_create(int device, crc32c_ctx **out) {
     if (!out) return fail(-EINVAL, "out == NULL");
     *out = nullptr;
-    crc32c_ctx_destroy(nullptr);  // (tears down contexts a plan's destroy left for later)
+    reap_zombies(false);  // (contexts a plan's destroy left for later, whose work is done)
     const int ndev = crc32c_device_count();
     if (ndev <= 0) return fail(-ENODEV, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(-ENODEV, "device %d out of range (%d visible)", device, ndev);
@@ -983,17 +991,38 @@ void ctx_teardown(crc32c_ctx *ctx) {
 }
 
 // Contexts whose last reference went with a plan's destroy: torn down by
-// the next crc32c_ctx_create / crc32c_ctx_destroy (plan destroy never
-// synchronises, frees device memory or destroys a stream: it may run while
-// another thread captures a graph), or left to process exit.
+// the next crc32c_ctx_destroy, or by the next crc32c_ctx_create once their
+// destroyed plans' launches are known complete (a non-blocking check, so a
+// create never waits for another context's work), or left to process exit
+// (plan destroy never synchronises, frees device memory or destroys a
+// stream: it may run while another thread captures a graph).
 std::mutex g_zombie_mu;
 std::vector<crc32c_ctx *> g_zombies;
 
-void reap_zombies() {
+// Nothing of a zombie's destroyed plans can still be running (non-blocking:
+// the release events are queried, counter read-backs issued, not awaited).
+bool zombie_idle(crc32c_ctx *ctx) {
+    std::lock_guard<std::mutex> lock(ctx->pool_mu);
+    reap_releases(ctx);
+    return ctx->releases.empty() && ctx->held.empty();
+}
+
+void reap_zombies(bool block) {
     std::vector<crc32c_ctx *> z;
     {
         std::lock_guard<std::mutex> lock(g_zombie_mu);
-        z.swap(g_zombies);
+        if (block) {
+            z.swap(g_zombies);
+        } else {
+            for (size_t i = 0; i < g_zombies.size();)
+                if (zombie_idle(g_zombies[i])) {
+                    z.push_back(g_zombies[i]);
+                    g_zombies[i] = g_zombies.back();
+                    g_zombies.pop_back();
+                } else {
+                    ++i;
+                }
+        }
     }
     for (crc32c_ctx *c : z) ctx_teardown(c);
 }
@@ -1013,7 +1042,7 @@ void ctx_release(crc32c_ctx *ctx, bool defer) {
 extern "C" {
 
 int crc32c_ctx_destroy(crc32c_ctx *ctx) {
-    reap_zombies();
+    reap_zombies(true);
     if (!ctx) return 0;
     ctx_release(ctx, false);
     return 0;

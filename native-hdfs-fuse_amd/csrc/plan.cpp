@@ -75,8 +75,9 @@ static bool padded_tiles_on() {
     static const bool on = env_long("HDFS_CRC32C_PADDED_TILES") != 0;
     return on;
 }
-// Half tiles for bpc <= 256 and 512 < bpc <= 768 (plan.h); A/B knob
-// HDFS_CRC32C_HALF_TILES=0 sends those chunks to the forms above instead.
+// Half tiles for bpc <= 256, 512 < bpc <= 768 (M = 1) and 1024 < bpc <= 1280
+// (M = 2) (plan.h); A/B knob HDFS_CRC32C_HALF_TILES=0 sends those chunks to
+// the forms above instead.
 static bool half_tiles_on() {
     static const bool on = env_long("HDFS_CRC32C_HALF_TILES") != 0;
     return on;

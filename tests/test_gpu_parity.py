@@ -782,7 +782,9 @@ def test_plan_destroyed_after_its_context(hdfs, orc):
     """A plan outliving crc32c_ctx_destroy (a garbage collector freeing a
     plan late, e.g. one a failed test's traceback held): the context is
     reference-counted by its plans, so the late destroy returns the plan's
-    block to a still-live pool and the context goes with its last plan."""
+    block to a still-live pool; the context's teardown is deferred past its
+    last plan (a plan destroy never synchronises) to the next context
+    create that finds its work done, or the next context destroy."""
     torch = _torch()
     pk = oracle.uniform_packets(8)
     n = hdfs.total_checksums(pk)

@@ -1546,3 +1546,26 @@ def test_block_queue_resident_hands_over_to_general_build(hdfs, gpu_ctx, orc):
         assert np.array_equal(got[i], orc.batch(host[sk:], pk, n)), i
     q.close()
     plan.close()
+
+
+def test_verify_bitmap_more_mismatches_than_a_workgroup_lists(hdfs, gpu_ctx, orc):
+    """a workgroup keeps its first 256 mismatching indices in LDS
+    until it sees its launch's key; the ones past the list wait for the key
+    per lane and set their bits directly.  A 64 MiB batch (32 tiles = 512
+    checksums per workgroup) verified against expected values that are ALL
+    wrong: every workgroup goes past its list.  The count, the lowest index
+    and the bitmap name every checksum, and no overlap bit is set (nothing
+    else runs)."""
+    torch = _torch()
+    s = torch.cuda.current_stream()
+    pk = oracle.uniform_packets(1024)
+    n = hdfs.total_checksums(pk)
+    payload = oracle.xorshift64_bytes(1024 * 65536, 2026)
+    want = orc.batch(payload, pk, n)
+    dev = torch.from_numpy(payload).cuda()
+    plan = hdfs.Plan(gpu_ctx, pk)
+    res, bad = _bitmap_verify(plan, ~want, s, dev.data_ptr())
+    assert res == [n, 0] and bad.size == n
+    res, bad = _bitmap_verify(plan, want, s, dev.data_ptr())  # (and clean again right after)
+    assert res == [0, 0xFFFFFFFF] and bad.size == 0
+    plan.close()

@@ -20,6 +20,12 @@ per step (HIP events on the launch stream, 1000 steps after 200 warm-up):
 Each multi step is also captured (kernel + RCCL group) into a graph of 100
 steps and replayed (*_graph_us), as bench.py replays config 4's steps.
 
+  pipe_in_place / pipe_self_send -- the same two with CRC32C_MULTI_PIPELINE
+                               (consecutive steps into 4 rotating root arrays
+                               overlap; joined at the end), host-issued and
+                               graph-replayed, checked against the plain
+                               plan's checksums.
+
 Prints one JSON line.  The model: step(N = 8) ~= shard time + gather time,
 with the gather at least (multi_self_send - multi_in_place); graph-replayed,
 step(N = 8) ~= multi_self_send_graph (the shard plus one RCCL group)."""
@@ -100,12 +106,63 @@ def main():
             torch.cuda.synchronize()
         mp.close()
         m.close()
+    # CRC32C_MULTI_PIPELINE: consecutive steps into rotating root arrays
+    # overlap (step k + 1's shard launch beside step k's tail and gather);
+    # joined at the end of the timed steps / inside the capture.
+    outs = [torch.zeros(256 * 128, dtype=torch.int32, device=dev) for _ in range(4)]
+    for name, flags in (("pipe_in_place", 0), ("pipe_self_send", hdfs.CRC32C_MULTI_SELF_SEND)):
+        m = hdfs.Multi([0])
+        mp = m.plan(pk, 64, flags | hdfs.CRC32C_MULTI_PIPELINE)
+        k = [0]
+
+        def step(sp):
+            mp.exec([payload.data_ptr()], outs[k[0] % 4].data_ptr(), [sp])
+            k[0] += 1
+
+        def timed_pipe(n=1000, warm=200):
+            for _ in range(warm):
+                step(stream.cuda_stream)
+            mp.join([stream.cuda_stream])
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(n):
+                step(stream.cuda_stream)
+            mp.join([stream.cuda_stream])
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / n * 1e3
+
+        res[name + "_us"] = round(timed_pipe(), 3)
+        exact = all(np.array_equal(o.cpu().numpy(), out.cpu().numpy()) for o in outs)
+        try:
+            gm = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gm, stream=cs, capture_error_mode="thread_local"):
+                for _ in range(100):
+                    step(cs.cuda_stream)
+                mp.join([cs.cuda_stream])
+            gm.replay()
+            torch.cuda.synchronize()
+            res[name + "_graph_us"] = round(timed(lambda: gm.replay(), n=50, warm=5) / 100, 3)
+            exact = exact and all(np.array_equal(o.cpu().numpy(), out.cpu().numpy()) for o in outs)
+            del gm
+        except RuntimeError as e:
+            res[name + "_graph_error"] = str(e)[:200]
+            torch.cuda.synchronize()
+        res[name + "_exact"] = exact
+        mp.close()
+        m.close()
     # One rank of config 4 at N = 8 checksums 4 of the 32 blocks (this shard)
     # and, at rank 0, receives 7 peers' 4 x 32 KiB; a peer's transfer costs at
     # least what the self-send adds to the in-place step (one RCCL group).
     res["gather_lower_bound_us"] = round(res["multi_self_send_us"] - res["multi_in_place_us"], 3)
     res["model_step_n8_us"] = round(res["shard_eager_us"] + res["gather_lower_bound_us"], 3)
     res["model_value_n8_gib_s"] = round(32 * (4 << 20) / (res["model_step_n8_us"] * 1e-6) / 2**30, 1)
+    if "pipe_self_send_graph_us" in res:  # (pipelined steps, the bench's default)
+        res["model_step_n8_pipe_graph_us"] = res["pipe_self_send_graph_us"]
+        res["model_value_n8_pipe_graph_gib_s"] = round(32 * (4 << 20) / (res["pipe_self_send_graph_us"] * 1e-6)
+                                                       / 2**30, 1)
     if "multi_self_send_graph_us" in res:  # the bench's config-4 steps are graph-replayed
         res["gather_lower_bound_graph_us"] = round(res["multi_self_send_graph_us"] - res["shard_graph_us"], 3)
         res["model_step_n8_graph_us"] = res["multi_self_send_graph_us"]
