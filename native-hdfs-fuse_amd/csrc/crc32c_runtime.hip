@@ -528,7 +528,15 @@ int launch(const crc32c_ctx *ctx, KParams p, SchedSlots &slots, hipStream_t stre
         if (rc) return rc;
         p.sched = slots.d;
     }
-    HIP_TRY(launch_plan_kernel(p, uint32_t(ctx->num_cu), stream, stop, grid));
+    // (A/B knob HDFS_CRC32C_CU_CAP=n: launches size their grid for at most n
+    // CUs, leaving the rest to kernels beside them -- an RCCL group
+    // overlapping a pipelined multi-plan step; measured no gain)
+    static const int cap = [] {
+        const char *e = std::getenv("HDFS_CRC32C_CU_CAP");
+        return e ? std::atoi(e) : 0;
+    }();
+    const uint32_t ncu = uint32_t(cap > 0 && cap < ctx->num_cu ? cap : ctx->num_cu);
+    HIP_TRY(launch_plan_kernel(p, ncu, stream, stop, grid));
     return 0;
 }
 
