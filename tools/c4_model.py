@@ -15,7 +15,11 @@ per step (HIP events on the launch stream, 1000 steps after 200 warm-up):
                                shard's 128 KiB go through one RCCL send/recv
                                group to rank 0's own staging slot, then the
                                scatter kernel -- a lower bound for one peer's
-                               gather at N = 8.
+                               gather at N = 8;
+  multi_self_send_4x        -- the same with the shard's four groups placed
+                               apart in the output (four 32 KiB transfers,
+                               as one peer's at N = 8, where its 4 blocks
+                               are 8 blocks apart in file order).
 
 Each multi step is also captured (kernel + RCCL group) into a graph of 100
 steps and replayed (*_graph_us), as bench.py replays config 4's steps.
@@ -85,18 +89,32 @@ def main():
     torch.cuda.synchronize()
     res["shard_graph_us"] = round(timed(lambda: g.replay(), n=50, warm=5) / 100, 3)
     plan.close()
-    for name, flags in (("multi_in_place", 0), ("multi_self_send", hdfs.CRC32C_MULTI_SELF_SEND)):
+    # (multi_self_send_4x: the four groups' checksum ranges 37 apart in the
+    # output, so they do not merge -- four 32 KiB transfers, one N = 8 peer's
+    # pattern: its 4 blocks are 8 blocks apart in file order)
+    pk4 = pk.copy()
+    gap = 37
+    pk4["out_idx"] = np.array([(i // 64) * (64 * 128 + gap) + (i % 64) * 128 for i in range(pk.size)], np.uint64)
+    out4 = torch.zeros(4 * (64 * 128 + gap), dtype=torch.int32, device=dev)
+    for name, flags, pkm, o in (("multi_in_place", 0, pk, out),
+                                ("multi_self_send", hdfs.CRC32C_MULTI_SELF_SEND, pk, out),
+                                ("multi_self_send_4x", hdfs.CRC32C_MULTI_SELF_SEND, pk4, out4)):
         m = hdfs.Multi([0])
-        mp = m.plan(pk, 64, flags)
-        res[name + "_us"] = round(timed(lambda: mp.exec([payload.data_ptr()], out.data_ptr(), [stream.cuda_stream])), 3)
+        mp = m.plan(pkm, 64, flags)
+        if name.endswith("_4x"):
+            res[name + "_transfers"] = int(hdfs.multi_transfers(pkm, 64, 1, flags)[1].shape[0])
+        res[name + "_us"] = round(timed(lambda: mp.exec([payload.data_ptr()], o.data_ptr(), [stream.cuda_stream])), 3)
+        if name.endswith("_4x"):
+            got = o.cpu().numpy().reshape(4, -1)[:, :64 * 128].reshape(-1)
+            res[name + "_exact"] = bool(np.array_equal(got, out.cpu().numpy()))
         # the whole step (kernel + RCCL group) captured 100 times into one graph
-        mp.exec([payload.data_ptr()], out.data_ptr(), [cs.cuda_stream])
+        mp.exec([payload.data_ptr()], o.data_ptr(), [cs.cuda_stream])
         torch.cuda.synchronize()
         try:
             gm = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gm, stream=cs, capture_error_mode="thread_local"):
                 for _ in range(100):
-                    mp.exec([payload.data_ptr()], out.data_ptr(), [cs.cuda_stream])
+                    mp.exec([payload.data_ptr()], o.data_ptr(), [cs.cuda_stream])
             gm.replay()
             torch.cuda.synchronize()
             res[name + "_graph_us"] = round(timed(lambda: gm.replay(), n=50, warm=5) / 100, 3)
@@ -159,7 +177,7 @@ def main():
     res["gather_lower_bound_us"] = round(res["multi_self_send_us"] - res["multi_in_place_us"], 3)
     res["model_step_n8_us"] = round(res["shard_eager_us"] + res["gather_lower_bound_us"], 3)
     res["model_value_n8_gib_s"] = round(32 * (4 << 20) / (res["model_step_n8_us"] * 1e-6) / 2**30, 1)
-    if "pipe_self_send_graph_us" in res:  # (pipelined steps, the bench's default)
+    if "pipe_self_send_graph_us" in res:  # (pipelined steps with a gather: measured slower, not used)
         res["model_step_n8_pipe_graph_us"] = res["pipe_self_send_graph_us"]
         res["model_value_n8_pipe_graph_gib_s"] = round(32 * (4 << 20) / (res["pipe_self_send_graph_us"] * 1e-6)
                                                        / 2**30, 1)
@@ -167,6 +185,8 @@ def main():
         res["gather_lower_bound_graph_us"] = round(res["multi_self_send_graph_us"] - res["shard_graph_us"], 3)
         res["model_step_n8_graph_us"] = res["multi_self_send_graph_us"]
         res["model_value_n8_graph_gib_s"] = round(32 * (4 << 20) / (res["multi_self_send_graph_us"] * 1e-6) / 2**30, 1)
+    if "multi_self_send_4x_graph_us" in res:  # the same with one N = 8 peer's four transfers
+        res["model_step_n8_graph_4x_us"] = res["multi_self_send_4x_graph_us"]
     print(json.dumps(res), flush=True)
     ctx.close()
 
