@@ -741,6 +741,7 @@ def run_config4(hdfs, args, env) -> dict:
     r["graphs"].clear()
     if rs is not None:
         rs["graphs"].clear()
+    gops = state["mplan"].gather_ops() if state.get("mplan") is not None else None
     close_multi()
     if splan is not None:
         splan.close()
@@ -766,6 +767,9 @@ def run_config4(hdfs, args, env) -> dict:
         # none without transfers -- N = 1 in place)
         "gather_us": None if (shard_max is None or not int(xs.shape[0])) else round(step_kernel_us - shard_max, 3),
         "transfers": int(xs.shape[0]), "self_send": self_send,
+        # (RCCL operations per step, whole communicator; packed: one send per
+        # rank into rank 0's staging array + the scatter kernel)
+        "gather_ops": None if gops is None else gops[0], "gather_packed": None if gops is None else gops[1],
         "bit_exact": exact,
         "bit_exact_checks": {"before_warmup_file0": gate,
                              "timed_files_buf%s" % "_".join(str(b) for b in timed_bufs): timed} if rank == 0 else None,

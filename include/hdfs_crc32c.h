@@ -417,13 +417,28 @@ int64_t crc32c_multi_shard_packets(const crc32c_packet *pkts, size_t npkts, uint
  * local array, index in the file-order output on rank 0, count} -- one per
  * received group, merged with the previous one when both come from the same
  * rank and stay contiguous on both sides.  Returns the number of transfers
- * (fills at most cap).  crc32c_multi_plan_exec issues exactly these: each
- * sender one ncclSend per transfer of its own, rank 0 one ncclRecv per
- * transfer straight into root_out (no staging copy), all in one RCCL group. */
+ * (fills at most cap).  These are the gather's placements.  When no sender
+ * has more than one (each rank's groups are one file-order range),
+ * crc32c_multi_plan_exec posts exactly these: each sender one ncclSend, rank
+ * 0 one ncclRecv straight into root_out.  Otherwise (round-robin blocks over
+ * N > 1 ranks) the exec is packed: each sender posts ONE ncclSend of its
+ * whole local array, rank 0 one ncclRecv per sender into a staging array of
+ * the plan's, and one scatter kernel on rank 0's stream copies every
+ * placement into root_out -- unless the plan has CRC32C_MULTI_PER_GROUP_RECV,
+ * which posts one ncclSend / ncclRecv pair per placement. */
 int64_t crc32c_multi_rank_packets(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
                                   int rank, uint32_t flags, crc32c_packet *local, size_t cap);
 int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
                                uint32_t flags, uint64_t *local_nout, uint64_t *xfers, size_t cap);
+/* crc32c_multi_scatter: the packed gather's layout (host only).  Returns the
+ * number of scatter tiles, 0 when the gather is not packed (no sender has
+ * more than one placement, or CRC32C_MULTI_PER_GROUP_RECV); stage_off[r]
+ * (nranks entries, optional) = index in rank 0's staging array where rank
+ * r's whole local array is received (senders in rank order); per tile t
+ * (fills at most cap), tiles[3t .. 3t+2] = {staging index, file index,
+ * count <= 1024}: what the scatter kernel copies into root_out. */
+int64_t crc32c_multi_scatter(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                             uint32_t flags, uint64_t *stage_off, uint64_t *tiles, size_t cap);
 
 /* Device-resident multi-GPU plan of a file's packets (offsets in the caller's
  * file layout; every process passes the same list).  Exec: dev_shards[i] =
@@ -441,9 +456,13 @@ int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t
  * execs on the same stream cost no extra HIP call; an exec on another stream
  * than the plan's previous one records an event on that previous stream, so
  * that stream must still exist then.  flags: CRC32C_BIG_ENDIAN,
- * CRC32C_TYPE_CRC32, CRC32C_MULTI_SELF_SEND, CRC32C_COUNT_COMPLETION.  A plan
- * whose gather would post more than 4096 transfers (crc32c_multi_transfers;
- * a tiny group_packets over a large file) is refused with -E2BIG. */
+ * CRC32C_TYPE_CRC32, CRC32C_MULTI_SELF_SEND, CRC32C_MULTI_PIPELINE,
+ * CRC32C_MULTI_PER_GROUP_RECV, CRC32C_COUNT_COMPLETION.  A plan with
+ * CRC32C_MULTI_PER_GROUP_RECV whose gather would post more than 4096
+ * transfers (a tiny group_packets over a large file) is refused with -E2BIG.
+ * crc32c_multi_plan_gather_ops: the point-to-point operations (sends +
+ * receives, whole communicator) one exec's RCCL group posts; *packed
+ * (optional) = 1 when the exec is packed (staging array + scatter kernel). */
 #define CRC32C_MULTI_SELF_SEND 0x10u /* crc32c_multi_plan_create: rank 0's own checksums also travel
                                        through RCCL (a send to itself) instead of being written in
                                        place -- exercises the transport on a one-GPU communicator */
@@ -463,6 +482,10 @@ int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t
  * root_out arrays overlap fully.  crc32c_multi_plan_join on a plan without
  * the flag does nothing. */
 #define CRC32C_MULTI_PIPELINE 0x40u
+/* CRC32C_MULTI_PER_GROUP_RECV (plan flag, A/B): one ncclSend / ncclRecv pair
+ * per placement (crc32c_multi_transfers), received straight into root_out,
+ * even when a sender has several -- instead of the packed gather. */
+#define CRC32C_MULTI_PER_GROUP_RECV 0x80u
 typedef struct crc32c_multi_plan crc32c_multi_plan;
 int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
                              uint32_t flags, crc32c_multi_plan **out);
@@ -472,6 +495,7 @@ int crc32c_multi_plan_join(crc32c_multi_plan *mp, void *const *streams);
 int crc32c_multi_plan_destroy(crc32c_multi_plan *mp);
 uint64_t crc32c_multi_plan_nchecksums(const crc32c_multi_plan *mp);
 uint64_t crc32c_multi_plan_shard_bytes(const crc32c_multi_plan *mp, int rank);
+uint64_t crc32c_multi_plan_gather_ops(const crc32c_multi_plan *mp, int *packed);
 
 /* Host-resident: each local device checksums its groups (dealt round-robin
  * over the local devices) from host memory over its own PCIe link and

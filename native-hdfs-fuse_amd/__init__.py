@@ -34,6 +34,7 @@ CRC32C_CPU_FALLBACK = 0x8  # crc32c_chunks / crc32c_batch_host: finish on the ho
 CRC32C_MULTI_SELF_SEND = 0x10  # multi plan: rank 0's own checksums also go through RCCL (one-GPU transport test)
 CRC32C_COUNT_COMPLETION = 0x20  # plan: launches count their completion on the GPU; destroy after the streams is safe
 CRC32C_MULTI_PIPELINE = 0x40  # multi plan: consecutive execs overlap; results complete after join()
+CRC32C_MULTI_PER_GROUP_RECV = 0x80  # multi plan (A/B): one send/recv pair per group range, no packed gather
 CRC32C_VERIFY_OVERLAP = 0x80000000  # bit 31 of a verify result's count: overlapping verify launches
 PATH_NONE, PATH_GPU, PATH_CPU = 0, 1, 2  # crc32c_last_path()
 
@@ -212,12 +213,14 @@ def _bind(L):
         "crc32c_multi_shard_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, vp, sz]),
         "crc32c_multi_rank_packets": (ctypes.c_int64, [vp, sz, u32, i32, i32, u32, vp, sz]),
         "crc32c_multi_transfers": (ctypes.c_int64, [vp, sz, u32, i32, u32, vp, vp, sz]),
+        "crc32c_multi_scatter": (ctypes.c_int64, [vp, sz, u32, i32, u32, vp, vp, sz]),
         "crc32c_multi_plan_create": (i32, [vp, vp, sz, u32, u32, pp]),
         "crc32c_multi_plan_exec": (i32, [vp, vp, vp, vp]),
         "crc32c_multi_plan_join": (i32, [vp, vp]),
         "crc32c_multi_plan_destroy": (i32, [vp]),
         "crc32c_multi_plan_nchecksums": (u64, [vp]),
         "crc32c_multi_plan_shard_bytes": (u64, [vp, i32]),
+        "crc32c_multi_plan_gather_ops": (u64, [vp, ctypes.POINTER(ctypes.c_int)]),
         "crc32c_parse_frames": (ctypes.c_int64, [vp, sz, vp, sz, ctypes.POINTER(u64)]),
         "crc32c_plan_exec_blocks": (i32, [vp, vp, vp, sz, vp]),
         "crc32c_blocks_create": (i32, [vp, u32, u32, pp]),
@@ -604,6 +607,13 @@ class MultiPlan:
     def shard_bytes(self, rank: int) -> int:
         return int(lib().crc32c_multi_plan_shard_bytes(self.handle, rank))
 
+    def gather_ops(self):
+        """crc32c_multi_plan_gather_ops: (point-to-point operations one exec
+        posts over the communicator, packed: staging array + scatter kernel)."""
+        packed = ctypes.c_int(0)
+        n = int(lib().crc32c_multi_plan_gather_ops(self.handle, ctypes.byref(packed)))
+        return n, bool(packed.value)
+
     def exec(self, dev_shards, root_out: int, streams=None) -> None:
         """``streams``: one per local device, handles or stream objects (kept
         alive until close(): the next exec on another stream records an event
@@ -682,6 +692,19 @@ def multi_transfers(pkts, group_packets: int, nranks: int, flags: int = 0):
     xs = np.zeros((max(n, 1), 4), np.uint64)
     lib().crc32c_multi_transfers(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, _np_ptr(ln), _np_ptr(xs), n)
     return ln, xs[:n]
+
+
+def multi_scatter(pkts, group_packets: int, nranks: int, flags: int = 0):
+    """crc32c_multi_scatter: the packed gather's layout -- (stage_off[nranks], tiles[T, 3] = {staging index,
+    file index, count}); T = 0 when the gather is not packed (one send / receive per placement)."""
+    pkts = as_packets(pkts)
+    n = int(lib().crc32c_multi_scatter(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, None, None, 0))
+    if n < 0:
+        _check(n, "crc32c_multi_scatter")
+    so = np.zeros(nranks, np.uint64)
+    ts = np.zeros((max(n, 1), 3), np.uint64)
+    lib().crc32c_multi_scatter(_np_ptr(pkts), pkts.size, group_packets, nranks, flags, _np_ptr(so), _np_ptr(ts), n)
+    return so, ts[:n]
 
 
 def verify_frames(frames: np.ndarray, bpc: int, chunk_offset: int, flags: int = 0, ctx: Context | None = None):

@@ -8,13 +8,20 @@
 // are the path's only exchange; no payload byte crosses GPUs.
 //
 // Rank 0 checksums its own groups straight into their final places; every
-// other rank checksums its groups into one local array and sends each group's
-// checksum range (merged where consecutive groups stay consecutive in file
-// order) with an ncclSend; rank 0 posts the matching ncclRecvs straight into
-// the groups' file-order places in its output -- no staging area, no copy
-// kernel.  (So a one-GPU communicator needs no transfer;
-// CRC32C_MULTI_SELF_SEND routes rank 0's own checksums through RCCL as well,
-// to exercise the transport on one GPU.)
+// other rank checksums its groups into one local array.  When each sender's
+// groups land in one file-order range (contiguous sharding, or N = 1), it
+// sends that range with one ncclSend and rank 0 receives it straight into
+// place.  When a sender's groups are spread over the file (round-robin
+// blocks: at N = 8 a rank's 4 blocks are 8 blocks apart), it still sends its
+// whole local array with ONE ncclSend, into a staging array on rank 0, and
+// one scatter kernel on rank 0 moves every group's range into file order:
+// point-to-point operations in one RCCL group are served one after another
+// per peer, each at a fixed cost (one GPU: a 16 MiB shard step 12.9 us with
+// one self-send, 34.7 us with four), so one operation
+// per peer plus a 1 MiB copy beats one per group.  CRC32C_MULTI_PER_GROUP_RECV
+// keeps one operation per group range (A/B).  (A one-GPU communicator needs
+// no transfer; CRC32C_MULTI_SELF_SEND routes rank 0's own checksums through
+// RCCL as well, to exercise the transport on one GPU.)
 //
 // Two ways to build the communicator: one process driving every device
 // (crc32c_multi_create, ncclCommInitAll) or one process per device
@@ -223,6 +230,62 @@ void build_transfers(const std::vector<Group> &groups, bool self_send, std::vect
     }
 }
 
+// The packed gather (one operation per sender): rank r's whole local array
+// lands at stage_off[r] of rank 0's staging array; the scatter kernel then
+// copies each group range into file order, in tiles of at most kScatterTile
+// checksums (one workgroup each).
+struct ScatterTile {
+    uint32_t src, dst, n, pad;
+};
+constexpr uint32_t kScatterTile = 1024;  // (4 per thread: one load round trip per workgroup)
+
+// true when some sender has more than one group range (placement) to send.
+bool wants_packed(const std::vector<Xfer> &xs) {
+    for (size_t k = 1; k < xs.size(); ++k)
+        for (size_t j = 0; j < k; ++j)
+            if (xs[j].rank == xs[k].rank) return true;
+    return false;
+}
+
+// Where each sender's local array lands in rank 0's staging array (rank
+// order); returns the staging array's length.
+uint64_t stage_offsets(const std::vector<uint64_t> &local_nout, bool self_send, std::vector<uint64_t> *stage_off) {
+    uint64_t n = 0;
+    stage_off->assign(local_nout.size(), 0);
+    for (size_t q = 0; q < local_nout.size(); ++q)
+        if (sends(int(q), self_send)) {
+            (*stage_off)[q] = n;
+            n += local_nout[q];
+        }
+    return n;
+}
+
+void build_scatter(const std::vector<Xfer> &xs, const std::vector<uint64_t> &stage_off,
+                   std::vector<ScatterTile> *tiles) {
+    tiles->clear();
+    for (const Xfer &x : xs)
+        for (uint64_t o = 0; o < x.count; o += kScatterTile)
+            tiles->push_back(ScatterTile{uint32_t(stage_off[size_t(x.rank)] + x.local + o), uint32_t(x.file + o),
+                                         uint32_t(std::min<uint64_t>(kScatterTile, x.count - o)), 0u});
+}
+
+__global__ __launch_bounds__(256) void hdfs_crc32c_gather_scatter(const uint32_t *__restrict__ stage,
+                                                                 uint32_t *__restrict__ out,
+                                                                 const ScatterTile *__restrict__ tiles) {
+    const ScatterTile t = tiles[blockIdx.x];
+    uint32_t v[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = threadIdx.x + 256u * j;
+        v[j] = k < t.n ? stage[t.src + k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t k = threadIdx.x + 256u * j;
+        if (k < t.n) out[t.dst + k] = v[j];
+    }
+}
+
 // The packets rank r's plan computes: payload offsets in its shard; out
 // indices in its local array, or the global ones when rank 0 works in place.
 void rank_plan_packets(const crc32c_packet *pkts, size_t npkts, uint32_t gp, const std::vector<Group> &groups, int r,
@@ -259,7 +322,15 @@ struct crc32c_multi_plan {
     std::vector<uint32_t *> d_local;     // per local device: its local array (none for rank 0 in place)
     uint64_t nchecksums = 0;
     bool self_send = false;
-    std::vector<Xfer> xfers;  // the gather's transfers, in posting order
+    std::vector<Xfer> xfers;  // the gather's placements (group ranges), in posting order
+    // packed gather: one send per sender of its whole local array into rank
+    // 0's staging array (stage_off per rank), then the scatter kernel
+    bool packed = false;
+    std::vector<uint64_t> stage_off;  // per rank (senders only)
+    uint64_t stage_n = 0;
+    uint32_t *d_stage = nullptr;       // on rank 0's device
+    ScatterTile *d_tiles = nullptr;    // on rank 0's device
+    uint32_t ntiles = 0;
     int root_local = -1;  // local device index of rank 0 (-1: not in this process)
     // Successive execs reuse d_local (an exec's sends read it while the next
     // exec's kernel rewrites it): per local device, the stream of the
@@ -328,12 +399,6 @@ int capture_id(hipStream_t s, uint64_t *id) {
     return 0;
 }
 
-// Records `e` on `s`.
-int record(hipEvent_t e, hipStream_t s) {
-    HIP_TRY(hipEventRecord(e, s));
-    return 0;
-}
-
 // The plan's exec streams of one local device follow the caller's stream
 // `s` into (or out of) a graph capture.  Entering one: they are drained by
 // the host first (they hold only work from before the capture), so no wait
@@ -355,6 +420,46 @@ int follow_capture(crc32c_multi_plan::Pipe &P, hipStream_t s) {
     return 0;
 }
 
+// One RCCL group of the gather, from every local device's local array
+// (src[i]) into root_out, on its stream -- per placement, or packed (one
+// operation per sender into the staging array) -- then, packed, the scatter
+// kernel on rank 0's stream.
+int post_gather(crc32c_multi_plan *mp, const std::vector<const uint32_t *> &src, uint32_t *root_out,
+                void *const *streams) {
+    crc32c_multi *m = mp->m;
+    NCCL_TRY(rccl().GroupStart());
+    ncclResult_t r = ncclSuccess;
+    for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
+        const hipStream_t s = local_stream(m, i, streams);
+        const int me = m->ranks[i];
+        if (mp->packed) {
+            if (sends(me, mp->self_send) && mp->local_nout[size_t(me)])
+                r = rccl().Send(src[i], mp->local_nout[size_t(me)], ncclUint32, 0, m->comms[i], s);
+            for (int q = 0; me == 0 && q < m->nranks && r == ncclSuccess; ++q)
+                if (sends(q, mp->self_send) && mp->local_nout[size_t(q)])
+                    r = rccl().Recv(mp->d_stage + mp->stage_off[size_t(q)], mp->local_nout[size_t(q)], ncclUint32, q,
+                                    m->comms[i], s);
+            continue;
+        }
+        for (const Xfer &x : mp->xfers) {
+            if (r != ncclSuccess) break;
+            if (x.rank == me) r = rccl().Send(src[i] + x.local, x.count, ncclUint32, 0, m->comms[i], s);
+            if (me == 0 && r == ncclSuccess) r = rccl().Recv(root_out + x.file, x.count, ncclUint32, x.rank, m->comms[i], s);
+        }
+    }
+    const ncclResult_t e = rccl().GroupEnd();
+    NCCL_TRY(r);
+    NCCL_TRY(e);
+    if (mp->packed && mp->root_local >= 0 && mp->ntiles) {
+        const size_t i = size_t(mp->root_local);
+        DeviceGuard guard(m->ctxs[i]->device);
+        hipLaunchKernelGGL(hdfs_crc32c_gather_scatter, dim3(mp->ntiles), dim3(256), 0, local_stream(m, i, streams),
+                           mp->d_stage, root_out, mp->d_tiles);
+        HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
 // The gather of the exec that used local arrays b, into root_out: on every
 // local device's caller stream, after that exec's launch (an event wait),
 // one RCCL group (the same transfers as an ordinary exec's).
@@ -368,22 +473,9 @@ int issue_gather(crc32c_multi_plan *mp, uint32_t b, uint32_t *root_out, void *co
         if (int rc = follow_capture(P, s)) return rc;
         if (P.kern_rec[b]) HIP_TRY(hipStreamWaitEvent(s, P.kern[b], 0));
     }
-    NCCL_TRY(rccl().GroupStart());
-    ncclResult_t r = ncclSuccess;
-    for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
-        const hipStream_t s = local_stream(m, i, streams);
-        const int me = m->ranks[i];
-        const uint32_t *src = b ? mp->d_local2[i] : mp->d_local[i];
-        for (const Xfer &x : mp->xfers) {
-            if (r != ncclSuccess) break;
-            if (x.rank == me) r = rccl().Send(src + x.local, x.count, ncclUint32, 0, m->comms[i], s);
-            if (me == 0 && r == ncclSuccess) r = rccl().Recv(root_out + x.file, x.count, ncclUint32, x.rank, m->comms[i], s);
-        }
-    }
-    const ncclResult_t e = rccl().GroupEnd();
-    NCCL_TRY(r);
-    NCCL_TRY(e);
-    return 0;
+    std::vector<const uint32_t *> src(m->ctxs.size());
+    for (size_t i = 0; i < m->ctxs.size(); ++i) src[i] = b ? mp->d_local2[i] : mp->d_local[i];
+    return post_gather(mp, src, root_out, streams);
 }
 
 // One pipelined exec (CRC32C_MULTI_PIPELINE; see crc32c_multi_plan_exec).
@@ -566,6 +658,29 @@ int64_t crc32c_multi_transfers(const crc32c_packet *pkts, size_t npkts, uint32_t
     return int64_t(xs.size());
 }
 
+int64_t crc32c_multi_scatter(const crc32c_packet *pkts, size_t npkts, uint32_t group_packets, int nranks,
+                             uint32_t flags, uint64_t *stage_off, uint64_t *tiles, size_t cap) {
+    std::vector<Group> groups;
+    std::vector<uint64_t> sb, ln;
+    if (int rc = build_layout(pkts, npkts, group_packets, nranks, &groups, &sb, &ln)) return rc;
+    const bool self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
+    std::vector<Xfer> xs;
+    build_transfers(groups, self_send, &xs);
+    for (int r = 0; stage_off && r < nranks; ++r) stage_off[r] = 0;
+    if ((flags & CRC32C_MULTI_PER_GROUP_RECV) || !wants_packed(xs)) return 0;
+    std::vector<uint64_t> so;
+    stage_offsets(ln, self_send, &so);
+    if (stage_off) std::copy(so.begin(), so.end(), stage_off);
+    std::vector<ScatterTile> ts;
+    build_scatter(xs, so, &ts);
+    for (size_t k = 0; tiles && k < std::min(cap, ts.size()); ++k) {
+        tiles[3 * k] = ts[k].src;
+        tiles[3 * k + 1] = ts[k].dst;
+        tiles[3 * k + 2] = ts[k].n;
+    }
+    return int64_t(ts.size());
+}
+
 int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t npkts, uint32_t group_packets,
                              uint32_t flags, crc32c_multi_plan **out) {
     if (!m || !out) return fail(-EINVAL, "multi/out == NULL");
@@ -592,7 +707,8 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
     }
     mp->self_send = (flags & CRC32C_MULTI_SELF_SEND) != 0;
     mp->pipeline = (flags & CRC32C_MULTI_PIPELINE) != 0;
-    flags &= ~(CRC32C_MULTI_SELF_SEND | CRC32C_MULTI_PIPELINE);
+    const bool per_group = (flags & CRC32C_MULTI_PER_GROUP_RECV) != 0;
+    flags &= ~(CRC32C_MULTI_SELF_SEND | CRC32C_MULTI_PIPELINE | CRC32C_MULTI_PER_GROUP_RECV);
     if (int rc = build_layout(pkts, npkts, group_packets, m->nranks, &mp->groups, &mp->shard_bytes, &mp->local_nout))
         return rc;
     for (const Group &G : mp->groups) mp->nchecksums = std::max(mp->nchecksums, G.omin + G.n);
@@ -631,14 +747,38 @@ int crc32c_multi_plan_create(crc32c_multi *m, const crc32c_packet *pkts, size_t 
     }
     build_transfers(mp->groups, mp->self_send, &mp->xfers);
     if (mp->nchecksums > UINT32_MAX) return fail(-E2BIG, "too many checksums");
-    // (every transfer is one ncclSend / ncclRecv of the exec's one RCCL
-    // group: bounded, so a tiny group_packets cannot post thousands of
-    // point-to-point operations per exec)
-    if (mp->xfers.size() > kMaxGatherTransfers)
+    mp->packed = !per_group && wants_packed(mp->xfers);
+    // (per placement, every transfer is one ncclSend / ncclRecv of the exec's
+    // one RCCL group: bounded, so a tiny group_packets cannot post thousands
+    // of point-to-point operations per exec)
+    if (!mp->packed && mp->xfers.size() > kMaxGatherTransfers)
         return fail(-E2BIG, "%zu gather transfers (at most %zu): use a larger group_packets", mp->xfers.size(),
                     kMaxGatherTransfers);
+    if (mp->packed) {
+        mp->stage_n = stage_offsets(mp->local_nout, mp->self_send, &mp->stage_off);
+        if (mp->root_local >= 0) {
+            std::vector<ScatterTile> tiles;
+            build_scatter(mp->xfers, mp->stage_off, &tiles);
+            if (tiles.size() > 0x7fffffffu) return fail(-E2BIG, "too many scatter tiles");
+            mp->ntiles = uint32_t(tiles.size());
+            DeviceGuard guard(m->ctxs[size_t(mp->root_local)]->device);
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_stage), std::max<uint64_t>(mp->stage_n, 1) * 4));
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&mp->d_tiles),
+                              std::max<size_t>(tiles.size(), 1) * sizeof(ScatterTile)));
+            HIP_TRY(hipMemcpy(mp->d_tiles, tiles.data(), tiles.size() * sizeof(ScatterTile), hipMemcpyHostToDevice));
+        }
+    }
     *out = mp.release();
     return 0;
+}
+
+uint64_t crc32c_multi_plan_gather_ops(const crc32c_multi_plan *mp, int *packed) {
+    if (packed) *packed = mp ? int(mp->packed) : 0;
+    if (!mp) return 0;
+    if (!mp->packed) return 2 * uint64_t(mp->xfers.size());
+    uint64_t senders = 0;
+    for (int q = 0; q < mp->m->nranks; ++q) senders += sends(q, mp->self_send) && mp->local_nout[size_t(q)] ? 1 : 0;
+    return 2 * senders;
 }
 
 uint64_t crc32c_multi_plan_nchecksums(const crc32c_multi_plan *mp) { return mp ? mp->nchecksums : 0; }
@@ -677,22 +817,8 @@ int crc32c_multi_plan_exec(crc32c_multi_plan *mp, const void *const *dev_shards,
     //    from its local array, rank 0's receives straight into file order
     if (mp->xfers.empty()) return 0;
     if (int rc = ensure_comms(m)) return rc;
-    NCCL_TRY(rccl().GroupStart());
-    ncclResult_t r = ncclSuccess;
-    for (size_t i = 0; i < m->ctxs.size() && r == ncclSuccess; ++i) {
-        const hipStream_t s = local_stream(m, i, streams);
-        const int me = m->ranks[i];
-        for (const Xfer &x : mp->xfers) {
-            if (r != ncclSuccess) break;
-            if (x.rank == me) r = rccl().Send(mp->d_local[i] + x.local, x.count, ncclUint32, 0, m->comms[i], s);
-            if (me == 0 && r == ncclSuccess)
-                r = rccl().Recv(root_out + x.file, x.count, ncclUint32, x.rank, m->comms[i], s);
-        }
-    }
-    const ncclResult_t e = rccl().GroupEnd();
-    NCCL_TRY(r);
-    NCCL_TRY(e);
-    return 0;
+    std::vector<const uint32_t *> src(mp->d_local.begin(), mp->d_local.end());
+    return post_gather(mp, src, root_out, streams);
 }
 
 int crc32c_multi_plan_join(crc32c_multi_plan *mp, void *const *streams) {
@@ -743,6 +869,11 @@ int crc32c_multi_plan_destroy(crc32c_multi_plan *mp) {
         DeviceGuard guard(mp->m->ctxs[i]->device);
         if (i < mp->d_local.size() && mp->d_local[i]) (void)hipFree(mp->d_local[i]);
         if (i < mp->d_local2.size() && mp->d_local2[i]) (void)hipFree(mp->d_local2[i]);
+    }
+    if (mp->root_local >= 0 && (mp->d_stage || mp->d_tiles)) {
+        DeviceGuard guard(mp->m->ctxs[size_t(mp->root_local)]->device);
+        if (mp->d_stage) (void)hipFree(mp->d_stage);
+        if (mp->d_tiles) (void)hipFree(mp->d_tiles);
     }
     for (size_t i = 0; i < mp->pipes.size(); ++i) {
         crc32c_multi_plan::Pipe &P = mp->pipes[i];

@@ -2,14 +2,15 @@
 
 The multi-GPU plan deals a file's blocks (groups of
 consecutive packets) round-robin over the ranks; each rank checksums its
-shard into one local u32 array and sends each group's range, and rank 0
-receives every range straight into its file-order place -- the path's only
-exchange.  Every part of that exchange that only N > 1 reaches is the
-library's own code here: each rank's shard and the packets its plan
-computes (payload offsets into the shard, out indices into its local array)
-come from crc32c_multi_layout / crc32c_multi_rank_packets, and the transfer
-list both sides post from crc32c_multi_transfers -- the same host code
-crc32c_multi_plan_create builds its exec from.  The checksums themselves come from the oracle
+shard into one local u32 array and sends it to rank 0 -- whole, into a
+staging array that rank 0 scatters into file order (the packed gather, when
+a sender has several group ranges), or range by range straight into place
+-- the path's only exchange.  Every part of that exchange that only N > 1
+reaches is the library's own code here: each rank's shard and the packets
+its plan computes (payload offsets into the shard, out indices into its
+local array) come from crc32c_multi_layout / crc32c_multi_rank_packets, and
+what both sides post from crc32c_multi_transfers / crc32c_multi_scatter --
+the same host code crc32c_multi_plan_create builds its exec from.  The checksums themselves come from the oracle
 (the GPU ranks run the HIP kernel); the transfers are gloo send / receive in
 place of RCCL's.  Rank 0's assembled array must equal the reference's golden
 digest of config 4's 128 MiB file, or the oracle over the whole file, bit for
@@ -31,6 +32,7 @@ from conftest import GOLDEN, load_package
 PKTS_PER_BLOCK = 4  # 256 KiB blocks keep the CPU oracle fast; the layout is size-independent
 PKT = 65536
 SELF_SEND = 0x10  # CRC32C_MULTI_SELF_SEND
+PER_GROUP = 0x80  # CRC32C_MULTI_PER_GROUP_RECV
 
 
 def _free_port() -> int:
@@ -118,7 +120,7 @@ def _worker(rank: int, world: int, port: int, case: tuple, flags: int, result_pa
 
 
 @pytest.mark.parametrize("world,case,flags", [
-    (2, ("c4",), 0), (3, ("c4",), 0), (8, ("c4",), 0), (8, ("c4",), SELF_SEND),
+    (2, ("c4",), 0), (3, ("c4",), 0), (8, ("c4",), 0), (8, ("c4",), SELF_SEND), (8, ("c4",), PER_GROUP),
     (2, ("f", 7, 512, False), 0), (2, ("f", 2, 4096, True), SELF_SEND), (3, ("f", 8, 512, True), 0),
     (2, ("f", 1, 512, False), 0), (3, ("f", 5, 1536, True), 0), (3, ("f", 5, 1536, True), SELF_SEND),
     (8, ("f", 11, 512, True), 0)])
@@ -166,6 +168,36 @@ def test_transfers_shape():
     assert list(ln) == [262144] and xs.tolist() == [[0, 0, 0, 262144]]
     ln, xs = shard.transfers(pk, 64, 1)
     assert list(ln) == [0] and xs.shape == (0, 4)
+
+
+def test_packed_gather_layout():
+    """crc32c_multi_scatter on config 4 at 8 ranks: each of the 7 senders has
+    4 placements 8 blocks apart, so the gather is packed -- rank r's whole
+    128 KiB local array lands at staging index 32768 (r - 1), and 224 tiles
+    of 1024 checksums copy every block into its file place, covering the
+    file's peer blocks exactly once; with CRC32C_MULTI_SELF_SEND rank 0's
+    array comes first.  Not packed: one placement per sender (N = 1
+    self-send, or groups of 8 blocks at N = 4), or CRC32C_MULTI_PER_GROUP_RECV."""
+    hdfs = load_package()
+    hdfs.lib()
+    import oracle
+    from hdfs_crc32c_amd import shard
+
+    pk = oracle.uniform_packets(2048, 65536, 512)
+    so, ts = shard.scatter(pk, 64, 8)
+    assert list(so) == [0] + [32768 * (r - 1) for r in range(1, 8)]
+    assert ts.shape == (224, 3) and set(ts[:, 2]) == {1024}
+    seen = np.zeros(2048 * 128, np.int32)
+    for src, dst, n in ts.astype(np.int64):
+        seen[dst:dst + n] += 1
+        g = dst // 8192  # block g of rank g % 8: its local index (g // 8) * 8192 + (dst % 8192)
+        assert src == 32768 * (g % 8 - 1) + (g // 8) * 8192 + dst % 8192
+    assert np.array_equal(seen.reshape(32, 8192).max(axis=1), np.array([0 if g % 8 == 0 else 1 for g in range(32)]))
+    so, ts = shard.scatter(pk, 64, 8, SELF_SEND)
+    assert list(so) == [32768 * r for r in range(8)] and ts.shape == (256, 3)
+    assert shard.scatter(pk, 64, 8, PER_GROUP)[1].shape == (0, 3)
+    assert shard.scatter(pk, 64, 1, SELF_SEND)[1].shape == (0, 3)
+    assert shard.scatter(pk, 512, 4)[1].shape == (0, 3)  # (group g on rank g: one range each)
 
 
 def test_layout_helpers():

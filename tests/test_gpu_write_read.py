@@ -386,17 +386,19 @@ def test_multi_plan_config4_rccl_gather(hdfs, golden, orc, self_send):
     m.close()
 
 
-def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc):
-    """several point-to-point transfers from ONE sender inside one
-    RCCL group, eagerly and graph-captured.  A file of 12 groups whose
-    checksum ranges leave gaps between groups (out_idx of group g starts at
-    g (n + 37)): the sender's local array is dense, the file-order places are
-    not, so no two transfers merge -- 12 ncclSend / ncclRecv pairs to self
-    (CRC32C_MULTI_SELF_SEND) match in posting order.  Every group's checksums
-    land in place, the gaps keep their sentinel, also after the stream
-    switches and in two graph replays; a second stream object freed before
-    the switch is kept alive by the plan (the next exec records an event on
-    it)."""
+@pytest.mark.parametrize("per_group", [False, True], ids=["packed", "per_group"])
+def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc, per_group):
+    """ONE sender with several group ranges to place, eagerly and
+    graph-captured.  A file of 12 groups whose checksum ranges leave gaps
+    between groups (out_idx of group g starts at g (n + 37)): the sender's
+    local array is dense, the file-order places are not, so no two
+    placements merge.  Packed (the default): one ncclSend / ncclRecv pair to
+    self (CRC32C_MULTI_SELF_SEND) into the plan's staging array, then the
+    scatter kernel; per group (CRC32C_MULTI_PER_GROUP_RECV): 12 pairs, matched
+    in posting order, straight into place.  Every group's checksums land in
+    place, the gaps keep their sentinel, also after the stream switches and
+    in two graph replays; a second stream object freed before the switch is
+    kept alive by the plan (the next exec records an event on it)."""
     import gc
 
     torch = _torch()
@@ -412,8 +414,9 @@ def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc):
     want_idx = np.concatenate([np.arange(g * (per + gap), g * (per + gap) + per) for g in range(ngroups)])
     want[want_idx] = orc.batch(payload, pk, total)[want_idx]
     m = hdfs.Multi([0])
-    mp = m.plan(pk, gp, hdfs.CRC32C_MULTI_SELF_SEND)
+    mp = m.plan(pk, gp, hdfs.CRC32C_MULTI_SELF_SEND | (hdfs.CRC32C_MULTI_PER_GROUP_RECV if per_group else 0))
     assert mp.nchecksums == total
+    assert mp.gather_ops() == ((2 * ngroups, False) if per_group else (2, True))
     layout, sb = hdfs.multi_layout(pk, gp, 1)
     host = np.zeros(int(sb[0]) + 16, np.uint8)
     for _, soff, poff, nbytes in layout.astype(np.int64):
@@ -449,7 +452,7 @@ def test_multi_plan_self_send_several_transfers_per_peer(hdfs, orc):
     m.close()
 
 
-@pytest.mark.parametrize("self_send", [False, True])
+@pytest.mark.parametrize("self_send", [False, True, "packed"])
 def test_multi_plan_pipelined(hdfs, orc, self_send):
     """CRC32C_MULTI_PIPELINE: consecutive execs overlap (two exec streams, two
     local arrays, the gather on the plan's comm stream); after
@@ -459,13 +462,18 @@ def test_multi_plan_pipelined(hdfs, orc, self_send):
     order: the last file's checksums win), and captured into a graph with
     the join inside the capture, replayed twice.  With
     CRC32C_MULTI_SELF_SEND every exec's checksums also travel through the
-    RCCL group on the comm stream."""
+    RCCL group on the comm stream; "packed": the groups' checksum ranges 37
+    apart in the file, so the gather is packed (staging array + scatter
+    kernel on the caller's stream)."""
     torch = _torch()
     gp, nfiles = 4, 4
     pk = oracle.uniform_packets(8 * gp)  # 8 blocks of 4 packets (2 MiB files)
+    if self_send == "packed":
+        pk["out_idx"] = np.array([(i // gp) * (gp * 128 + 37) + (i % gp) * 128 for i in range(pk.size)], np.uint64)
     flags = hdfs.CRC32C_MULTI_PIPELINE | (hdfs.CRC32C_MULTI_SELF_SEND if self_send else 0)
     m = hdfs.Multi([0])
     mp = m.plan(pk, gp, flags)
+    assert mp.gather_ops() == ((2, True) if self_send == "packed" else (2 if self_send else 0, False))
     layout, sb = hdfs.multi_layout(pk, gp, 1)
     shards, wants = [], []
     for f in range(nfiles):
@@ -513,18 +521,39 @@ def test_multi_plan_pipelined(hdfs, orc, self_send):
     m.close()
 
 
-def test_multi_plan_refuses_too_many_gather_transfers(hdfs):
-    """A gather of more than 4096 point-to-point transfers in one RCCL group
-    (here 4100 one-packet groups whose checksum ranges leave gaps, sent to
-    self) is refused at plan creation with -E2BIG instead of being posted."""
+def test_multi_plan_refuses_too_many_gather_transfers(hdfs, orc):
+    """Per group (CRC32C_MULTI_PER_GROUP_RECV), a gather of more than 4096
+    point-to-point transfers in one RCCL group (here 4100 one-packet groups
+    whose checksum ranges leave gaps, sent to self) is refused at plan
+    creation with -E2BIG instead of being posted.  Packed (the default), the
+    same plan posts one pair and its scatter kernel places all 4100 ranges:
+    bit-exact, gaps untouched."""
+    torch = _torch()
     pk = oracle.uniform_packets(4100, 512, 512)
     pk["out_idx"] = np.arange(4100, dtype=np.uint64) * 2  # (a gap after every group)
     m = hdfs.Multi([0])
+    per_group = hdfs.CRC32C_MULTI_SELF_SEND | hdfs.CRC32C_MULTI_PER_GROUP_RECV
     try:
         with pytest.raises(hdfs.Crc32cError) as e:
-            m.plan(pk, 1, hdfs.CRC32C_MULTI_SELF_SEND)
+            m.plan(pk, 1, per_group)
         assert e.value.rc == -7 and "group_packets" in str(e.value)  # -E2BIG
-        m.plan(pk[:4000], 1, hdfs.CRC32C_MULTI_SELF_SEND).close()  # (4000 transfers: accepted)
+        m.plan(pk[:4000], 1, per_group).close()  # (4000 transfers: accepted)
+        mp = m.plan(pk, 1, hdfs.CRC32C_MULTI_SELF_SEND)
+        assert mp.gather_ops() == (2, True)
+        payload = oracle.xorshift64_bytes(4100 * 512 + 16, 516)
+        layout, sb = hdfs.multi_layout(pk, 1, 1)
+        host = np.zeros(int(sb[0]) + 16, np.uint8)
+        for _, soff, poff, nbytes in layout.astype(np.int64):
+            host[soff:soff + nbytes] = payload[poff:poff + nbytes]
+        shard = torch.from_numpy(host).cuda()
+        out = torch.full((2 * 4100,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        mp.exec([shard.data_ptr()], out.data_ptr())
+        m.sync()
+        want = np.full(2 * 4100, 0x5A5A5A5A, np.uint32)
+        want[0::2] = orc.batch(payload, pk, 2 * 4100)[0::2]
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        mp.close()
     finally:
         m.close()
 

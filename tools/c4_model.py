@@ -17,9 +17,12 @@ per step (HIP events on the launch stream, 1000 steps after 200 warm-up):
                                scatter kernel -- a lower bound for one peer's
                                gather at N = 8;
   multi_self_send_4x        -- the same with the shard's four groups placed
-                               apart in the output (four 32 KiB transfers,
-                               as one peer's at N = 8, where its 4 blocks
-                               are 8 blocks apart in file order).
+                               apart in the output (four 32 KiB ranges, as
+                               one peer's at N = 8, where its 4 blocks are 8
+                               blocks apart in file order): packed (one
+                               send/recv pair into the staging array, then
+                               the scatter kernel) and _per_group (four
+                               pairs, CRC32C_MULTI_PER_GROUP_RECV).
 
 Each multi step is also captured (kernel + RCCL group) into a graph of 100
 steps and replayed (*_graph_us), as bench.py replays config 4's steps.
@@ -98,13 +101,15 @@ def main():
     out4 = torch.zeros(4 * (64 * 128 + gap), dtype=torch.int32, device=dev)
     for name, flags, pkm, o in (("multi_in_place", 0, pk, out),
                                 ("multi_self_send", hdfs.CRC32C_MULTI_SELF_SEND, pk, out),
-                                ("multi_self_send_4x", hdfs.CRC32C_MULTI_SELF_SEND, pk4, out4)):
+                                ("multi_self_send_4x", hdfs.CRC32C_MULTI_SELF_SEND, pk4, out4),
+                                ("multi_self_send_4x_per_group",
+                                 hdfs.CRC32C_MULTI_SELF_SEND | hdfs.CRC32C_MULTI_PER_GROUP_RECV, pk4, out4)):
         m = hdfs.Multi([0])
         mp = m.plan(pkm, 64, flags)
-        if name.endswith("_4x"):
-            res[name + "_transfers"] = int(hdfs.multi_transfers(pkm, 64, 1, flags)[1].shape[0])
+        if "_4x" in name:
+            res[name + "_gather_ops"] = list(mp.gather_ops())
         res[name + "_us"] = round(timed(lambda: mp.exec([payload.data_ptr()], o.data_ptr(), [stream.cuda_stream])), 3)
-        if name.endswith("_4x"):
+        if "_4x" in name:
             got = o.cpu().numpy().reshape(4, -1)[:, :64 * 128].reshape(-1)
             res[name + "_exact"] = bool(np.array_equal(got, out.cpu().numpy()))
         # the whole step (kernel + RCCL group) captured 100 times into one graph
@@ -185,7 +190,7 @@ def main():
         res["gather_lower_bound_graph_us"] = round(res["multi_self_send_graph_us"] - res["shard_graph_us"], 3)
         res["model_step_n8_graph_us"] = res["multi_self_send_graph_us"]
         res["model_value_n8_graph_gib_s"] = round(32 * (4 << 20) / (res["multi_self_send_graph_us"] * 1e-6) / 2**30, 1)
-    if "multi_self_send_4x_graph_us" in res:  # the same with one N = 8 peer's four transfers
+    if "multi_self_send_4x_graph_us" in res:  # the same with one N = 8 peer's four ranges (packed)
         res["model_step_n8_graph_4x_us"] = res["multi_self_send_4x_graph_us"]
     print(json.dumps(res), flush=True)
     ctx.close()
