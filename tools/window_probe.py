@@ -15,7 +15,10 @@ times, on one GPU, the host-side pieces of that window:
   launch_spin_us     -- the same, completion seen by spinning on an event;
   k20_sync / k20_spin -- bench-like windows of 20 launches (4 host-issued +
                         a graph of 16) ended by synchronize / by an event
-                        spin, host clock per step, beside the GPU window.
+                        spin, host clock per step, beside the GPU window;
+  lead_pos_us / graph16_us_per_step -- GPU time of each of the four
+                        host-issued lead steps (events between them) and
+                        per step of the graph of 16 after them.
 
 Prints one JSON line."""
 from __future__ import annotations
@@ -132,6 +135,26 @@ def main():
         res["k20_%s_host_us_per_step" % mode] = med(hs)
         res["k20_%s_gpu_us_per_step" % mode] = med(ws)
         res["k20_%s_gap_us_total" % mode] = round((med(hs) - med(ws)) * 20, 2)
+    # per-position GPU time inside a bench-like window: events between the
+    # four host-issued lead launches, then the graph of 16
+    pos = [[] for _ in range(6)]
+    for rep in range(30):
+        for i in range(200):
+            step(i)
+        torch.cuda.synchronize()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        evs[0].record(stream)
+        for i in range(4):
+            step(i)
+            evs[i + 1].record(stream)
+        g.replay()
+        evs[5].record(stream)
+        torch.cuda.synchronize()
+        for k in range(4):
+            pos[k].append(evs[k].elapsed_time(evs[k + 1]) * 1e3)
+        pos[5].append(evs[4].elapsed_time(evs[5]) * 1e3 / 16)
+    res["lead_pos_us"] = [med(pos[k]) for k in range(4)]
+    res["graph16_us_per_step"] = med(pos[5])
     print(json.dumps(res))
 
 
