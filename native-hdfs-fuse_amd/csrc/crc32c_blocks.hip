@@ -411,6 +411,10 @@ int crc32c_blocks_create_resident(crc32c_plan *plan, uint32_t idle_us, crc32c_bl
     std::unique_ptr<crc32c_blocks> q(new crc32c_blocks);
     q->plan = plan;
     q->device = plan->ctx->device;
+    {
+        DeviceGuard guard(q->device);
+        HIP_TRY(resident_preload_product());
+    }
     if (int rc = resident_create(plan, idle_us, resident_launch_product, false, &q->res, resident_launch_product_general))
         return rc;
     *out = q.release();

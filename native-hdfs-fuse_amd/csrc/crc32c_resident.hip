@@ -143,6 +143,15 @@ hipError_t resident_launch_product_general(const RParams &p, uint32_t grid, hipS
     hipLaunchKernelGGL((resident_kernel<16, 7, 2, true>), dim3(grid), dim3(16 * 64), 0, stream, p);
     return hipGetLastError();
 }
+// Loads both builds' code onto the current device now (HIP loads a code
+// object at its first use), so the queue's first blocks do not pay for it.
+hipError_t resident_preload_product() {
+    hipFuncAttributes a;
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&resident_kernel<16, 7, 2, false>));
+    if (e == hipSuccess)
+        e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&resident_kernel<16, 7, 2, true>));
+    return e;
+}
 
 namespace {
 

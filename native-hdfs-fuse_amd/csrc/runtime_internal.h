@@ -263,5 +263,6 @@ int resident_destroy(ResidentEngine *r, bool drain);
 // its aligned-only and general builds.
 hipError_t resident_launch_product(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
 hipError_t resident_launch_product_general(const hdfs_crc_res::RParams &p, uint32_t grid, hipStream_t stream);
+hipError_t resident_preload_product();
 
 }  // namespace hdfs_crc
