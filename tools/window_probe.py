@@ -18,7 +18,9 @@ times, on one GPU, the host-side pieces of that window:
                         spin, host clock per step, beside the GPU window;
   lead_pos_us / graph16_us_per_step -- GPU time of each of the four
                         host-issued lead steps (events between them) and
-                        per step of the graph of 16 after them.
+                        per step of the graph of 16 after them;
+  ab_host16 / ab_graph16 -- after 4 host-issued steps, 16 more host-issued
+                        back to back against the graph of 16 (interleaved).
 
 Prints one JSON line."""
 from __future__ import annotations
@@ -155,6 +157,29 @@ def main():
         pos[5].append(evs[4].elapsed_time(evs[5]) * 1e3 / 16)
     res["lead_pos_us"] = [med(pos[k]) for k in range(4)]
     res["graph16_us_per_step"] = med(pos[5])
+    # 16 steps host-issued back to back against the graph of 16, after the
+    # same 4 host-issued steps, interleaved (per step, GPU time)
+    ab = {"host16": [], "graph16": []}
+    for rep in range(40):
+        for mode in ("host16", "graph16") if rep % 2 else ("graph16", "host16"):
+            for i in range(200):
+                step(i)
+            torch.cuda.synchronize()
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            for i in range(4):
+                step(i)
+            e0.record(stream)
+            if mode == "graph16":
+                g.replay()
+            else:
+                for i in range(4, 20):
+                    step(i)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ab[mode].append(e0.elapsed_time(e1) * 1e3 / 16)
+    res["ab_host16_us_per_step"] = med(ab["host16"])
+    res["ab_graph16_us_per_step"] = med(ab["graph16"])
     print(json.dumps(res))
 
 
