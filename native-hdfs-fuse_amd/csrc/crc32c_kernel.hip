@@ -112,4 +112,14 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     return hipGetLastError();
 }
 
+// Loads this file's code object (every build above) onto the current
+// device: HIP loads it at its first use, which would otherwise land in the
+// process's first checksum call (1.2-2.2 ms against 16 us,
+// tools/first_call_probe.py).  crc32c_ctx_create calls it.
+hipError_t preload_plan_kernels() {
+    using namespace hdfs_crc_dev;
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(&hdfs_crc32c_plan_kernel<768, 3, kModeS4 | kModeNt>));
+}
+
 }  // namespace hdfs_crc

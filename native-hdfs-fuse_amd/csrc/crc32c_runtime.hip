@@ -953,6 +953,7 @@ int crc32c_ctx_create(int device, crc32c_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
         return fail(-ENODEV, "device %d is %s; this library is built for gfx950 (MI355X)", device, prop.gcnArchName);
     c->num_cu = prop.multiProcessorCount;
+    HIP_TRY(preload_plan_kernels());
     c->host_pool.pinned = true;
     HIP_TRY(hipStreamCreateWithFlags(&c->upload_stream, hipStreamNonBlocking));
     for (int ty = 0; ty < 2; ++ty) {

@@ -135,5 +135,7 @@ inline void init_sched_slots(uint32_t *w) {
 // `grid` (optional): the workgroups launched.
 hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop = nullptr,
                               uint32_t *grid = nullptr);
+// Loads the production kernels' code object onto the current device.
+hipError_t preload_plan_kernels();
 
 }  // namespace hdfs_crc
