@@ -19,7 +19,10 @@
 //   * the same with quarter units (each tile split over 4 waves, 2 pieces
 //     per lane): batches of at most kQuarterTilesPerCu tiles per CU, where
 //     one wave's load -> lookups chain is the launch (one 4 MiB block,
-//     graph-replayed: 4.36 -> 3.71 us);
+//     graph-replayed: 4.36 -> 3.71 us); up to kEarlyTilesPerCu tiles per
+//     CU with the first unit's loads issued before the table staging (their
+//     latencies overlap: one 4 MiB block 3.71-3.74 -> 3.57 us; at 3 tiles
+//     per CU the staging queues behind them, 4.16-4.22 -> 4.41-4.46, round 6);
 //   * full image with the general-tile code and half tiles (bpc <= 256,
 //     513..768 and 1025..1280), with and without the shifted loads, for any batch holding
 //     half tiles (compiled into the builds above, their code cost those
@@ -44,6 +47,11 @@ constexpr uint64_t kSmallBatchItemsPerCu = 16;
 // profiles/r02/launch_probe_crossover.json: 512 tiles 3.71 vs 4.36 us, 768
 // tiles 4.24 vs 4.72, 1024 tiles 5.56 vs 4.95).
 constexpr uint64_t kQuarterTilesPerCu = 3;
+// Tiles per CU up to which the quarter-unit build issues the first unit's
+// loads before the table staging (tools/launch_probe.py, debug variants 82 /
+// 83, profiles/r06/early/: 512 tiles 3.57 vs 3.71-3.74 us, 768 tiles
+// 4.41-4.46 vs 4.16-4.22).
+constexpr uint64_t kEarlyTilesPerCu = 2;
 }  // namespace
 
 hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop,
@@ -59,6 +67,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     // builds: their code in the small-batch builds cost config 3 ~4 %)
     const bool small = !half && !(p.general & kGeneralPadded) && items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
+    const bool early = quarter && p.ntiles <= kEarlyTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
     if (grid) *grid = g.x;
 #define LAUNCH(K)                                                                  \
@@ -78,6 +87,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeHalfT | kModeVerify>));
         else if (half)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT | kModeVerify>));
+        else if (early)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly | kModeVerify>));
         else if (quarter)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>));
         else if (small)
@@ -95,6 +106,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeHalfT>));
         else if (half)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT>));
+        else if (early)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly>));
         else if (quarter)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>));
         else if (small)

@@ -77,6 +77,10 @@ constexpr Variant kVariants[] = {
     // issued right after the staging's, before the barrier; stamped twin
     {80, "s4_nt_pow2only_ovl_prodgrid", 768, 1, true, true},
     {81, "s4_nt_pow2only_ovl_stamps_prodgrid", 768, 1, true, true},
+    // (round 6) the production quarter-unit build (no padded tiles), and the
+    // same with the first unit's loads issued before the table staging
+    {82, "s4c_nt_quarter_nopad_prodgrid", 768, 1, true, true},
+    {83, "s4c_nt_quarter_nopad_early_prodgrid", 768, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -90,12 +94,18 @@ const Variant *find(int v) {
 hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
-    const uint32_t units = (v.id >= 51 && v.id <= 55) ? 4u : (v.id == 60 || v.id == 61) ? 2u : 1u;
+    const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83) ? 4u
+                           : (v.id == 60 || v.id == 61)                           ? 2u
+                                                                                  : 1u;
     uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, units) : (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{v.threads, 1, 1};
+    // (82 / 83 leave the padded- and half-tile code out, as the production
+    // small-batch builds do: plans with such tiles are refused)
+    if ((v.id == 82 || v.id == 83) && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
+        return hipErrorInvalidValue;
     switch (v.id) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
     case 2: HDFS_LAUNCH(1024, 4, kS4Nt); break;
@@ -136,6 +146,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 79: HDFS_LAUNCH(768, 3, kS4Nt | kModeNoShift); break;
     case 80: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeOvl); break;
     case 81: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeOvl | kModeStamps); break;
+    case 82: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter); break;
+    case 83: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeEarly); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

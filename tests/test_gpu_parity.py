@@ -554,6 +554,50 @@ def test_debug_library_variants_exact(hdfs, golden, orc, variant):
         ctx.close()
 
 
+@pytest.mark.parametrize("variant", [82, 83])
+def test_debug_quarter_nopad_variants_exact(hdfs, golden, orc, variant):
+    """Round 6's A/B of the production quarter-unit build (82) against the
+    same with the first unit's loads before the table staging (83): like
+    the production small-batch builds they carry no padded- or half-tile
+    code, so they are exact on the golden config-3 block, the mixed and
+    ragged digests and a ragged batch of power-of-two bpc, and refuse a plan
+    with padded tiles (bpc 1000)."""
+    torch = _torch()
+    ctx = hdfs.Context(0)
+    stream = torch.cuda.current_stream()
+
+    def run(payload, pk):
+        dev = torch.from_numpy(payload).cuda()
+        n = hdfs.total_checksums(pk)
+        out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        plan = hdfs.Plan(ctx, pk)
+        try:
+            plan.exec_variant(dev.data_ptr(), out.data_ptr(), variant, 0, stream.cuda_stream)
+            stream.synchronize()
+        finally:
+            plan.close()
+        return out.cpu().numpy().view(np.uint32)[:n]
+
+    try:
+        for nm in ("c3_one_block_4MiB", "c5_mixed_bpc_96", "ragged_tail_257", "c2_4096_packets"):
+            spec = [b for b in golden["batches"] if b["name"] == nm][0]
+            got = run(oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"]), golden_batch_packets(spec))
+            assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"], nm
+        rng = np.random.default_rng(variant)
+        pk = oracle.mixed_packets(24)
+        pk["len"] = rng.integers(0, 65537, pk.size).astype(np.uint32)
+        pk["payload_off"] = np.arange(pk.size, dtype=np.uint64) * np.uint64(65536 + 48) + np.uint64(16)
+        per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+        pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+        payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 99 + variant)
+        assert np.array_equal(run(payload, pk), orc.batch(payload, pk, hdfs.total_checksums(pk)))
+        padded = oracle.uniform_packets(8, 65536, 1000)
+        with pytest.raises(hdfs.Crc32cError):
+            run(oracle.xorshift64_bytes(8 * 65536 + 64, 5), padded)
+    finally:
+        ctx.close()
+
+
 def test_crc32_type_matches_zlib(hdfs, gpu_ctx):
     """CHECKSUM_CRC32 (CRC32C_TYPE_CRC32): same kernel, zlib-polynomial tables;
     per-chunk results equal zlib.crc32 (the reference returns -ENOSYS here,
