@@ -81,6 +81,11 @@ constexpr Variant kVariants[] = {
     // same with the first unit's loads issued before the table staging
     {82, "s4c_nt_quarter_nopad_prodgrid", 768, 1, true, true},
     {83, "s4c_nt_quarter_nopad_early_prodgrid", 768, 1, true, true},
+    // (round 6) the production small-batch build (compact image, whole
+    // tiles, no padded tiles), and the same with the first tile's loads
+    // before the table staging
+    {84, "s4c_nt_nopad_prodgrid", 768, 1, true, true},
+    {85, "s4c_nt_nopad_early_prodgrid", 768, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -102,9 +107,9 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{v.threads, 1, 1};
-    // (82 / 83 leave the padded- and half-tile code out, as the production
+    // (82-85 leave the padded- and half-tile code out, as the production
     // small-batch builds do: plans with such tiles are refused)
-    if ((v.id == 82 || v.id == 83) && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
+    if (v.id >= 82 && v.id <= 85 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
         return hipErrorInvalidValue;
     switch (v.id) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
@@ -148,6 +153,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 81: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeOvl | kModeStamps); break;
     case 82: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter); break;
     case 83: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeEarly); break;
+    case 84: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT); break;
+    case 85: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeEarly); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -554,10 +554,11 @@ def test_debug_library_variants_exact(hdfs, golden, orc, variant):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [82, 83])
+@pytest.mark.parametrize("variant", [82, 83, 84, 85])
 def test_debug_quarter_nopad_variants_exact(hdfs, golden, orc, variant):
-    """Round 6's A/B of the production quarter-unit build (82) against the
-    same with the first unit's loads before the table staging (83): like
+    """Round 6's A/Bs of the production quarter-unit build (82) and
+    small-batch build (84) against the same with the first unit's / tile's
+    loads before the table staging (83, 85): like
     the production small-batch builds they carry no padded- or half-tile
     code, so they are exact on the golden config-3 block, the mixed and
     ragged digests and a ragged batch of power-of-two bpc, and refuse a plan
