@@ -92,7 +92,7 @@ constexpr int kModeNoStage = 32;    // DIAGNOSTIC (memory-only): no table stagin
 constexpr int kModeVerify = 64;     // read side: compare with p.expect[] instead of storing (crc32c_plan_verify)
 constexpr int kModeS4C = 512;      // small batches: compact S4 image (T0..T3 once, 28 KiB staged)
 constexpr int kModeEarly = 1024;    // the first tile's loads are issued before the table staging
-constexpr int kModeHalves = 16384;  // A/B: with kModeQuarter, 2 units of 8 blocks per tile instead of 4
+constexpr int kModeHalves = 16384;  // with kModeQuarter, 2 units of 8 blocks per tile instead of 4 (3-6 tiles per CU)
 constexpr int kModeQuarter = 4096;  // small batches: power-of-two tiles of chunks <= 2 KiB run as 4 work
                                     // units of 4 blocks each (4x the waves, 1/4 of each wave's latency chain)
 constexpr int kModeXcdMap = 2048;   // A/B: workgroup ranges remapped so that each XCD's workgroups hold one

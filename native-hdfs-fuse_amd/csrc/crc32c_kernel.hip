@@ -23,6 +23,10 @@
 //     CU with the first unit's loads issued before the table staging (their
 //     latencies overlap: one 4 MiB block 3.71-3.74 -> 3.57 us; at 3 tiles
 //     per CU the staging queues behind them, 4.16-4.22 -> 4.41-4.46, round 6);
+//   * the same with half units (each tile over 2 waves): batches of more
+//     than kQuarterTilesPerCu and at most kHalvesTilesPerCu tiles per CU
+//     (2-3 blocks: 896 tiles 5.23-5.27 -> 4.69-4.73 us, 1024 tiles
+//     5.29-5.35 -> 4.76-4.82, 1536 tiles 6.09-6.16 -> 5.73-5.79, round 6);
 //   * full image with the general-tile code and half tiles (bpc <= 256,
 //     513..768 and 1025..1280), with and without the shifted loads, for any batch holding
 //     half tiles (compiled into the builds above, their code cost those
@@ -52,6 +56,12 @@ constexpr uint64_t kQuarterTilesPerCu = 3;
 // 83, profiles/r06/early/: 512 tiles 3.57 vs 3.71-3.74 us, 768 tiles
 // 4.41-4.46 vs 4.16-4.22).
 constexpr uint64_t kEarlyTilesPerCu = 2;
+// Tiles per CU up to which half units win over whole tiles (debug variant
+// 86 against production, tools/launch_probe.py, profiles/r06/halves/: 1280
+// tiles 5.50-5.55 vs 5.95-5.98 us, 1536 5.73-5.79 vs 6.09-6.16, 1792
+// 6.80-6.84 vs 6.56-6.58, 2048 7.02-7.13 vs 6.79-6.94).  (Round 2 measured
+// halves only with the padded-tile code in the build: 2-5 %.)
+constexpr uint64_t kHalvesTilesPerCu = 6;
 }  // namespace
 
 hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t stream, hipEvent_t stop,
@@ -68,7 +78,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     const bool small = !half && !(p.general & kGeneralPadded) && items <= kSmallBatchItemsPerCu * num_cu;
     const bool quarter = small && p.ntiles <= kQuarterTilesPerCu * num_cu;
     const bool early = quarter && p.ntiles <= kEarlyTilesPerCu * num_cu;
-    const dim3 g{production_grid(p, num_cu, quarter ? 4u : 1u), 1, 1}, b{768, 1, 1};
+    const bool halves = small && !quarter && p.ntiles <= kHalvesTilesPerCu * num_cu;
+    const dim3 g{production_grid(p, num_cu, quarter ? 4u : halves ? 2u : 1u), 1, 1}, b{768, 1, 1};
     if (grid) *grid = g.x;
 #define LAUNCH(K)                                                                  \
     do {                                                                           \
@@ -91,6 +102,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly | kModeVerify>));
         else if (quarter)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeVerify>));
+        else if (halves)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeHalves | kModeVerify>));
         else if (small)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall | kModeVerify>));
         else if (p.general == kGeneralItems)
@@ -110,6 +123,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly>));
         else if (quarter)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter>));
+        else if (halves)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeHalves>));
         else if (small)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kSmall>));
         else if (p.general == kGeneralItems)

@@ -554,7 +554,7 @@ def test_debug_library_variants_exact(hdfs, golden, orc, variant):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [82, 83, 84, 85])
+@pytest.mark.parametrize("variant", [82, 83, 84, 85, 86])
 def test_debug_quarter_nopad_variants_exact(hdfs, golden, orc, variant):
     """Round 6's A/Bs of the production quarter-unit build (82) and
     small-batch build (84) against the same with the first unit's / tile's
@@ -923,6 +923,40 @@ def test_fuzz_mixed_batches(hdfs, gpu_ctx, orc, seed):
         stream.synchronize()
         assert res.cpu().numpy().view(np.uint32).tolist() == [1, bad], size
         plan.close()
+
+
+@pytest.mark.parametrize("npk", [64, 96, 112, 128, 192, 224, 256])
+def test_small_batch_builds_by_size(hdfs, gpu_ctx, orc, npk):
+    """Batches of bpc 512 / 1024 / 4096 packets (ragged tails, skewed
+    offsets) sized to select each small-batch build: quarter units with the
+    first unit's loads before the staging (64 packets: 512 tiles, <= 2 per
+    CU), quarter units (96), half units (112-192: 3-6 tiles per CU), whole
+    tiles on the compact image (224, 256); exec and verify (one flipped
+    checksum) against the oracle."""
+    torch = _torch()
+    rng = np.random.default_rng(npk)
+    pk = oracle.mixed_packets(npk)
+    pk["len"][3::7] = rng.integers(1, 65536, pk["len"][3::7].size).astype(np.uint32)
+    pk["payload_off"] = np.arange(npk, dtype=np.uint64) * np.uint64(65536 + 64) + np.uint64(5) * (
+        np.arange(npk, dtype=np.uint64) % np.uint64(3))
+    per = (pk["len"].astype(np.uint64) + pk["bpc"] - 1) // pk["bpc"]
+    pk["out_idx"] = np.concatenate([[0], np.cumsum(per)[:-1]]).astype(np.uint64)
+    n = int(per.sum())
+    payload = oracle.xorshift64_bytes(int((pk["payload_off"] + pk["len"]).max()) + 64, 700 + npk)
+    want = orc.batch(payload, pk, n)
+    got = run_dev(hdfs, gpu_ctx, payload, pk)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+    plan = hdfs.Plan(gpu_ctx, pk)
+    dev = torch.from_numpy(payload).cuda()
+    exp = torch.from_numpy(want.view(np.int32).copy()).cuda()
+    bad = int(rng.integers(0, n))
+    exp[bad] ^= 0x100
+    res = torch.zeros(2, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream()
+    plan.verify(dev.data_ptr(), exp.data_ptr(), res.data_ptr(), stream.cuda_stream)
+    stream.synchronize()
+    assert res.cpu().numpy().view(np.uint32).tolist() == [1, bad]
+    plan.close()
 
 
 def test_entry_points_reject_bad_arguments(hdfs, gpu_ctx):
