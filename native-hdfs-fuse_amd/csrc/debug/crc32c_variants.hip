@@ -88,6 +88,10 @@ constexpr Variant kVariants[] = {
     {85, "s4c_nt_nopad_early_prodgrid", 768, 1, true, true},
     // (round 6) 82 with 2 units of 8 blocks per tile (halves)
     {86, "s4c_nt_halves_nopad_prodgrid", 768, 1, true, true},
+    // (round 6) 86 and 84 with 16 waves per workgroup (one round of half
+    // units / tiles at 4-8 tiles per CU)
+    {87, "s4c_wg1024_nt_halves_nopad_prodgrid", 1024, 1, true, true},
+    {88, "s4c_wg1024_nt_nopad_prodgrid", 1024, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -102,16 +106,16 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
     const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83) ? 4u
-                           : (v.id == 60 || v.id == 61 || v.id == 86)             ? 2u
+                           : (v.id == 60 || v.id == 61 || v.id == 86 || v.id == 87) ? 2u
                                                                                   : 1u;
     uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, units) : (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
     if (grid > cap) grid = cap;
     if (grid == 0) grid = 1;
     const dim3 g{uint32_t(grid), 1, 1}, b{v.threads, 1, 1};
-    // (82-86 leave the padded- and half-tile code out, as the production
+    // (82-88 leave the padded- and half-tile code out, as the production
     // small-batch builds do: plans with such tiles are refused)
-    if (v.id >= 82 && v.id <= 86 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
+    if (v.id >= 82 && v.id <= 88 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
         return hipErrorInvalidValue;
     switch (v.id) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
@@ -158,6 +162,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 84: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT); break;
     case 85: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeEarly); break;
     case 86: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeHalves); break;
+    case 87: HDFS_LAUNCH(1024, 4, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeHalves); break;
+    case 88: HDFS_LAUNCH(1024, 4, kS4Nt | kModeS4C | kModeNoPadT); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
