@@ -23,6 +23,9 @@
 //     CU with the first unit's loads issued before the table staging (their
 //     latencies overlap: one 4 MiB block 3.71-3.74 -> 3.57 us; at 3 tiles
 //     per CU the staging queues behind them, 4.16-4.22 -> 4.41-4.46, round 6);
+//     a batch with no general tiles and no tile off 16-byte alignment (a
+//     whole aligned block) runs that form without the general-tile code
+//     (one 4 MiB block 3.57 -> 3.42 us, round 6);
 //   * the same with half units (each tile over 2 waves): batches of more
 //     than kQuarterTilesPerCu and at most kHalvesTilesPerCu tiles per CU
 //     (2-3 blocks: 896 tiles 5.23-5.27 -> 4.69-4.73 us, 1024 tiles
@@ -98,6 +101,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeHalfT | kModeVerify>));
         else if (half)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT | kModeVerify>));
+        else if (early && !p.general)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeS4C | kModeQuarter | kModeEarly | kModeVerify>));
         else if (early)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly | kModeVerify>));
         else if (quarter)
@@ -119,6 +124,8 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeGHoist | kModeHalfT>));
         else if (half)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT>));
+        else if (early && !p.general)
+            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeS4C | kModeQuarter | kModeEarly>));
         else if (early)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly>));
         else if (quarter)

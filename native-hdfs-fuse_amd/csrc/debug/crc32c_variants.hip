@@ -92,6 +92,13 @@ constexpr Variant kVariants[] = {
     // units / tiles at 4-8 tiles per CU)
     {87, "s4c_wg1024_nt_halves_nopad_prodgrid", 1024, 1, true, true},
     {88, "s4c_wg1024_nt_nopad_prodgrid", 1024, 1, true, true},
+    // (round 6) the small-batch builds without the general-tile code (for
+    // batches of aligned power-of-two tiles only): quarter units + early
+    // loads, quarter units, half units
+    {89, "s4c_nt_pow2only_quarter_early_prodgrid", 768, 1, true, true},
+    {90, "s4c_nt_pow2only_quarter_prodgrid", 768, 1, true, true},
+    {91, "s4c_nt_pow2only_halves_prodgrid", 768, 1, true, true},
+    {92, "s4c_nt_pow2only_prodgrid", 768, 1, true, true},  // whole tiles, compact image
 };
 
 const Variant *find(int v) {
@@ -105,9 +112,9 @@ const Variant *find(int v) {
 hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
-    const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83) ? 4u
-                           : (v.id == 60 || v.id == 61 || v.id == 86 || v.id == 87) ? 2u
-                                                                                  : 1u;
+    const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83 || v.id == 89 || v.id == 90) ? 4u
+                           : (v.id == 60 || v.id == 61 || v.id == 86 || v.id == 87 || v.id == 91)             ? 2u
+                                                                                                              : 1u;
     uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, units) : (items + waves - 1) / waves;
     const uint64_t cap = uint64_t(num_cu) * v.wg_per_cu;
     if (grid > cap) grid = cap;
@@ -117,6 +124,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     // small-batch builds do: plans with such tiles are refused)
     if (v.id >= 82 && v.id <= 88 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
         return hipErrorInvalidValue;
+    // (89-92 carry no general-tile code at all: aligned power-of-two plans only)
+    if (v.id >= 89 && v.id <= 92 && p.general) return hipErrorInvalidValue;
     switch (v.id) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
     case 2: HDFS_LAUNCH(1024, 4, kS4Nt); break;
@@ -164,6 +173,10 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 86: HDFS_LAUNCH(768, 3, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeHalves); break;
     case 87: HDFS_LAUNCH(1024, 4, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeHalves); break;
     case 88: HDFS_LAUNCH(1024, 4, kS4Nt | kModeS4C | kModeNoPadT); break;
+    case 89: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeEarly); break;
+    case 90: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C | kModeQuarter); break;
+    case 91: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeHalves); break;
+    case 92: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

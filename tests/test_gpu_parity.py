@@ -599,6 +599,41 @@ def test_debug_quarter_nopad_variants_exact(hdfs, golden, orc, variant):
         ctx.close()
 
 
+@pytest.mark.parametrize("variant", [89, 90, 91, 92])
+def test_debug_pow2only_small_variants_exact(hdfs, golden, variant):
+    """Round 6's small-batch builds without the general-tile code (89
+    quarter units + early loads, 90 quarter units, 91 half units): exact on
+    the golden config-3 block, the mixed-bpc batch and config 2 (aligned
+    whole chunks only), and refusing a plan of tiles off 16-byte alignment."""
+    torch = _torch()
+    ctx = hdfs.Context(0)
+    stream = torch.cuda.current_stream()
+
+    def run(payload, pk):
+        dev = torch.from_numpy(payload).cuda()
+        n = hdfs.total_checksums(pk)
+        out = torch.full((max(n, 1),), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+        plan = hdfs.Plan(ctx, pk)
+        try:
+            plan.exec_variant(dev.data_ptr(), out.data_ptr(), variant, 0, stream.cuda_stream)
+            stream.synchronize()
+        finally:
+            plan.close()
+        return out.cpu().numpy().view(np.uint32)[:n]
+
+    try:
+        for nm in ("c3_one_block_4MiB", "c5_mixed_bpc_96", "c2_4096_packets"):
+            spec = [b for b in golden["batches"] if b["name"] == nm][0]
+            got = run(oracle.xorshift64_bytes(spec["payload_bytes"], spec["seed"]), golden_batch_packets(spec))
+            assert hashlib.sha256(got.astype("<u4").tobytes()).hexdigest() == spec["sha256_le"], nm
+        skewed = oracle.uniform_packets(8)
+        skewed["payload_off"] += np.uint64(5)  # (tiles off 16-byte alignment: the general build's)
+        with pytest.raises(hdfs.Crc32cError):
+            run(oracle.xorshift64_bytes(8 * 65536 + 64, 6), skewed)
+    finally:
+        ctx.close()
+
+
 def test_crc32_type_matches_zlib(hdfs, gpu_ctx):
     """CHECKSUM_CRC32 (CRC32C_TYPE_CRC32): same kernel, zlib-polynomial tables;
     per-chunk results equal zlib.crc32 (the reference returns -ENOSYS here,
