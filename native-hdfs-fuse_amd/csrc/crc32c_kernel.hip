@@ -24,8 +24,9 @@
 //     latencies overlap: one 4 MiB block 3.71-3.74 -> 3.57 us; at 3 tiles
 //     per CU the staging queues behind them, 4.16-4.22 -> 4.41-4.46, round 6);
 //     a batch with no general tiles and no tile off 16-byte alignment (a
-//     whole aligned block) runs that form without the general-tile code
-//     (one 4 MiB block 3.57 -> 3.42 us, round 6);
+//     whole aligned block) runs that form without the general-tile code and
+//     with 8 waves per workgroup, one per unit (one 4 MiB block 3.57 ->
+//     3.42 us without the code, -> 3.35 us with 8 waves, round 6);
 //   * the same with half units (each tile over 2 waves): batches of more
 //     than kQuarterTilesPerCu and at most kHalvesTilesPerCu tiles per CU
 //     (2-3 blocks: 896 tiles 5.23-5.27 -> 4.69-4.73 us, 1024 tiles
@@ -84,13 +85,15 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
     const bool halves = small && !quarter && p.ntiles <= kHalvesTilesPerCu * num_cu;
     const dim3 g{production_grid(p, num_cu, quarter ? 4u : halves ? 2u : 1u), 1, 1}, b{768, 1, 1};
     if (grid) *grid = g.x;
-#define LAUNCH(K)                                                                  \
+#define LAUNCH_B(K, B)                                                             \
     do {                                                                           \
         if (stop)                                                                  \
-            hipExtLaunchKernelGGL(K, g, b, 0, stream, nullptr, stop, 0u, p);       \
+            hipExtLaunchKernelGGL(K, g, B, 0, stream, nullptr, stop, 0u, p);       \
         else                                                                       \
-            hipLaunchKernelGGL(K, g, b, 0, stream, p);                             \
+            hipLaunchKernelGGL(K, g, B, 0, stream, p);                             \
     } while (0)
+#define LAUNCH(K) LAUNCH_B(K, b)
+    const dim3 b8{512, 1, 1};  // (the aligned one-block form: 8 waves)
     // Half tiles run in builds of their own, any batch size (the full image):
     // with the shifted loads only where some tile is off 16-byte alignment
     // (padded general items -- a packet's tail -- do not need them there).
@@ -102,7 +105,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
         else if (half)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT | kModeVerify>));
         else if (early && !p.general)
-            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeS4C | kModeQuarter | kModeEarly | kModeVerify>));
+            LAUNCH_B((hdfs_crc32c_plan_kernel<512, 2, kProd | kModeS4C | kModeQuarter | kModeEarly | kModeVerify>), b8);
         else if (early)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly | kModeVerify>));
         else if (quarter)
@@ -125,7 +128,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
         else if (half)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kGen | kModeNoShift | kModeHalfT>));
         else if (early && !p.general)
-            LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kModeS4C | kModeQuarter | kModeEarly>));
+            LAUNCH_B((hdfs_crc32c_plan_kernel<512, 2, kProd | kModeS4C | kModeQuarter | kModeEarly>), b8);
         else if (early)
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd | kQuarter | kModeEarly>));
         else if (quarter)
@@ -144,6 +147,7 @@ hipError_t launch_plan_kernel(const KParams &p, uint32_t num_cu, hipStream_t str
             LAUNCH((hdfs_crc32c_plan_kernel<768, 3, kProd>));
     }
 #undef LAUNCH
+#undef LAUNCH_B
     return hipGetLastError();
 }
 

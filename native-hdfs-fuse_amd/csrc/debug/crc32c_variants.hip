@@ -99,6 +99,8 @@ constexpr Variant kVariants[] = {
     {90, "s4c_nt_pow2only_quarter_prodgrid", 768, 1, true, true},
     {91, "s4c_nt_pow2only_halves_prodgrid", 768, 1, true, true},
     {92, "s4c_nt_pow2only_prodgrid", 768, 1, true, true},  // whole tiles, compact image
+    // (round 6) 89 with 8 waves per workgroup (config 3: 8 units per CU, one per wave)
+    {93, "s4c_wg512_nt_pow2only_quarter_early_prodgrid", 512, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -112,7 +114,9 @@ const Variant *find(int v) {
 hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t num_cu, hipStream_t stream) {
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
-    const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83 || v.id == 89 || v.id == 90) ? 4u
+    const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83 || v.id == 89 || v.id == 90 ||
+                            v.id == 93)
+                               ? 4u
                            : (v.id == 60 || v.id == 61 || v.id == 86 || v.id == 87 || v.id == 91)             ? 2u
                                                                                                               : 1u;
     uint64_t grid = v.prod_grid ? hdfs_crc::production_grid(p, num_cu, units) : (items + waves - 1) / waves;
@@ -124,8 +128,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     // small-batch builds do: plans with such tiles are refused)
     if (v.id >= 82 && v.id <= 88 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
         return hipErrorInvalidValue;
-    // (89-92 carry no general-tile code at all: aligned power-of-two plans only)
-    if (v.id >= 89 && v.id <= 92 && p.general) return hipErrorInvalidValue;
+    // (89-93 carry no general-tile code at all: aligned power-of-two plans only)
+    if (v.id >= 89 && v.id <= 93 && p.general) return hipErrorInvalidValue;
     switch (v.id) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
     case 2: HDFS_LAUNCH(1024, 4, kS4Nt); break;
@@ -177,6 +181,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 90: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C | kModeQuarter); break;
     case 91: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeHalves); break;
     case 92: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C); break;
+    case 93: HDFS_LAUNCH(512, 2, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeEarly); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
