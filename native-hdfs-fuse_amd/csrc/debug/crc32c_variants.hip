@@ -101,6 +101,8 @@ constexpr Variant kVariants[] = {
     {92, "s4c_nt_pow2only_prodgrid", 768, 1, true, true},  // whole tiles, compact image
     // (round 6) 89 with 8 waves per workgroup (config 3: 8 units per CU, one per wave)
     {93, "s4c_wg512_nt_pow2only_quarter_early_prodgrid", 512, 1, true, true},
+    // (round 6) 92 with 8 waves per workgroup (the 16 MiB shard: 8 tiles per CU)
+    {94, "s4c_wg512_nt_pow2only_prodgrid", 512, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -128,8 +130,8 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     // small-batch builds do: plans with such tiles are refused)
     if (v.id >= 82 && v.id <= 88 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
         return hipErrorInvalidValue;
-    // (89-93 carry no general-tile code at all: aligned power-of-two plans only)
-    if (v.id >= 89 && v.id <= 93 && p.general) return hipErrorInvalidValue;
+    // (89-94 carry no general-tile code at all: aligned power-of-two plans only)
+    if (v.id >= 89 && v.id <= 94 && p.general) return hipErrorInvalidValue;
     switch (v.id) {
     case 1: HDFS_LAUNCH(1024, 8, kModeNt | kModeGeneral); break;
     case 2: HDFS_LAUNCH(1024, 4, kS4Nt); break;
@@ -182,6 +184,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 91: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeHalves); break;
     case 92: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C); break;
     case 93: HDFS_LAUNCH(512, 2, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeEarly); break;
+    case 94: HDFS_LAUNCH(512, 2, kModeS4 | kModeNt | kModeS4C); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -599,7 +599,7 @@ def test_debug_quarter_nopad_variants_exact(hdfs, golden, orc, variant):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [89, 90, 91, 92, 93])
+@pytest.mark.parametrize("variant", [89, 90, 91, 92, 93, 94])
 def test_debug_pow2only_small_variants_exact(hdfs, golden, variant):
     """Round 6's small-batch builds without the general-tile code (89
     quarter units + early loads, 90 quarter units, 91 half units): exact on
