@@ -103,6 +103,9 @@ constexpr Variant kVariants[] = {
     {93, "s4c_wg512_nt_pow2only_quarter_early_prodgrid", 512, 1, true, true},
     // (round 6) 92 with 8 waves per workgroup (the 16 MiB shard: 8 tiles per CU)
     {94, "s4c_wg512_nt_pow2only_prodgrid", 512, 1, true, true},
+    // (round 6) 83 (quarter units + early loads, general-tile code) with 8
+    // waves per workgroup: one block off 16-byte alignment (an append)
+    {95, "s4c_wg512_nt_quarter_nopad_early_prodgrid", 512, 1, true, true},
 };
 
 const Variant *find(int v) {
@@ -117,7 +120,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     const uint64_t items = uint64_t(p.ntiles) + (uint64_t(p.ngen) + 1) / 2 + (uint64_t(p.nseg) + 1) / 2 + p.nconst;
     const uint64_t waves = v.threads / 64;
     const uint32_t units = ((v.id >= 51 && v.id <= 55) || v.id == 82 || v.id == 83 || v.id == 89 || v.id == 90 ||
-                            v.id == 93)
+                            v.id == 93 || v.id == 95)
                                ? 4u
                            : (v.id == 60 || v.id == 61 || v.id == 86 || v.id == 87 || v.id == 91)             ? 2u
                                                                                                               : 1u;
@@ -128,7 +131,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     const dim3 g{uint32_t(grid), 1, 1}, b{v.threads, 1, 1};
     // (82-88 leave the padded- and half-tile code out, as the production
     // small-batch builds do: plans with such tiles are refused)
-    if (v.id >= 82 && v.id <= 88 && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
+    if (((v.id >= 82 && v.id <= 88) || v.id == 95) && (p.general & (hdfs_crc::kGeneralPadded | hdfs_crc::kGeneralHalf)))
         return hipErrorInvalidValue;
     // (89-94 carry no general-tile code at all: aligned power-of-two plans only)
     if (v.id >= 89 && v.id <= 94 && p.general) return hipErrorInvalidValue;
@@ -185,6 +188,7 @@ hipError_t launch_variant(const hdfs_crc::KParams &p, const Variant &v, uint32_t
     case 92: HDFS_LAUNCH(768, 3, kModeS4 | kModeNt | kModeS4C); break;
     case 93: HDFS_LAUNCH(512, 2, kModeS4 | kModeNt | kModeS4C | kModeQuarter | kModeEarly); break;
     case 94: HDFS_LAUNCH(512, 2, kModeS4 | kModeNt | kModeS4C); break;
+    case 95: HDFS_LAUNCH(512, 2, kS4Nt | kModeS4C | kModeNoPadT | kModeQuarter | kModeEarly); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

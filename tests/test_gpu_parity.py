@@ -554,7 +554,7 @@ def test_debug_library_variants_exact(hdfs, golden, orc, variant):
         ctx.close()
 
 
-@pytest.mark.parametrize("variant", [82, 83, 84, 85, 86, 87, 88])
+@pytest.mark.parametrize("variant", [82, 83, 84, 85, 86, 87, 88, 95])
 def test_debug_quarter_nopad_variants_exact(hdfs, golden, orc, variant):
     """Round 6's A/Bs of the production quarter-unit build (82) and
     small-batch build (84) against the same with the first unit's / tile's
