@@ -52,12 +52,14 @@ def test_exports_every_declared_symbol(hdfs):
 def test_product_library_has_no_variant_switch(hdfs):
     """The public path launches only the production kernel: the product .so
     exports no variant entry point or read probe, never reads a kernel-variant
-    environment variable, and holds exactly the sixteen production kernels
-    (exec, verify; full image without general-tile code, with general tiles
-    and shifted tiles, general tiles only, shifted tiles only; compact
-    image, compact image with quarter units; half tiles with general tiles,
-    with and without shifted tiles); the A/B kernels live in the
-    debug library."""
+    environment variable, and holds exactly the twenty-two production
+    kernels (exec, verify; full image without general-tile code, with
+    general tiles and shifted tiles, general tiles only, shifted tiles only;
+    compact image, compact image with quarter units, with quarter units and
+    early loads, with half units, and the aligned one-block form -- quarter
+    units, early loads, no general-tile code, 8 waves; half tiles with
+    general tiles, with and without shifted tiles); the A/B kernels live in
+    the debug library."""
     import ctypes
 
     lib = ctypes.CDLL(hdfs.LIB_PATH)
@@ -70,11 +72,14 @@ def test_product_library_has_no_variant_switch(hdfs):
     # + 4096 quarter units (the smallest batches), + 32768 no shifted tiles, + 65536 no general tiles,
     # + 131072 general items' next subtile facts hoisted (the build with both general and shifted tiles),
     # + 1048576 half tiles (their own builds: general tiles, with and without shifted tiles),
-    # + 2097152 (NP) no padded power-of-two tiles (the small-batch builds)
+    # + 2097152 (NP) no padded power-of-two tiles (the small-batch builds),
+    # + 1024 first unit's loads before the staging, + 16384 half units (2 per tile)
     NP = 2097152
-    assert kernels == {b"_Z23hdfs_crc32c_plan_kernelILi768ELi3ELi%dEEvN8hdfs_crc7KParamsE" % m
-                       for m in (3, 67, 131331, 131395, 771 + NP, 835 + NP, 4867 + NP, 4931 + NP, 33027, 33091, 65795,
-                                 65859, 1081603, 1081667, 1179907, 1179971)}, kernels
+    want = {b"_Z23hdfs_crc32c_plan_kernelILi768ELi3ELi%dEEvN8hdfs_crc7KParamsE" % m
+            for m in (3, 67, 131331, 131395, 771 + NP, 835 + NP, 4867 + NP, 4931 + NP, 5891 + NP, 5955 + NP,
+                      21251 + NP, 21315 + NP, 33027, 33091, 65795, 65859, 1081603, 1081667, 1179907, 1179971)}
+    want |= {b"_Z23hdfs_crc32c_plan_kernelILi512ELi2ELi%dEEvN8hdfs_crc7KParamsE" % m for m in (5635, 5699)}
+    assert kernels == want, kernels
     dblob = open(hdfs.DEBUG_LIB_PATH, "rb").read()
     assert len(set(re.findall(rb"_Z23hdfs_crc32c_plan_kernelILi\d+ELi\d+ELi\d+EEvN8hdfs_crc7KParamsE", dblob))) >= 9
 
